@@ -1,0 +1,267 @@
+#!/usr/bin/env python3
+"""Benchmark: Mpps classified (device-resident), 64 B packets x 64 PMR rules.
+
+One step = one pass of the receive-path classifier (parse + RX checksum
+verdict + PMR -> CoS walk, odpg_classify) over one batch of 2^20 synthetic
+frames already resident in HBM, writing the 4-byte verdict per packet.
+
+Launch:  python bench.py [--gpus N --steps K --warmup W --config c2]
+         torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+Packets are independent: each rank classifies its own shard (weak scaling,
+no data-path collective). The only collective is the end-of-run RCCL
+all-reduce of the CoS / pktio counters (odp_cls_cos_stats semantics).
+
+Rank 0 prints one JSON line (contract in the task description) with a
+`roofline` object (kernel time from HIP events on the classify stream) and a
+`cpu_baseline` object (the CPU restatement timed on this host's cores).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "Mpps classified (device-resident), 64B pkts × 64 PMR rules"
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c4"])
+    ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--buffers", type=int, default=0,
+                    help="rotating input batches (default: enough to exceed the 256 MiB "
+                         "Infinity Cache so every launch streams from HBM)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--e2e", action="store_true",
+                    help="also time the host-buffer path (pinned H2D + kernel + D2H)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", rank=rank, world_size=world)
+        dist = tdist
+
+    import ctypes as C
+
+    import numpy as np
+
+    from odp_amd import _lib as L
+    from odp_amd import cls, gen, gpu
+
+    opt = L.PKTIN_IPV4_CHKSUM | L.PKTIN_UDP_CHKSUM | L.PKTIN_TCP_CHKSUM
+    cls.reset()
+    if args.config == "c4":
+        assert cls.set_limits(2048, 2048, 32) == 0
+    pktio = cls.loop_pktio(pktin=opt)
+    if args.config == "c1":
+        gen.build_c1_rules(cls, pktio)
+        nrules = 1
+        frames_fn = gen.c1_frames
+        workload = ("C1: 64B IPv4/UDP x 1 PMR (SIP 10.10.10.0/24 -> queue1, "
+                    "example/classifier rule)")
+    elif args.config == "c4":
+        gen.build_c4_rules(cls, pktio)
+        nrules = 1024
+        frames_fn = gen.c2_frames
+        workload = "C4: 64B IPv4/UDP x 1024 PMR (32x SIP/21 -> 32x31 UDP_DPORT), raised limits"
+    else:
+        gen.build_c2_rules(cls, pktio)
+        nrules = 64
+        frames_fn = gen.c2_frames
+        workload = ("C2: 64B IPv4/UDP x 64 PMR (default -> 8x SIP_ADDR/19 -> 8x7 UDP_DPORT "
+                    "-> 55 leaf CoS), pktin ipv4+udp+tcp checksum verify")
+    assert cls.pktio_start(pktio) == 0
+    rules = cls.pktio_rules(pktio)
+
+    n = args.batch
+    stride = 64
+    # each rank owns a distinct shard of the synthetic capture
+    frames = frames_fn(n, seed=gen.C_SEED + rank)
+    ctx = gpu.Context(local)
+    tbl = ctx.table(rules)
+    nbuf = args.buffers or max(2, -(-300 * (1 << 20) // (n * stride)))
+    fbufs, obufs = [], []
+    for _ in range(nbuf):
+        fb = ctx.buffer(n * stride)
+        fb.upload(frames)
+        fbufs.append(fb)
+        obufs.append(ctx.buffer(4 * n))
+    nstats = 4 + tbl.num_cos
+    sbuf = ctx.buffer(8 * nstats)
+    sbuf.zero()
+    batches = [L.odpg_batch_t(fb.ptr, None, stride, n, opt, L.LAYER_ALL, 1) for fb in fbufs]
+    results = [L.odpg_result_t(ob.ptr, None, None, None) for ob in obufs]
+    res_stats = L.odpg_result_t(obufs[0].ptr, None, None, sbuf.ptr)
+    lib = L.lib
+
+    def launch(i, stats=False):
+        r = res_stats if stats else results[i % nbuf]
+        b = batches[0] if stats else batches[i % nbuf]
+        rc = lib.odpg_classify(ctx.h, tbl.h, C.byref(b), C.byref(r))
+        if rc:
+            raise RuntimeError(f"odpg_classify rc={rc}")
+
+    def barrier():
+        ctx.sync()
+        if dist is not None:
+            dist.barrier()
+
+    # counters pass (counts every packet once, checked below)
+    launch(0, stats=True)
+    for i in range(args.warmup):
+        launch(i)
+    barrier()
+    t0 = time.perf_counter()
+    lib.odpg_event_record(ctx.h, 0)
+    for i in range(args.steps):
+        launch(i)
+    lib.odpg_event_record(ctx.h, 1)
+    ctx.sync()
+    t1 = time.perf_counter()
+    barrier()
+    wall = t1 - t0
+    ev_ms = C.c_float(0)
+    L.check(lib.odpg_event_elapsed_ms(ctx.h, 0, 1, C.byref(ev_ms)), "event")
+    kernel_ms = ev_ms.value / max(args.steps, 1)
+
+    stats = sbuf.download(np.uint64, nstats)
+    if dist is not None:
+        import torch
+        t = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+        st = torch.tensor(stats.astype(np.int64), device=f"cuda:{local}")
+        dist.all_reduce(st, op=dist.ReduceOp.SUM)      # CoS / pktio counters across GPUs
+        stats = st.cpu().numpy().astype(np.uint64)
+    assert int(stats[0]) == n * world, ("not every packet was delivered", stats[:4])
+
+    ms_per_step = wall * 1e3 / max(args.steps, 1)
+    total_pkts = n * world * args.steps
+    value = total_pkts / wall / 1e6
+    bytes_per_pkt = stride + 4
+    achieved = bytes_per_pkt * n / (kernel_ms * 1e-3) / 1e9
+
+    out = None
+    if rank == 0:
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": None, "kernel_ms": round(kernel_ms, 5),
+                    "bytes_per_pkt": bytes_per_pkt, "pkts_per_launch": n}
+        tf = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
+        if os.path.exists(tf):
+            try:
+                roofline["traffic"] = json.load(open(tf)).get("bytes_per_launch")
+            except Exception:
+                pass
+        cpu = None
+        if not args.no_cpu and world == 1:
+            cpu = cpu_baseline(rules, frames, n, stride, opt, args)
+        out = {
+            "metric": METRIC if args.config == "c2" else METRIC.replace("64 PMR", f"{nrules} PMR"),
+            "value": round(value, 1), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": workload, "batch_per_gpu": n, "frame_bytes": stride,
+                       "pmr_rules": nrules, "rotating_buffers": nbuf,
+                       "parallelism": f"dp{world} (packet shards, no data-path collective)"},
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        if args.e2e:
+            out["e2e_host_path"] = e2e(ctx, tbl, frames, n, stride, opt)
+        print(json.dumps(out), flush=True)
+    del tbl
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(rules, frames, n, stride, opt, args):
+    """The CPU restatement of linux-generic's classifier (oracle/, a literal
+    port of the reference's per-packet path) timed on this host's cores over
+    the same batch, ~cpu_seconds of work."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    threads = args.cpu_threads or max(1, min(16, ncpu))
+    sub = min(n, 1 << 18)
+    # single-thread calibration pass
+    t = time.perf_counter()
+    oracle.classify_mt(rules, frames, sub, stride=stride, opt=opt, nthreads=1, reps=1)
+    one = sub / (time.perf_counter() - t) / 1e6
+    reps = max(1, int(args.cpu_seconds * one * threads * 1e6 / n * 0.8))
+    t = time.perf_counter()
+    _, used = oracle.classify_mt(rules, frames, n, stride=stride, opt=opt, nthreads=threads,
+                                 reps=reps)
+    dt = time.perf_counter() - t
+    model = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(n * reps / dt / 1e6, 2), "unit": "Mpps", "cores": used,
+            "kind": "port", "value_1thread": round(one, 2), "cpu_model": model,
+            "sample": f"{reps} passes x {n} pkts of the same C2 batch in host DRAM "
+                      f"({dt:.1f} s, {used} threads)"}
+
+
+def e2e(ctx, tbl, frames, n, stride, opt):
+    """Host (pinned) buffers -> H2D -> classify -> D2H verdicts, double-buffered."""
+    import ctypes as C
+
+    import numpy as np
+
+    from odp_amd import _lib as L
+    lib = L.lib
+    hp = C.c_void_p()
+    L.check(lib.odpg_host_alloc_pinned(frames.nbytes, C.byref(hp)), "pinned")
+    ho = C.c_void_p()
+    L.check(lib.odpg_host_alloc_pinned(4 * n, C.byref(ho)), "pinned")
+    C.memmove(hp.value, frames.ctypes.data, frames.nbytes)
+    b = L.odpg_batch_t(hp.value, None, stride, n, opt, L.LAYER_ALL, 1)
+    r = L.odpg_result_t(ho.value, None, None, None)
+    res = {}
+    for chunk in (1 << 16, 1 << 18):
+        lib.odpg_classify_host(ctx.h, tbl.h, C.byref(b), C.byref(r), chunk)
+        reps = 10
+        t = time.perf_counter()
+        for _ in range(reps):
+            L.check(lib.odpg_classify_host(ctx.h, tbl.h, C.byref(b), C.byref(r), chunk), "host")
+        dt = (time.perf_counter() - t) / reps
+        res[f"chunk_{chunk}"] = {"mpps": round(n / dt / 1e6, 1),
+                                 "gbps_h2d": round(n * stride / dt / 1e9, 2)}
+    lib.odpg_host_free_pinned(hp.value)
+    lib.odpg_host_free_pinned(ho.value)
+    del np
+    return res
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,367 @@
+/* SPDX-License-Identifier: BSD-3-Clause
+ *
+ * odp_cls.h — ODP classification API (odp_cls_* / odp_cos_* / pktio
+ * classifier setters) served by the MI355X classifier library.
+ *
+ * Names, argument meaning, handle encoding (index + 1, 0 = invalid) and
+ * error behaviour follow the reference:
+ *   API spec      include/odp/api/spec/classification.h:697-1073
+ *   pktio setters include/odp/api/spec/packet_io.h:677-724
+ *   semantics     platform/linux-generic/odp_classification.c:137-1877
+ * The loop-pktio subset (open/config/start/recv) is the minimum needed to
+ * drive the classifier the way pktio/loop.c does; it is not the full
+ * odp_pktio API.
+ *
+ * Struct layouts follow the spec's field order; nested types the classifier
+ * does not interpret (queue parameters, RED/BP, packet vectors) are
+ * simplified — see INTEGRATION.md "ABI notes".
+ */
+#ifndef ODP_CLS_H_
+#define ODP_CLS_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#include "odpg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int odp_bool_t;
+
+typedef struct _odp_cos_hdl   *odp_cos_t;
+typedef struct _odp_pmr_hdl   *odp_pmr_t;
+typedef struct _odp_queue_hdl *odp_queue_t;
+typedef struct _odp_pool_hdl  *odp_pool_t;
+typedef struct _odp_pktio_hdl *odp_pktio_t;
+
+#define ODP_COS_INVALID   ((odp_cos_t)0)
+#define ODP_PMR_INVALID   ((odp_pmr_t)0)
+#define ODP_QUEUE_INVALID ((odp_queue_t)0)
+#define ODP_POOL_INVALID  ((odp_pool_t)0)
+#define ODP_PKTIO_INVALID ((odp_pktio_t)0)
+
+#define ODP_COS_NAME_LEN  32
+
+typedef enum {
+	ODP_PMR_LEN = 0,
+	ODP_PMR_ETHTYPE_0,
+	ODP_PMR_ETHTYPE_X,
+	ODP_PMR_VLAN_ID_0,
+	ODP_PMR_VLAN_ID_X,
+	ODP_PMR_VLAN_PCP_0,
+	ODP_PMR_DMAC,
+	ODP_PMR_IPPROTO,
+	ODP_PMR_IP_DSCP,
+	ODP_PMR_UDP_DPORT,
+	ODP_PMR_TCP_DPORT,
+	ODP_PMR_UDP_SPORT,
+	ODP_PMR_TCP_SPORT,
+	ODP_PMR_SIP_ADDR,
+	ODP_PMR_DIP_ADDR,
+	ODP_PMR_SIP6_ADDR,
+	ODP_PMR_DIP6_ADDR,
+	ODP_PMR_IPSEC_SPI,
+	ODP_PMR_LD_VNI,
+	ODP_PMR_CUSTOM_FRAME,
+	ODP_PMR_CUSTOM_L3,
+	ODP_PMR_IGMP_GRP_ADDR,
+	ODP_PMR_ICMP_ID,
+	ODP_PMR_ICMP_TYPE,
+	ODP_PMR_ICMP_CODE,
+	ODP_PMR_SCTP_SPORT,
+	ODP_PMR_SCTP_DPORT,
+	ODP_PMR_GTPV1_TEID,
+	ODP_PMR_INNER_HDR_OFF = 32
+} odp_cls_pmr_term_t;
+
+typedef struct odp_pmr_param_t {
+	odp_cls_pmr_term_t term;
+	odp_bool_t range_term;
+	union {
+		struct {
+			const void *value;
+			const void *mask;
+		} match;
+		struct {
+			const void *val_start;
+			const void *val_end;
+		} range;
+	};
+	uint32_t val_sz;
+	uint32_t offset;
+} odp_pmr_param_t;
+
+typedef struct odp_pmr_create_opt_t {
+	odp_pmr_param_t *terms;
+	int num_terms;
+	uint64_t mark;
+} odp_pmr_create_opt_t;
+
+typedef enum {
+	ODP_COS_ACTION_ENQUEUE,
+	ODP_COS_ACTION_DROP
+} odp_cos_action_t;
+
+typedef union odp_pktin_hash_proto_t {
+	struct {
+		uint32_t ipv4_udp : 1;
+		uint32_t ipv4_tcp : 1;
+		uint32_t ipv4     : 1;
+		uint32_t ipv6_udp : 1;
+		uint32_t ipv6_tcp : 1;
+		uint32_t ipv6     : 1;
+	} proto;
+	uint32_t all_bits;
+} odp_pktin_hash_proto_t;
+
+/* simplified: the classifier only stores these */
+typedef struct odp_queue_param_t {
+	int type;
+	int sched_prio;
+	int sched_sync;
+	int sched_group;
+	uint32_t size;
+	uint32_t reserved[7];
+} odp_queue_param_t;
+
+typedef struct odp_red_param_t {
+	odp_bool_t enable;
+	uint32_t reserved[5];
+} odp_red_param_t;
+
+typedef struct odp_bp_param_t {
+	odp_bool_t enable;
+	uint32_t reserved[5];
+} odp_bp_param_t;
+
+typedef struct odp_pktin_vector_config_t {
+	odp_bool_t enable;
+	odp_pool_t pool;
+	uint32_t max_size;
+	uint64_t max_tmo_ns;
+} odp_pktin_vector_config_t;
+
+typedef struct odp_cls_cos_param {
+	odp_cos_action_t action;
+	odp_bool_t stats_enable;
+	uint32_t num_queue;
+	union {
+		odp_queue_t queue;
+		struct {
+			odp_queue_param_t queue_param;
+			odp_pktin_hash_proto_t hash_proto;
+		};
+	};
+	odp_pool_t pool;
+	odp_red_param_t red;
+	odp_bp_param_t bp;
+	odp_pktin_vector_config_t vector;
+} odp_cls_cos_param_t;
+
+typedef union odp_cls_pmr_terms_t {
+	struct {
+		uint64_t len : 1;
+		uint64_t ethtype_0 : 1;
+		uint64_t ethtype_x : 1;
+		uint64_t vlan_id_0 : 1;
+		uint64_t vlan_id_x : 1;
+		uint64_t vlan_pcp_0 : 1;
+		uint64_t dmac : 1;
+		uint64_t ip_proto : 1;
+		uint64_t ip_dscp : 1;
+		uint64_t udp_dport : 1;
+		uint64_t tcp_dport : 1;
+		uint64_t udp_sport : 1;
+		uint64_t tcp_sport : 1;
+		uint64_t sip_addr : 1;
+		uint64_t dip_addr : 1;
+		uint64_t sip6_addr : 1;
+		uint64_t dip6_addr : 1;
+		uint64_t ipsec_spi : 1;
+		uint64_t ld_vni : 1;
+		uint64_t custom_frame : 1;
+		uint64_t custom_l3 : 1;
+		uint64_t igmp_grp_addr : 1;
+		uint64_t icmp_id : 1;
+		uint64_t icmp_type : 1;
+		uint64_t icmp_code : 1;
+		uint64_t sctp_sport : 1;
+		uint64_t sctp_dport : 1;
+		uint64_t gtpv1_teid : 1;
+	} bit;
+	uint64_t all_bits;
+} odp_cls_pmr_terms_t;
+
+typedef struct odp_cls_capability_t {
+	odp_cls_pmr_terms_t supported_terms;
+	uint32_t max_pmr;
+	uint32_t max_pmr_per_cos;
+	uint32_t max_terms_per_pmr;
+	uint32_t max_cos;
+	uint32_t max_cos_stats;
+	uint32_t max_hash_queues;
+	odp_pktin_hash_proto_t hash_protocols;
+	odp_bool_t pmr_range_supported;
+	int random_early_detection;
+	uint64_t threshold_red;
+	int back_pressure;
+	uint64_t threshold_bp;
+	uint64_t max_mark;
+	struct {
+		struct { uint64_t all_counters; } cos;
+		struct { uint64_t all_counters; } queue;
+	} stats;
+} odp_cls_capability_t;
+
+typedef struct odp_cls_cos_stats_t {
+	uint64_t octets;
+	uint64_t packets;
+	uint64_t discards;
+	uint64_t errors;
+} odp_cls_cos_stats_t;
+
+typedef struct odp_cls_queue_stats_t {
+	uint64_t octets;
+	uint64_t packets;
+	uint64_t discards;
+	uint64_t errors;
+} odp_cls_queue_stats_t;
+
+/* ---- classification API (classification.h:697-1073) -------------------- */
+int  odp_cls_capability(odp_cls_capability_t *capability);
+void odp_cls_cos_param_init(odp_cls_cos_param_t *param);
+void odp_cls_pmr_param_init(odp_pmr_param_t *param);
+void odp_cls_pmr_create_opt_init(odp_pmr_create_opt_t *opt);
+odp_cos_t odp_cls_cos_create(const char *name, const odp_cls_cos_param_t *param);
+int  odp_cls_cos_create_multi(const char *name[], const odp_cls_cos_param_t param[],
+			      odp_cos_t cos[], int num);
+int  odp_cos_destroy(odp_cos_t cos);
+int  odp_cos_destroy_multi(odp_cos_t cos[], int num);
+int  odp_cos_queue_set(odp_cos_t cos, odp_queue_t queue);
+odp_queue_t odp_cos_queue(odp_cos_t cos);
+uint32_t odp_cls_cos_num_queue(odp_cos_t cos);
+uint32_t odp_cls_cos_queues(odp_cos_t cos, odp_queue_t queue[], uint32_t num);
+odp_pmr_t odp_cls_pmr_create(const odp_pmr_param_t *terms, int num_terms,
+			     odp_cos_t src_cos, odp_cos_t dst_cos);
+odp_pmr_t odp_cls_pmr_create_opt(const odp_pmr_create_opt_t *opt,
+				 odp_cos_t src_cos, odp_cos_t dst_cos);
+int  odp_cls_pmr_create_multi(const odp_pmr_create_opt_t opt[], odp_cos_t src_cos[],
+			      odp_cos_t dst_cos[], odp_pmr_t pmr[], int num);
+int  odp_cls_pmr_destroy(odp_pmr_t pmr);
+int  odp_cls_pmr_destroy_multi(odp_pmr_t pmr[], int num);
+int  odp_cls_cos_pool_set(odp_cos_t cos, odp_pool_t pool);
+odp_pool_t odp_cls_cos_pool(odp_cos_t cos);
+int  odp_cls_cos_stats(odp_cos_t cos, odp_cls_cos_stats_t *stats);
+int  odp_cls_queue_stats(odp_cos_t cos, odp_queue_t queue, odp_cls_queue_stats_t *stats);
+void odp_cls_print_all(void);
+uint64_t odp_cos_to_u64(odp_cos_t hdl);
+uint64_t odp_pmr_to_u64(odp_pmr_t hdl);
+
+/* ---- loop pktio subset (packet_io.h) ----------------------------------- */
+typedef union odp_pktin_config_opt_t {
+	struct {
+		uint64_t ts_all        : 1;
+		uint64_t ts_ptp        : 1;
+		uint64_t ipv4_chksum   : 1;
+		uint64_t udp_chksum    : 1;
+		uint64_t tcp_chksum    : 1;
+		uint64_t sctp_chksum   : 1;
+		uint64_t drop_ipv4_err : 1;
+		uint64_t drop_ipv6_err : 1;
+		uint64_t drop_udp_err  : 1;
+		uint64_t drop_tcp_err  : 1;
+		uint64_t drop_sctp_err : 1;
+	} bit;
+	uint64_t all_bits;
+} odp_pktin_config_opt_t;
+
+typedef enum odp_proto_layer_t {
+	ODP_PROTO_LAYER_NONE = 0,
+	ODP_PROTO_LAYER_L2,
+	ODP_PROTO_LAYER_L3,
+	ODP_PROTO_LAYER_L4,
+	ODP_PROTO_LAYER_ALL
+} odp_proto_layer_t;
+
+typedef struct odp_pktio_config_t {
+	odp_pktin_config_opt_t pktin;
+	uint64_t pktout_all_bits;
+	struct {
+		odp_proto_layer_t layer;
+	} parser;
+} odp_pktio_config_t;
+
+typedef struct odp_pktin_queue_param_t {
+	int op_mode;
+	odp_bool_t classifier_enable;
+	odp_bool_t hash_enable;
+	odp_pktin_hash_proto_t hash_proto;
+	uint32_t num_queues;
+} odp_pktin_queue_param_t;
+
+typedef struct odp_pktio_stats_t {
+	uint64_t in_octets;
+	uint64_t in_packets;
+	uint64_t in_ucast_pkts;
+	uint64_t in_mcast_pkts;
+	uint64_t in_bcast_pkts;
+	uint64_t in_discards;
+	uint64_t in_errors;
+	uint64_t out_octets;
+	uint64_t out_packets;
+	uint64_t out_ucast_pkts;
+	uint64_t out_mcast_pkts;
+	uint64_t out_bcast_pkts;
+	uint64_t out_discards;
+	uint64_t out_errors;
+} odp_pktio_stats_t;
+
+odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const void *param);
+int  odp_pktio_close(odp_pktio_t pktio);
+void odp_pktio_config_init(odp_pktio_config_t *config);
+int  odp_pktio_config(odp_pktio_t pktio, const odp_pktio_config_t *config);
+void odp_pktin_queue_param_init(odp_pktin_queue_param_t *param);
+int  odp_pktin_queue_config(odp_pktio_t pktio, const odp_pktin_queue_param_t *param);
+int  odp_pktio_start(odp_pktio_t pktio);
+int  odp_pktio_stop(odp_pktio_t pktio);
+int  odp_pktio_stats(odp_pktio_t pktio, odp_pktio_stats_t *stats);
+int  odp_pktio_stats_reset(odp_pktio_t pktio);
+uint64_t odp_pktio_to_u64(odp_pktio_t pktio);
+
+/* classifier setters (odp_classification.c:580-643) */
+int odp_pktio_default_cos_set(odp_pktio_t pktio, odp_cos_t default_cos);
+int odp_pktio_error_cos_set(odp_pktio_t pktio, odp_cos_t error_cos);
+int odp_pktio_skip_set(odp_pktio_t pktio, uint32_t offset);
+int odp_pktio_headroom_set(odp_pktio_t pktio, uint32_t headroom);
+
+/* ---- MI355X extensions ------------------------------------------------- */
+/* Raise the CoS / PMR table limits above the reference's
+ * (odp_classification_datamodel.h:31-46). Only before the first create. */
+int odpg_cls_set_limits(uint32_t max_cos, uint32_t max_pmr, uint32_t max_pmr_per_cos);
+/* Reset the whole classifier state (all CoS, PMR, pktio). Test helper. */
+void odpg_cls_reset(void);
+/* Monotonic generation, bumped by every rule/pktio-classifier change. */
+uint64_t odpg_cls_generation(void);
+
+/* Snapshot the classifier view of a pktio into `rules`. The arrays stay valid
+ * until the next snapshot call or reset. */
+int odpg_pktio_rules(odp_pktio_t pktio, odpg_rules_t *rules);
+
+/* The receive path of a started loop pktio (body of loopback_recv(),
+ * pktio/loop.c:276-374) for a whole batch on the GPU: parse layer ALL when
+ * the classifier is enabled (odp_packet_io.c:709-711), the pktio's pktin
+ * checksum options, the current rule table (compiled and cached per
+ * generation), then the pktio (in_*) and CoS / queue counters are updated.
+ * device_ptrs != 0: frames/desc/out/mark are device pointers; otherwise host
+ * pointers (pinned preferred) streamed through odpg_classify_host(). */
+int odpg_pktio_recv_batch(odp_pktio_t pktio, odpg_ctx_t *ctx,
+			  const uint8_t *frames, const odpg_desc_t *desc, uint32_t stride,
+			  uint32_t num, int device_ptrs, odpg_out_t *out, uint16_t *mark);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ODP_CLS_H_ */

@@ -1,0 +1,1014 @@
+/* SPDX-License-Identifier: BSD-3-Clause
+ *
+ * gfx950 (MI355X, CDNA4) kernels for ODP's receive-path classifier.
+ *
+ * One lane = one packet, 256-lane workgroups (4 wave64s). Per packet:
+ *   1. stage the first W bytes of the frame in LDS (bytes past the frame end
+ *      are zero). For the fixed 64-byte stride layout the workgroup loads its
+ *      256 x 64 B = 16 KiB slice with fully coalesced 16-byte-per-lane loads
+ *      and transposes it into per-packet LDS rows (row stride W+4 bytes = an
+ *      odd number of dwords, so same-offset reads by 32 lanes hit 32 banks);
+ *   2. parse L2/L3/L4 exactly like _odp_packet_parse_common()
+ *      (odp_parse_internal.h:80-112, odp_parse.c:23-475) and verify the IPv4
+ *      header / UDP / TCP / SCTP checksums (odp_packet.c:1906-1984);
+ *   3. walk the CoS graph like match_pmr_cos() (odp_classification.c:1599-1642).
+ *      The walk is wave-cooperative: the wave repeatedly takes the CoS of its
+ *      first unfinished lane (readfirstlane), and every lane sitting on that
+ *      CoS evaluates its rules together, so rule and term descriptors are
+ *      wave-uniform scalar loads and only the packet bytes are per lane.
+ *      First-match order, invalid-destination skipping, marks and per-CoS
+ *      counters follow the reference;
+ *   4. write one 4-byte verdict word (odpg.h) and optional mark / metadata.
+ * Packets are independent: no inter-workgroup communication. Per-workgroup
+ * counter partials are summed by a second small kernel (no same-address
+ * global atomics).
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/odpg.h"
+#include "odpg_internal.h"
+
+#define BLOCK 256
+
+#define IF(x)  (1ull << (x))
+#define FB(x)  (1u << (x))
+
+/* ----------------------------------------------------------------------- */
+/* packet byte access: LDS window, optional global tail, zero past frame    */
+template <int W, bool GF>
+struct Pkt {
+	const uint32_t *row;   /* LDS, W/4 dwords of the frame start */
+	const uint8_t  *g;     /* global frame start (16-byte aligned) */
+	uint32_t        len;
+
+	__device__ __forceinline__ uint32_t word(uint32_t w) const
+	{
+		if (w < (uint32_t)(W / 4))
+			return row[w];
+		if (GF) {
+			uint32_t nw = (len + 3u) >> 2;
+
+			if (w < nw) {
+				uint32_t x = *(const uint32_t *)(g + 4u * w);
+				uint32_t rem = len - 4u * w;
+
+				if (rem < 4u)
+					x &= (1u << (8u * rem)) - 1u;
+				return x;
+			}
+		}
+		return 0u;
+	}
+
+	/* little-endian u32 of bytes [pos, pos + 4) */
+	__device__ __forceinline__ uint32_t rd32(uint32_t pos) const
+	{
+		uint32_t w = pos >> 2;
+		uint32_t lo = word(w);
+
+		if ((pos & 3u) == 0u)
+			return lo;
+		uint32_t hi = word(w + 1u);
+
+		return __builtin_amdgcn_alignbyte(hi, lo, pos & 3u);
+	}
+
+	__device__ __forceinline__ uint32_t u8(uint32_t pos) const
+	{
+		return (word(pos >> 2) >> (8u * (pos & 3u))) & 0xffu;
+	}
+
+	/* network-order 16-bit field */
+	__device__ __forceinline__ uint32_t be16(uint32_t pos) const
+	{
+		uint32_t x = rd32(pos);
+
+		return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu);
+	}
+
+	/* raw little-endian 16-bit load (what the reference's u16 reads see) */
+	__device__ __forceinline__ uint32_t raw16(uint32_t pos) const
+	{
+		return rd32(pos) & 0xffffu;
+	}
+};
+
+/* one's-complement accumulate (end-around carry): keeps the residue mod
+ * 0xffff of the reference's 64-bit sum of little-endian words
+ * (chksum_partial, odp_chksum_internal.h:60-196) and is zero only when every
+ * added word is zero, so the folded verdict is identical. */
+__device__ __forceinline__ uint32_t oc_add(uint32_t s, uint32_t x)
+{
+	uint32_t r = s + x;
+
+	return r + (r < x ? 1u : 0u);
+}
+
+/* chksum_finalize (odp_chksum_internal.h:22-31) of a one's-complement sum */
+__device__ __forceinline__ uint32_t oc_fold(uint32_t s)
+{
+	s = (s >> 16) + (s & 0xffffu);
+	s = (s >> 16) + (s & 0xffffu);
+	return s;
+}
+
+/* sum of bytes [a, b) of the frame, a even, bytes past the frame zero */
+template <int W, bool GF>
+__device__ uint32_t sum_range(const Pkt<W, GF> &v, uint32_t a, uint32_t b)
+{
+	if (b > v.len)
+		b = v.len;
+	if (b <= a)
+		return 0u;
+	uint32_t w0 = a >> 2, w1 = (b - 1u) >> 2;
+	uint32_t s = 0;
+	uint32_t lim = w1 < (uint32_t)(W / 4 - 1) ? w1 : (uint32_t)(W / 4 - 1);
+	uint32_t w = w0;
+
+	/* part inside the LDS window */
+	for (; w <= lim; ++w) {
+		uint32_t x = v.row[w];
+
+		if (w == w0 && (a & 3u))
+			x &= 0xffff0000u;
+		if (w == w1 && (b & 3u))
+			x &= (1u << (8u * (b & 3u))) - 1u;
+		s = oc_add(s, x);
+	}
+	if (GF && w <= w1) {
+		/* tail beyond the window, straight from HBM: 16 B per load once
+		 * the word index is 16-byte aligned */
+		for (; w <= w1 && (w & 3u); ++w) {
+			uint32_t x = v.word(w);
+
+			if (w == w0 && (a & 3u))
+				x &= 0xffff0000u;
+			if (w == w1 && (b & 3u))
+				x &= (1u << (8u * (b & 3u))) - 1u;
+			s = oc_add(s, x);
+		}
+		while (w + 4u <= w1) {
+			uint4 q = *(const uint4 *)(v.g + 4u * w);
+
+			if (w == w0 && (a & 3u))
+				q.x &= 0xffff0000u;
+			s = oc_add(s, q.x);
+			s = oc_add(s, q.y);
+			s = oc_add(s, q.z);
+			s = oc_add(s, q.w);
+			w += 4u;
+		}
+		for (; w <= w1; ++w) {
+			uint32_t x = v.word(w);
+
+			if (w == w0 && (a & 3u))
+				x &= 0xffff0000u;
+			if (w == w1 && (b & 3u))
+				x &= (1u << (8u * (b & 3u))) - 1u;
+			s = oc_add(s, x);
+		}
+	}
+	return s;
+}
+
+/* CRC32C (reflected Castagnoli, no final xor: arch/default/odp_hash_crc32.c) */
+__device__ __forceinline__ uint32_t crc32c_byte(uint32_t crc, uint32_t b)
+{
+	crc ^= b;
+#pragma unroll
+	for (int k = 0; k < 8; ++k)
+		crc = (crc >> 1) ^ (0x82F63B78u & (0u - (crc & 1u)));
+	return crc;
+}
+
+template <int W, bool GF>
+__device__ uint32_t crc32c_range(const Pkt<W, GF> &v, uint32_t off, uint32_t len, uint32_t crc)
+{
+	for (uint32_t i = 0; i < len; ++i)
+		crc = crc32c_byte(crc, v.u8(off + i));
+	return crc;
+}
+
+/* ----------------------------------------------------------------------- */
+struct Prs {
+	uint64_t inf;
+	uint32_t fl;
+	uint32_t l2, l3, l4;
+};
+
+enum { LAYER_NONE = 0, LAYER_L2, LAYER_L3, LAYER_L4, LAYER_ALL };
+
+/* _odp_parse_eth (odp_parse.c:23-106) */
+template <int W, bool GF>
+__device__ __forceinline__ uint32_t parse_eth(Prs &p, const Pkt<W, GF> &v, uint32_t &off)
+{
+	uint64_t inf = IF(IFL_L2) | IF(IFL_ETH);
+	uint32_t len = v.len;
+	uint32_t w0 = v.word(0), w1 = v.word(1), w3 = v.word(3);
+	uint32_t mac0 = ((w0 & 0xffu) << 8) | ((w0 >> 8) & 0xffu);
+	uint32_t ethtype = ((w3 & 0xffu) << 8) | ((w3 >> 8) & 0xffu);
+
+	if (len - off > 1514u)
+		inf |= IF(IFL_JUMBO);
+	if (mac0 & 0x0100u)
+		inf |= IF(IFL_ETH_MCAST);
+	if (mac0 == 0xffffu && (w0 >> 16) == 0xffffu && (w1 & 0xffffu) == 0xffffu)
+		inf |= IF(IFL_ETH_BCAST);
+	off += 14u;
+
+	if (ethtype < 1514u) {
+		inf |= IF(IFL_SNAP);
+		if (ethtype > len - off) {
+			p.fl |= FB(FL_SNAP_LEN_ERR);
+			p.inf |= inf;
+			return 0u;
+		}
+		ethtype = v.be16(off + 6u);
+		off += 8u;
+	}
+	if (ethtype == 0x88A8u) {
+		inf |= IF(IFL_VLAN_QINQ) | IF(IFL_VLAN);
+		ethtype = v.be16(off + 2u);
+		off += 4u;
+	}
+	if (ethtype == 0x8100u) {
+		inf |= IF(IFL_VLAN);
+		ethtype = v.be16(off + 2u);
+		off += 4u;
+	}
+	if (off > len) {
+		inf = IF(IFL_L2);
+		ethtype = 0u;
+	}
+	p.inf |= inf;
+	return ethtype;
+}
+
+/* parse_ipv4 (odp_parse.c:113-169); returns proto, accumulates pseudo header */
+template <int W, bool GF>
+__device__ __forceinline__ uint32_t parse_ipv4(Prs &p, const Pkt<W, GF> &v, uint32_t &off,
+					       uint64_t opt, uint32_t &l4sum)
+{
+	uint32_t o = off;
+	uint32_t len = v.len;
+	uint32_t h0 = v.rd32(o);            /* ver_ihl tos tot_len */
+	uint32_t h1 = v.rd32(o + 4u);       /* id frag_offset */
+	uint32_t h2 = v.rd32(o + 8u);       /* ttl proto chksum */
+	uint32_t dst = v.rd32(o + 16u);     /* raw */
+	uint32_t ver = (h0 & 0xf0u) >> 4, ihl = h0 & 0x0fu;
+	uint32_t l3_len = ((h0 >> 8) & 0xff00u) | (h0 >> 24);
+	uint32_t frag = ((h1 >> 8) & 0xff00u) | (h1 >> 24);
+	uint32_t dst_be = __builtin_bswap32(dst);
+
+	if ((p.fl & FB(FL_L3_CHKSUM_ERR)) || ihl < 5u || ver != 4u || 20u > len - o ||
+	    l3_len > len - o) {
+		p.fl |= FB(FL_IP_ERR);
+		return 0u;
+	}
+	if (opt & ODPG_PKTIN_IPV4_CHKSUM) {
+		p.inf |= IF(IFL_L3_CHKSUM_DONE);
+		if (oc_fold(sum_range(v, o, o + ihl * 4u)) != 0xffffu) {
+			p.fl |= FB(FL_IP_ERR) | FB(FL_L3_CHKSUM_ERR);
+			return 0u;
+		}
+	}
+	off += ihl * 4u;
+	if (opt & (ODPG_PKTIN_UDP_CHKSUM | ODPG_PKTIN_TCP_CHKSUM))
+		l4sum = sum_range(v, o + 12u, o + 20u);
+	if (ihl > 5u)
+		p.inf |= IF(IFL_IPOPT);
+	if (frag & 0x3fffu)
+		p.inf |= IF(IFL_IPFRAG);
+	if (dst_be == 0xffffffffu)
+		p.inf |= IF(IFL_IP_BCAST);
+	if ((dst_be >> 28) == 0xeu)
+		p.inf |= IF(IFL_IP_MCAST);
+	return (h2 >> 8) & 0xffu;
+}
+
+/* parse_ipv6 (odp_parse.c:179-245) */
+template <int W, bool GF>
+__device__ __forceinline__ uint32_t parse_ipv6(Prs &p, const Pkt<W, GF> &v, uint32_t &off,
+					       uint32_t seg_end, uint64_t opt, uint32_t &l4sum)
+{
+	uint32_t o = off;
+	uint32_t len = v.len;
+	uint32_t h0 = v.rd32(o);            /* ver_tc_flow */
+	uint32_t h1 = v.rd32(o + 4u);       /* payload_len next_hdr hop_limit */
+	uint32_t vtf = __builtin_bswap32(h0);
+	uint32_t payload_len = ((h1 & 0xffu) << 8) | ((h1 >> 8) & 0xffu);
+	uint32_t next_hdr = (h1 >> 16) & 0xffu;
+	uint32_t dst0 = v.u8(o + 24u);
+
+	if ((p.fl & FB(FL_L3_CHKSUM_ERR)) || (vtf >> 28) != 6u || 40u > len - o ||
+	    payload_len + 40u > len - o) {
+		p.fl |= FB(FL_IP_ERR);
+		return 0u;
+	}
+	if (dst0 == 0xffu)
+		p.inf |= IF(IFL_IP_MCAST);
+	else
+		p.inf &= ~IF(IFL_IP_MCAST);
+	p.inf &= ~IF(IFL_IP_BCAST);
+	off += 40u;
+	if (opt & (ODPG_PKTIN_UDP_CHKSUM | ODPG_PKTIN_TCP_CHKSUM))
+		l4sum = sum_range(v, o + 8u, o + 40u);
+
+	if (next_hdr == 0x00u || next_hdr == 0x2Bu) {
+		uint32_t ext_next;
+
+		p.inf |= IF(IFL_IPOPT);
+		do {
+			uint32_t e = off;
+
+			ext_next = v.u8(e);
+			off += 8u + v.u8(e + 1u) * 8u;
+		} while ((ext_next == 0x00u || ext_next == 0x2Bu) && off < seg_end);
+
+		if (off >= p.l3 + payload_len) {
+			p.fl |= FB(FL_IP_ERR);
+			return 0u;
+		}
+		if (ext_next == 0x2Cu)
+			p.inf |= IF(IFL_IPFRAG);
+		return ext_next;
+	}
+	if (next_hdr == 0x2Cu)
+		p.inf |= IF(IFL_IPOPT) | IF(IFL_IPFRAG);
+	return next_hdr;
+}
+
+/* _odp_packet_parse_common (odp_parse_internal.h:80-112) incl. the L3/L4
+ * switch (odp_parse.c:360-475) and _odp_packet_l4_chksum (odp_packet.c:1906-1984) */
+template <int W, bool GF>
+__device__ int parse_common(Prs &p, const Pkt<W, GF> &v, uint32_t layer, uint64_t opt)
+{
+	uint32_t off = 0, len = v.len, seg_end = v.len;
+	uint32_t l4sum = 0;
+	uint32_t sctp_crc = 0;
+	uint32_t ip_proto;
+
+	if (layer == LAYER_NONE)
+		return 0;
+	p.l2 = 0;
+	uint32_t ethtype = parse_eth(p, v, off);
+
+	/* _odp_packet_parse_common_l3_l4 */
+	p.l3 = off;
+	if (layer <= LAYER_L2)
+		return (p.fl & FL_ERROR_MASK) != 0u;
+	p.inf |= IF(IFL_L3);
+	if (ethtype == 0x0800u) {
+		p.inf |= IF(IFL_IPV4);
+		ip_proto = parse_ipv4(p, v, off, opt, l4sum);
+		if (!(p.fl & FB(FL_IP_ERR)))
+			p.l4 = off;
+		else if (opt & ODPG_PKTIN_DROP_IPV4_ERR)
+			return -1;
+	} else if (ethtype == 0x86ddu) {
+		p.inf |= IF(IFL_IPV6);
+		ip_proto = parse_ipv6(p, v, off, seg_end, opt, l4sum);
+		if (!(p.fl & FB(FL_IP_ERR)))
+			p.l4 = off;
+		else if (opt & ODPG_PKTIN_DROP_IPV6_ERR)
+			return -1;
+	} else if (ethtype == 0x0806u) {
+		p.inf |= IF(IFL_ARP);
+		ip_proto = 255u;
+	} else {
+		p.inf &= ~IF(IFL_L3);
+		ip_proto = 255u;
+	}
+	if (layer == LAYER_L3)
+		return (p.fl & FL_ERROR_MASK) != 0u;
+
+	p.inf |= IF(IFL_L4);
+	bool frag = (p.inf & IF(IFL_IPFRAG)) != 0;
+
+	switch (ip_proto) {
+	case 0x01u:
+	case 0x3Au:
+		p.inf |= IF(IFL_ICMP);
+		break;
+	case 0x04u:
+		break;
+	case 0x06u: {                                       /* parse_tcp :252-274 */
+		if (off + 20u > seg_end)
+			return -1;
+		p.inf |= IF(IFL_TCP);
+		if ((v.u8(off + 12u) >> 4) < 5u)
+			p.fl |= FB(FL_TCP_ERR);
+		if ((opt & ODPG_PKTIN_TCP_CHKSUM) && !frag) {
+			uint32_t tl = (len - p.l4) & 0xffffu;
+
+			l4sum = oc_add(l4sum, ((tl >> 8) | (tl << 8)) & 0xffffu);
+			l4sum = oc_add(l4sum, 0x06u << 8);
+		}
+		if ((p.fl & FB(FL_TCP_ERR)) && (opt & ODPG_PKTIN_DROP_TCP_ERR))
+			return -1;
+		break;
+	}
+	case 0x11u: {                                       /* parse_udp :281-322 */
+		if (off + 8u > seg_end)
+			return -1;
+		p.inf |= IF(IFL_UDP);
+		uint32_t u1 = v.rd32(off + 4u);            /* length chksum */
+		uint32_t ulen_raw = u1 & 0xffffu, csum_raw = u1 >> 16;
+		uint32_t udplen = ((ulen_raw & 0xffu) << 8) | (ulen_raw >> 8);
+
+		if (udplen < 8u) {
+			p.fl |= FB(FL_UDP_ERR);
+		} else {
+			if ((opt & ODPG_PKTIN_UDP_CHKSUM) && !frag) {
+				if (csum_raw == 0u) {
+					p.inf |= IF(IFL_L4_CHKSUM_DONE) | IF(IFL_UDP_CHKSUM_ZERO);
+					if (!(p.inf & IF(IFL_IPV4)))
+						p.fl |= FB(FL_L4_CHKSUM_ERR);
+				} else {
+					l4sum = oc_add(l4sum, ulen_raw);
+					l4sum = oc_add(l4sum, 0x11u << 8);
+				}
+			}
+			if (v.be16(off + 2u) == 4500u && udplen > 4u && v.rd32(off + 8u) != 0u)
+				p.inf |= IF(IFL_IPSEC) | IF(IFL_IPSEC_UDP);
+		}
+		if ((p.fl & FB(FL_UDP_ERR)) && (opt & ODPG_PKTIN_DROP_UDP_ERR))
+			return -1;
+		break;
+	}
+	case 0x33u:
+		p.inf |= IF(IFL_IPSEC) | IF(IFL_IPSEC_AH);
+		break;
+	case 0x32u:
+		p.inf |= IF(IFL_IPSEC) | IF(IFL_IPSEC_ESP);
+		break;
+	case 0x84u: {                                       /* parse_sctp :329-352 */
+		p.inf |= IF(IFL_SCTP);
+		if (((len - p.l4) & 0xffffu) < 12u) {
+			p.fl |= FB(FL_SCTP_ERR);
+		} else if ((opt & ODPG_PKTIN_SCTP_CHKSUM) && !frag) {
+			uint32_t crc = crc32c_range(v, off, 8u, 0xffffffffu);
+
+			for (int k = 0; k < 4; ++k)
+				crc = crc32c_byte(crc, 0u);
+			sctp_crc = crc;
+		}
+		if ((p.fl & FB(FL_SCTP_ERR)) && (opt & ODPG_PKTIN_DROP_SCTP_ERR))
+			return -1;
+		break;
+	}
+	case 0x3Bu:
+		p.inf |= IF(IFL_NO_NEXT_HDR);
+		break;
+	default:
+		p.inf &= ~IF(IFL_L4);
+		break;
+	}
+	if (p.fl & FL_ERROR_MASK)
+		return 1;
+	if (layer < LAYER_L4)
+		return 0;
+
+	/* _odp_packet_l4_chksum (odp_packet.c:1906-1984) */
+	uint64_t inf = p.inf;
+
+	if ((opt & ODPG_PKTIN_UDP_CHKSUM) && (inf & IF(IFL_UDP)) && !(inf & IF(IFL_IPFRAG)) &&
+	    !(inf & IF(IFL_UDP_CHKSUM_ZERO))) {
+		uint32_t s = oc_add(l4sum, sum_range(v, p.l4, len));
+
+		p.inf |= IF(IFL_L4_CHKSUM_DONE);
+		if (oc_fold(s) != 0xffffu) {
+			p.fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_UDP_ERR);
+			if (opt & ODPG_PKTIN_DROP_UDP_ERR)
+				return -1;
+		}
+	}
+	if ((opt & ODPG_PKTIN_TCP_CHKSUM) && (inf & IF(IFL_TCP)) && !(inf & IF(IFL_IPFRAG))) {
+		uint32_t s = oc_add(l4sum, sum_range(v, p.l4, len));
+
+		p.inf |= IF(IFL_L4_CHKSUM_DONE);
+		if (oc_fold(s) != 0xffffu) {
+			p.fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_TCP_ERR);
+			if (opt & ODPG_PKTIN_DROP_TCP_ERR)
+				return -1;
+		}
+	}
+	if ((opt & ODPG_PKTIN_SCTP_CHKSUM) && (inf & IF(IFL_SCTP)) && !(inf & IF(IFL_IPFRAG))) {
+		uint32_t crc = crc32c_range(v, p.l4 + 12u, len - p.l4 - 12u, sctp_crc);
+
+		p.inf |= IF(IFL_L4_CHKSUM_DONE);
+		if (~crc != v.rd32(p.l4 + 8u)) {
+			p.fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_SCTP_ERR);
+			if (opt & ODPG_PKTIN_DROP_SCTP_ERR)
+				return -1;
+		}
+	}
+	return (p.fl & FL_ERROR_MASK) != 0u;
+}
+
+/* ----------------------------------------------------------------------- */
+/* compiled term evaluation (odp_classification.c:1338-1490 via cls_compile) */
+struct Bases {
+	uint32_t l2, l3, l4, vlanx, len, inf_lo;
+};
+
+template <int W, bool GF>
+__device__ __forceinline__ bool term_cmp(const dterm_t *__restrict__ t, const Pkt<W, GF> &v,
+					 const Bases &b)
+{
+	uint32_t kind = t->kind;
+
+	if (kind == DK_LEN)
+		return (b.len & t->mask[0]) == t->value[0];
+	if (kind != DK_CMP)
+		return false;
+	uint32_t base_k = t->base;
+	uint32_t base = base_k == DB_L3 ? b.l3 : base_k == DB_L4 ? b.l4 :
+			base_k == DB_L2 ? b.l2 : base_k == DB_VLANX ? b.vlanx : 0u;
+	uint32_t pos = base + (uint32_t)t->off;
+
+	if ((t->tflags & DT_GUARD) && !(b.len > pos + t->size))
+		return false;
+	bool ok = true;
+	uint32_t nw = t->nwords;
+
+	for (uint32_t k = 0; k < nw; ++k)
+		ok = ok && ((v.rd32(pos + 4u * k) & t->mask[k]) == t->value[k]);
+	return ok;
+}
+
+template <int W, bool GF>
+__device__ __forceinline__ bool pmr_match(const dterm_t *__restrict__ terms, uint32_t start,
+					  uint32_t n, const Pkt<W, GF> &v, const Bases &b)
+{
+	bool ok = true;
+	uint32_t end = start + n;
+
+	for (uint32_t ti = start; ti < end;) {
+		const dterm_t *t = terms + ti;
+		bool r;
+
+		if (t->tflags & DT_ALT_NEXT) {
+			const dterm_t *t2 = t + 1;
+
+			if ((b.inf_lo & t->req) == t->req)
+				r = term_cmp(t, v, b);
+			else
+				r = ((b.inf_lo & t2->req) == t2->req) && term_cmp(t2, v, b);
+			ti += 2;
+		} else {
+			r = ((b.inf_lo & t->req) == t->req) && term_cmp(t, v, b);
+			ti += 1;
+		}
+		ok = ok && r;
+	}
+	return ok;
+}
+
+/* thash_softrss (protocols/thash.h:81-99) with the default key
+ * (odp_classification.c:50-58) */
+__constant__ uint32_t c_rss_key_be[11] = {
+	0x6d5a56dau, 0x255b0ec2u, 0x4167253du, 0x43a38fb0u, 0xd0ca2bcbu,
+	0xae7b30b4u, 0x77cb2da3u, 0x8030f20cu, 0x6a42b73bu, 0xbeac01fau, 0u
+};
+
+__device__ uint32_t thash(const uint32_t *tuple, uint32_t n)
+{
+	uint32_t ret = 0;
+
+	for (uint32_t j = 0; j < n; ++j) {
+		uint32_t k0 = c_rss_key_be[j], k1 = c_rss_key_be[j + 1];
+
+		for (uint32_t i = 0; i < 32; ++i)
+			if (tuple[j] & (1u << (31 - i)))
+				ret ^= (k0 << i) | (i ? (k1 >> (32 - i)) : 0u);
+	}
+	return ret;
+}
+
+/* packet_rss_hash (odp_classification.c:1751-1817) */
+template <int W, bool GF>
+__device__ uint32_t rss_hash(const Prs &p, const Pkt<W, GF> &v, uint32_t hp)
+{
+	uint32_t tuple[9];
+	uint32_t n = 0;
+
+#pragma unroll
+	for (int k = 0; k < 9; ++k)
+		tuple[k] = 0u;
+	if (p.inf & IF(IFL_IPV4)) {
+		if (hp & 1u) {
+			tuple[0] = v.rd32(p.l3 + 12u);
+			tuple[1] = v.rd32(p.l3 + 16u);
+			n += 2;
+		}
+		if (((p.inf & IF(IFL_TCP)) && (hp & 8u)) || (!(p.inf & IF(IFL_TCP)) &&
+		    (p.inf & IF(IFL_UDP)) && (hp & 4u))) {
+			tuple[2] = v.rd32(p.l4);
+			n += 1;
+		}
+	} else if (p.inf & IF(IFL_IPV6)) {
+		if (hp & 2u) {
+#pragma unroll
+			for (int k = 0; k < 4; ++k) {
+				tuple[k] = __builtin_bswap32(v.rd32(p.l3 + 8u + 4u * k));
+				tuple[4 + k] = __builtin_bswap32(v.rd32(p.l3 + 24u + 4u * k));
+			}
+			n += 8;
+		}
+		if (((p.inf & IF(IFL_TCP)) && (hp & 8u)) || (!(p.inf & IF(IFL_TCP)) &&
+		    (p.inf & IF(IFL_UDP)) && (hp & 4u))) {
+			tuple[8] = v.rd32(p.l4);
+			n += 1;
+		}
+	}
+	return n ? thash(tuple, n) : 0u;
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x)
+{
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1)
+		x += __shfl_xor(x, o, 64);
+	return x;
+}
+
+/* ----------------------------------------------------------------------- */
+template <int W, bool COOP, bool GF, bool DESC>
+__global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
+	const uint8_t *__restrict__ frames, const odpg_desc_t *__restrict__ desc,
+	uint32_t stride, uint32_t num, uint64_t opt, uint32_t layer, uint32_t classify,
+	const dterm_t *__restrict__ terms, const dpmr_t *__restrict__ pmrs,
+	const dcos_t *__restrict__ coses, uint32_t num_cos, int32_t default_cos,
+	int32_t error_cos, uint32_t tbl_flags,
+	odpg_out_t *__restrict__ out, uint16_t *__restrict__ mark_out,
+	odpg_meta_t *__restrict__ meta_out, uint64_t *__restrict__ pk_partial,
+	uint32_t *__restrict__ cos_partial)
+{
+	constexpr uint32_t RW = W / 4 + 1;       /* odd dword row stride */
+	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+	uint32_t *cos_cnt = smem + BLOCK * RW;
+	__shared__ unsigned long long blk_pk[4];
+
+	const uint32_t tid = threadIdx.x;
+	const uint32_t blk0 = blockIdx.x * BLOCK;
+	const uint32_t i = blk0 + tid;
+	const bool live = i < num;
+	const bool do_stats = pk_partial != nullptr;
+	const bool do_cos_stats = cos_partial != nullptr;
+	uint32_t *row = smem + tid * RW;
+
+	if (tid < 4)
+		blk_pk[tid] = 0ull;
+	if (do_cos_stats)
+		for (uint32_t c = tid; c < num_cos; c += BLOCK)
+			cos_cnt[c] = 0u;
+
+	/* ---- 1. stage the frame window in LDS ---------------------------- */
+	const uint8_t *g;
+	uint32_t len;
+
+	if (DESC) {
+		odpg_desc_t d = live ? desc[i] : odpg_desc_t{0u, 0u};
+
+		g = frames + d.offset;
+		len = d.len;
+	} else {
+		g = frames + (size_t)i * stride;
+		len = live ? stride : 0u;
+	}
+
+	if (COOP) {
+		/* stride == W: the block's frames are one contiguous span */
+		constexpr uint32_t CPP = W / 16;
+		const uint4 *src = (const uint4 *)(frames + (size_t)blk0 * W);
+		uint32_t nvalid = num - blk0 < BLOCK ? num - blk0 : BLOCK;
+
+#pragma unroll
+		for (uint32_t k = 0; k < CPP; ++k) {
+			uint32_t c = k * BLOCK + tid;
+			uint32_t pk = c / CPP, part = c % CPP;
+			uint4 x = make_uint4(0u, 0u, 0u, 0u);
+
+			if (pk < nvalid)
+				x = src[c];
+			uint32_t *dst = smem + pk * RW + part * 4u;
+
+			dst[0] = x.x;
+			dst[1] = x.y;
+			dst[2] = x.z;
+			dst[3] = x.w;
+		}
+	} else {
+#pragma unroll
+		for (uint32_t part = 0; part < W / 16; ++part) {
+			uint32_t b0 = part * 16u;
+			uint4 x = make_uint4(0u, 0u, 0u, 0u);
+
+			if (b0 < len) {
+				x = *(const uint4 *)(g + b0);
+				uint32_t rem = len - b0;
+
+				if (rem < 16u) {
+					uint32_t m[4];
+
+#pragma unroll
+					for (int q = 0; q < 4; ++q) {
+						int nb = (int)rem - 4 * q;
+
+						m[q] = nb >= 4 ? 0xffffffffu : nb <= 0 ? 0u :
+						       (1u << (8 * nb)) - 1u;
+					}
+					x.x &= m[0];
+					x.y &= m[1];
+					x.z &= m[2];
+					x.w &= m[3];
+				}
+			}
+			row[part * 4u + 0u] = x.x;
+			row[part * 4u + 1u] = x.y;
+			row[part * 4u + 2u] = x.z;
+			row[part * 4u + 3u] = x.w;
+		}
+	}
+	__syncthreads();
+
+	Pkt<W, GF> v;
+
+	v.row = row;
+	v.g = g;
+	v.len = len;
+
+	/* ---- 2. parse + checksum verdicts --------------------------------- */
+	Prs p;
+
+	p.inf = 0ull;
+	p.fl = 0u;
+	p.l2 = p.l3 = p.l4 = 0xffffu;
+	int ret = 0;
+
+	if (live && layer)
+		ret = parse_common(p, v, layer, opt);
+
+	/* ---- 3. CoS walk ------------------------------------------------- */
+	uint32_t cos = ODPG_COS_NOCLS;
+	int cret = 0;
+	bool any_match = false;
+	uint32_t mark = 0u;
+	const bool want_cls = live && layer && classify && ret >= 0;
+	bool active = false;
+	uint32_t steps = 0;
+
+	if (want_cls) {
+		if (p.fl & FL_ERROR_MASK) {
+			cos = error_cos < 0 ? ODPG_COS_NONE : (uint32_t)error_cos;
+		} else if (default_cos >= 0 && coses[default_cos].valid) {
+			cos = (uint32_t)default_cos;
+			active = coses[default_cos].nrule != 0;
+		} else {
+			cos = default_cos < 0 ? ODPG_COS_NONE : (uint32_t)default_cos;
+		}
+	}
+
+	Bases b;
+
+	b.l2 = p.l2;
+	b.l3 = p.l3;
+	b.l4 = p.l4;
+	b.vlanx = 14u + ((p.inf & IF(IFL_VLAN_QINQ)) ? 4u : 0u);
+	b.len = len;
+	b.inf_lo = (uint32_t)p.inf;
+
+	while (__ballot(active)) {
+		if (active) {
+			const uint32_t c = __builtin_amdgcn_readfirstlane(cos);
+
+			if (cos == c) {
+				const dcos_t *ce = coses + c;
+				const uint32_t rs = ce->rule_start, nr = ce->nrule;
+				bool hit = false;
+				uint32_t nd = 0u, nmark = 0u;
+
+				for (uint32_t r = 0; r < nr; ++r) {
+					const dpmr_t pm = pmrs[rs + r];
+					bool ok = false;
+
+					if (!hit)
+						ok = pmr_match(terms, pm.term_start, pm.nterms, v, b);
+					if (ok) {
+						hit = true;
+						nd = pm.dst;
+						nmark = pm.mark;
+					}
+					if (do_cos_stats && coses[pm.dst].stats) {
+						uint64_t bm = __ballot(ok);
+
+						if (bm && (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(true))))
+							atomicAdd(&cos_cnt[pm.dst], (uint32_t)__popcll(bm));
+					}
+					if (__ballot(!hit) == 0ull)
+						break;
+				}
+				if (hit) {
+					cos = nd;
+					mark = nmark;
+					any_match = true;
+					if (++steps >= num_cos) {
+						cos = ODPG_COS_LOOP;
+						active = false;
+					} else if (coses[nd].nrule == 0) {
+						active = false;
+					}
+				} else {
+					active = false;
+				}
+			}
+		}
+	}
+
+	if (want_cls) {
+		/* cls_select_cos() "done" path counts default / error CoS once
+		 * (odp_classification.c:1696-1698): error packets, and packets
+		 * that matched nothing below the default CoS */
+		bool err = (p.fl & FL_ERROR_MASK) != 0u;
+		bool at_done = err || !any_match;
+
+		if (do_cos_stats && at_done && cos < num_cos && coses[cos].stats)
+			atomicAdd(&cos_cnt[cos], 1u);
+
+		if (cos == ODPG_COS_LOOP) {
+			cret = -2;
+		} else if (cos == ODPG_COS_NONE) {
+			cret = -1;
+		} else if (coses[cos].action == 1u) {
+			cret = 1;
+		} else {
+			cret = 0;
+			p.inf |= IF(IFL_DST_QUEUE);
+		}
+		if (any_match && !err && cos != ODPG_COS_LOOP) {
+			p.inf &= ~IF(IFL_CLS_MARK);
+			if (mark)
+				p.inf |= IF(IFL_CLS_MARK);
+		}
+	} else if (live && ret < 0) {
+		cos = ODPG_COS_PDROP;
+	}
+
+	/* ---- 4. outputs --------------------------------------------------- */
+	if (live) {
+		uint32_t w = cos & 0xffffu;
+
+		if (cret == 1)
+			w |= ODPG_OUT_CLS_DROP;
+		if (cret == 0 && want_cls && (tbl_flags & TBL_ANY_HASHQ) && coses[cos].num_queue > 1u) {
+			uint32_t h = rss_hash(p, v, coses[cos].hash_proto);
+
+			w |= ((h & 31u) % coses[cos].num_queue) << 24;
+		}
+		if (p.inf & IF(IFL_L3_CHKSUM_DONE))
+			w |= (p.fl & FB(FL_L3_CHKSUM_ERR) ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 16;
+		if (p.inf & IF(IFL_L4_CHKSUM_DONE))
+			w |= (p.fl & FB(FL_L4_CHKSUM_ERR) ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 18;
+		if (p.fl & FL_ERROR_MASK)
+			w |= ODPG_OUT_ERROR;
+		if (p.inf & IF(IFL_CLS_MARK))
+			w |= ODPG_OUT_MARK_VALID;
+		if (ret)
+			w |= ODPG_OUT_PARSE_ERR;
+		out[i] = w;
+		uint32_t mk = (p.inf & IF(IFL_CLS_MARK)) ? mark : 0u;
+
+		if (mark_out)
+			mark_out[i] = (uint16_t)mk;
+		if (meta_out) {
+			odpg_meta_t m;
+
+			m.input_flags = p.inf;
+			m.flags = p.fl;
+			m.l2_offset = (uint16_t)p.l2;
+			m.l3_offset = (uint16_t)p.l3;
+			m.l4_offset = (uint16_t)p.l4;
+			m.cls_mark = (uint16_t)mk;
+			m.reserved = 0u;
+			meta_out[i] = m;
+		}
+	}
+
+	/* ---- 5. per-workgroup counter partials ---------------------------- */
+	if (do_stats) {
+		/* loopback_recv accounting (loop.c:304-374) */
+		uint32_t is_err = (live && layer && ret != 0) ? 1u : 0u;
+		uint32_t is_disc = (live && (cret == -1 || cret == -2)) ? 1u : 0u;
+		uint32_t is_pkt = (live && ret >= 0 && cret == 0 && !(p.fl & FL_ERROR_MASK)) ? 1u : 0u;
+		uint64_t oct = is_pkt ? (uint64_t)len : 0ull;
+		uint32_t n_pkt = (uint32_t)__popcll(__ballot(is_pkt));
+		uint32_t n_err = (uint32_t)__popcll(__ballot(is_err));
+		uint32_t n_disc = (uint32_t)__popcll(__ballot(is_disc));
+
+		oct = wave_sum_u64(oct);
+		if (__lane_id() == 0) {
+			atomicAdd(&blk_pk[0], (unsigned long long)n_pkt);
+			atomicAdd(&blk_pk[1], (unsigned long long)oct);
+			atomicAdd(&blk_pk[2], (unsigned long long)n_err);
+			atomicAdd(&blk_pk[3], (unsigned long long)n_disc);
+		}
+	}
+	if (do_stats || do_cos_stats)
+		__syncthreads();
+	if (do_stats && tid < 4)
+		pk_partial[(size_t)blockIdx.x * 4u + tid] = blk_pk[tid];
+	if (do_cos_stats)
+		for (uint32_t c = tid; c < num_cos; c += BLOCK)
+			cos_partial[(size_t)blockIdx.x * num_cos + c] = cos_cnt[c];
+}
+
+/* sum per-workgroup partials into the caller's 64-bit counters */
+__global__ __launch_bounds__(BLOCK) void odpg_stats_reduce_kernel(
+	const uint64_t *__restrict__ pk_partial, const uint32_t *__restrict__ cos_partial,
+	uint32_t nblocks, uint32_t num_cos, uint64_t *__restrict__ stats)
+{
+	const uint32_t tid = threadIdx.x;
+	const uint32_t nwords = 4u + (cos_partial ? num_cos : 0u);
+
+	for (uint32_t wd = blockIdx.x; wd < nwords; wd += gridDim.x) {
+		uint64_t s = 0;
+
+		if (wd < 4u) {
+			for (uint32_t bl = tid; bl < nblocks; bl += BLOCK)
+				s += pk_partial[(size_t)bl * 4u + wd];
+		} else {
+			uint32_t c = wd - 4u;
+
+			for (uint32_t bl = tid; bl < nblocks; bl += BLOCK)
+				s += cos_partial[(size_t)bl * num_cos + c];
+		}
+		s = wave_sum_u64(s);
+		__shared__ unsigned long long red[BLOCK / 64];
+
+		if (__lane_id() == 0)
+			red[tid / 64] = s;
+		__syncthreads();
+		if (tid == 0) {
+			uint64_t t = 0;
+
+			for (int k = 0; k < BLOCK / 64; ++k)
+				t += red[k];
+			stats[wd] += t;
+		}
+		__syncthreads();
+	}
+}
+
+/* ----------------------------------------------------------------------- */
+/* host-side launch helper (called from runtime.cpp)                        */
+
+template <int W, bool COOP, bool GF, bool DESC>
+static hipError_t launch_one(const odpg_launch_args &a, uint32_t grid, hipStream_t s)
+{
+	size_t lds = (size_t)BLOCK * (W / 4 + 1) * 4u + (a.cos_partial ? (size_t)a.num_cos * 4u : 0u);
+
+	hipLaunchKernelGGL((odpg_classify_kernel<W, COOP, GF, DESC>), dim3(grid), dim3(BLOCK), lds, s,
+			   a.frames, a.desc, a.stride, a.num, a.opt, a.layer, a.classify, a.terms,
+			   a.pmrs, a.coses, a.num_cos, a.default_cos, a.error_cos, a.tbl_flags,
+			   a.out, a.mark, a.meta, a.pk_partial, a.cos_partial);
+	return hipGetLastError();
+}
+
+extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
+{
+	if (a->num == 0)
+		return 0;
+	uint32_t grid = (a->num + BLOCK - 1) / BLOCK;
+	hipError_t e;
+
+	if (a->desc) {
+		e = launch_one<128, false, true, true>(*a, grid, s);
+	} else if (a->stride == 64) {
+		e = launch_one<64, true, false, false>(*a, grid, s);
+	} else if (a->stride == 128) {
+		e = launch_one<128, true, false, false>(*a, grid, s);
+	} else if (a->stride < 128) {
+		e = launch_one<128, false, false, false>(*a, grid, s);
+	} else {
+		e = launch_one<128, false, true, false>(*a, grid, s);
+	}
+	if (e != hipSuccess)
+		return -EIO;
+	if (a->stats && (a->pk_partial || a->cos_partial)) {
+		uint32_t nwords = 4u + (a->cos_partial ? a->num_cos : 0u);
+		uint32_t rgrid = nwords < 1024u ? nwords : 1024u;
+
+		hipLaunchKernelGGL(odpg_stats_reduce_kernel, dim3(rgrid), dim3(BLOCK), 0, s,
+				   a->pk_partial, a->cos_partial, grid, a->num_cos, a->stats);
+		if (hipGetLastError() != hipSuccess)
+			return -EIO;
+	}
+	return 0;
+}
+
+extern "C" uint32_t odpg_launch_grid(uint32_t num)
+{
+	return (num + BLOCK - 1) / BLOCK;
+}

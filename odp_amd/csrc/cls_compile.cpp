@@ -1,0 +1,308 @@
+/* SPDX-License-Identifier: BSD-3-Clause
+ *
+ * Rule-table compiler: odpg_rules_t (a snapshot of the reference's CoS/PMR
+ * data model, odp_classification_datamodel.h:66-174) -> flat immutable device
+ * table (odpg_internal.h). Runs on the host once per table generation.
+ *
+ * Each reference term matcher (odp_classification.c:906-1332) is lowered to
+ * a byte-wise masked compare at a parser-relative offset. The lowering keeps
+ * the reference's raw-memory compare semantics: values and masks are the
+ * caller's bytes (network order, except ODP_PMR_LEN which is CPU endian).
+ */
+#include <string.h>
+#include <errno.h>
+#include <vector>
+
+#include "../../include/odpg.h"
+#include "odpg_internal.h"
+#include "cls_compile.h"
+
+namespace {
+
+dterm_t make_cmp(uint32_t req, uint8_t base, int32_t off, const uint8_t *mask,
+		 const uint8_t *value, uint32_t nbytes, uint8_t tflags = 0)
+{
+	dterm_t t;
+
+	memset(&t, 0, sizeof(t));
+	t.kind = DK_CMP;
+	t.base = base;
+	t.req = req;
+	t.off = off;
+	t.size = nbytes;
+	t.nwords = (uint8_t)((nbytes + 3) / 4);
+	t.tflags = tflags;
+	uint8_t m[16] = {0}, v[16] = {0};
+
+	memcpy(m, mask, nbytes);
+	memcpy(v, value, nbytes);
+	for (uint32_t i = 0; i < nbytes; i++)
+		v[i] &= 0xff;   /* value already & mask by pmr_create_term() */
+	memcpy(t.mask, m, 16);
+	memcpy(t.value, v, 16);
+	return t;
+}
+
+dterm_t make_never()
+{
+	dterm_t t;
+
+	memset(&t, 0, sizeof(t));
+	t.kind = DK_NEVER;
+	return t;
+}
+
+#define RQ(bit) (1u << (bit))
+
+/* Lower one reference term; appends 0, 1 or 2 compiled entries. */
+int lower_term(const odpg_term_t *src, std::vector<dterm_t> &out)
+{
+	const uint8_t *m = src->mask, *v = src->value;
+	uint32_t sz = src->val_sz;
+
+	if (sz > 16)
+		return -EINVAL;
+
+	switch (src->term) {
+	case PMR_LEN: {                           /* verify_pmr_packet_len :906-914 */
+		dterm_t t;
+
+		memset(&t, 0, sizeof(t));
+		t.kind = DK_LEN;
+		memcpy(t.mask, m, sz < 4 ? sz : 4);
+		memcpy(t.value, v, sz < 4 ? sz : 4);
+		out.push_back(t);
+		return 0;
+	}
+	case PMR_ETHTYPE_0:                       /* :1290-1307 eth->type */
+		out.push_back(make_cmp(RQ(IFL_ETH), DB_L2, 12, m, v, sz));
+		return 0;
+	case PMR_ETHTYPE_X:                       /* :1309-1332 innermost vlan->type */
+		/* vlan_qinq is only ever set together with vlan (odp_parse.c:74-82),
+		 * so "vlan || vlan_qinq" == vlan */
+		out.push_back(make_cmp(RQ(IFL_VLAN), DB_VLANX, 2, m, v, sz));
+		return 0;
+	case PMR_VLAN_ID_0:                       /* :1132-1153 tci & be16(0x0fff) */
+	case PMR_VLAN_ID_X: {                     /* :1155-1180 */
+		uint8_t mm[2] = { (uint8_t)(m[0] & 0x0f), m[1] };
+
+		if (src->term == PMR_VLAN_ID_0)
+			out.push_back(make_cmp(RQ(IFL_ETH) | RQ(IFL_VLAN), DB_L2, 14, mm, v, sz));
+		else
+			out.push_back(make_cmp(RQ(IFL_VLAN), DB_VLANX, 0, mm, v, sz));
+		return 0;
+	}
+	case PMR_VLAN_PCP_0: {                    /* :1182-1202 pcp = be16(tci) >> 13 */
+		if (v[0] & ~0x07) {               /* pcp & mask can never equal value */
+			out.push_back(make_never());
+			return 0;
+		}
+		uint8_t mm = (uint8_t)((m[0] & 0x07) << 5), vv = (uint8_t)(v[0] << 5);
+
+		out.push_back(make_cmp(RQ(IFL_ETH) | RQ(IFL_VLAN), DB_L2, 14, &mm, &vv, 1));
+		return 0;
+	}
+	case PMR_DMAC:                            /* :1062-1084 */
+		out.push_back(make_cmp(RQ(IFL_ETH), DB_L2, 0, m, v, sz));
+		return 0;
+	case PMR_IPPROTO:                         /* :1397-1407 ipv4->proto / ipv6->next_hdr */
+		out.push_back(make_cmp(RQ(IFL_IPV4), DB_L3, 9, m, v, sz, DT_ALT_NEXT));
+		out.push_back(make_cmp(RQ(IFL_IPV6), DB_L3, 6, m, v, sz));
+		return 0;
+	case PMR_IP_DSCP: {                       /* :1408-1418, :938-958 */
+		if (v[0] & ~0x3f) {
+			out.push_back(make_never());
+			return 0;
+		}
+		uint8_t m6 = m[0] & 0x3f, v6 = v[0];
+		/* v4: dscp = (tos & 0xfc) >> 2 */
+		uint8_t m4 = (uint8_t)(m6 << 2), v4 = (uint8_t)(v6 << 2);
+		/* v6: dscp = (be32(ver_tc_flow) >> 22) & 0x3f = bits of bytes 0..1 */
+		uint8_t mv6[2] = { (uint8_t)(m6 >> 2), (uint8_t)((m6 & 3) << 6) };
+		uint8_t vv6[2] = { (uint8_t)(v6 >> 2), (uint8_t)((v6 & 3) << 6) };
+
+		out.push_back(make_cmp(RQ(IFL_IPV4), DB_L3, 1, &m4, &v4, 1, DT_ALT_NEXT));
+		out.push_back(make_cmp(RQ(IFL_IPV6), DB_L3, 0, mv6, vv6, 2));
+		return 0;
+	}
+	case PMR_UDP_DPORT:                       /* :1028-1043 */
+		out.push_back(make_cmp(RQ(IFL_UDP), DB_L4, 2, m, v, sz));
+		return 0;
+	case PMR_TCP_DPORT:                       /* :1011-1026 */
+		out.push_back(make_cmp(RQ(IFL_TCP), DB_L4, 2, m, v, sz));
+		return 0;
+	case PMR_UDP_SPORT:                       /* :1045-1060 */
+		out.push_back(make_cmp(RQ(IFL_UDP), DB_L4, 0, m, v, sz));
+		return 0;
+	case PMR_TCP_SPORT:                       /* :994-1009 */
+		out.push_back(make_cmp(RQ(IFL_TCP), DB_L4, 0, m, v, sz));
+		return 0;
+	case PMR_SIP_ADDR:                        /* :960-975 */
+		out.push_back(make_cmp(RQ(IFL_IPV4), DB_L3, 12, m, v, sz));
+		return 0;
+	case PMR_DIP_ADDR:                        /* :977-992 */
+		out.push_back(make_cmp(RQ(IFL_IPV4), DB_L3, 16, m, v, sz));
+		return 0;
+	case PMR_SIP6_ADDR:                       /* :1086-1107 */
+		out.push_back(make_cmp(RQ(IFL_IPV6), DB_L3, 8, m, v, sz));
+		return 0;
+	case PMR_DIP6_ADDR:                       /* :1109-1130 */
+		out.push_back(make_cmp(RQ(IFL_IPV6), DB_L3, 24, m, v, sz));
+		return 0;
+	case PMR_IPSEC_SPI:                       /* :1204-1223 AH spi @4, ESP spi @0 */
+		out.push_back(make_cmp(RQ(IFL_IPSEC_AH), DB_L4, 4, m, v, sz, DT_ALT_NEXT));
+		out.push_back(make_cmp(RQ(IFL_IPSEC_ESP), DB_L4, 0, m, v, sz));
+		return 0;
+	case PMR_CUSTOM_FRAME:                    /* :1233-1257 */
+		out.push_back(make_cmp(0, DB_ABS, (int32_t)src->offset, m, v, sz, DT_GUARD));
+		return 0;
+	case PMR_CUSTOM_L3:                       /* :1259-1288 (l2 flag, l3 valid) */
+		out.push_back(make_cmp(RQ(IFL_L2), DB_L3, (int32_t)src->offset, m, v, sz, DT_GUARD));
+		return 0;
+	case PMR_INNER_HDR_OFF:                   /* :1479-1480 always passes */
+		return 0;
+	case PMR_LD_VNI:                          /* :1225-1231 unimplemented -> 0 */
+	default:                                  /* :1481-1483 */
+		out.push_back(make_never());
+		return 0;
+	}
+}
+
+} /* namespace */
+
+int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable_hdr_t *hdr_out)
+{
+	std::vector<dcos_t> cos;
+	std::vector<dpmr_t> pmr;
+	std::vector<dterm_t> terms;
+
+	if (!r || r->num_cos > ODPG_MAX_COS || (r->num_cos && !r->cos))
+		return -EINVAL;
+	if (r->default_cos >= (int32_t)r->num_cos || r->error_cos >= (int32_t)r->num_cos)
+		return -EINVAL;
+
+	cos.resize(r->num_cos);
+	for (uint32_t c = 0; c < r->num_cos; c++) {
+		const odpg_cos_t *ce = &r->cos[c];
+		dcos_t &d = cos[c];
+
+		memset(&d, 0, sizeof(d));
+		d.valid = ce->valid ? 1 : 0;
+		d.action = (uint8_t)ce->action;
+		d.num_queue = (uint8_t)(ce->num_queue ? ce->num_queue : 1);
+		d.hash_proto = (uint8_t)ce->hash_proto;
+		d.stats = ce->stats_enable ? 1 : 0;
+		d.rule_start = (uint32_t)pmr.size();
+		if (ce->num_queue > ODPG_COS_QUEUE_MAX || ce->num_rule > ODPG_MAX_RULES_PER_COS)
+			return -EINVAL;
+
+		for (uint32_t i = 0; i < ce->num_rule; i++) {
+			uint32_t slot = ce->rule_start + i;
+
+			if (slot >= r->num_slots)
+				return -EINVAL;
+			uint32_t pi = r->rule_pmr[slot], dst = r->rule_dst[slot];
+
+			if (pi >= r->num_pmr || dst >= r->num_cos)
+				return -EINVAL;
+			/* match_pmr_cos skips rules whose linked CoS is invalid
+			 * (odp_classification.c:1610-1611); the snapshot is
+			 * immutable, so drop them here. */
+			if (!r->cos[dst].valid)
+				continue;
+			const odpg_pmr_t *p = &r->pmr[pi];
+			dpmr_t dp;
+
+			if (p->num_terms > ODPG_MAX_TERMS)
+				return -EINVAL;
+			dp.term_start = (uint16_t)terms.size();
+			for (uint32_t t = 0; t < p->num_terms; t++) {
+				int rc = lower_term(&p->terms[t], terms);
+
+				if (rc)
+					return rc;
+			}
+			if (terms.size() > 65535)
+				return -E2BIG;
+			dp.nterms = (uint16_t)(terms.size() - dp.term_start);
+			dp.mark = (uint16_t)p->mark;
+			dp.dst = (uint16_t)dst;
+			pmr.push_back(dp);
+			if (pmr.size() > ODPG_MAX_PMR * 4)
+				return -E2BIG;
+		}
+		d.nrule = (uint16_t)(pmr.size() - d.rule_start);
+	}
+
+	dtable_hdr_t h;
+
+	memset(&h, 0, sizeof(h));
+	h.num_cos = r->num_cos;
+	h.default_cos = r->default_cos;
+	h.error_cos = r->error_cos;
+	h.num_pmr = (uint32_t)pmr.size();
+	h.num_terms = (uint32_t)terms.size();
+	for (const dpmr_t &p : pmr)
+		if (p.mark)
+			h.flags |= TBL_ANY_MARK;
+	for (const dcos_t &c : cos) {
+		if (c.num_queue > 1)
+			h.flags |= TBL_ANY_HASHQ;
+		if (c.stats)
+			h.flags |= TBL_ANY_STATS;
+	}
+
+	auto align = [](uint32_t x) { return (x + 63u) & ~63u; };
+	h.term_off = 0;
+	h.pmr_off = align(h.term_off + (uint32_t)(terms.size() * sizeof(dterm_t)));
+	h.cos_off = align(h.pmr_off + (uint32_t)(pmr.size() * sizeof(dpmr_t)));
+	h.blob_bytes = align(h.cos_off + (uint32_t)(cos.size() * sizeof(dcos_t)));
+	if (h.blob_bytes == 0)
+		h.blob_bytes = 64;
+	blob.assign(h.blob_bytes, 0);
+	if (!terms.empty())
+		memcpy(blob.data() + h.term_off, terms.data(), terms.size() * sizeof(dterm_t));
+	if (!pmr.empty())
+		memcpy(blob.data() + h.pmr_off, pmr.data(), pmr.size() * sizeof(dpmr_t));
+	if (!cos.empty())
+		memcpy(blob.data() + h.cos_off, cos.data(), cos.size() * sizeof(dcos_t));
+	*hdr_out = h;
+	return 0;
+}
+
+/* Does any packet path revisit a CoS? (reference loops forever on a matching
+ * cycle, odp_classification.c:1603-1631) */
+int odpg_rules_has_cycle(const std::vector<uint8_t> &blob, const dtable_hdr_t &h)
+{
+	const dcos_t *cos = (const dcos_t *)(blob.data() + h.cos_off);
+	const dpmr_t *pmr = (const dpmr_t *)(blob.data() + h.pmr_off);
+	std::vector<int> state(h.num_cos, 0);
+	std::vector<std::pair<uint32_t, uint32_t>> stack;
+
+	for (uint32_t s = 0; s < h.num_cos; s++) {
+		if (state[s])
+			continue;
+		stack.push_back({s, 0});
+		state[s] = 1;
+		while (!stack.empty()) {
+			auto &top = stack.back();
+			uint32_t c = top.first;
+
+			if (top.second < cos[c].nrule) {
+				uint32_t d = pmr[cos[c].rule_start + top.second].dst;
+
+				top.second++;
+				if (state[d] == 1)
+					return 1;
+				if (state[d] == 0) {
+					state[d] = 1;
+					stack.push_back({d, 0});
+				}
+			} else {
+				state[c] = 2;
+				stack.pop_back();
+			}
+		}
+	}
+	return 0;
+}

@@ -1,0 +1,1245 @@
+/* SPDX-License-Identifier: BSD-3-Clause
+ *
+ * Host control plane: the ODP CoS / PMR object model (odp_cls_* API) and the
+ * loop-pktio classifier glue, re-implemented for the MI355X classifier.
+ *
+ * Semantics follow platform/linux-generic/odp_classification.c exactly where
+ * an application can observe them: handles are index + 1 (:60-78), slots are
+ * taken first-free (:276-343, :419-437), a CoS holds at most
+ * max_pmr_per_cos rules (:807-808), rule creation appends in cos->pmr[] order
+ * (:826-829), rule destruction swaps the last rule into the freed slot
+ * (:757-761), destroyed CoS keep their slot contents until reuse (:464-478).
+ * The data plane never reads these structures: every change bumps a
+ * generation and odpg_pktio_recv_batch() compiles an immutable snapshot
+ * (odpg_rules_t -> device table) the first time a generation is used.
+ */
+#include <errno.h>
+#include <inttypes.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/odp_cls.h"
+
+#define REF_MAX_COS          64      /* CLS_COS_MAX_ENTRY   */
+#define REF_MAX_PMR          256     /* CLS_PMR_MAX_ENTRY   */
+#define REF_MAX_PMR_PER_COS  8       /* CLS_PMR_PER_COS_MAX */
+#define MAX_TERMS            8       /* CLS_PMRTERM_MAX     */
+#define MAX_TERM_SIZE        16
+#define COS_QUEUE_MAX        32
+#define MAX_MARK             UINT16_MAX
+#define MAX_PKTIO            64
+
+#define ERR(...) fprintf(stderr, "odp_cls: " __VA_ARGS__)
+
+typedef struct {
+	int valid;
+	char name[ODP_COS_NAME_LEN];
+	uint32_t *pmr;          /* [max_pmr_per_cos] pmr index    */
+	uint32_t *linked;       /* [max_pmr_per_cos] cos index    */
+	uint32_t num_rule;
+	int stats_enable;
+	int action;
+	odp_queue_t queue;
+	uint32_t num_queue;
+	odp_pool_t pool;
+	uint32_t index;
+	int queue_group;
+	uint32_t hash_proto;    /* odp_cls_hash_proto_t bits */
+	odp_pktin_vector_config_t vector;
+	odp_queue_param_t queue_param;
+	uint64_t st_packets, st_discards;
+	uint64_t q_packets[COS_QUEUE_MAX], q_discards[COS_QUEUE_MAX];
+	odp_queue_t hq[COS_QUEUE_MAX];   /* implementation-created hash queues */
+} cos_e;
+
+typedef struct {
+	int valid;
+	uint32_t num_pmr;
+	uint16_t mark;
+	odpg_term_t terms[MAX_TERMS];
+	int src_cos;            /* -1 = none */
+} pmr_e;
+
+typedef struct {
+	int valid;
+	int started;
+	char name[64];
+	odp_pool_t pool;
+	odp_pktio_config_t config;
+	int cls_enabled;
+	int parse_layer;
+	int default_cos;        /* -1 = NULL */
+	int error_cos;          /* -1 = NULL */
+	uint32_t headroom;
+	odp_pktio_stats_t stats;
+	/* compiled table cache */
+	odpg_table_t *tbl;
+	odpg_ctx_t *tbl_ctx;
+	uint64_t tbl_gen;
+	uint64_t *dstats;
+	odpg_ctx_t *dstats_ctx;
+} pktio_e;
+
+static struct {
+	int init;
+	pthread_mutex_t lock;
+	uint32_t max_cos, max_pmr, max_per_cos;
+	cos_e *cos;
+	pmr_e *pmr;
+	pktio_e pktio[MAX_PKTIO];
+	uint64_t generation;
+	uintptr_t next_queue_id;
+	/* snapshot buffers */
+	odpg_cos_t *s_cos;
+	odpg_pmr_t *s_pmr;
+	uint32_t *s_rule_pmr, *s_rule_dst;
+} g = { 0, PTHREAD_MUTEX_INITIALIZER, REF_MAX_COS, REF_MAX_PMR, REF_MAX_PMR_PER_COS,
+	NULL, NULL, {{0}}, 1, 0x40000000u, NULL, NULL, NULL, NULL };
+
+static void free_tables(void)
+{
+	if (g.cos) {
+		for (uint32_t i = 0; i < g.max_cos; i++) {
+			free(g.cos[i].pmr);
+			free(g.cos[i].linked);
+		}
+	}
+	free(g.cos);
+	free(g.pmr);
+	free(g.s_cos);
+	free(g.s_pmr);
+	free(g.s_rule_pmr);
+	free(g.s_rule_dst);
+	g.cos = NULL;
+	g.pmr = NULL;
+	g.s_cos = NULL;
+	g.s_pmr = NULL;
+	g.s_rule_pmr = NULL;
+	g.s_rule_dst = NULL;
+}
+
+/* _odp_classification_init_global (odp_classification.c:92-125) */
+static int ensure_init(void)
+{
+	if (g.init)
+		return 0;
+	g.cos = calloc(g.max_cos, sizeof(cos_e));
+	g.pmr = calloc(g.max_pmr, sizeof(pmr_e));
+	if (!g.cos || !g.pmr)
+		goto fail;
+	for (uint32_t i = 0; i < g.max_cos; i++) {
+		g.cos[i].pmr = calloc(g.max_per_cos, sizeof(uint32_t));
+		g.cos[i].linked = calloc(g.max_per_cos, sizeof(uint32_t));
+		if (!g.cos[i].pmr || !g.cos[i].linked)
+			goto fail;
+	}
+	for (uint32_t i = 0; i < g.max_pmr; i++)
+		g.pmr[i].src_cos = -1;
+	g.init = 1;
+	return 0;
+fail:
+	free_tables();
+	return -ENOMEM;
+}
+
+#define LOCK()   pthread_mutex_lock(&g.lock)
+#define UNLOCK() pthread_mutex_unlock(&g.lock)
+
+static inline uint32_t cos_to_ndx(odp_cos_t c)
+{
+	return (uint32_t)((uintptr_t)c - 1u);
+}
+
+static inline odp_cos_t cos_from_ndx(uint32_t n)
+{
+	return (odp_cos_t)(uintptr_t)(n + 1u);
+}
+
+static inline uint32_t pmr_to_ndx(odp_pmr_t p)
+{
+	return (uint32_t)((uintptr_t)p - 1u);
+}
+
+static inline odp_pmr_t pmr_from_ndx(uint32_t n)
+{
+	return (odp_pmr_t)(uintptr_t)(n + 1u);
+}
+
+/* get_cos_entry (odp_classification.c:439-449) */
+static cos_e *get_cos(odp_cos_t c)
+{
+	uint32_t n = cos_to_ndx(c);
+
+	if (!g.init || c == ODP_COS_INVALID || n >= g.max_cos || !g.cos[n].valid)
+		return NULL;
+	return &g.cos[n];
+}
+
+static pmr_e *get_pmr(odp_pmr_t p)
+{
+	uint32_t n = pmr_to_ndx(p);
+
+	if (!g.init || p == ODP_PMR_INVALID || n >= g.max_pmr || !g.pmr[n].valid)
+		return NULL;
+	return &g.pmr[n];
+}
+
+static pktio_e *get_pktio(odp_pktio_t p)
+{
+	uintptr_t n = (uintptr_t)p;
+
+	if (n == 0 || n > MAX_PKTIO || !g.pktio[n - 1].valid)
+		return NULL;
+	return &g.pktio[n - 1];
+}
+
+static void bump(void)
+{
+	g.generation++;
+}
+
+int odpg_cls_set_limits(uint32_t max_cos, uint32_t max_pmr, uint32_t max_pmr_per_cos)
+{
+	int rc = 0;
+
+	LOCK();
+	if (g.init) {
+		rc = -EBUSY;
+	} else if (max_cos == 0 || max_cos > ODPG_MAX_COS || max_pmr == 0 ||
+		   max_pmr > ODPG_MAX_PMR || max_pmr_per_cos == 0 ||
+		   max_pmr_per_cos > ODPG_MAX_RULES_PER_COS) {
+		rc = -EINVAL;
+	} else {
+		g.max_cos = max_cos;
+		g.max_pmr = max_pmr;
+		g.max_per_cos = max_pmr_per_cos;
+	}
+	UNLOCK();
+	return rc;
+}
+
+void odpg_cls_reset(void)
+{
+	LOCK();
+	for (int i = 0; i < MAX_PKTIO; i++) {
+		if (g.pktio[i].tbl)
+			odpg_table_destroy(g.pktio[i].tbl);
+		if (g.pktio[i].dstats)
+			odpg_dev_free(g.pktio[i].dstats_ctx, g.pktio[i].dstats);
+	}
+	memset(g.pktio, 0, sizeof(g.pktio));
+	free_tables();
+	g.init = 0;
+	g.max_cos = REF_MAX_COS;
+	g.max_pmr = REF_MAX_PMR;
+	g.max_per_cos = REF_MAX_PMR_PER_COS;
+	g.generation++;
+	UNLOCK();
+}
+
+uint64_t odpg_cls_generation(void)
+{
+	return g.generation;
+}
+
+/* odp_cls_capability (odp_classification.c:153-201) */
+int odp_cls_capability(odp_cls_capability_t *capa)
+{
+	memset(capa, 0, sizeof(*capa));
+	capa->max_pmr = g.max_pmr;
+	capa->max_pmr_per_cos = g.max_per_cos;
+	capa->max_terms_per_pmr = MAX_TERMS;
+	capa->max_cos = g.max_cos;
+	capa->max_cos_stats = capa->max_cos;
+	capa->pmr_range_supported = 0;
+	capa->supported_terms.bit.len = 1;
+	capa->supported_terms.bit.ethtype_0 = 1;
+	capa->supported_terms.bit.ethtype_x = 1;
+	capa->supported_terms.bit.vlan_id_0 = 1;
+	capa->supported_terms.bit.vlan_id_x = 1;
+	capa->supported_terms.bit.vlan_pcp_0 = 1;
+	capa->supported_terms.bit.dmac = 1;
+	capa->supported_terms.bit.ip_proto = 1;
+	capa->supported_terms.bit.ip_dscp = 1;
+	capa->supported_terms.bit.udp_dport = 1;
+	capa->supported_terms.bit.udp_sport = 1;
+	capa->supported_terms.bit.tcp_dport = 1;
+	capa->supported_terms.bit.tcp_sport = 1;
+	capa->supported_terms.bit.sip_addr = 1;
+	capa->supported_terms.bit.dip_addr = 1;
+	capa->supported_terms.bit.sip6_addr = 1;
+	capa->supported_terms.bit.dip6_addr = 1;
+	capa->supported_terms.bit.ipsec_spi = 1;
+	capa->supported_terms.bit.custom_frame = 1;
+	capa->supported_terms.bit.custom_l3 = 1;
+	capa->max_hash_queues = COS_QUEUE_MAX;
+	capa->hash_protocols.proto.ipv4_udp = 1;
+	capa->hash_protocols.proto.ipv4_tcp = 1;
+	capa->hash_protocols.proto.ipv4 = 1;
+	capa->hash_protocols.proto.ipv6_udp = 1;
+	capa->hash_protocols.proto.ipv6_tcp = 1;
+	capa->hash_protocols.proto.ipv6 = 1;
+	capa->max_mark = MAX_MARK;
+	capa->stats.cos.all_counters = 0x2 | 0x4;     /* packets, discards */
+	capa->stats.queue.all_counters = 0x2 | 0x4;
+	return 0;
+}
+
+void odp_cls_cos_param_init(odp_cls_cos_param_t *param)
+{
+	memset(param, 0, sizeof(*param));
+	param->queue = ODP_QUEUE_INVALID;
+	param->pool = ODP_POOL_INVALID;
+	param->num_queue = 1;
+	param->vector.enable = 0;
+}
+
+void odp_cls_pmr_param_init(odp_pmr_param_t *param)
+{
+	memset(param, 0, sizeof(*param));
+}
+
+void odp_cls_pmr_create_opt_init(odp_pmr_create_opt_t *opt)
+{
+	opt->terms = NULL;
+	opt->num_terms = 0;
+	opt->mark = 0;
+}
+
+/* _odp_cls_update_hash_proto (odp_classification.c:210-223) */
+static uint32_t hash_proto_bits(odp_pktin_hash_proto_t hp)
+{
+	uint32_t b = 0;
+
+	if (hp.proto.ipv4 || hp.proto.ipv4_tcp || hp.proto.ipv4_udp)
+		b |= 1;
+	if (hp.proto.ipv6 || hp.proto.ipv6_tcp || hp.proto.ipv6_udp)
+		b |= 2;
+	if (hp.proto.ipv4_udp || hp.proto.ipv6_udp)
+		b |= 4;
+	if (hp.proto.ipv4_tcp || hp.proto.ipv6_tcp)
+		b |= 8;
+	return b;
+}
+
+/* odp_cls_cos_create (odp_classification.c:231-347) */
+odp_cos_t odp_cls_cos_create(const char *name, const odp_cls_cos_param_t *param_in)
+{
+	odp_cls_cos_param_t param = *param_in;
+	odp_cos_t ret = ODP_COS_INVALID;
+
+	if (param.action == ODP_COS_ACTION_DROP) {
+		param.num_queue = 1;
+		param.queue = ODP_QUEUE_INVALID;
+		param.pool = ODP_POOL_INVALID;
+		param.vector.enable = 0;
+	} else if (param.num_queue == 1 && param.queue == ODP_QUEUE_INVALID) {
+		return ODP_COS_INVALID;
+	}
+	if (param.num_queue > COS_QUEUE_MAX || param.num_queue < 1)
+		return ODP_COS_INVALID;
+	if (param.vector.enable) {
+		if (param.vector.pool == ODP_POOL_INVALID) {
+			ERR("invalid packet vector pool\n");
+			return ODP_COS_INVALID;
+		}
+		if (param.vector.max_size == 0) {
+			ERR("vector.max_size is zero\n");
+			return ODP_COS_INVALID;
+		}
+	}
+
+	LOCK();
+	if (ensure_init()) {
+		UNLOCK();
+		return ODP_COS_INVALID;
+	}
+	for (uint32_t i = 0; i < g.max_cos; i++) {
+		cos_e *c = &g.cos[i];
+
+		if (c->valid)
+			continue;
+		if (name == NULL)
+			c->name[0] = 0;
+		else
+			snprintf(c->name, ODP_COS_NAME_LEN, "%s", name);
+		for (uint32_t j = 0; j < g.max_per_cos; j++) {
+			c->pmr[j] = 0;
+			c->linked[j] = 0;
+		}
+		c->num_queue = param.num_queue;
+		c->hash_proto = 0;
+		if (param.num_queue > 1) {
+			c->queue_param = param.queue_param;
+			c->queue_group = 1;
+			c->queue = ODP_QUEUE_INVALID;
+			c->hash_proto = hash_proto_bits(param.hash_proto);
+			for (uint32_t j = 0; j < param.num_queue; j++)
+				c->hq[j] = (odp_queue_t)(g.next_queue_id++);
+		} else {
+			c->queue_group = 0;
+			c->queue = param.queue;
+		}
+		c->st_packets = 0;
+		c->st_discards = 0;
+		memset(c->q_packets, 0, sizeof(c->q_packets));
+		memset(c->q_discards, 0, sizeof(c->q_discards));
+		c->action = param.action;
+		c->pool = param.pool;
+		c->valid = 1;
+		c->num_rule = 0;
+		c->index = i;
+		c->vector = param.vector;
+		c->stats_enable = param.stats_enable;
+		ret = cos_from_ndx(i);
+		bump();
+		break;
+	}
+	if (ret == ODP_COS_INVALID)
+		ERR("CLS_COS_MAX_ENTRY reached\n");
+	UNLOCK();
+	return ret;
+}
+
+int odp_cls_cos_create_multi(const char *name[], const odp_cls_cos_param_t param[],
+			     odp_cos_t cos[], int num)
+{
+	int i;
+
+	for (i = 0; i < num; i++) {
+		odp_cos_t c = odp_cls_cos_create(name ? name[i] : NULL, &param[i]);
+
+		if (c == ODP_COS_INVALID)
+			return i == 0 ? -1 : i;
+		cos[i] = c;
+	}
+	return i;
+}
+
+/* odp_cos_destroy (odp_classification.c:464-478) */
+int odp_cos_destroy(odp_cos_t cos_id)
+{
+	int rc = 0;
+
+	LOCK();
+	cos_e *c = get_cos(cos_id);
+
+	if (!c) {
+		ERR("Invalid odp_cos_t handle\n");
+		rc = -1;
+	} else {
+		c->valid = 0;
+		bump();
+	}
+	UNLOCK();
+	return rc;
+}
+
+int odp_cos_destroy_multi(odp_cos_t cos[], int num)
+{
+	int i;
+
+	for (i = 0; i < num; i++) {
+		int r = odp_cos_destroy(cos[i]);
+
+		if (r)
+			return i == 0 ? r : i;
+	}
+	return i;
+}
+
+int odp_cos_queue_set(odp_cos_t cos_id, odp_queue_t queue)
+{
+	int rc = -1;
+
+	LOCK();
+	cos_e *c = get_cos(cos_id);
+
+	if (!c)
+		ERR("Invalid odp_cos_t handle\n");
+	else if (queue == ODP_QUEUE_INVALID)
+		ERR("Invalid queue\n");
+	else if (c->num_queue != 1)
+		ERR("Hashing enabled, cannot set queue\n");
+	else {
+		c->queue = queue;
+		rc = 0;
+		bump();
+	}
+	UNLOCK();
+	return rc;
+}
+
+odp_queue_t odp_cos_queue(odp_cos_t cos_id)
+{
+	cos_e *c = get_cos(cos_id);
+
+	if (!c) {
+		ERR("Invalid odp_cos_t handle\n");
+		return ODP_QUEUE_INVALID;
+	}
+	return c->queue;
+}
+
+uint32_t odp_cls_cos_num_queue(odp_cos_t cos_id)
+{
+	cos_e *c = get_cos(cos_id);
+
+	if (!c) {
+		ERR("Invalid odp_cos_t handle\n");
+		return 0;
+	}
+	return c->num_queue;
+}
+
+/* odp_cls_cos_queues (odp_classification.c:546-578) */
+uint32_t odp_cls_cos_queues(odp_cos_t cos_id, odp_queue_t queue[], uint32_t num)
+{
+	cos_e *c = get_cos(cos_id);
+
+	if (!c) {
+		ERR("Invalid odp_cos_t handle\n");
+		return 0;
+	}
+	if (c->num_queue == 1) {
+		if (num == 0)
+			return 1;
+		queue[0] = c->queue;
+		return 1;
+	}
+	uint32_t n = num < c->num_queue ? num : c->num_queue;
+
+	for (uint32_t i = 0; i < n; i++)
+		queue[i] = c->hq[i];
+	return c->num_queue;
+}
+
+/* pmr_create_term (odp_classification.c:645-738) */
+static int pmr_create_term(odpg_term_t *v, const odp_pmr_param_t *param)
+{
+	uint32_t size;
+	int custom = 0;
+
+	if (param->range_term) {
+		ERR("PMR value range not supported\n");
+		return -1;
+	}
+	switch (param->term) {
+	case ODP_PMR_VLAN_PCP_0:
+	case ODP_PMR_IPPROTO:
+	case ODP_PMR_IP_DSCP:
+		size = 1;
+		break;
+	case ODP_PMR_ETHTYPE_0:
+	case ODP_PMR_ETHTYPE_X:
+	case ODP_PMR_VLAN_ID_0:
+	case ODP_PMR_VLAN_ID_X:
+	case ODP_PMR_UDP_DPORT:
+	case ODP_PMR_TCP_DPORT:
+	case ODP_PMR_UDP_SPORT:
+	case ODP_PMR_TCP_SPORT:
+		size = 2;
+		break;
+	case ODP_PMR_LEN:
+	case ODP_PMR_SIP_ADDR:
+	case ODP_PMR_DIP_ADDR:
+	case ODP_PMR_IPSEC_SPI:
+	case ODP_PMR_LD_VNI:
+		size = 4;
+		break;
+	case ODP_PMR_DMAC:
+		size = 6;
+		break;
+	case ODP_PMR_SIP6_ADDR:
+	case ODP_PMR_DIP6_ADDR:
+		size = 16;
+		break;
+	case ODP_PMR_CUSTOM_FRAME:
+	case ODP_PMR_CUSTOM_L3:
+		custom = 1;
+		size = MAX_TERM_SIZE;
+		break;
+	default:
+		ERR("Bad PMR term\n");
+		return -1;
+	}
+	if ((!custom && param->val_sz != size) || (custom && param->val_sz > size)) {
+		ERR("Bad PMR value size: %u\n", param->val_sz);
+		return -1;
+	}
+	memset(v, 0, sizeof(*v));
+	v->term = (uint32_t)param->term;
+	if (param->val_sz) {
+		memcpy(v->value, param->match.value, param->val_sz);
+		memcpy(v->mask, param->match.mask, param->val_sz);
+	}
+	for (uint32_t i = 0; i < param->val_sz; i++)
+		v->value[i] &= v->mask[i];
+	v->offset = param->offset;
+	v->val_sz = param->val_sz;
+	return 0;
+}
+
+/* cls_pmr_create (odp_classification.c:787-833) */
+static odp_pmr_t cls_pmr_create(const odp_pmr_param_t *terms, int num_terms, uint16_t mark,
+				odp_cos_t src_cos, odp_cos_t dst_cos)
+{
+	odp_pmr_t id = ODP_PMR_INVALID;
+
+	LOCK();
+	cos_e *src = get_cos(src_cos);
+	cos_e *dst = get_cos(dst_cos);
+
+	if (!src || !dst) {
+		ERR("Invalid odp_cos_t handle\n");
+		goto out;
+	}
+	if (num_terms > MAX_TERMS) {
+		ERR("no of terms greater than supported CLS_PMRTERM_MAX\n");
+		goto out;
+	}
+	if (src->num_rule == g.max_per_cos)
+		goto out;
+	for (uint32_t i = 0; i < g.max_pmr; i++) {
+		pmr_e *p = &g.pmr[i];
+
+		if (p->valid)
+			continue;
+		/* alloc_pmr (:419-437) marks the slot valid before the terms
+		 * are checked; a bad term releases it again */
+		p->valid = 1;
+		p->num_pmr = num_terms > 0 ? (uint32_t)num_terms : 0;
+		for (int t = 0; t < num_terms; t++) {
+			if (pmr_create_term(&p->terms[t], &terms[t])) {
+				p->valid = 0;
+				goto out;
+			}
+		}
+		p->mark = mark;
+		src->pmr[src->num_rule] = i;
+		src->linked[src->num_rule] = (uint32_t)(dst - g.cos);
+		src->num_rule++;
+		p->src_cos = (int)(src - g.cos);
+		id = pmr_from_ndx(i);
+		bump();
+		goto out;
+	}
+	ERR("CLS_PMR_MAX_ENTRY reached\n");
+out:
+	UNLOCK();
+	return id;
+}
+
+odp_pmr_t odp_cls_pmr_create(const odp_pmr_param_t *terms, int num_terms,
+			     odp_cos_t src_cos, odp_cos_t dst_cos)
+{
+	return cls_pmr_create(terms, num_terms, 0, src_cos, dst_cos);
+}
+
+odp_pmr_t odp_cls_pmr_create_opt(const odp_pmr_create_opt_t *opt,
+				 odp_cos_t src_cos, odp_cos_t dst_cos)
+{
+	if (opt == NULL) {
+		ERR("Bad parameter\n");
+		return ODP_PMR_INVALID;
+	}
+	if (opt->mark > MAX_MARK) {
+		ERR("Too large mark value: %" PRIu64 "\n", opt->mark);
+		return ODP_PMR_INVALID;
+	}
+	return cls_pmr_create(opt->terms, opt->num_terms, (uint16_t)opt->mark, src_cos, dst_cos);
+}
+
+int odp_cls_pmr_create_multi(const odp_pmr_create_opt_t opt[], odp_cos_t src_cos[],
+			     odp_cos_t dst_cos[], odp_pmr_t pmr[], int num)
+{
+	int i;
+
+	for (i = 0; i < num; i++) {
+		odp_pmr_t p = odp_cls_pmr_create_opt(&opt[i], src_cos[i], dst_cos[i]);
+
+		if (p == ODP_PMR_INVALID)
+			return i == 0 ? -1 : i;
+		pmr[i] = p;
+	}
+	return i;
+}
+
+/* odp_cls_pmr_destroy (odp_classification.c:740-768), including its
+ * unconditional num_rule decrement */
+int odp_cls_pmr_destroy(odp_pmr_t pmr_id)
+{
+	int rc = 0;
+
+	LOCK();
+	pmr_e *p = get_pmr(pmr_id);
+
+	if (!p || p->src_cos < 0) {
+		rc = -1;
+	} else {
+		cos_e *src = &g.cos[p->src_cos];
+		uint32_t idx = pmr_to_ndx(pmr_id);
+		uint32_t loc = src->num_rule;
+
+		if (loc != 0) {
+			loc -= 1;
+			for (uint32_t i = 0; i <= loc; i++)
+				if (src->pmr[i] == idx) {
+					src->pmr[i] = src->pmr[loc];
+					src->linked[i] = src->linked[loc];
+				}
+			src->num_rule--;
+		}
+		p->valid = 0;
+		bump();
+	}
+	UNLOCK();
+	return rc;
+}
+
+int odp_cls_pmr_destroy_multi(odp_pmr_t pmr[], int num)
+{
+	int i;
+
+	for (i = 0; i < num; i++) {
+		int r = odp_cls_pmr_destroy(pmr[i]);
+
+		if (r)
+			return i == 0 ? r : i;
+	}
+	return i;
+}
+
+int odp_cls_cos_pool_set(odp_cos_t cos_id, odp_pool_t pool)
+{
+	int rc = -1;
+
+	LOCK();
+	cos_e *c = get_cos(cos_id);
+
+	if (!c) {
+		ERR("Invalid odp_cos_t handle\n");
+	} else {
+		c->pool = pool;
+		rc = 0;
+	}
+	UNLOCK();
+	return rc;
+}
+
+odp_pool_t odp_cls_cos_pool(odp_cos_t cos_id)
+{
+	cos_e *c = get_cos(cos_id);
+
+	if (!c) {
+		ERR("Invalid odp_cos_t handle\n");
+		return ODP_POOL_INVALID;
+	}
+	return c->pool;
+}
+
+/* odp_cls_cos_stats (odp_classification.c:1829-1847) */
+int odp_cls_cos_stats(odp_cos_t cos_id, odp_cls_cos_stats_t *stats)
+{
+	cos_e *c = get_cos(cos_id);
+
+	if (!c) {
+		ERR("Invalid odp_cos_t handle\n");
+		return -1;
+	}
+	if (!stats) {
+		ERR("Output structure NULL\n");
+		return -1;
+	}
+	memset(stats, 0, sizeof(*stats));
+	LOCK();
+	stats->discards = c->st_discards;
+	stats->packets = c->st_packets;
+	UNLOCK();
+	return 0;
+}
+
+/* _odp_cos_queue_idx (odp_classification_internal.h:43-60) */
+static int cos_queue_idx(const cos_e *c, odp_queue_t q)
+{
+	if (c->num_queue == 1)
+		return c->queue == q ? 0 : -1;
+	for (uint32_t i = 0; i < c->num_queue; i++)
+		if (c->hq[i] == q)
+			return (int)i;
+	return -1;
+}
+
+/* odp_cls_queue_stats (odp_classification.c:1849-1877) */
+int odp_cls_queue_stats(odp_cos_t cos_id, odp_queue_t queue, odp_cls_queue_stats_t *stats)
+{
+	cos_e *c = get_cos(cos_id);
+	int qi;
+
+	if (!c) {
+		ERR("Invalid odp_cos_t handle\n");
+		return -1;
+	}
+	if (!stats) {
+		ERR("Output structure NULL\n");
+		return -1;
+	}
+	qi = cos_queue_idx(c, queue);
+	if (qi < 0) {
+		ERR("Invalid odp_queue_t handle\n");
+		return -1;
+	}
+	memset(stats, 0, sizeof(*stats));
+	LOCK();
+	stats->discards = c->q_discards[qi];
+	stats->packets = c->q_packets[qi];
+	UNLOCK();
+	return 0;
+}
+
+/* odp_cls_print_all (odp_classification.c:1879-1981), reduced */
+void odp_cls_print_all(void)
+{
+	LOCK();
+	printf("\nClassifier info\n---------------\n");
+	if (g.init) {
+		for (uint32_t i = 0; i < g.max_cos; i++) {
+			cos_e *c = &g.cos[i];
+
+			if (!c->valid)
+				continue;
+			printf("  %s(%u): %u rule(s)%s\n", c->name, i + 1, c->num_rule,
+			       c->action == ODP_COS_ACTION_DROP ? " [drop]" : "");
+			for (uint32_t r = 0; r < c->num_rule; r++) {
+				pmr_e *p = &g.pmr[c->pmr[r]];
+
+				printf("    pmr(%u) terms=%u mark=%u -> %s(%u)\n", c->pmr[r] + 1,
+				       p->num_pmr, p->mark, g.cos[c->linked[r]].name,
+				       c->linked[r] + 1);
+			}
+		}
+	}
+	printf("\n");
+	UNLOCK();
+}
+
+uint64_t odp_cos_to_u64(odp_cos_t hdl)
+{
+	return (uint64_t)(uintptr_t)hdl;
+}
+
+uint64_t odp_pmr_to_u64(odp_pmr_t hdl)
+{
+	return (uint64_t)(uintptr_t)hdl;
+}
+
+/* ---- loop pktio subset -------------------------------------------------- */
+odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const void *param)
+{
+	odp_pktio_t ret = ODP_PKTIO_INVALID;
+
+	(void)param;
+	if (!name || strncmp(name, "loop", 4) != 0) {
+		ERR("only loop pktio is supported: %s\n", name ? name : "(null)");
+		return ODP_PKTIO_INVALID;
+	}
+	LOCK();
+	for (int i = 0; i < MAX_PKTIO; i++) {
+		pktio_e *p = &g.pktio[i];
+
+		if (p->valid)
+			continue;
+		memset(p, 0, sizeof(*p));
+		p->valid = 1;
+		snprintf(p->name, sizeof(p->name), "%s", name);
+		p->pool = pool;
+		odp_pktio_config_init(&p->config);
+		p->default_cos = -1;
+		p->error_cos = -1;
+		ret = (odp_pktio_t)(uintptr_t)(i + 1);
+		bump();
+		break;
+	}
+	UNLOCK();
+	return ret;
+}
+
+int odp_pktio_close(odp_pktio_t hdl)
+{
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+
+	if (!p) {
+		UNLOCK();
+		return -1;
+	}
+	if (p->tbl)
+		odpg_table_destroy(p->tbl);
+	if (p->dstats)
+		odpg_dev_free(p->dstats_ctx, p->dstats);
+	memset(p, 0, sizeof(*p));
+	bump();
+	UNLOCK();
+	return 0;
+}
+
+void odp_pktio_config_init(odp_pktio_config_t *config)
+{
+	memset(config, 0, sizeof(*config));
+	config->parser.layer = ODP_PROTO_LAYER_ALL;
+}
+
+/* odp_pktio_config (odp_packet_io.c:602-682) with the loop capability
+ * (pktio/loop.c:650-670): timestamps + ipv4/udp/tcp/sctp checksum checks */
+int odp_pktio_config(odp_pktio_t hdl, const odp_pktio_config_t *config)
+{
+	odp_pktio_config_t def;
+	const uint64_t capa = ODPG_PKTIN_TS_ALL | ODPG_PKTIN_TS_PTP | ODPG_PKTIN_IPV4_CHKSUM |
+			      ODPG_PKTIN_UDP_CHKSUM | ODPG_PKTIN_TCP_CHKSUM |
+			      ODPG_PKTIN_SCTP_CHKSUM;
+	int rc = 0;
+
+	if (!config) {
+		odp_pktio_config_init(&def);
+		config = &def;
+	}
+	if (config->pktin.all_bits & ~capa) {
+		ERR("Unsupported input configuration option\n");
+		return -1;
+	}
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+
+	if (!p) {
+		rc = -1;
+	} else if (p->started) {
+		rc = -1;
+	} else {
+		p->config = *config;
+		bump();
+	}
+	UNLOCK();
+	return rc;
+}
+
+void odp_pktin_queue_param_init(odp_pktin_queue_param_t *param)
+{
+	memset(param, 0, sizeof(*param));
+	param->num_queues = 1;
+}
+
+int odp_pktin_queue_config(odp_pktio_t hdl, const odp_pktin_queue_param_t *param)
+{
+	int rc = 0;
+
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+
+	if (!p || p->started) {
+		rc = -1;
+	} else {
+		p->cls_enabled = param ? !!param->classifier_enable : 0;
+		bump();
+	}
+	UNLOCK();
+	return rc;
+}
+
+/* odp_pktio_start (odp_packet_io.c:684-720): parse_layer = ALL with cls */
+int odp_pktio_start(odp_pktio_t hdl)
+{
+	int rc = 0;
+
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+
+	if (!p || p->started) {
+		rc = -1;
+	} else {
+		p->parse_layer = p->cls_enabled ? ODP_PROTO_LAYER_ALL : (int)p->config.parser.layer;
+		p->started = 1;
+		bump();
+	}
+	UNLOCK();
+	return rc;
+}
+
+int odp_pktio_stop(odp_pktio_t hdl)
+{
+	int rc = 0;
+
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+
+	if (!p || !p->started)
+		rc = -1;
+	else
+		p->started = 0;
+	UNLOCK();
+	return rc;
+}
+
+int odp_pktio_stats(odp_pktio_t hdl, odp_pktio_stats_t *stats)
+{
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+
+	if (!p || !stats) {
+		UNLOCK();
+		return -1;
+	}
+	*stats = p->stats;
+	UNLOCK();
+	return 0;
+}
+
+int odp_pktio_stats_reset(odp_pktio_t hdl)
+{
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+
+	if (!p) {
+		UNLOCK();
+		return -1;
+	}
+	memset(&p->stats, 0, sizeof(p->stats));
+	UNLOCK();
+	return 0;
+}
+
+uint64_t odp_pktio_to_u64(odp_pktio_t hdl)
+{
+	return (uint64_t)(uintptr_t)hdl;
+}
+
+/* odp_pktio_default_cos_set (odp_classification.c:580-601) */
+int odp_pktio_default_cos_set(odp_pktio_t hdl, odp_cos_t default_cos)
+{
+	int rc = 0;
+
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+	cos_e *c = NULL;
+
+	if (!p) {
+		ERR("Invalid odp_pktio_t handle\n");
+		rc = -1;
+		goto out;
+	}
+	if (default_cos != ODP_COS_INVALID) {
+		c = get_cos(default_cos);
+		if (!c) {
+			ERR("Invalid odp_cos_t handle\n");
+			rc = -1;
+			goto out;
+		}
+	}
+	p->default_cos = c ? (int)(c - g.cos) : -1;
+	bump();
+out:
+	UNLOCK();
+	return rc;
+}
+
+/* odp_pktio_error_cos_set (odp_classification.c:603-622) */
+int odp_pktio_error_cos_set(odp_pktio_t hdl, odp_cos_t error_cos)
+{
+	int rc = 0;
+
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+	cos_e *c;
+
+	if (!p) {
+		ERR("Invalid odp_pktio_t handle\n");
+		rc = -1;
+		goto out;
+	}
+	c = get_cos(error_cos);
+	if (!c) {
+		ERR("Invalid odp_cos_t handle\n");
+		rc = -1;
+		goto out;
+	}
+	p->error_cos = (int)(c - g.cos);
+	bump();
+out:
+	UNLOCK();
+	return rc;
+}
+
+int odp_pktio_skip_set(odp_pktio_t hdl, uint32_t offset)
+{
+	(void)hdl;
+	(void)offset;
+	return -ENOTSUP;
+}
+
+int odp_pktio_headroom_set(odp_pktio_t hdl, uint32_t headroom)
+{
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+
+	if (!p) {
+		UNLOCK();
+		ERR("Invalid odp_pktio_t handle\n");
+		return -1;
+	}
+	p->headroom = headroom;
+	UNLOCK();
+	return 0;
+}
+
+/* ---- snapshot + GPU receive path ---------------------------------------- */
+static int snapshot_locked(const pktio_e *p, odpg_rules_t *r)
+{
+	uint32_t slots = 0;
+
+	if (ensure_init())
+		return -ENOMEM;
+	if (!g.s_cos) {
+		g.s_cos = calloc(g.max_cos, sizeof(odpg_cos_t));
+		g.s_pmr = calloc(g.max_pmr, sizeof(odpg_pmr_t));
+		g.s_rule_pmr = calloc((size_t)g.max_cos * g.max_per_cos, sizeof(uint32_t));
+		g.s_rule_dst = calloc((size_t)g.max_cos * g.max_per_cos, sizeof(uint32_t));
+		if (!g.s_cos || !g.s_pmr || !g.s_rule_pmr || !g.s_rule_dst)
+			return -ENOMEM;
+	}
+	for (uint32_t i = 0; i < g.max_cos; i++) {
+		const cos_e *c = &g.cos[i];
+		odpg_cos_t *s = &g.s_cos[i];
+
+		s->valid = (uint32_t)c->valid;
+		s->action = (uint32_t)c->action;
+		s->num_queue = c->num_queue ? c->num_queue : 1;
+		s->hash_proto = c->hash_proto;
+		s->stats_enable = (uint32_t)c->stats_enable;
+		s->num_rule = c->num_rule;
+		s->rule_start = slots;
+		for (uint32_t k = 0; k < c->num_rule; k++) {
+			g.s_rule_pmr[slots] = c->pmr[k];
+			g.s_rule_dst[slots] = c->linked[k];
+			slots++;
+		}
+	}
+	for (uint32_t i = 0; i < g.max_pmr; i++) {
+		const pmr_e *pe = &g.pmr[i];
+		odpg_pmr_t *s = &g.s_pmr[i];
+
+		s->num_terms = pe->num_pmr;
+		s->mark = pe->mark;
+		memcpy(s->terms, pe->terms, sizeof(s->terms));
+	}
+	r->num_cos = g.max_cos;
+	r->cos = g.s_cos;
+	r->num_pmr = g.max_pmr;
+	r->pmr = g.s_pmr;
+	r->num_slots = slots;
+	r->rule_pmr = g.s_rule_pmr;
+	r->rule_dst = g.s_rule_dst;
+	r->default_cos = p ? p->default_cos : -1;
+	r->error_cos = p ? p->error_cos : -1;
+	return 0;
+}
+
+int odpg_pktio_rules(odp_pktio_t hdl, odpg_rules_t *r)
+{
+	int rc;
+
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+
+	rc = p ? snapshot_locked(p, r) : -EINVAL;
+	UNLOCK();
+	return rc;
+}
+
+int odpg_pktio_recv_batch(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
+			  const odpg_desc_t *desc, uint32_t stride, uint32_t num,
+			  int device_ptrs, odpg_out_t *out, uint16_t *mark)
+{
+	int rc = 0;
+	odpg_rules_t r;
+	odpg_batch_t b;
+	odpg_result_t res;
+	uint32_t nstats;
+	uint64_t *hstats = NULL;
+
+	if (!ctx || !out)
+		return -EINVAL;
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+
+	if (!p || !p->started) {
+		rc = -EINVAL;
+		goto out;
+	}
+	if (!p->tbl || p->tbl_gen != g.generation || p->tbl_ctx != ctx) {
+		if (p->tbl)
+			odpg_table_destroy(p->tbl);
+		p->tbl = NULL;
+		if ((rc = snapshot_locked(p, &r)))
+			goto out;
+		if ((rc = odpg_table_create(ctx, &r, &p->tbl)))
+			goto out;
+		p->tbl_gen = g.generation;
+		p->tbl_ctx = ctx;
+	}
+	nstats = ODPG_STATS_WORDS(g.max_cos);
+	hstats = calloc(nstats, sizeof(uint64_t));
+	if (!hstats) {
+		rc = -ENOMEM;
+		goto out;
+	}
+	memset(&b, 0, sizeof(b));
+	b.frames = frames;
+	b.desc = desc;
+	b.stride = stride;
+	b.num = num;
+	b.pktin_opt = p->config.pktin.all_bits;
+	b.layer = (uint32_t)p->parse_layer;
+	b.classify = (uint32_t)p->cls_enabled;
+	res.out = out;
+	res.mark = mark;
+	res.meta = NULL;
+	if (device_ptrs) {
+		if (!p->dstats || p->dstats_ctx != ctx) {
+			if (p->dstats)
+				odpg_dev_free(p->dstats_ctx, p->dstats);
+			p->dstats = NULL;
+			if ((rc = odpg_dev_alloc(ctx, nstats * 8u, (void **)&p->dstats)))
+				goto out;
+			p->dstats_ctx = ctx;
+		}
+		res.stats = p->dstats;
+		if ((rc = odpg_memset_dev(ctx, p->dstats, 0, nstats * 8u)) ||
+		    (rc = odpg_classify(ctx, p->tbl, &b, &res)) ||
+		    (rc = odpg_memcpy_d2h(ctx, hstats, p->dstats, nstats * 8u)))
+			goto out;
+	} else {
+		res.stats = hstats;
+		if ((rc = odpg_classify_host(ctx, p->tbl, &b, &res, 0)))
+			goto out;
+		/* per-queue enqueue counters (_odp_cos_queue_stats_add,
+		 * odp_classification_internal.h:64-78) from the verdicts */
+		for (uint32_t i = 0; i < num; i++) {
+			uint32_t w = out[i], c = ODPG_OUT_COS(w);
+
+			if (c >= g.max_cos || (w & ODPG_OUT_CLS_DROP))
+				continue;
+			g.cos[c].q_packets[g.cos[c].num_queue > 1 ? ODPG_OUT_HASHQ(w) : 0]++;
+		}
+	}
+	p->stats.in_packets += hstats[0];
+	p->stats.in_octets += hstats[1];
+	p->stats.in_errors += hstats[2];
+	p->stats.in_discards += hstats[3];
+	for (uint32_t c = 0; c < g.max_cos; c++)
+		g.cos[c].st_packets += hstats[4 + c];
+out:
+	free(hstats);
+	UNLOCK();
+	return rc;
+}

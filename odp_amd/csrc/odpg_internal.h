@@ -1,0 +1,122 @@
+/* SPDX-License-Identifier: BSD-3-Clause
+ *
+ * Internal layout shared by the host table compiler (cls_compile.cpp) and
+ * the gfx950 kernels (classify.hip). Not part of the public ABI.
+ */
+#ifndef ODPG_INTERNAL_H_
+#define ODPG_INTERNAL_H_
+
+#include <stdint.h>
+
+/* _odp_packet_input_flags_t bit positions (packet_inline_types.h:60-113) */
+enum {
+	IFL_DST_QUEUE = 0, IFL_CLS_MARK, IFL_FLOW_HASH, IFL_TIMESTAMP,
+	IFL_L2, IFL_L3, IFL_L4,
+	IFL_ETH, IFL_ETH_BCAST, IFL_ETH_MCAST, IFL_JUMBO, IFL_VLAN, IFL_VLAN_QINQ,
+	IFL_SNAP, IFL_ARP,
+	IFL_IPV4, IFL_IPV6, IFL_IP_BCAST, IFL_IP_MCAST, IFL_IPFRAG, IFL_IPOPT,
+	IFL_IPSEC, IFL_IPSEC_AH, IFL_IPSEC_ESP,
+	IFL_UDP, IFL_TCP, IFL_SCTP, IFL_ICMP, IFL_NO_NEXT_HDR,
+	IFL_COLOR0, IFL_COLOR1, IFL_NODROP,
+	IFL_L3_CHKSUM_DONE, IFL_L4_CHKSUM_DONE, IFL_IPSEC_UDP, IFL_UDP_CHKSUM_ZERO
+};
+
+/* _odp_packet_flags_t error bits (packet_inline_types.h:150-164) */
+enum {
+	FL_SNAP_LEN_ERR = 25, FL_IP_ERR, FL_L3_CHKSUM_ERR, FL_TCP_ERR, FL_UDP_ERR,
+	FL_SCTP_ERR, FL_L4_CHKSUM_ERR
+};
+#define FL_ERROR_MASK 0xFE000000u
+
+/* odp_cls_pmr_term_t (include/odp/api/spec/classification.h:68-195) */
+enum {
+	PMR_LEN = 0, PMR_ETHTYPE_0, PMR_ETHTYPE_X, PMR_VLAN_ID_0, PMR_VLAN_ID_X,
+	PMR_VLAN_PCP_0, PMR_DMAC, PMR_IPPROTO, PMR_IP_DSCP, PMR_UDP_DPORT,
+	PMR_TCP_DPORT, PMR_UDP_SPORT, PMR_TCP_SPORT, PMR_SIP_ADDR, PMR_DIP_ADDR,
+	PMR_SIP6_ADDR, PMR_DIP6_ADDR, PMR_IPSEC_SPI, PMR_LD_VNI, PMR_CUSTOM_FRAME,
+	PMR_CUSTOM_L3, PMR_IGMP_GRP_ADDR, PMR_ICMP_ID, PMR_ICMP_TYPE, PMR_ICMP_CODE,
+	PMR_SCTP_SPORT, PMR_SCTP_DPORT, PMR_GTPV1_TEID, PMR_INNER_HDR_OFF = 32
+};
+
+/* ---- compiled device table ---------------------------------------------
+ * Every reference term matcher (odp_classification.c:906-1332) reduces to a
+ * byte-wise masked compare of up to 16 bytes at (base + off), gated by a set
+ * of parser input flags that must all be present. Terms whose matcher
+ * depends on the IP version / IPsec header kind (IPPROTO, IP_DSCP,
+ * IPSEC_SPI) compile to two alternatives: the first applies when its flags
+ * are present, otherwise the second is evaluated. */
+enum { DK_CMP = 0, DK_LEN = 1, DK_NEVER = 2 };
+enum { DB_ABS = 0, DB_L2 = 1, DB_L3 = 2, DB_L4 = 3, DB_VLANX = 4 };
+#define DT_GUARD    0x1   /* require frame_len > pos + size (custom terms)    */
+#define DT_ALT_NEXT 0x2   /* if req flags absent, result = next term's result */
+
+typedef struct dterm_s {
+	uint8_t  kind;
+	uint8_t  base;
+	uint8_t  nwords;    /* 0..4 compared 32-bit little-endian words */
+	uint8_t  tflags;
+	uint32_t req;       /* low 32 input flags that must all be set */
+	int32_t  off;
+	uint32_t size;      /* bytes compared (guard length) */
+	uint32_t mask[4];
+	uint32_t value[4];
+} dterm_t;              /* 48 bytes */
+
+typedef struct dpmr_s {
+	uint16_t term_start;
+	uint16_t nterms;    /* compiled entries, including ALT_NEXT partners */
+	uint16_t mark;
+	uint16_t dst;
+} dpmr_t;               /* 8 bytes */
+
+typedef struct dcos_s {
+	uint32_t rule_start;
+	uint16_t nrule;
+	uint8_t  action;
+	uint8_t  num_queue;
+	uint8_t  hash_proto;
+	uint8_t  stats;
+	uint8_t  valid;
+	uint8_t  pad;
+} dcos_t;               /* 12 bytes */
+
+#define TBL_ANY_MARK   0x1
+#define TBL_ANY_HASHQ  0x2
+#define TBL_ANY_STATS  0x4
+
+typedef struct dtable_hdr_s {
+	uint32_t num_cos;
+	int32_t  default_cos;
+	int32_t  error_cos;
+	uint32_t flags;
+	uint32_t num_pmr;
+	uint32_t num_terms;
+	uint32_t cos_off;    /* byte offsets inside the device blob */
+	uint32_t pmr_off;
+	uint32_t term_off;
+	uint32_t blob_bytes;
+} dtable_hdr_t;
+
+/* kernel launch arguments (runtime.hip -> classify.hip) */
+#include "../../include/odpg.h"
+typedef struct odpg_launch_args {
+	const uint8_t *frames;
+	const odpg_desc_t *desc;
+	uint32_t stride, num;
+	uint64_t opt;
+	uint32_t layer, classify;
+	const dterm_t *terms;
+	const dpmr_t *pmrs;
+	const dcos_t *coses;
+	uint32_t num_cos;
+	int32_t default_cos, error_cos;
+	uint32_t tbl_flags;
+	odpg_out_t *out;
+	uint16_t *mark;
+	odpg_meta_t *meta;
+	uint64_t *pk_partial;
+	uint32_t *cos_partial;
+	uint64_t *stats;
+} odpg_launch_args;
+
+#endif

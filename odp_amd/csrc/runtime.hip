@@ -1,0 +1,545 @@
+/* SPDX-License-Identifier: BSD-3-Clause
+ *
+ * Host runtime behind the odpg.h C-ABI: contexts (device + stream + scratch),
+ * compiled rule tables in HBM, device-resident and host-buffer batch
+ * classification, and thin memory / timing helpers.
+ */
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdio.h>
+#include <string.h>
+#include <stdlib.h>
+#include <mutex>
+#include <vector>
+
+#include "../../include/odpg.h"
+#include "odpg_internal.h"
+#include "cls_compile.h"
+
+
+extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s);
+extern "C" uint32_t odpg_launch_grid(uint32_t num);
+
+#define NUM_EVENTS 16
+
+struct odpg_ctx_s {
+	int device;
+	hipStream_t stream;
+	bool own_stream;
+	hipStream_t copy_stream;
+	void *ws;          /* per-workgroup counter partials */
+	size_t ws_bytes;
+	hipEvent_t ev[NUM_EVENTS];
+	std::mutex lock;
+};
+
+struct odpg_table_s {
+	dtable_hdr_t hdr;
+	std::vector<uint8_t> blob;
+	void *dblob;
+	int device;
+	int cycle;
+};
+
+#define HIPCHK(x)                                                              \
+	do {                                                                   \
+		hipError_t e_ = (x);                                           \
+		if (e_ != hipSuccess) {                                        \
+			fprintf(stderr, "odpg: %s failed: %s (%s:%d)\n", #x,    \
+				hipGetErrorString(e_), __FILE__, __LINE__);    \
+			return -EIO;                                           \
+		}                                                              \
+	} while (0)
+
+extern "C" {
+
+int odpg_abi_version(void)
+{
+	return ODPG_ABI_VERSION;
+}
+
+const char *odpg_build_info(void)
+{
+	return "odpg gfx950 classifier, ABI 1";
+}
+
+int odpg_device_count(void)
+{
+	int n = 0;
+
+	if (hipGetDeviceCount(&n) != hipSuccess)
+		return 0;
+	return n;
+}
+
+int odpg_ctx_create(int device, void *stream, odpg_ctx_t **out)
+{
+	if (!out)
+		return -EINVAL;
+	int n = odpg_device_count();
+
+	if (device < 0 || device >= n)
+		return -ENODEV;
+	odpg_ctx_t *c = new odpg_ctx_t();
+
+	c->device = device;
+	c->ws = nullptr;
+	c->ws_bytes = 0;
+	if (hipSetDevice(device) != hipSuccess) {
+		delete c;
+		return -EIO;
+	}
+	if (stream) {
+		c->stream = (hipStream_t)stream;
+		c->own_stream = false;
+	} else {
+		if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+			delete c;
+			return -EIO;
+		}
+		c->own_stream = true;
+	}
+	if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) {
+		delete c;
+		return -EIO;
+	}
+	for (int k = 0; k < NUM_EVENTS; k++)
+		if (hipEventCreate(&c->ev[k]) != hipSuccess) {
+			delete c;
+			return -EIO;
+		}
+	*out = c;
+	return 0;
+}
+
+void odpg_ctx_destroy(odpg_ctx_t *c)
+{
+	if (!c)
+		return;
+	hipSetDevice(c->device);
+	hipStreamSynchronize(c->stream);
+	hipStreamSynchronize(c->copy_stream);
+	if (c->ws)
+		hipFree(c->ws);
+	for (int k = 0; k < NUM_EVENTS; k++)
+		hipEventDestroy(c->ev[k]);
+	hipStreamDestroy(c->copy_stream);
+	if (c->own_stream)
+		hipStreamDestroy(c->stream);
+	delete c;
+}
+
+void *odpg_ctx_stream(odpg_ctx_t *c)
+{
+	return c ? (void *)c->stream : nullptr;
+}
+
+int odpg_ctx_sync(odpg_ctx_t *c)
+{
+	if (!c)
+		return -EINVAL;
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int odpg_table_create(odpg_ctx_t *c, const odpg_rules_t *rules, odpg_table_t **out)
+{
+	if (!c || !rules || !out)
+		return -EINVAL;
+	odpg_table_t *t = new odpg_table_t();
+	int rc = odpg_compile_rules(rules, t->blob, &t->hdr);
+
+	if (rc) {
+		delete t;
+		return rc;
+	}
+	t->cycle = odpg_rules_has_cycle(t->blob, t->hdr);
+	t->device = c->device;
+	hipSetDevice(c->device);
+	if (hipMalloc(&t->dblob, t->hdr.blob_bytes) != hipSuccess) {
+		delete t;
+		return -ENOMEM;
+	}
+	if (hipMemcpyAsync(t->dblob, t->blob.data(), t->hdr.blob_bytes, hipMemcpyHostToDevice,
+			   c->stream) != hipSuccess ||
+	    hipStreamSynchronize(c->stream) != hipSuccess) {
+		hipFree(t->dblob);
+		delete t;
+		return -EIO;
+	}
+	*out = t;
+	return 0;
+}
+
+void odpg_table_destroy(odpg_table_t *t)
+{
+	if (!t)
+		return;
+	hipSetDevice(t->device);
+	hipFree(t->dblob);
+	delete t;
+}
+
+uint32_t odpg_table_num_cos(const odpg_table_t *t)
+{
+	return t ? t->hdr.num_cos : 0;
+}
+
+int odpg_table_has_cycle(const odpg_table_t *t)
+{
+	return t ? t->cycle : 0;
+}
+
+static int ensure_ws(odpg_ctx_t *c, size_t bytes)
+{
+	if (c->ws_bytes >= bytes)
+		return 0;
+	if (c->ws) {
+		HIPCHK(hipStreamSynchronize(c->stream));
+		HIPCHK(hipFree(c->ws));
+		c->ws = nullptr;
+		c->ws_bytes = 0;
+	}
+	HIPCHK(hipMalloc(&c->ws, bytes));
+	c->ws_bytes = bytes;
+	return 0;
+}
+
+static int validate_batch(const odpg_batch_t *b)
+{
+	if (!b)
+		return -EINVAL;
+	if (b->num && !b->frames)
+		return -EINVAL;
+	if (!b->desc && (b->stride == 0 || (b->stride & 15u)))
+		return -EINVAL;
+	if (b->layer > 4)
+		return -EINVAL;
+	return 0;
+}
+
+static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
+		       const odpg_batch_t *b, const odpg_result_t *r, void *ws)
+{
+	odpg_launch_args a;
+	const dtable_hdr_t &h = t->hdr;
+	uint32_t grid = odpg_launch_grid(b->num);
+	bool cos_stats = r->stats && (h.flags & TBL_ANY_STATS);
+
+	memset(&a, 0, sizeof(a));
+	a.frames = b->frames;
+	a.desc = b->desc;
+	a.stride = b->stride;
+	a.num = b->num;
+	a.opt = b->pktin_opt;
+	a.layer = b->layer;
+	a.classify = b->classify;
+	a.terms = (const dterm_t *)((const uint8_t *)t->dblob + h.term_off);
+	a.pmrs = (const dpmr_t *)((const uint8_t *)t->dblob + h.pmr_off);
+	a.coses = (const dcos_t *)((const uint8_t *)t->dblob + h.cos_off);
+	a.num_cos = h.num_cos;
+	a.default_cos = h.default_cos;
+	a.error_cos = h.error_cos;
+	a.tbl_flags = h.flags;
+	a.out = r->out;
+	a.mark = r->mark;
+	a.meta = r->meta;
+	a.stats = r->stats;
+	if (r->stats) {
+		a.pk_partial = (uint64_t *)ws;
+		if (cos_stats)
+			a.cos_partial = (uint32_t *)((uint8_t *)ws + (size_t)grid * 32u);
+	}
+	(void)c;
+	return odpg_launch_classify(&a, s);
+}
+
+static size_t ws_need(const odpg_table_t *t, uint32_t num, bool stats)
+{
+	if (!stats)
+		return 0;
+	uint32_t grid = odpg_launch_grid(num);
+	size_t need = (size_t)grid * 32u;
+
+	if (t->hdr.flags & TBL_ANY_STATS)
+		need += (size_t)grid * t->hdr.num_cos * 4u;
+	return need;
+}
+
+int odpg_classify(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t *b,
+		  const odpg_result_t *r)
+{
+	int rc;
+
+	if (!c || !t || !r || (b && b->num && !r->out))
+		return -EINVAL;
+	if ((rc = validate_batch(b)))
+		return rc;
+	if (t->device != c->device)
+		return -EXDEV;
+	if (b->num == 0)
+		return 0;
+	std::lock_guard<std::mutex> g(c->lock);
+
+	hipSetDevice(c->device);
+	if ((rc = ensure_ws(c, ws_need(t, b->num, r->stats != nullptr))))
+		return rc;
+	return classify_on(c, c->stream, t, b, r, c->ws);
+}
+
+/* Host-buffer path: frames/desc/results in host memory (pinned is fastest).
+ * Two device buffer sets alternate between the copy stream (H2D) and the
+ * compute stream (kernel + D2H). */
+int odpg_classify_host(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t *b,
+		       const odpg_result_t *r, uint32_t chunk)
+{
+	int rc;
+
+	if (!c || !t || !r || (b && b->num && !r->out))
+		return -EINVAL;
+	if ((rc = validate_batch(b)))
+		return rc;
+	if (b->num == 0)
+		return 0;
+	if (chunk == 0)
+		chunk = 1u << 18;
+	if (chunk > b->num)
+		chunk = b->num;
+	std::lock_guard<std::mutex> g(c->lock);
+
+	hipSetDevice(c->device);
+
+	/* size the frame staging buffers */
+	size_t max_span = 0;
+	uint32_t nchunks = (b->num + chunk - 1) / chunk;
+	std::vector<size_t> span_lo(nchunks), span_hi(nchunks);
+
+	for (uint32_t k = 0; k < nchunks; k++) {
+		uint32_t first = k * chunk, n = b->num - first < chunk ? b->num - first : chunk;
+		size_t lo, hi;
+
+		if (b->desc) {
+			lo = (size_t)-1;
+			hi = 0;
+			for (uint32_t j = first; j < first + n; j++) {
+				size_t o = b->desc[j].offset, e = o + b->desc[j].len;
+
+				if (o & 15u)
+					return -EINVAL;
+				lo = o < lo ? o : lo;
+				e = (e + 15u) & ~(size_t)15u;
+				hi = e > hi ? e : hi;
+			}
+		} else {
+			lo = (size_t)first * b->stride;
+			hi = lo + (size_t)n * b->stride;
+		}
+		span_lo[k] = lo;
+		span_hi[k] = hi;
+		if (hi - lo > max_span)
+			max_span = hi - lo;
+	}
+
+	struct Buf {
+		uint8_t *frames;
+		odpg_desc_t *desc;
+		odpg_out_t *out;
+		uint16_t *mark;
+		odpg_meta_t *meta;
+		hipEvent_t h2d_done, compute_done;
+		std::vector<odpg_desc_t> hdesc;
+	} buf[2];
+	uint64_t *dstats = nullptr;
+	uint32_t nstats = ODPG_STATS_WORDS(t->hdr.num_cos);
+	int err = 0;
+
+	memset(buf, 0, sizeof(buf[0]) * 0);
+	for (int k = 0; k < 2; k++) {
+		buf[k].frames = nullptr;
+		buf[k].desc = nullptr;
+		buf[k].out = nullptr;
+		buf[k].mark = nullptr;
+		buf[k].meta = nullptr;
+		if (hipMalloc(&buf[k].frames, max_span + 16) != hipSuccess ||
+		    hipMalloc(&buf[k].out, (size_t)chunk * sizeof(odpg_out_t)) != hipSuccess)
+			err = -ENOMEM;
+		if (b->desc && hipMalloc(&buf[k].desc, (size_t)chunk * sizeof(odpg_desc_t)) != hipSuccess)
+			err = -ENOMEM;
+		if (r->mark && hipMalloc(&buf[k].mark, (size_t)chunk * 2u) != hipSuccess)
+			err = -ENOMEM;
+		if (r->meta && hipMalloc(&buf[k].meta, (size_t)chunk * sizeof(odpg_meta_t)) != hipSuccess)
+			err = -ENOMEM;
+		hipEventCreateWithFlags(&buf[k].h2d_done, hipEventDisableTiming);
+		hipEventCreateWithFlags(&buf[k].compute_done, hipEventDisableTiming);
+		if (b->desc)
+			buf[k].hdesc.resize(chunk);
+	}
+	if (!err && r->stats) {
+		if (hipMalloc(&dstats, nstats * 8u) != hipSuccess ||
+		    hipMemsetAsync(dstats, 0, nstats * 8u, c->stream) != hipSuccess)
+			err = -ENOMEM;
+	}
+	if (!err)
+		err = ensure_ws(c, ws_need(t, chunk, r->stats != nullptr));
+
+	for (uint32_t k = 0; k < nchunks && !err; k++) {
+		Buf &B = buf[k & 1];
+		uint32_t first = k * chunk, n = b->num - first < chunk ? b->num - first : chunk;
+		size_t lo = span_lo[k], bytes = span_hi[k] - span_lo[k];
+
+		/* buffer reuse: wait until the chunk that used it has finished */
+		if (k >= 2 && hipStreamWaitEvent(c->copy_stream, B.compute_done, 0) != hipSuccess) {
+			err = -EIO;
+			break;
+		}
+		if (hipMemcpyAsync(B.frames, b->frames + lo, bytes, hipMemcpyHostToDevice,
+				   c->copy_stream) != hipSuccess) {
+			err = -EIO;
+			break;
+		}
+		if (b->desc) {
+			if (k >= 2)
+				hipEventSynchronize(B.compute_done);
+			for (uint32_t j = 0; j < n; j++) {
+				B.hdesc[j].offset = (uint32_t)(b->desc[first + j].offset - lo);
+				B.hdesc[j].len = b->desc[first + j].len;
+			}
+			if (hipMemcpyAsync(B.desc, B.hdesc.data(), (size_t)n * sizeof(odpg_desc_t),
+					   hipMemcpyHostToDevice, c->copy_stream) != hipSuccess) {
+				err = -EIO;
+				break;
+			}
+		}
+		hipEventRecord(B.h2d_done, c->copy_stream);
+		hipStreamWaitEvent(c->stream, B.h2d_done, 0);
+
+		odpg_batch_t cb = *b;
+		odpg_result_t cr;
+
+		cb.frames = B.frames;
+		cb.desc = b->desc ? B.desc : nullptr;
+		cb.num = n;
+		cr.out = B.out;
+		cr.mark = r->mark ? B.mark : nullptr;
+		cr.meta = r->meta ? B.meta : nullptr;
+		cr.stats = dstats;
+		if (classify_on(c, c->stream, t, &cb, &cr, c->ws)) {
+			err = -EIO;
+			break;
+		}
+		hipMemcpyAsync(r->out + first, B.out, (size_t)n * sizeof(odpg_out_t),
+			       hipMemcpyDeviceToHost, c->stream);
+		if (r->mark)
+			hipMemcpyAsync(r->mark + first, B.mark, (size_t)n * 2u, hipMemcpyDeviceToHost,
+				       c->stream);
+		if (r->meta)
+			hipMemcpyAsync(r->meta + first, B.meta, (size_t)n * sizeof(odpg_meta_t),
+				       hipMemcpyDeviceToHost, c->stream);
+		hipEventRecord(B.compute_done, c->stream);
+	}
+	if (!err && r->stats) {
+		std::vector<uint64_t> hs(nstats);
+
+		if (hipMemcpyAsync(hs.data(), dstats, nstats * 8u, hipMemcpyDeviceToHost,
+				   c->stream) != hipSuccess ||
+		    hipStreamSynchronize(c->stream) != hipSuccess)
+			err = -EIO;
+		else
+			for (uint32_t k = 0; k < nstats; k++)
+				r->stats[k] += hs[k];
+	}
+	if (hipStreamSynchronize(c->stream) != hipSuccess ||
+	    hipStreamSynchronize(c->copy_stream) != hipSuccess)
+		err = err ? err : -EIO;
+	for (int k = 0; k < 2; k++) {
+		hipFree(buf[k].frames);
+		hipFree(buf[k].desc);
+		hipFree(buf[k].out);
+		hipFree(buf[k].mark);
+		hipFree(buf[k].meta);
+		hipEventDestroy(buf[k].h2d_done);
+		hipEventDestroy(buf[k].compute_done);
+	}
+	if (dstats)
+		hipFree(dstats);
+	return err;
+}
+
+int odpg_dev_alloc(odpg_ctx_t *c, size_t bytes, void **ptr)
+{
+	if (!c || !ptr)
+		return -EINVAL;
+	hipSetDevice(c->device);
+	if (hipMalloc(ptr, bytes ? bytes : 16) != hipSuccess)
+		return -ENOMEM;
+	return 0;
+}
+
+int odpg_dev_free(odpg_ctx_t *c, void *ptr)
+{
+	if (!c)
+		return -EINVAL;
+	hipSetDevice(c->device);
+	HIPCHK(hipFree(ptr));
+	return 0;
+}
+
+int odpg_host_alloc_pinned(size_t bytes, void **ptr)
+{
+	if (!ptr)
+		return -EINVAL;
+	if (hipHostMalloc(ptr, bytes ? bytes : 16, hipHostMallocDefault) != hipSuccess)
+		return -ENOMEM;
+	return 0;
+}
+
+int odpg_host_free_pinned(void *ptr)
+{
+	HIPCHK(hipHostFree(ptr));
+	return 0;
+}
+
+int odpg_memcpy_h2d(odpg_ctx_t *c, void *dst, const void *src, size_t bytes)
+{
+	if (!c)
+		return -EINVAL;
+	HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int odpg_memcpy_d2h(odpg_ctx_t *c, void *dst, const void *src, size_t bytes)
+{
+	if (!c)
+		return -EINVAL;
+	HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int odpg_memset_dev(odpg_ctx_t *c, void *dst, int value, size_t bytes)
+{
+	if (!c)
+		return -EINVAL;
+	HIPCHK(hipMemsetAsync(dst, value, bytes, c->stream));
+	return 0;
+}
+
+int odpg_event_record(odpg_ctx_t *c, int slot)
+{
+	if (!c || slot < 0 || slot >= NUM_EVENTS)
+		return -EINVAL;
+	HIPCHK(hipEventRecord(c->ev[slot], c->stream));
+	return 0;
+}
+
+int odpg_event_elapsed_ms(odpg_ctx_t *c, int a, int b, float *ms)
+{
+	if (!c || !ms || a < 0 || b < 0 || a >= NUM_EVENTS || b >= NUM_EVENTS)
+		return -EINVAL;
+	HIPCHK(hipEventSynchronize(c->ev[b]));
+	HIPCHK(hipEventElapsedTime(ms, c->ev[a], c->ev[b]));
+	return 0;
+}
+
+} /* extern "C" */

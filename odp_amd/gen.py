@@ -1,0 +1,269 @@
+"""Synthetic traffic and rule sets for the BASELINE.json configurations.
+
+Frames are built vectorised in numpy with valid IPv4 header and UDP/TCP
+checksums (RFC 1071), laid out either at a fixed 64-byte stride (C1/C2/C4)
+or in a 64-byte-aligned buffer with (offset, len) descriptors (IMIX, C3).
+The shapes follow SURVEY.md §8(d).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ETH_IPV4 = 0x0800
+ETH_IPV6 = 0x86DD
+PROTO_TCP = 6
+PROTO_UDP = 17
+
+DESC_DT = np.dtype([("offset", "<u4"), ("len", "<u4")])
+
+
+def xorshift64(seed, n):
+    """Deterministic u64 stream (xorshift64), vectorised over blocks."""
+    out = np.empty(n, np.uint64)
+    x = np.uint64(seed) if seed else np.uint64(0x9E3779B97F4A7C15)
+    with np.errstate(over="ignore"):
+        # generate a short serial seed table, then use a counter-based mix for the rest
+        for i in range(min(n, 64)):
+            x ^= (x << np.uint64(13)) & np.uint64(0xFFFFFFFFFFFFFFFF)
+            x ^= x >> np.uint64(7)
+            x ^= (x << np.uint64(17)) & np.uint64(0xFFFFFFFFFFFFFFFF)
+            out[i] = x
+        if n > 64:
+            idx = np.arange(64, n, dtype=np.uint64)
+            z = idx * np.uint64(0x9E3779B97F4A7C15) + out[idx % np.uint64(64)]
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            out[64:] = z ^ (z >> np.uint64(31))
+    return out
+
+
+def _be16(a, off, v):
+    v = np.asarray(v, dtype=np.uint32)
+    a[:, off] = (v >> 8) & 0xFF
+    a[:, off + 1] = v & 0xFF
+
+
+def _be32(a, off, v):
+    v = np.asarray(v, dtype=np.uint64)
+    for k in range(4):
+        a[:, off + k] = (v >> np.uint64(24 - 8 * k)) & np.uint64(0xFF)
+
+
+def ones_sum(a, lo, hi, extra=None):
+    """One's-complement 16-bit sum (unfolded, int64) of bytes [lo, hi) per row."""
+    seg = a[:, lo:hi].astype(np.int64)
+    if seg.shape[1] % 2:
+        seg = np.concatenate([seg, np.zeros((seg.shape[0], 1), np.int64)], axis=1)
+    s = (seg[:, 0::2] << 8).sum(axis=1) + seg[:, 1::2].sum(axis=1)
+    if extra is not None:
+        s = s + extra
+    return s
+
+
+def fold(s):
+    s = np.asarray(s, dtype=np.int64)
+    while np.any(s >> 16):
+        s = (s & 0xFFFF) + (s >> 16)
+    return s
+
+
+def csum(s):
+    return (~fold(s)) & 0xFFFF
+
+
+def ipv4_frames(n, length, src, dst, proto, sport, dport, *, smac=None, dmac=None, ttl=64,
+                tos=0, ident=None, payload_seed=1, vlan=None, l4_csum=True, ip_csum=True):
+    """Eth/[VLAN]/IPv4/UDP|TCP frames of `length` bytes each, shape (n, length)."""
+    length = int(length)
+    l2 = 14 + (4 if vlan is not None else 0)
+    l4h = 8 if proto == PROTO_UDP else 20
+    assert length >= l2 + 20 + l4h
+    a = np.zeros((n, length), np.uint8)
+    dm = np.array(dmac if dmac is not None else [0x02, 0x00, 0x00, 0x00, 0x00, 0x01], np.uint8)
+    sm = np.array(smac if smac is not None else [0x02, 0x00, 0x00, 0x00, 0x00, 0x02], np.uint8)
+    a[:, 0:6] = dm
+    a[:, 6:12] = sm
+    if vlan is not None:
+        _be16(a, 12, 0x8100)
+        _be16(a, 14, vlan)
+        _be16(a, 16, ETH_IPV4)
+    else:
+        _be16(a, 12, ETH_IPV4)
+    o = l2
+    tot_len = length - l2
+    a[:, o] = 0x45
+    a[:, o + 1] = tos
+    _be16(a, o + 2, tot_len)
+    _be16(a, o + 4, np.arange(n) & 0xFFFF if ident is None else ident)
+    a[:, o + 8] = ttl
+    a[:, o + 9] = proto
+    _be32(a, o + 12, src)
+    _be32(a, o + 16, dst)
+    l4 = o + 20
+    _be16(a, l4, sport)
+    _be16(a, l4 + 2, dport)
+    # deterministic payload
+    pl = length - (l4 + l4h)
+    if pl > 0:
+        r = xorshift64(payload_seed, n * ((pl + 7) // 8)).view(np.uint8)
+        a[:, l4 + l4h:] = r[: n * pl].reshape(n, pl)
+    if proto == PROTO_UDP:
+        _be16(a, l4 + 4, length - l4)
+    else:
+        _be32(a, l4 + 4, np.arange(n, dtype=np.uint64) * np.uint64(7919))
+        a[:, l4 + 12] = 0x50
+        a[:, l4 + 13] = 0x18
+        _be16(a, l4 + 14, 8192)
+    if ip_csum:
+        _be16(a, o + 10, csum(ones_sum(a, o, o + 20)))
+    if l4_csum:
+        pseudo = ones_sum(a, o + 12, o + 20) + proto + (length - l4)
+        c = csum(ones_sum(a, l4, length, pseudo))
+        if proto == PROTO_UDP:
+            c = np.where(c == 0, 0xFFFF, c)
+            _be16(a, l4 + 6, c)
+        else:
+            _be16(a, l4 + 16, c)
+    return a
+
+
+def ipv6_frames(n, length, src_lo, dst_lo, proto, sport, dport, *, payload_seed=2, l4_csum=True):
+    """Eth/IPv6/UDP|TCP frames; addresses 2001:db8::<src_lo> / 2001:db8:1::<dst_lo>."""
+    length = int(length)
+    l4h = 8 if proto == PROTO_UDP else 20
+    assert length >= 14 + 40 + l4h
+    a = np.zeros((n, length), np.uint8)
+    a[:, 0:6] = [0x02, 0, 0, 0, 0, 1]
+    a[:, 6:12] = [0x02, 0, 0, 0, 0, 2]
+    _be16(a, 12, ETH_IPV6)
+    o = 14
+    a[:, o] = 0x60
+    _be16(a, o + 4, length - o - 40)
+    a[:, o + 6] = proto
+    a[:, o + 7] = 64
+    a[:, o + 8:o + 12] = [0x20, 0x01, 0x0d, 0xb8]
+    _be32(a, o + 20, src_lo)
+    a[:, o + 24:o + 28] = [0x20, 0x01, 0x0d, 0xb8]
+    a[:, o + 28] = 0
+    a[:, o + 29] = 1
+    _be32(a, o + 36, dst_lo)
+    l4 = o + 40
+    _be16(a, l4, sport)
+    _be16(a, l4 + 2, dport)
+    pl = length - (l4 + l4h)
+    if pl > 0:
+        r = xorshift64(payload_seed, n * ((pl + 7) // 8)).view(np.uint8)
+        a[:, l4 + l4h:] = r[: n * pl].reshape(n, pl)
+    if proto == PROTO_UDP:
+        _be16(a, l4 + 4, length - l4)
+    else:
+        a[:, l4 + 12] = 0x50
+        a[:, l4 + 13] = 0x10
+    if l4_csum:
+        pseudo = ones_sum(a, o + 8, o + 40) + proto + (length - l4)
+        c = csum(ones_sum(a, l4, length, pseudo))
+        if proto == PROTO_UDP:
+            c = np.where(c == 0, 0xFFFF, c)
+            _be16(a, l4 + 6, c)
+        else:
+            _be16(a, l4 + 16, c)
+    return a
+
+
+def ip4(s):
+    p = [int(x) for x in s.split(".")]
+    return (p[0] << 24) | (p[1] << 16) | (p[2] << 8) | p[3]
+
+
+def be_bytes(v, n):
+    return int(v).to_bytes(n, "big")
+
+
+# ---- BASELINE.json configurations -----------------------------------------
+C_SEED = 0x0DDC0FFEE
+
+
+def c1_frames(n, seed=C_SEED):
+    """C1: 64 B IPv4/UDP, 50 % src 10.10.10.x (matches the one PMR), 50 % 10.1.x.x."""
+    r = xorshift64(seed, n)
+    half = (r & np.uint64(1)).astype(bool)
+    lo = ((r >> np.uint64(8)) & np.uint64(0xFFFF)).astype(np.uint64)
+    src = np.where(half, np.uint64(ip4("10.10.10.0")) + (lo & np.uint64(0xFF)),
+                   np.uint64(ip4("10.1.0.0")) + lo)
+    dst = np.full(n, ip4("10.0.0.100"), np.uint64)
+    return ipv4_frames(n, 64, src, dst, PROTO_UDP, 1024, 2048).reshape(-1)
+
+
+def c2_frames(n, seed=C_SEED):
+    """C2: 64 B IPv4/UDP, src 10.0.R16, dst 10.1.R16, sport R16, dport R & 63."""
+    r = xorshift64(seed, n)
+    m16 = np.uint64(0xFFFF)
+    src = np.uint64(ip4("10.0.0.0")) + (r & m16)
+    dst = np.uint64(ip4("10.1.0.0")) + ((r >> np.uint64(16)) & m16)
+    sport = (r >> np.uint64(32)) & m16
+    dport = (r >> np.uint64(48)) & np.uint64(63)
+    return ipv4_frames(n, 64, src, dst, PROTO_UDP, sport, dport).reshape(-1)
+
+
+def c2_dport(a, j):
+    return (a + 8 * j) & 63
+
+
+def build_c1_rules(cls, pktio):
+    """example/classifier run script rule: ODP_PMR_SIP_ADDR:10.10.10.0:0xFFFFFF00:queue1
+    (example/classifier/odp_classifier_run.sh:17-19)."""
+    default = cls.cos_create("DefaultCos", queue=cls.queue(0))
+    q1 = cls.cos_create("CoSqueue1", queue=cls.queue(1))
+    assert default and q1
+    assert cls.default_cos_set(pktio, default) == 0
+    pmr = cls.pmr_create([cls.Term(cls.PMR_SIP_ADDR, be_bytes(ip4("10.10.10.0"), 4),
+                                   be_bytes(0xFFFFFF00, 4))], default, q1)
+    assert pmr
+    return {"default": default, "queue1": q1, "pmr": pmr}
+
+
+def build_c2_rules(cls, pktio, stats=False):
+    """C2: 64 PMRs in the reference limits (64 CoS, <= 8 PMR per CoS):
+    default -> 8 x SIP_ADDR 10.0.(a<<5).0/19 -> L1[a] -> 7 x UDP_DPORT -> 55 leaves."""
+    default = cls.cos_create("c2_default", queue=cls.queue(0), stats_enable=stats)
+    l1 = [cls.cos_create(f"c2_l1_{a}", queue=cls.queue(1 + a), stats_enable=stats)
+          for a in range(8)]
+    leaves = [cls.cos_create(f"c2_leaf_{k}", queue=cls.queue(9 + k), stats_enable=stats)
+              for k in range(55)]
+    assert default and all(l1) and all(leaves)
+    assert cls.default_cos_set(pktio, default) == 0
+    pmrs = []
+    for a in range(8):
+        pmrs.append(cls.pmr_create([cls.Term(cls.PMR_SIP_ADDR,
+                                             be_bytes(ip4("10.0.0.0") | (a << 13), 4),
+                                             be_bytes(0xFFFFE000, 4))], default, l1[a]))
+    for a in range(8):
+        for j in range(7):
+            leaf = leaves[(a * 7 + j) % 55]
+            pmrs.append(cls.pmr_create([cls.Term(cls.PMR_UDP_DPORT, be_bytes(c2_dport(a, j), 2),
+                                                 b"\xff\xff")], l1[a], leaf))
+    assert all(pmrs) and len(pmrs) == 64
+    return {"default": default, "l1": l1, "leaves": leaves, "pmrs": pmrs}
+
+
+def build_c4_rules(cls, pktio, n_l1=32, per_l1=31):
+    """C4 (raised limits, cls.set_limits before any create): default ->
+    32 x SIP_ADDR /21 -> L1[a] -> 31 x UDP_DPORT -> 992 leaves = 1024 PMRs."""
+    default = cls.cos_create("c4_default", queue=cls.queue(0))
+    l1 = [cls.cos_create(f"c4_l1_{a}", queue=cls.queue(1 + a)) for a in range(n_l1)]
+    pmrs = []
+    for a in range(n_l1):
+        pmrs.append(cls.pmr_create([cls.Term(cls.PMR_SIP_ADDR,
+                                             be_bytes(ip4("10.0.0.0") | (a << 11), 4),
+                                             be_bytes(0xFFFFF800, 4))], default, l1[a]))
+    k = 0
+    for a in range(n_l1):
+        for j in range(per_l1):
+            leaf = cls.cos_create(f"c4_leaf_{k}", queue=cls.queue(100 + k))
+            k += 1
+            pmrs.append(cls.pmr_create([cls.Term(cls.PMR_UDP_DPORT,
+                                                 be_bytes((a + 2 * j) & 63, 2), b"\xff\xff")],
+                                       l1[a], leaf))
+    assert default and all(l1) and all(pmrs)
+    assert cls.default_cos_set(pktio, default) == 0
+    return {"default": default, "l1": l1, "pmrs": pmrs}

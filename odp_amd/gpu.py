@@ -1,0 +1,170 @@
+"""Thin Python driver for the odpg.h C-ABI (device buffers, tables, launches).
+
+All compute happens in ``libodpg.so``'s gfx950 kernels; this module moves
+numpy arrays in and out of HBM through the library's own helpers.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+lib = L.lib
+
+
+class DeviceBuffer:
+    def __init__(self, ctx, nbytes):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        L.check(lib.odpg_dev_alloc(ctx.h, max(self.nbytes, 16), C.byref(p)), "odpg_dev_alloc")
+        self.ptr = p.value
+
+    def upload(self, arr):
+        a = np.ascontiguousarray(arr)
+        assert a.nbytes <= self.nbytes
+        L.check(lib.odpg_memcpy_h2d(self.ctx.h, self.ptr, a.ctypes.data, a.nbytes), "h2d")
+
+    def download(self, dtype, count):
+        out = np.empty(count, dtype=dtype)
+        if out.nbytes:
+            L.check(lib.odpg_memcpy_d2h(self.ctx.h, out.ctypes.data, self.ptr, out.nbytes),
+                    "d2h")
+        return out
+
+    def zero(self):
+        L.check(lib.odpg_memset_dev(self.ctx.h, self.ptr, 0, self.nbytes), "memset")
+
+    def free(self):
+        if self.ptr:
+            lib.odpg_dev_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Table:
+    def __init__(self, ctx, rules):
+        t = C.c_void_p()
+        L.check(lib.odpg_table_create(ctx.h, C.byref(rules), C.byref(t)), "odpg_table_create")
+        self.h = t.value
+        self.num_cos = lib.odpg_table_num_cos(self.h)
+        self.has_cycle = bool(lib.odpg_table_has_cycle(self.h))
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib.odpg_table_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class Context:
+    def __init__(self, device=0, stream=None):
+        n = lib.odpg_device_count()
+        if n <= 0:
+            raise RuntimeError("no HIP device visible (odpg_device_count() == 0)")
+        h = C.c_void_p()
+        L.check(lib.odpg_ctx_create(device, stream, C.byref(h)), "odpg_ctx_create")
+        self.h = h.value
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib.odpg_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        L.check(lib.odpg_ctx_sync(self.h), "odpg_ctx_sync")
+
+    def buffer(self, nbytes):
+        return DeviceBuffer(self, nbytes)
+
+    def table(self, rules):
+        return Table(self, rules)
+
+    def classify_dev(self, table, frames_buf, num, stride=0, desc_buf=None, opt=0,
+                     layer=L.LAYER_ALL, classify=True, out_buf=None, mark_buf=None,
+                     meta_buf=None, stats_buf=None):
+        b = L.odpg_batch_t(frames_buf.ptr, desc_buf.ptr if desc_buf else None, stride, num,
+                           opt, layer, int(bool(classify)))
+        r = L.odpg_result_t(out_buf.ptr if out_buf else None,
+                            mark_buf.ptr if mark_buf else None,
+                            meta_buf.ptr if meta_buf else None,
+                            stats_buf.ptr if stats_buf else None)
+        L.check(lib.odpg_classify(self.h, table.h, C.byref(b), C.byref(r)), "odpg_classify")
+
+    def classify(self, table, frames, num, stride=0, desc=None, opt=0, layer=L.LAYER_ALL,
+                 classify=True, want_mark=True, want_meta=True, want_stats=True):
+        """Upload host arrays, classify on the GPU, download results."""
+        meta_dt, desc_dt = L.np_dtypes()
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        fb = self.buffer(frames.nbytes + 64)
+        fb.upload(frames)
+        db = None
+        if desc is not None:
+            desc = np.ascontiguousarray(desc, dtype=desc_dt)
+            db = self.buffer(desc.nbytes)
+            db.upload(desc)
+        ob = self.buffer(4 * num)
+        mb = self.buffer(2 * num) if want_mark else None
+        eb = self.buffer(24 * num) if want_meta else None
+        nst = 4 + table.num_cos
+        sb = self.buffer(8 * nst) if want_stats else None
+        if sb:
+            sb.zero()
+        self.classify_dev(table, fb, num, stride, db, opt, layer, classify, ob, mb, eb, sb)
+        self.sync()
+        res = {"out": ob.download(np.uint32, num)}
+        if mb:
+            res["mark"] = mb.download(np.uint16, num)
+        if eb:
+            res["meta"] = eb.download(meta_dt, num)
+        if sb:
+            res["stats"] = sb.download(np.uint64, nst)
+        for b in (fb, db, ob, mb, eb, sb):
+            if b:
+                b.free()
+        return res
+
+    def classify_host(self, table, frames, num, stride=0, desc=None, opt=0,
+                      layer=L.LAYER_ALL, classify=True, chunk=0, want_mark=False,
+                      want_meta=False, want_stats=True):
+        meta_dt, desc_dt = L.np_dtypes()
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        dptr = None
+        if desc is not None:
+            desc = np.ascontiguousarray(desc, dtype=desc_dt)
+            dptr = desc.ctypes.data
+        out = np.zeros(num, np.uint32)
+        mark = np.zeros(num, np.uint16) if want_mark else None
+        meta = np.zeros(num, meta_dt) if want_meta else None
+        stats = np.zeros(4 + table.num_cos, np.uint64) if want_stats else None
+        b = L.odpg_batch_t(frames.ctypes.data, dptr, stride, num, opt, layer,
+                           int(bool(classify)))
+        r = L.odpg_result_t(out.ctypes.data, mark.ctypes.data if mark is not None else None,
+                            meta.ctypes.data if meta is not None else None,
+                            stats.ctypes.data if stats is not None else None)
+        L.check(lib.odpg_classify_host(self.h, table.h, C.byref(b), C.byref(r), chunk),
+                "odpg_classify_host")
+        res = {"out": out}
+        if mark is not None:
+            res["mark"] = mark
+        if meta is not None:
+            res["meta"] = meta
+        if stats is not None:
+            res["stats"] = stats
+        return res

@@ -1,0 +1,118 @@
+"""Rule sets and frame corpora shared by the parity tests.
+
+`all_terms_rules` builds a CoS graph that exercises every PMR term the
+reference can create (odp_classification.c:661-720), multi-term PMRs, marks,
+a DROP CoS, an error CoS and a second rule level, with values taken from the
+golden frames so that rules do match part of the corpus.
+"""
+import numpy as np
+
+from helpers import GOLDEN, golden_frames
+from odp_amd import gen
+
+
+def _b(h):
+    return bytes.fromhex(h)
+
+
+def all_terms_rules(cls, pktio, stats=True):
+    T = cls.Term
+    q = cls.queue
+    default = cls.cos_create("default", queue=q(0), stats_enable=stats)
+    error = cls.cos_create("error", queue=q(1), stats_enable=stats)
+    drop = cls.cos_create("drop", action=cls.COS_ACTION_DROP, stats_enable=stats)
+    mk = lambda name, n: cls.cos_create(name, queue=q(n), stats_enable=stats)  # noqa: E731
+    c = {name: mk(name, 10 + i) for i, name in enumerate([
+        "vlan", "ipv6", "tcp", "udp", "ipsec", "custom", "l2", "len", "dscp", "mcast",
+        "sctp_l3", "vlan_leaf", "udp_leaf", "tcp_leaf", "v6_leaf"])}
+    assert cls.default_cos_set(pktio, default) == 0
+    assert cls.error_cos_set(pktio, error) == 0
+    P = []
+
+    def pmr(terms, src, dst, mark=None):
+        h = cls.pmr_create(terms, src, dst, mark=mark)
+        assert h, (terms, src, dst)
+        P.append(h)
+        return h
+
+    # level 1 (default CoS): <= 8 rules, first match wins
+    pmr([T(cls.PMR_ETHTYPE_0, b"\x81\x00", b"\xff\xff")], default, c["vlan"], mark=11)
+    pmr([T(cls.PMR_ETHTYPE_0, b"\x86\xdd", b"\xff\xff"),
+         T(cls.PMR_IPPROTO, b"\x11", b"\xff")], default, c["ipv6"], mark=12)
+    pmr([T(cls.PMR_IPPROTO, b"\x06", b"\xff")], default, c["tcp"])
+    pmr([T(cls.PMR_IPSEC_SPI, b"\x00\x00\x00\x7b", b"\xff\xff\xff\xff")], default, c["ipsec"], mark=14)
+    pmr([T(cls.PMR_DMAC, b"\x01\x00\x5e\x00\x00\x00", b"\xff\xff\xff\x00\x00\x00")],
+        default, c["mcast"], mark=15)
+    pmr([T(cls.PMR_CUSTOM_FRAME, b"\x88\xb5", b"\xff\xff", offset=12)], default, c["custom"])
+    pmr([T(cls.PMR_IP_DSCP, b"\x00", b"\x3f"), T(cls.PMR_IPPROTO, b"\x11", b"\xff"),
+         T(cls.PMR_LEN, (1500).to_bytes(4, "little"), b"\xff\xff\xff\xff")], default, c["len"])
+    pmr([T(cls.PMR_IPPROTO, b"\x11", b"\xff")], default, c["udp"], mark=0)
+
+    # level 2
+    pmr([T(cls.PMR_VLAN_ID_0, b"\x00\x0a", b"\x0f\xff")], c["vlan"], c["vlan_leaf"], mark=21)
+    pmr([T(cls.PMR_VLAN_ID_X, b"\x00\x14", b"\xff\xff")], c["vlan"], c["vlan_leaf"], mark=22)
+    pmr([T(cls.PMR_ETHTYPE_X, b"\x08\x00", b"\xff\xff"),
+         T(cls.PMR_VLAN_PCP_0, b"\x00", b"\x07")], c["vlan"], drop)
+    pmr([T(cls.PMR_UDP_DPORT, b"\x00\x3f", b"\xff\xff")], c["udp"], c["udp_leaf"], mark=31)
+    pmr([T(cls.PMR_UDP_SPORT, b"\x00\x00", b"\xff\x00")], c["udp"], c["udp_leaf"], mark=32)
+    pmr([T(cls.PMR_SIP_ADDR, b"\xc0\xa8\x00\x00", b"\xff\xff\x00\x00"),
+         T(cls.PMR_DIP_ADDR, b"\xc0\xa8\x00\x00", b"\xff\xff\x00\x00")], c["udp"], c["l2"])
+    pmr([T(cls.PMR_CUSTOM_L3, b"\x40", b"\xff", offset=8)], c["udp"], c["dscp"], mark=33)
+    pmr([T(cls.PMR_TCP_DPORT, b"\x00\x00", b"\x00\x00"),
+         T(cls.PMR_TCP_SPORT, b"\x04\x00", b"\xff\x00")], c["tcp"], c["tcp_leaf"], mark=41)
+    pmr([T(cls.PMR_LD_VNI, b"\x00\x00\x00\x01", b"\xff\xff\xff\xff")], c["tcp"], drop)
+    pmr([T(cls.PMR_SIP6_ADDR, bytes(16), bytes(16))], c["ipv6"], c["v6_leaf"], mark=51)
+    pmr([T(cls.PMR_DIP6_ADDR, b"\xff" + bytes(15), b"\xff" + bytes(15))], c["ipv6"], c["v6_leaf"])
+    pmr([T(cls.PMR_IP_DSCP, b"\x2e", b"\x3f")], c["ipv6"], c["dscp"])
+    pmr([T(cls.PMR_IPPROTO, b"\x84", b"\xff")], c["mcast"], c["sctp_l3"], mark=61)
+    return {"default": default, "error": error, "drop": drop, "cos": c, "pmrs": P}
+
+
+def mutate_corpus(n, seed=7, max_len=220):
+    """Golden frames + generated VLAN / QinQ / SNAP / IPv6-ext / fragment frames,
+    then random byte flips and truncations (edge cases the reference tests:
+    short, ragged, malformed)."""
+    rng = np.random.default_rng(seed)
+    _, base = golden_frames()
+    extra = []
+    v4 = gen.ipv4_frames(4, 80, np.array([gen.ip4("192.168.1.1")] * 4, np.uint64),
+                         np.array([gen.ip4("192.168.2.2")] * 4, np.uint64), gen.PROTO_UDP,
+                         [0x3f, 1024, 63, 7], [63, 2048, 9, 0x3f], vlan=None)
+    extra += [bytes(r) for r in v4]
+    vl = gen.ipv4_frames(4, 96, np.arange(4, dtype=np.uint64), np.arange(4, dtype=np.uint64),
+                         gen.PROTO_TCP, 1024, 80, vlan=0x00a)
+    extra += [bytes(r) for r in vl]
+    v6 = gen.ipv6_frames(4, 120, np.arange(4, dtype=np.uint64), np.arange(4, dtype=np.uint64),
+                         gen.PROTO_UDP, 0x3f, 63)
+    extra += [bytes(r) for r in v6]
+    # QinQ around an IPv4/UDP frame
+    f = bytearray(bytes(v4[0]))
+    extra.append(bytes(f[:12]) + b"\x88\xa8\x00\x14\x81\x00\x00\x0a" + bytes(f[12:]))
+    # IPv6 with hop-by-hop + routing ext headers then UDP
+    f6 = bytearray(bytes(v6[1]))
+    ext = bytes([0x2B, 0]) + bytes(6) + bytes([0x11, 0]) + bytes(6)
+    f6[20] = 0x00
+    f6 = f6[:54] + ext + f6[54:]
+    pl = int.from_bytes(f6[18:20], "big") + len(ext)
+    f6[18:20] = pl.to_bytes(2, "big")
+    extra.append(bytes(f6))
+    corpus = base + extra
+    out = []
+    for i in range(n):
+        f = bytearray(corpus[rng.integers(len(corpus))])
+        k = rng.integers(10)
+        if k < 3:                                  # keep intact
+            pass
+        elif k < 6:                                # flip 1..3 bytes in the headers
+            for _ in range(rng.integers(1, 4)):
+                if len(f):
+                    j = int(rng.integers(min(len(f), 64)))
+                    f[j] = int(rng.integers(256))
+        elif k < 8:                                # truncate
+            f = f[: int(rng.integers(0, len(f) + 1))]
+        elif k < 9:                                # random bytes
+            f = bytearray(rng.integers(0, 256, int(rng.integers(0, max_len)), dtype=np.uint8))
+        else:                                      # extend with junk
+            f = f + bytearray(rng.integers(0, 256, int(rng.integers(1, 64)), dtype=np.uint8))
+        out.append(bytes(f))
+    return out

@@ -1,0 +1,249 @@
+"""GPU parity: libodpg.so's gfx950 kernels vs the CPU restatement (oracle) on
+the same inputs, through the C-ABI. Bit-exact on every output: verdict word,
+mark, full parser metadata (packet_parser_t) and the pktio / CoS counters."""
+import numpy as np
+import pytest
+
+import oracle
+import rulesets
+from helpers import ALL_CHKSUM, GOLDEN, assert_same, golden_frames, pack
+from odp_amd import _lib as L
+from odp_amd import gen
+
+pytestmark = pytest.mark.gpu
+
+OPTS = [0, L.PKTIN_IPV4_CHKSUM, L.PKTIN_UDP_CHKSUM | L.PKTIN_TCP_CHKSUM, ALL_CHKSUM]
+
+
+def both(ctx, rules, buf, num, stride=0, desc=None, opt=0, layer=L.LAYER_ALL, classify=True):
+    tbl = ctx.table(rules)
+    g = ctx.classify(tbl, buf, num, stride=stride, desc=desc, opt=opt, layer=layer,
+                     classify=classify)
+    o = oracle.classify(rules, buf, num, stride=stride, desc=desc, opt=opt, layer=layer,
+                        classify=classify)
+    return g, o
+
+
+def default_only(cls, pktin=0):
+    p = cls.loop_pktio(pktin=pktin)
+    d = cls.cos_create("DefaultCos", queue=cls.queue(0), stats_enable=True)
+    e = cls.cos_create("ErrorCos", queue=cls.queue(1), stats_enable=True)
+    assert cls.default_cos_set(p, d) == 0 and cls.error_cos_set(p, e) == 0
+    assert cls.pktio_start(p) == 0
+    return p
+
+
+@pytest.mark.parametrize("opt", OPTS)
+def test_golden_frames(gpu_ctx, fresh_cls, opt):
+    p = default_only(fresh_cls, pktin=opt)
+    names, frames = golden_frames()
+    buf, desc = pack(frames)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), buf, len(frames), desc=desc, opt=opt)
+    assert_same(g, o, f"golden opt={opt}")
+
+
+@pytest.mark.parametrize("layer", [L.LAYER_NONE, L.LAYER_L2, L.LAYER_L3, L.LAYER_L4])
+def test_parse_layers_no_cls(gpu_ctx, fresh_cls, layer):
+    p = default_only(fresh_cls, pktin=ALL_CHKSUM)
+    names, frames = golden_frames()
+    buf, desc = pack(frames)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), buf, len(frames), desc=desc,
+                opt=ALL_CHKSUM, layer=layer, classify=False)
+    assert_same(g, o, f"layer {layer}")
+
+
+def test_example_classifier_pcap(gpu_ctx, fresh_cls):
+    p = fresh_cls.loop_pktio()
+    r = gen.build_c1_rules(fresh_cls, p)
+    assert fresh_cls.pktio_start(p) == 0
+    frames = [bytes.fromhex(h) for h in GOLDEN["pcap"]["classifier_udp64"]]
+    buf, desc = pack(frames)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), buf, len(frames), desc=desc)
+    assert_same(g, o, "classifier pcap")
+    cos = g["out"] & 0xFFFF
+    assert (cos == fresh_cls.to_index(r["queue1"])).sum() == 100
+    assert (cos == fresh_cls.to_index(r["default"])).sum() == 100
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_all_terms_fuzz(gpu_ctx, fresh_cls, seed):
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    rulesets.all_terms_rules(fresh_cls, p)
+    assert fresh_cls.pktio_start(p) == 0
+    frames = rulesets.mutate_corpus(20000, seed=seed)
+    buf, desc = pack(frames)
+    for opt in (0, ALL_CHKSUM):
+        g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), buf, len(frames), desc=desc, opt=opt)
+        assert_same(g, o, f"fuzz seed={seed} opt={opt}")
+
+
+def test_c1_stride64(gpu_ctx, fresh_cls):
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    gen.build_c1_rules(fresh_cls, p)
+    assert fresh_cls.pktio_start(p) == 0
+    n = 1 << 16
+    fr = gen.c1_frames(n)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, n, stride=64, opt=ALL_CHKSUM)
+    assert_same(g, o, "C1")
+
+
+@pytest.mark.parametrize("n", [1, 63, 255, 257, 4097, 1 << 20])
+def test_c2_stride64_sizes(gpu_ctx, fresh_cls, n):
+    """Ragged batch sizes up to the headline 2^20 batch, bit-exact end to end."""
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    gen.build_c2_rules(fresh_cls, p, stats=True)
+    assert fresh_cls.pktio_start(p) == 0
+    fr = gen.c2_frames(n)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, n, stride=64, opt=ALL_CHKSUM)
+    assert_same(g, o, f"C2 n={n}")
+    assert g["stats"][0] == n                        # every packet delivered
+
+
+def test_c2_stride_variants(gpu_ctx, fresh_cls):
+    """Same frames at strides 64 / 128 / 256 / 2048 (different kernel variants)."""
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    gen.build_c2_rules(fresh_cls, p)
+    assert fresh_cls.pktio_start(p) == 0
+    n = 5000
+    fr = gen.c2_frames(n).reshape(n, 64)
+    rules = fresh_cls.pktio_rules(p)
+    ref = None
+    for stride in (64, 128, 256, 2048):
+        buf = np.zeros((n, stride), np.uint8)
+        buf[:, :64] = fr
+        # stride > 64 makes the frame length = stride: zero padding is summed
+        g, o = both(gpu_ctx, rules, buf.reshape(-1), n, stride=stride, opt=ALL_CHKSUM)
+        assert_same(g, o, f"stride {stride}")
+        if ref is None:
+            ref = g["out"] & 0xFFFF
+        assert np.array_equal(g["out"] & 0xFFFF, ref)
+
+
+def test_host_path_matches_device(gpu_ctx, fresh_cls):
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    gen.build_c2_rules(fresh_cls, p, stats=True)
+    assert fresh_cls.pktio_start(p) == 0
+    n = 300000
+    fr = gen.c2_frames(n)
+    rules = fresh_cls.pktio_rules(p)
+    tbl = gpu_ctx.table(rules)
+    d = gpu_ctx.classify(tbl, fr, n, stride=64, opt=ALL_CHKSUM)
+    h = gpu_ctx.classify_host(tbl, fr, n, stride=64, opt=ALL_CHKSUM, chunk=65536,
+                              want_mark=True, want_meta=True)
+    assert_same(h, d, "host vs device")
+    frames = rulesets.mutate_corpus(9000, seed=11)
+    buf, desc = pack(frames)
+    d = gpu_ctx.classify(tbl, buf, len(frames), desc=desc, opt=ALL_CHKSUM)
+    h = gpu_ctx.classify_host(tbl, buf, len(frames), desc=desc, opt=ALL_CHKSUM, chunk=1000,
+                              want_mark=True, want_meta=True)
+    assert_same(h, d, "host vs device (desc)")
+
+
+def test_cycle_is_bounded(gpu_ctx, fresh_cls):
+    """A matching CoS cycle makes the reference loop forever
+    (odp_classification.c:1603-1631); here it ends as ODPG_COS_LOOP."""
+    p = fresh_cls.loop_pktio()
+    a = fresh_cls.cos_create("a", queue=fresh_cls.queue(1))
+    b = fresh_cls.cos_create("b", queue=fresh_cls.queue(2))
+    fresh_cls.default_cos_set(p, a)
+    any_udp = fresh_cls.Term(fresh_cls.PMR_IPPROTO, b"\x11", b"\xff")
+    assert fresh_cls.pmr_create([any_udp], a, b)
+    assert fresh_cls.pmr_create([any_udp], b, a)
+    assert fresh_cls.pktio_start(p) == 0
+    fr = gen.c2_frames(1000)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, 1000, stride=64)
+    assert_same(g, o, "cycle")
+    assert np.all((g["out"] & 0xFFFF) == L.ODPG_COS_LOOP)
+
+
+def test_destroyed_and_invalid_cos(gpu_ctx, fresh_cls):
+    """Rules to a destroyed CoS are skipped (:1610-1611); a destroyed default
+    CoS is still returned (:1687-1694); no default -> discard (-1)."""
+    p = fresh_cls.loop_pktio()
+    d = fresh_cls.cos_create("d", queue=fresh_cls.queue(1), stats_enable=True)
+    x = fresh_cls.cos_create("x", queue=fresh_cls.queue(2))
+    y = fresh_cls.cos_create("y", queue=fresh_cls.queue(3))
+    fresh_cls.default_cos_set(p, d)
+    any_udp = fresh_cls.Term(fresh_cls.PMR_IPPROTO, b"\x11", b"\xff")
+    assert fresh_cls.pmr_create([any_udp], d, x, mark=5)
+    assert fresh_cls.pmr_create([any_udp], d, y, mark=6)
+    assert fresh_cls.pktio_start(p) == 0
+    fr = gen.c2_frames(512)
+    fresh_cls.cos_destroy(x)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, 512, stride=64)
+    assert_same(g, o, "dst destroyed")
+    assert np.all((g["out"] & 0xFFFF) == fresh_cls.to_index(y)) and np.all(g["mark"] == 6)
+    fresh_cls.cos_destroy(d)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, 512, stride=64)
+    assert_same(g, o, "default destroyed")
+    assert np.all((g["out"] & 0xFFFF) == fresh_cls.to_index(d))
+    fresh_cls.default_cos_set(p, None)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, 512, stride=64)
+    assert_same(g, o, "no default")
+    assert np.all((g["out"] & 0xFFFF) == L.ODPG_COS_NONE) and g["stats"][3] == 512
+
+
+def test_hash_queues(gpu_ctx, fresh_cls):
+    """num_queue > 1: Toeplitz RSS -> queue index (odp_classification.c:372-382,
+    :1751-1817) for IPv4/IPv6 x UDP/TCP hash protocol mixes."""
+    for hp in (fresh_cls.HASH_IPV4 | fresh_cls.HASH_IPV4_UDP,
+               fresh_cls.HASH_IPV4_TCP | fresh_cls.HASH_IPV6_TCP,
+               fresh_cls.HASH_IPV6 | fresh_cls.HASH_IPV4 | fresh_cls.HASH_IPV6_UDP):
+        fresh_cls.reset()
+        p = fresh_cls.loop_pktio()
+        d = fresh_cls.cos_create("d", num_queue=7, hash_proto=hp)
+        assert d
+        fresh_cls.default_cos_set(p, d)
+        assert fresh_cls.pktio_start(p) == 0
+        frames = rulesets.mutate_corpus(4000, seed=hp)
+        buf, desc = pack(frames)
+        g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), buf, len(frames), desc=desc)
+        assert_same(g, o, f"hash {hp}")
+        q = L.out_hashq(g["out"])
+        assert q.max() < 7 and len(np.unique(q)) > 1
+
+
+def test_pktio_recv_batch_counters(gpu_ctx, fresh_cls):
+    """odpg_pktio_recv_batch updates odp_cls_cos_stats / odp_pktio_stats like
+    loopback_recv (loop.c:304-374) and match_pmr_cos (:1621-1622)."""
+    import ctypes as C
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    r = gen.build_c2_rules(fresh_cls, p, stats=True)
+    assert fresh_cls.pktio_start(p) == 0
+    n = 100000
+    fr = gen.c2_frames(n)
+    out = np.zeros(n, np.uint32)
+    rc = L.lib.odpg_pktio_recv_batch(p, gpu_ctx.h, fr.ctypes.data, None, 64, n, 0,
+                                     out.ctypes.data, None)
+    assert rc == 0
+    o = oracle.classify(fresh_cls.pktio_rules(p), fr, n, stride=64, opt=ALL_CHKSUM)
+    assert np.array_equal(out, o["out"])
+    st = fresh_cls.pktio_stats(p)
+    assert st.in_packets == n and st.in_octets == 64 * n and st.in_errors == 0
+    for c in [r["default"]] + r["l1"] + r["leaves"]:
+        rc, cs = fresh_cls.cos_stats(c)
+        assert rc == 0 and cs.packets == o["stats"][4 + fresh_cls.to_index(c)]
+    # queue counters of the leaf CoS equal the packets delivered there
+    leaf = r["leaves"][3]
+    rc, qs = fresh_cls.queue_stats(leaf, fresh_cls.cos_queue(leaf))
+    assert rc == 0 and qs.packets == int(((out & 0xFFFF) == fresh_cls.to_index(leaf)).sum())
+    # device-pointer variant adds the same counts again
+    fb = gpu_ctx.buffer(fr.nbytes)
+    fb.upload(fr)
+    ob = gpu_ctx.buffer(4 * n)
+    rc = L.lib.odpg_pktio_recv_batch(p, gpu_ctx.h, fb.ptr, None, 64, n, 1, ob.ptr, None)
+    assert rc == 0
+    assert np.array_equal(ob.download(np.uint32, n), out)
+    assert fresh_cls.pktio_stats(p).in_packets == 2 * n
+    del C
+
+
+def test_raised_limits_1024_pmr(gpu_ctx, fresh_cls):
+    assert fresh_cls.set_limits(2048, 2048, 32) == 0
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    gen.build_c4_rules(fresh_cls, p)
+    assert fresh_cls.pktio_start(p) == 0
+    n = 1 << 18
+    fr = gen.c2_frames(n)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, n, stride=64, opt=ALL_CHKSUM)
+    assert_same(g, o, "C4 1024 PMR")
