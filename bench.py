@@ -43,6 +43,8 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--kernel-mode", type=int, default=0,
+                    help="0 auto, 1 wave-cooperative walk, 2 evaluate-all")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-buffer path (pinned H2D + kernel + D2H)")
     return ap.parse_args()
@@ -99,6 +101,7 @@ def main():
     # each rank owns a distinct shard of the synthetic capture
     frames = frames_fn(n, seed=gen.C_SEED + rank)
     ctx = gpu.Context(local)
+    ctx.set_kernel_mode(args.kernel_mode)
     tbl = ctx.table(rules)
     nbuf = args.buffers or max(2, -(-300 * (1 << 20) // (n * stride)))
     fbufs, obufs = [], []
@@ -185,6 +188,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": workload, "batch_per_gpu": n, "frame_bytes": stride,
                        "pmr_rules": nrules, "rotating_buffers": nbuf,
+                       "kernel_mode": ["auto", "walk", "evaluate-all"][args.kernel_mode],
                        "parallelism": f"dp{world} (packet shards, no data-path collective)"},
             "roofline": roofline, "cpu_baseline": cpu,
         }

@@ -210,6 +210,10 @@ int         odpg_device_count(void);
 int  odpg_ctx_create(int device, void *stream, odpg_ctx_t **ctx);
 void odpg_ctx_destroy(odpg_ctx_t *ctx);
 void *odpg_ctx_stream(odpg_ctx_t *ctx);
+/* Kernel strategy: 0 = auto (evaluate-all for tables up to 1024 compiled
+ * PMRs, wave-cooperative walk above), 1 = walk, 2 = evaluate-all. All
+ * strategies produce identical results; this only selects the code path. */
+int  odpg_ctx_set_kernel_mode(odpg_ctx_t *ctx, int mode);
 int  odpg_ctx_sync(odpg_ctx_t *ctx);
 
 /* Rule table: compiled, immutable snapshot of the CoS/PMR graph. The

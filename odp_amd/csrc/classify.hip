@@ -634,14 +634,130 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x)
 	return x;
 }
 
+
+/* ---- evaluate-all helpers ---------------------------------------------- */
+/* extract the key slots the table reads (odpg_internal.h "key slots") */
+template <int W, bool GF>
+__device__ __forceinline__ void extract_key(uint32_t (&key)[KEY_SLOTS], const Pkt<W, GF> &v,
+					    const Bases &b, uint32_t slot_mask)
+{
+#pragma unroll
+	for (int s = 0; s < KEY_SLOTS; ++s)
+		key[s] = 0u;
+#pragma unroll
+	for (int s = 0; s < 5; ++s)
+		if (slot_mask & (1u << (SLOT_L2 + s)))
+			key[SLOT_L2 + s] = v.rd32(b.l2 + 4u * s);
+	if (slot_mask & (1u << SLOT_VLANX))
+		key[SLOT_VLANX] = v.rd32(b.vlanx);
+	if (slot_mask & (0x3ffu << SLOT_L3)) {
+		/* L3 words: read the covering aligned words once, then funnel */
+		uint32_t base = b.l3, w0 = base >> 2, sh = base & 3u;
+		uint32_t prev = v.word(w0);
+#pragma unroll
+		for (int s = 0; s < 10; ++s) {
+			if ((slot_mask >> (SLOT_L3 + s)) & (0x3ffu >> s)) {   /* slot s or later used */
+				uint32_t nxt = v.word(w0 + s + 1);
+
+				key[SLOT_L3 + s] = sh ? __builtin_amdgcn_alignbyte(nxt, prev, sh) : prev;
+				prev = nxt;
+			}
+		}
+	}
+#pragma unroll
+	for (int s = 0; s < 2; ++s)
+		if (slot_mask & (1u << (SLOT_L4 + s)))
+			key[SLOT_L4 + s] = v.rd32(b.l4 + 4u * s);
+	key[SLOT_LEN] = b.len;
+}
+
+template <int W, bool GF>
+__device__ __forceinline__ bool term_eval(const dterm_t *__restrict__ t, const dslot_t *__restrict__ sl,
+					  const uint32_t (&key)[KEY_SLOTS], const Pkt<W, GF> &v,
+					  const Bases &b)
+{
+	if ((b.inf_lo & t->req) != t->req)
+		return false;
+	if (sl->slot == SLOT_NONE)
+		return term_cmp(t, v, b);
+	bool ok = true;
+	const uint32_t s0 = sl->slot, nw = sl->nw;
+
+	for (uint32_t k = 0; k < nw; ++k)
+		ok = ok && ((key[s0 + k] & sl->mask[k]) == sl->value[k]);
+	return ok;
+}
+
+/* verify_pmr (odp_classification.c:1338-1490) for one compiled PMR */
+template <int W, bool GF>
+__device__ __forceinline__ bool pmr_eval(const dterm_t *__restrict__ terms,
+					 const dslot_t *__restrict__ slots, uint32_t start,
+					 uint32_t n, const uint32_t (&key)[KEY_SLOTS],
+					 const Pkt<W, GF> &v, const Bases &b)
+{
+	bool ok = true;
+	const uint32_t end = start + n;
+
+	for (uint32_t ti = start; ti < end;) {
+		const dterm_t *t = terms + ti;
+		bool r;
+
+		if (t->tflags & DT_ALT_NEXT) {
+			if ((b.inf_lo & t->req) == t->req)
+				r = term_eval(t, slots + ti, key, v, b);
+			else
+				r = term_eval(t + 1, slots + ti + 1, key, v, b);
+			ti += 2;
+		} else {
+			r = term_eval(t, slots + ti, key, v, b);
+			ti += 1;
+		}
+		ok = ok && r;
+	}
+	return ok;
+}
+
+/* first set bit of the rule range [rs, rs + nr) in a per-lane hit map */
+__device__ __forceinline__ int first_hit64(uint64_t hits, uint32_t rs, uint32_t nr)
+{
+	if (nr == 0u || rs >= 64u)
+		return -1;
+	uint64_t x = hits >> rs;
+
+	if (nr < 64u)
+		x &= (1ull << nr) - 1ull;
+	return x ? (int)__builtin_ctzll(x) : -1;
+}
+
+__device__ __forceinline__ int first_hit_lds(const uint32_t *hrow, uint32_t rs, uint32_t nr)
+{
+	const uint32_t end = rs + nr;
+
+	for (uint32_t bpos = rs; bpos < end;) {
+		uint32_t sh = bpos & 31u, take = 32u - sh;
+
+		if (take > end - bpos)
+			take = end - bpos;
+		uint32_t x = hrow[bpos >> 5] >> sh;
+
+		if (take < 32u)
+			x &= (1u << take) - 1u;
+		if (x)
+			return (int)(bpos - rs + (uint32_t)__builtin_ctz(x));
+		bpos += take;
+	}
+	return -1;
+}
+
 /* ----------------------------------------------------------------------- */
-template <int W, bool COOP, bool GF, bool DESC>
+template <int W, bool COOP, bool GF, bool DESC, int MODE>
 __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 	const uint8_t *__restrict__ frames, const odpg_desc_t *__restrict__ desc,
 	uint32_t stride, uint32_t num, uint64_t opt, uint32_t layer, uint32_t classify,
 	const dterm_t *__restrict__ terms, const dpmr_t *__restrict__ pmrs,
 	const dcos_t *__restrict__ coses, uint32_t num_cos, int32_t default_cos,
-	int32_t error_cos, uint32_t tbl_flags,
+	int32_t error_cos, uint32_t tbl_flags, uint32_t num_pmr, uint32_t slot_mask,
+	const dslot_t *__restrict__ slots, const dsimple_t *__restrict__ simple,
 	odpg_out_t *__restrict__ out, uint16_t *__restrict__ mark_out,
 	odpg_meta_t *__restrict__ meta_out, uint64_t *__restrict__ pk_partial,
 	uint32_t *__restrict__ cos_partial)
@@ -649,6 +765,9 @@ __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 	constexpr uint32_t RW = W / 4 + 1;       /* odd dword row stride */
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 	uint32_t *cos_cnt = smem + BLOCK * RW;
+	/* MODE 2: per-lane PMR hit bitmap after the CoS counters */
+	const uint32_t hrw = ((num_pmr + 31u) >> 5) | 1u;
+	uint32_t *hitmap = cos_cnt + (cos_partial ? ((num_cos + 3u) & ~3u) : 0u);
 	__shared__ unsigned long long blk_pk[4];
 
 	const uint32_t tid = threadIdx.x;
@@ -780,7 +899,80 @@ __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 	b.len = len;
 	b.inf_lo = (uint32_t)p.inf;
 
-	while (__ballot(active)) {
+	if constexpr (MODE != 0) {
+		/* evaluate every PMR of the table (branch-free, wave-uniform
+		 * descriptors), then resolve match_pmr_cos's depth-first
+		 * first-match walk (odp_classification.c:1599-1642) on the hit
+		 * bits. Same verdict as evaluating rules only at visited CoS:
+		 * rule evaluation has no side effects. */
+		uint32_t key[KEY_SLOTS];
+		uint64_t hits = 0ull;
+		uint32_t *hrow = hitmap + tid * hrw;
+
+		if (__ballot(active)) {
+			extract_key(key, v, b, slot_mask);
+			if (tbl_flags & TBL_SIMPLE) {
+				uint32_t acc = 0u;
+
+#pragma unroll 4
+				for (uint32_t pi = 0; pi < num_pmr; ++pi) {
+					const dsimple_t e = simple[pi];
+					const bool ok = ((b.inf_lo & e.req) == e.req) &&
+							((key[e.slot] & e.mask) == e.value);
+
+					if (MODE == 1) {
+						hits |= (uint64_t)ok << pi;
+					} else {
+						acc |= (uint32_t)ok << (pi & 31u);
+						if ((pi & 31u) == 31u || pi + 1u == num_pmr) {
+							hrow[pi >> 5] = acc;
+							acc = 0u;
+						}
+					}
+				}
+			} else {
+				uint32_t acc = 0u;
+
+				for (uint32_t pi = 0; pi < num_pmr; ++pi) {
+					const dpmr_t pm = pmrs[pi];
+					const bool ok = pmr_eval(terms, slots, pm.term_start, pm.nterms,
+								 key, v, b);
+
+					if (MODE == 1) {
+						hits |= (uint64_t)ok << pi;
+					} else {
+						acc |= (uint32_t)ok << (pi & 31u);
+						if ((pi & 31u) == 31u || pi + 1u == num_pmr) {
+							hrow[pi >> 5] = acc;
+							acc = 0u;
+						}
+					}
+				}
+			}
+		}
+		while (active) {
+			const dcos_t ce = coses[cos];
+			const int k = MODE == 1 ? first_hit64(hits, ce.rule_start, ce.nrule)
+						: first_hit_lds(hrow, ce.rule_start, ce.nrule);
+
+			if (k < 0)
+				break;
+			const dpmr_t pm = pmrs[ce.rule_start + (uint32_t)k];
+
+			cos = pm.dst;
+			mark = pm.mark;
+			any_match = true;
+			if (do_cos_stats && coses[cos].stats)
+				atomicAdd(&cos_cnt[cos], 1u);
+			if (++steps >= num_cos) {
+				cos = ODPG_COS_LOOP;
+				break;
+			}
+		}
+		active = false;
+	}
+
+	while (MODE == 0 && __ballot(active)) {
 		if (active) {
 			const uint32_t c = __builtin_amdgcn_readfirstlane(cos);
 
@@ -964,16 +1156,35 @@ __global__ __launch_bounds__(BLOCK) void odpg_stats_reduce_kernel(
 /* ----------------------------------------------------------------------- */
 /* host-side launch helper (called from runtime.cpp)                        */
 
-template <int W, bool COOP, bool GF, bool DESC>
+template <int W, bool COOP, bool GF, bool DESC, int MODE>
 static hipError_t launch_one(const odpg_launch_args &a, uint32_t grid, hipStream_t s)
 {
-	size_t lds = (size_t)BLOCK * (W / 4 + 1) * 4u + (a.cos_partial ? (size_t)a.num_cos * 4u : 0u);
+	size_t lds = (size_t)BLOCK * (W / 4 + 1) * 4u;
 
-	hipLaunchKernelGGL((odpg_classify_kernel<W, COOP, GF, DESC>), dim3(grid), dim3(BLOCK), lds, s,
-			   a.frames, a.desc, a.stride, a.num, a.opt, a.layer, a.classify, a.terms,
-			   a.pmrs, a.coses, a.num_cos, a.default_cos, a.error_cos, a.tbl_flags,
-			   a.out, a.mark, a.meta, a.pk_partial, a.cos_partial);
+	if (a.cos_partial)
+		lds += (size_t)((a.num_cos + 3u) & ~3u) * 4u;
+	if (MODE == 2)
+		lds += (size_t)BLOCK * (((a.num_pmr + 31u) >> 5) | 1u) * 4u;
+	hipLaunchKernelGGL((odpg_classify_kernel<W, COOP, GF, DESC, MODE>), dim3(grid), dim3(BLOCK),
+			   lds, s, a.frames, a.desc, a.stride, a.num, a.opt, a.layer, a.classify,
+			   a.terms, a.pmrs, a.coses, a.num_cos, a.default_cos, a.error_cos,
+			   a.tbl_flags, a.num_pmr, a.slot_mask, a.slots, a.simple, a.out, a.mark,
+			   a.meta, a.pk_partial, a.cos_partial);
 	return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_layout(const odpg_launch_args &a, uint32_t grid, hipStream_t s)
+{
+	if (a.desc)
+		return launch_one<128, false, true, true, MODE>(a, grid, s);
+	if (a.stride == 64)
+		return launch_one<64, true, false, false, MODE>(a, grid, s);
+	if (a.stride == 128)
+		return launch_one<128, true, false, false, MODE>(a, grid, s);
+	if (a.stride < 128)
+		return launch_one<128, false, false, false, MODE>(a, grid, s);
+	return launch_one<128, false, true, false, MODE>(a, grid, s);
 }
 
 extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
@@ -981,19 +1192,19 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 	if (a->num == 0)
 		return 0;
 	uint32_t grid = (a->num + BLOCK - 1) / BLOCK;
+	int mode = a->mode;
 	hipError_t e;
 
-	if (a->desc) {
-		e = launch_one<128, false, true, true>(*a, grid, s);
-	} else if (a->stride == 64) {
-		e = launch_one<64, true, false, false>(*a, grid, s);
-	} else if (a->stride == 128) {
-		e = launch_one<128, true, false, false>(*a, grid, s);
-	} else if (a->stride < 128) {
-		e = launch_one<128, false, false, false>(*a, grid, s);
-	} else {
-		e = launch_one<128, false, true, false>(*a, grid, s);
-	}
+	if (mode == 0)
+		mode = a->num_pmr <= EVAL_ALL_MAX_PMR ? 2 : 1;
+	if (mode == 2 && a->num_pmr > EVAL_ALL_MAX_PMR)
+		mode = 1;
+	if (mode == 1)
+		e = launch_layout<0>(*a, grid, s);
+	else if (a->num_pmr <= 64)
+		e = launch_layout<1>(*a, grid, s);
+	else
+		e = launch_layout<2>(*a, grid, s);
 	if (e != hipSuccess)
 		return -EIO;
 	if (a->stats && (a->pk_partial || a->cos_partial)) {

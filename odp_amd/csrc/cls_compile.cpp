@@ -36,8 +36,6 @@ dterm_t make_cmp(uint32_t req, uint8_t base, int32_t off, const uint8_t *mask,
 
 	memcpy(m, mask, nbytes);
 	memcpy(v, value, nbytes);
-	for (uint32_t i = 0; i < nbytes; i++)
-		v[i] &= 0xff;   /* value already & mask by pmr_create_term() */
 	memcpy(t.mask, m, 16);
 	memcpy(t.value, v, 16);
 	return t;
@@ -168,6 +166,71 @@ int lower_term(const odpg_term_t *src, std::vector<dterm_t> &out)
 	}
 }
 
+/* Re-express a compiled term as a compare of consecutive key slots
+ * (odpg_internal.h), or SLOT_NONE when it must use the generic compare. */
+dslot_t slotify(const dterm_t &t)
+{
+	dslot_t s;
+
+	memset(&s, 0, sizeof(s));
+	s.slot = SLOT_NONE;
+	if (t.kind == DK_LEN) {
+		s.slot = SLOT_LEN;
+		s.nw = 1;
+		s.mask[0] = t.mask[0];
+		s.value[0] = t.value[0];
+		return s;
+	}
+	if (t.kind == DK_NEVER) {
+		s.slot = 0;
+		s.nw = 1;
+		s.mask[0] = 0;
+		s.value[0] = 1;    /* (x & 0) == 1 never holds */
+		return s;
+	}
+	if (t.kind != DK_CMP || (t.tflags & DT_GUARD) || t.size == 0 || t.off < 0)
+		return s;
+
+	int first, count;
+
+	switch (t.base) {
+	case DB_L2:
+		first = SLOT_L2;
+		count = SLOT_VLANX - SLOT_L2;
+		break;
+	case DB_VLANX:
+		first = SLOT_VLANX;
+		count = 1;
+		break;
+	case DB_L3:
+		first = SLOT_L3;
+		count = SLOT_L4 - SLOT_L3;
+		break;
+	case DB_L4:
+		first = SLOT_L4;
+		count = SLOT_LEN - SLOT_L4;
+		break;
+	default:
+		return s;
+	}
+	uint32_t w0 = (uint32_t)t.off / 4, w1 = ((uint32_t)t.off + t.size - 1) / 4;
+
+	if (w1 >= (uint32_t)count || w1 - w0 + 1 > 4)
+		return s;
+	for (uint32_t j = 0; j < t.size; j++) {
+		uint32_t mb = (t.mask[j / 4] >> (8 * (j % 4))) & 0xff;
+		uint32_t vb = (t.value[j / 4] >> (8 * (j % 4))) & 0xff;
+		uint32_t pos = (uint32_t)t.off + j;
+		uint32_t w = pos / 4 - w0, lane = pos % 4;
+
+		s.mask[w] |= mb << (8 * lane);
+		s.value[w] |= vb << (8 * lane);
+	}
+	s.slot = (uint8_t)(first + w0);
+	s.nw = (uint8_t)(w1 - w0 + 1);
+	return s;
+}
+
 } /* namespace */
 
 int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable_hdr_t *hdr_out)
@@ -234,9 +297,46 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		d.nrule = (uint16_t)(pmr.size() - d.rule_start);
 	}
 
+	/* key-slot forms and the compact single-compare table */
+	std::vector<dslot_t> slots(terms.size());
+	std::vector<dsimple_t> simple;
+	uint32_t slot_mask = 0;
+	bool is_simple = true;
+
+	for (size_t k = 0; k < terms.size(); k++) {
+		slots[k] = slotify(terms[k]);
+		if (slots[k].slot != SLOT_NONE)
+			for (uint32_t w = 0; w < slots[k].nw; w++)
+				slot_mask |= 1u << (slots[k].slot + w);
+	}
+	for (const dpmr_t &p : pmr) {
+		dsimple_t e;
+
+		memset(&e, 0, sizeof(e));
+		if (p.nterms == 0) {
+			simple.push_back(e);            /* no terms: always matches */
+			continue;
+		}
+		const dterm_t &t = terms[p.term_start];
+		const dslot_t &sl = slots[p.term_start];
+
+		if (p.nterms != 1 || sl.slot == SLOT_NONE || sl.nw != 1 || (t.tflags & DT_ALT_NEXT)) {
+			is_simple = false;
+			break;
+		}
+		e.req = t.req;
+		e.slot = sl.slot;
+		e.mask = sl.mask[0];
+		e.value = sl.value[0];
+		simple.push_back(e);
+	}
+
 	dtable_hdr_t h;
 
 	memset(&h, 0, sizeof(h));
+	h.slot_mask = slot_mask;
+	if (is_simple)
+		h.flags |= TBL_SIMPLE;
 	h.num_cos = r->num_cos;
 	h.default_cos = r->default_cos;
 	h.error_cos = r->error_cos;
@@ -254,7 +354,9 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 
 	auto align = [](uint32_t x) { return (x + 63u) & ~63u; };
 	h.term_off = 0;
-	h.pmr_off = align(h.term_off + (uint32_t)(terms.size() * sizeof(dterm_t)));
+	h.slot_off = align(h.term_off + (uint32_t)(terms.size() * sizeof(dterm_t)));
+	h.simple_off = align(h.slot_off + (uint32_t)(slots.size() * sizeof(dslot_t)));
+	h.pmr_off = align(h.simple_off + (uint32_t)(is_simple ? simple.size() * sizeof(dsimple_t) : 0));
 	h.cos_off = align(h.pmr_off + (uint32_t)(pmr.size() * sizeof(dpmr_t)));
 	h.blob_bytes = align(h.cos_off + (uint32_t)(cos.size() * sizeof(dcos_t)));
 	if (h.blob_bytes == 0)
@@ -262,6 +364,10 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	blob.assign(h.blob_bytes, 0);
 	if (!terms.empty())
 		memcpy(blob.data() + h.term_off, terms.data(), terms.size() * sizeof(dterm_t));
+	if (!slots.empty())
+		memcpy(blob.data() + h.slot_off, slots.data(), slots.size() * sizeof(dslot_t));
+	if (is_simple && !simple.empty())
+		memcpy(blob.data() + h.simple_off, simple.data(), simple.size() * sizeof(dsimple_t));
 	if (!pmr.empty())
 		memcpy(blob.data() + h.pmr_off, pmr.data(), pmr.size() * sizeof(dpmr_t));
 	if (!cos.empty())

@@ -83,6 +83,44 @@ typedef struct dcos_s {
 #define TBL_ANY_MARK   0x1
 #define TBL_ANY_HASHQ  0x2
 #define TBL_ANY_STATS  0x4
+#define TBL_SIMPLE     0x8   /* every PMR is one single-word slotted compare */
+
+/* ---- per-packet key slots (evaluate-all kernels) -------------------------
+ * The parser-relative 32-bit words the terms can compare, extracted once per
+ * packet into registers:
+ *   0..4   L2 + 0, 4, 8, 12, 16   (DMAC, ETHTYPE_0, VLAN_ID_0 / PCP)
+ *   5      VLANX + 0              (innermost VLAN tci + ethertype)
+ *   6..15  L3 + 0 .. 36           (IPv4 / IPv6 header fields and addresses)
+ *   16..17 L4 + 0, 4              (ports, AH / ESP SPI)
+ *   18     frame length           (ODP_PMR_LEN)
+ * A term compares up to four consecutive slots, masks re-aligned to the slot
+ * words by the compiler. Terms outside these windows (custom terms) keep the
+ * generic (base + off) compare. */
+#define KEY_SLOTS     19
+#define SLOT_L2       0
+#define SLOT_VLANX    5
+#define SLOT_L3       6
+#define SLOT_L4       16
+#define SLOT_LEN      18
+#define SLOT_NONE     0xFF
+
+typedef struct dslot_s {
+	uint8_t  slot;      /* first slot, SLOT_NONE = generic compare */
+	uint8_t  nw;        /* consecutive slots compared */
+	uint16_t pad;
+	uint32_t mask[4];
+	uint32_t value[4];
+} dslot_t;              /* 36 bytes, parallel to dterm_t */
+
+/* TBL_SIMPLE tables: one entry per PMR in table order */
+typedef struct dsimple_s {
+	uint32_t req;
+	uint32_t slot;
+	uint32_t mask;
+	uint32_t value;
+} dsimple_t;            /* 16 bytes */
+
+#define EVAL_ALL_MAX_PMR 1024
 
 typedef struct dtable_hdr_s {
 	uint32_t num_cos;
@@ -94,6 +132,9 @@ typedef struct dtable_hdr_s {
 	uint32_t cos_off;    /* byte offsets inside the device blob */
 	uint32_t pmr_off;
 	uint32_t term_off;
+	uint32_t slot_off;   /* dslot_t[num_terms] */
+	uint32_t simple_off; /* dsimple_t[num_pmr] when TBL_SIMPLE */
+	uint32_t slot_mask;  /* key slots any slotted term reads */
 	uint32_t blob_bytes;
 } dtable_hdr_t;
 
@@ -111,6 +152,11 @@ typedef struct odpg_launch_args {
 	uint32_t num_cos;
 	int32_t default_cos, error_cos;
 	uint32_t tbl_flags;
+	uint32_t num_pmr;
+	uint32_t slot_mask;
+	const dslot_t *slots;
+	const dsimple_t *simple;
+	int mode;           /* 0 auto, 1 walk, 2 evaluate-all */
 	odpg_out_t *out;
 	uint16_t *mark;
 	odpg_meta_t *meta;

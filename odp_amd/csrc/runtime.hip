@@ -30,6 +30,7 @@ struct odpg_ctx_s {
 	void *ws;          /* per-workgroup counter partials */
 	size_t ws_bytes;
 	hipEvent_t ev[NUM_EVENTS];
+	int kernel_mode;   /* 0 auto, 1 walk, 2 evaluate-all */
 	std::mutex lock;
 };
 
@@ -85,6 +86,7 @@ int odpg_ctx_create(int device, void *stream, odpg_ctx_t **out)
 	c->device = device;
 	c->ws = nullptr;
 	c->ws_bytes = 0;
+	c->kernel_mode = 0;
 	if (hipSetDevice(device) != hipSuccess) {
 		delete c;
 		return -EIO;
@@ -127,6 +129,14 @@ void odpg_ctx_destroy(odpg_ctx_t *c)
 	if (c->own_stream)
 		hipStreamDestroy(c->stream);
 	delete c;
+}
+
+int odpg_ctx_set_kernel_mode(odpg_ctx_t *c, int mode)
+{
+	if (!c || mode < 0 || mode > 2)
+		return -EINVAL;
+	c->kernel_mode = mode;
+	return 0;
 }
 
 void *odpg_ctx_stream(odpg_ctx_t *c)
@@ -241,6 +251,11 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.default_cos = h.default_cos;
 	a.error_cos = h.error_cos;
 	a.tbl_flags = h.flags;
+	a.num_pmr = h.num_pmr;
+	a.slot_mask = h.slot_mask;
+	a.slots = (const dslot_t *)((const uint8_t *)t->dblob + h.slot_off);
+	a.simple = (const dsimple_t *)((const uint8_t *)t->dblob + h.simple_off);
+	a.mode = c->kernel_mode;
 	a.out = r->out;
 	a.mark = r->mark;
 	a.meta = r->meta;
@@ -250,7 +265,6 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 		if (cos_stats)
 			a.cos_partial = (uint32_t *)((uint8_t *)ws + (size_t)grid * 32u);
 	}
-	(void)c;
 	return odpg_launch_classify(&a, s);
 }
 

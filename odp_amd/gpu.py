@@ -87,6 +87,10 @@ class Context:
         except Exception:
             pass
 
+    def set_kernel_mode(self, mode):
+        """0 auto, 1 wave-cooperative walk, 2 evaluate-all (same results)."""
+        L.check(lib.odpg_ctx_set_kernel_mode(self.h, mode), "odpg_ctx_set_kernel_mode")
+
     def sync(self):
         L.check(lib.odpg_ctx_sync(self.h), "odpg_ctx_sync")
 

@@ -16,12 +16,19 @@ OPTS = [0, L.PKTIN_IPV4_CHKSUM, L.PKTIN_UDP_CHKSUM | L.PKTIN_TCP_CHKSUM, ALL_CHK
 
 
 def both(ctx, rules, buf, num, stride=0, desc=None, opt=0, layer=L.LAYER_ALL, classify=True):
+    """Classify on the GPU with every kernel strategy (walk, evaluate-all,
+    auto) and on the oracle; the strategies must agree bit for bit."""
     tbl = ctx.table(rules)
-    g = ctx.classify(tbl, buf, num, stride=stride, desc=desc, opt=opt, layer=layer,
-                     classify=classify)
+    res = {}
+    for mode in (1, 2, 0):
+        ctx.set_kernel_mode(mode)
+        res[mode] = ctx.classify(tbl, buf, num, stride=stride, desc=desc, opt=opt,
+                                 layer=layer, classify=classify)
+    ctx.set_kernel_mode(0)
+    assert_same(res[1], res[2], "walk vs evaluate-all")
     o = oracle.classify(rules, buf, num, stride=stride, desc=desc, opt=opt, layer=layer,
                         classify=classify)
-    return g, o
+    return res[0], o
 
 
 def default_only(cls, pktin=0):
