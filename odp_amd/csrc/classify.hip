@@ -635,6 +635,160 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x)
 }
 
 
+
+/* ---- register fast path: plain 64-byte Eth/IPv4/UDP|TCP frames ----------
+ * Frames whose generic parse takes the straight path (no SNAP / VLAN, IPv4
+ * IHL 5, UDP length >= 8 or TCP header >= 20 B) are parsed from the 16
+ * registers holding the frame with compile-time offsets (l3 = 14, l4 = 34).
+ * A wave takes it only when all its live lanes qualify (ballot); results are
+ * bit-identical to parse_common() for those frames. */
+template <int K>
+__device__ __forceinline__ uint32_t fw(const uint32_t (&f)[16])
+{
+	/* little-endian u32 of frame bytes [K, K + 4), K constant */
+	if constexpr ((K & 3) == 0)
+		return f[K >> 2];
+	else
+		return __builtin_amdgcn_alignbyte(f[(K >> 2) + 1], f[K >> 2], K & 3);
+}
+
+__device__ __forceinline__ uint32_t swap16(uint32_t x)
+{
+	return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu);
+}
+
+__device__ __forceinline__ bool plain_v4(const uint32_t (&f)[16])
+{
+	const uint32_t w3 = f[3];
+	const uint32_t tot_len = swap16(f[4] & 0xffffu);
+	const uint32_t proto = f[5] >> 24;
+
+	if ((w3 & 0x00ffffffu) != 0x00450008u)      /* ethtype 0x0800, ver_ihl 0x45 */
+		return false;
+	if (tot_len > 64u - 14u)
+		return false;
+	if (proto == 0x11u)
+		return swap16(f[9] >> 16) >= 8u;         /* udp length */
+	if (proto == 0x06u)
+		return ((f[11] >> 20) & 0xfu) >= 5u;     /* tcp data offset */
+	return false;
+}
+
+__device__ __forceinline__ int parse_fast(Prs &p, const uint32_t (&f)[16], uint64_t opt)
+{
+	const uint32_t len = 64u;
+	uint64_t inf = IF(IFL_L2) | IF(IFL_ETH) | IF(IFL_L3) | IF(IFL_IPV4) | IF(IFL_L4);
+	uint32_t fl = 0u;
+
+	p.l2 = 0u;
+	p.l3 = 14u;
+	if (f[0] & 0x1u)
+		inf |= IF(IFL_ETH_MCAST);
+	if (f[0] == 0xffffffffu && (f[1] & 0xffffu) == 0xffffu)
+		inf |= IF(IFL_ETH_BCAST);
+	if (opt & ODPG_PKTIN_IPV4_CHKSUM) {
+		uint32_t s = oc_add(f[3] & 0xffff0000u, f[4]);
+
+		s = oc_add(s, f[5]);
+		s = oc_add(s, f[6]);
+		s = oc_add(s, f[7]);
+		s = oc_add(s, f[8] & 0xffffu);
+		inf |= IF(IFL_L3_CHKSUM_DONE);
+		if (oc_fold(s) != 0xffffu) {
+			/* ip_err: no l4 offset, ip_proto 0 -> l4 flag cleared */
+			p.inf = inf & ~IF(IFL_L4);
+			p.fl = FB(FL_IP_ERR) | FB(FL_L3_CHKSUM_ERR);
+			p.l4 = 0xffffu;
+			return 1;
+		}
+	}
+	const bool frag = (swap16(f[5] & 0xffffu) & 0x3fffu) != 0u;
+	const uint32_t dst_be = __builtin_bswap32(fw<30>(f));
+
+	if (frag)
+		inf |= IF(IFL_IPFRAG);
+	if (dst_be == 0xffffffffu)
+		inf |= IF(IFL_IP_BCAST);
+	if ((dst_be >> 28) == 0xeu)
+		inf |= IF(IFL_IP_MCAST);
+	p.l4 = 34u;
+	uint32_t l4sum = 0u;
+
+	if (opt & (ODPG_PKTIN_UDP_CHKSUM | ODPG_PKTIN_TCP_CHKSUM))
+		l4sum = oc_add(oc_add(f[6] & 0xffff0000u, f[7]), f[8] & 0xffffu);
+	bool do_sum = false;
+
+	if ((f[5] >> 24) == 0x11u) {                 /* parse_udp */
+		const uint32_t u1 = fw<38>(f);
+		const uint32_t ulen_raw = u1 & 0xffffu, csum_raw = u1 >> 16;
+		const uint32_t udplen = swap16(ulen_raw);
+
+		inf |= IF(IFL_UDP);
+		if ((opt & ODPG_PKTIN_UDP_CHKSUM) && !frag) {
+			if (csum_raw == 0u) {
+				inf |= IF(IFL_L4_CHKSUM_DONE) | IF(IFL_UDP_CHKSUM_ZERO);
+			} else {
+				l4sum = oc_add(oc_add(l4sum, ulen_raw), 0x11u << 8);
+				do_sum = true;
+			}
+		}
+		if (swap16(f[9] & 0xffffu) == 4500u && udplen > 4u && fw<42>(f) != 0u)
+			inf |= IF(IFL_IPSEC) | IF(IFL_IPSEC_UDP);
+		if (do_sum) {
+			uint32_t s = oc_add(l4sum, f[8] & 0xffff0000u);
+
+#pragma unroll
+			for (int k = 9; k < 16; ++k)
+				s = oc_add(s, f[k]);
+			inf |= IF(IFL_L4_CHKSUM_DONE);
+			if (oc_fold(s) != 0xffffu)
+				fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_UDP_ERR);
+		}
+	} else {                                     /* parse_tcp */
+		inf |= IF(IFL_TCP);
+		if ((opt & ODPG_PKTIN_TCP_CHKSUM) && !frag) {
+			uint32_t tl = (len - 34u) & 0xffffu;
+			uint32_t s = oc_add(oc_add(l4sum, swap16(tl)), 0x06u << 8);
+
+			s = oc_add(s, f[8] & 0xffff0000u);
+#pragma unroll
+			for (int k = 9; k < 16; ++k)
+				s = oc_add(s, f[k]);
+			inf |= IF(IFL_L4_CHKSUM_DONE);
+			if (oc_fold(s) != 0xffffu)
+				fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_TCP_ERR);
+		}
+	}
+	p.inf = inf;
+	p.fl = fl;
+	return fl ? 1 : 0;
+}
+
+__device__ __forceinline__ void extract_key_fast(uint32_t (&key)[KEY_SLOTS], const uint32_t (&f)[16],
+						 const Prs &p, uint32_t slot_mask)
+{
+#pragma unroll
+	for (int s = 0; s < 5; ++s)
+		key[SLOT_L2 + s] = f[s];
+	key[SLOT_VLANX] = fw<14>(f);
+	key[SLOT_L3 + 0] = fw<14>(f);
+	key[SLOT_L3 + 1] = fw<18>(f);
+	key[SLOT_L3 + 2] = fw<22>(f);
+	key[SLOT_L3 + 3] = fw<26>(f);
+	key[SLOT_L3 + 4] = fw<30>(f);
+	key[SLOT_L3 + 5] = fw<34>(f);
+	key[SLOT_L3 + 6] = fw<38>(f);
+	key[SLOT_L3 + 7] = fw<42>(f);
+	key[SLOT_L3 + 8] = fw<46>(f);
+	key[SLOT_L3 + 9] = fw<50>(f);
+	const bool l4ok = p.l4 != 0xffffu;
+
+	key[SLOT_L4 + 0] = l4ok ? fw<34>(f) : 0u;
+	key[SLOT_L4 + 1] = l4ok ? fw<38>(f) : 0u;
+	key[SLOT_LEN] = 64u;
+	(void)slot_mask;
+}
+
 /* ---- evaluate-all helpers ---------------------------------------------- */
 /* extract the key slots the table reads (odpg_internal.h "key slots") */
 template <int W, bool GF>
@@ -750,7 +904,7 @@ __device__ __forceinline__ int first_hit_lds(const uint32_t *hrow, uint32_t rs, 
 }
 
 /* ----------------------------------------------------------------------- */
-template <int W, bool COOP, bool GF, bool DESC, int MODE>
+template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST>
 __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 	const uint8_t *__restrict__ frames, const odpg_desc_t *__restrict__ desc,
 	uint32_t stride, uint32_t num, uint64_t opt, uint32_t layer, uint32_t classify,
@@ -758,6 +912,7 @@ __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 	const dcos_t *__restrict__ coses, uint32_t num_cos, int32_t default_cos,
 	int32_t error_cos, uint32_t tbl_flags, uint32_t num_pmr, uint32_t slot_mask,
 	const dslot_t *__restrict__ slots, const dsimple_t *__restrict__ simple,
+	const drun_t *__restrict__ runs, uint32_t num_runs,
 	odpg_out_t *__restrict__ out, uint16_t *__restrict__ mark_out,
 	odpg_meta_t *__restrict__ meta_out, uint64_t *__restrict__ pk_partial,
 	uint32_t *__restrict__ cos_partial)
@@ -798,7 +953,34 @@ __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 		len = live ? stride : 0u;
 	}
 
-	if (COOP) {
+	uint32_t f[16];
+	bool wave_fast = false;
+
+	if constexpr (FAST) {
+		/* 64-byte frames straight into 16 registers, 4 x 16 B per lane */
+		const uint4 *src = (const uint4 *)(frames + (size_t)i * 64u);
+
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			uint4 x = live ? src[k] : make_uint4(0u, 0u, 0u, 0u);
+
+			f[4 * k + 0] = x.x;
+			f[4 * k + 1] = x.y;
+			f[4 * k + 2] = x.z;
+			f[4 * k + 3] = x.w;
+		}
+		const bool plain = live && layer >= LAYER_L4 &&
+				   !(opt & (ODPG_PKTIN_DROP_IPV4_ERR | ODPG_PKTIN_DROP_IPV6_ERR |
+					    ODPG_PKTIN_DROP_UDP_ERR | ODPG_PKTIN_DROP_TCP_ERR |
+					    ODPG_PKTIN_DROP_SCTP_ERR)) && plain_v4(f);
+
+		wave_fast = __ballot(live && !plain) == 0ull;
+		if (!wave_fast || (tbl_flags & (TBL_GENERIC | TBL_ANY_HASHQ))) {
+#pragma unroll
+			for (int k = 0; k < 16; ++k)
+				row[k] = f[k];
+		}
+	} else if (COOP) {
 		/* stride == W: the block's frames are one contiguous span */
 		constexpr uint32_t CPP = W / 16;
 		const uint4 *src = (const uint4 *)(frames + (size_t)blk0 * W);
@@ -851,7 +1033,8 @@ __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 			row[part * 4u + 3u] = x.w;
 		}
 	}
-	__syncthreads();
+	if (COOP)
+		__syncthreads();
 
 	Pkt<W, GF> v;
 
@@ -867,8 +1050,12 @@ __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 	p.l2 = p.l3 = p.l4 = 0xffffu;
 	int ret = 0;
 
-	if (live && layer)
+	if (FAST && wave_fast) {
+		if (live)
+			ret = parse_fast(p, f, opt);
+	} else if (live && layer) {
 		ret = parse_common(p, v, layer, opt);
+	}
 
 	/* ---- 3. CoS walk ------------------------------------------------- */
 	uint32_t cos = ODPG_COS_NOCLS;
@@ -910,26 +1097,40 @@ __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 		uint32_t *hrow = hitmap + tid * hrw;
 
 		if (__ballot(active)) {
-			extract_key(key, v, b, slot_mask);
+			if (FAST && wave_fast)
+				extract_key_fast(key, f, p, slot_mask);
+			else
+				extract_key(key, v, b, slot_mask);
 			if (tbl_flags & TBL_SIMPLE) {
-				uint32_t acc = 0u;
+				uint32_t lo = 0u, hi = 0u;
+
+				if (MODE == 2)
+					for (uint32_t w = 0; w < hrw; ++w)
+						hrow[w] = 0u;
+				for (uint32_t r = 0; r < num_runs; ++r) {
+					const drun_t run = runs[r];
+					const uint32_t kv = key[run.slot];
+					const dsimple_t *e = simple + run.start;
+					uint32_t acc = 0u;
 
 #pragma unroll 4
-				for (uint32_t pi = 0; pi < num_pmr; ++pi) {
-					const dsimple_t e = simple[pi];
-					const bool ok = ((b.inf_lo & e.req) == e.req) &&
-							((key[e.slot] & e.mask) == e.value);
+					for (uint32_t q = 0; q < run.count; ++q) {
+						const dsimple_t x = e[q];
+						const bool ok = ((b.inf_lo & x.req) == x.req) &&
+								((kv & x.mask) == x.value);
 
+						acc |= ok ? (1u << (x.idx & 31u)) : 0u;
+					}
 					if (MODE == 1) {
-						hits |= (uint64_t)ok << pi;
+						if (run.word == 0)
+							lo |= acc;
+						else
+							hi |= acc;
 					} else {
-						acc |= (uint32_t)ok << (pi & 31u);
-						if ((pi & 31u) == 31u || pi + 1u == num_pmr) {
-							hrow[pi >> 5] = acc;
-							acc = 0u;
-						}
+						hrow[run.word] |= acc;
 					}
 				}
+				hits = ((uint64_t)hi << 32) | lo;
 			} else {
 				uint32_t acc = 0u;
 
@@ -1156,7 +1357,7 @@ __global__ __launch_bounds__(BLOCK) void odpg_stats_reduce_kernel(
 /* ----------------------------------------------------------------------- */
 /* host-side launch helper (called from runtime.cpp)                        */
 
-template <int W, bool COOP, bool GF, bool DESC, int MODE>
+template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST = false>
 static hipError_t launch_one(const odpg_launch_args &a, uint32_t grid, hipStream_t s)
 {
 	size_t lds = (size_t)BLOCK * (W / 4 + 1) * 4u;
@@ -1165,11 +1366,11 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t grid, hipStream
 		lds += (size_t)((a.num_cos + 3u) & ~3u) * 4u;
 	if (MODE == 2)
 		lds += (size_t)BLOCK * (((a.num_pmr + 31u) >> 5) | 1u) * 4u;
-	hipLaunchKernelGGL((odpg_classify_kernel<W, COOP, GF, DESC, MODE>), dim3(grid), dim3(BLOCK),
-			   lds, s, a.frames, a.desc, a.stride, a.num, a.opt, a.layer, a.classify,
-			   a.terms, a.pmrs, a.coses, a.num_cos, a.default_cos, a.error_cos,
-			   a.tbl_flags, a.num_pmr, a.slot_mask, a.slots, a.simple, a.out, a.mark,
-			   a.meta, a.pk_partial, a.cos_partial);
+	hipLaunchKernelGGL((odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST>), dim3(grid),
+			   dim3(BLOCK), lds, s, a.frames, a.desc, a.stride, a.num, a.opt, a.layer,
+			   a.classify, a.terms, a.pmrs, a.coses, a.num_cos, a.default_cos,
+			   a.error_cos, a.tbl_flags, a.num_pmr, a.slot_mask, a.slots, a.simple,
+			   a.runs, a.num_runs, a.out, a.mark, a.meta, a.pk_partial, a.cos_partial);
 	return hipGetLastError();
 }
 
@@ -1178,8 +1379,11 @@ static hipError_t launch_layout(const odpg_launch_args &a, uint32_t grid, hipStr
 {
 	if (a.desc)
 		return launch_one<128, false, true, true, MODE>(a, grid, s);
-	if (a.stride == 64)
+	if (a.stride == 64) {
+		if (MODE != 0)   /* register fast path for plain frames */
+			return launch_one<64, false, false, false, MODE, true>(a, grid, s);
 		return launch_one<64, true, false, false, MODE>(a, grid, s);
+	}
 	if (a.stride == 128)
 		return launch_one<128, true, false, false, MODE>(a, grid, s);
 	if (a.stride < 128)

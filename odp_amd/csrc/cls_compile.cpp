@@ -11,6 +11,7 @@
  */
 #include <string.h>
 #include <errno.h>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/odpg.h"
@@ -309,12 +310,21 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			for (uint32_t w = 0; w < slots[k].nw; w++)
 				slot_mask |= 1u << (slots[k].slot + w);
 	}
-	for (const dpmr_t &p : pmr) {
+	std::vector<uint32_t> simple_slot;
+	bool generic = false;
+
+	for (size_t k = 0; k < terms.size(); k++)
+		if (slots[k].slot == SLOT_NONE && terms[k].kind == DK_CMP)
+			generic = true;
+	for (size_t pi = 0; pi < pmr.size(); pi++) {
+		const dpmr_t &p = pmr[pi];
 		dsimple_t e;
 
 		memset(&e, 0, sizeof(e));
+		e.idx = (uint32_t)pi;
 		if (p.nterms == 0) {
 			simple.push_back(e);            /* no terms: always matches */
+			simple_slot.push_back(0);
 			continue;
 		}
 		const dterm_t &t = terms[p.term_start];
@@ -325,10 +335,47 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			break;
 		}
 		e.req = t.req;
-		e.slot = sl.slot;
 		e.mask = sl.mask[0];
 		e.value = sl.value[0];
 		simple.push_back(e);
+		simple_slot.push_back(sl.slot);
+	}
+	std::vector<drun_t> runs;
+
+	if (is_simple) {
+		/* order by (slot, hit word, index): one key-slot read and one
+		 * hit-word update per run */
+		std::vector<size_t> ord(simple.size());
+
+		for (size_t k = 0; k < ord.size(); k++)
+			ord[k] = k;
+		std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
+			uint64_t ka = ((uint64_t)simple_slot[a] << 40) | ((uint64_t)(simple[a].idx >> 5) << 20) | simple[a].idx;
+			uint64_t kb = ((uint64_t)simple_slot[b] << 40) | ((uint64_t)(simple[b].idx >> 5) << 20) | simple[b].idx;
+			return ka < kb;
+		});
+		std::vector<dsimple_t> sorted;
+
+		for (size_t k = 0; k < ord.size(); k++) {
+			const dsimple_t &e = simple[ord[k]];
+			uint32_t sl = simple_slot[ord[k]], wd = e.idx >> 5;
+
+			if (runs.empty() || runs.back().slot != sl || runs.back().word != wd ||
+			    runs.back().count == 0xffff) {
+				drun_t r;
+
+				memset(&r, 0, sizeof(r));
+				r.slot = (uint8_t)sl;
+				r.word = (uint16_t)wd;
+				r.start = (uint16_t)k;
+				runs.push_back(r);
+			}
+			runs.back().count++;
+			sorted.push_back(e);
+		}
+		simple.swap(sorted);
+		if (simple.size() > 65535)
+			is_simple = false;
 	}
 
 	dtable_hdr_t h;
@@ -337,6 +384,9 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.slot_mask = slot_mask;
 	if (is_simple)
 		h.flags |= TBL_SIMPLE;
+	if (generic)
+		h.flags |= TBL_GENERIC;
+	h.num_runs = is_simple ? (uint32_t)runs.size() : 0;
 	h.num_cos = r->num_cos;
 	h.default_cos = r->default_cos;
 	h.error_cos = r->error_cos;
@@ -356,7 +406,8 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.term_off = 0;
 	h.slot_off = align(h.term_off + (uint32_t)(terms.size() * sizeof(dterm_t)));
 	h.simple_off = align(h.slot_off + (uint32_t)(slots.size() * sizeof(dslot_t)));
-	h.pmr_off = align(h.simple_off + (uint32_t)(is_simple ? simple.size() * sizeof(dsimple_t) : 0));
+	h.run_off = align(h.simple_off + (uint32_t)(is_simple ? simple.size() * sizeof(dsimple_t) : 0));
+	h.pmr_off = align(h.run_off + (uint32_t)(is_simple ? runs.size() * sizeof(drun_t) : 0));
 	h.cos_off = align(h.pmr_off + (uint32_t)(pmr.size() * sizeof(dpmr_t)));
 	h.blob_bytes = align(h.cos_off + (uint32_t)(cos.size() * sizeof(dcos_t)));
 	if (h.blob_bytes == 0)
@@ -366,8 +417,10 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		memcpy(blob.data() + h.term_off, terms.data(), terms.size() * sizeof(dterm_t));
 	if (!slots.empty())
 		memcpy(blob.data() + h.slot_off, slots.data(), slots.size() * sizeof(dslot_t));
-	if (is_simple && !simple.empty())
+	if (is_simple && !simple.empty()) {
 		memcpy(blob.data() + h.simple_off, simple.data(), simple.size() * sizeof(dsimple_t));
+		memcpy(blob.data() + h.run_off, runs.data(), runs.size() * sizeof(drun_t));
+	}
 	if (!pmr.empty())
 		memcpy(blob.data() + h.pmr_off, pmr.data(), pmr.size() * sizeof(dpmr_t));
 	if (!cos.empty())

@@ -84,6 +84,7 @@ typedef struct dcos_s {
 #define TBL_ANY_HASHQ  0x2
 #define TBL_ANY_STATS  0x4
 #define TBL_SIMPLE     0x8   /* every PMR is one single-word slotted compare */
+#define TBL_GENERIC    0x10  /* some term needs the generic (base + off) compare */
 
 /* ---- per-packet key slots (evaluate-all kernels) -------------------------
  * The parser-relative 32-bit words the terms can compare, extracted once per
@@ -112,13 +113,22 @@ typedef struct dslot_s {
 	uint32_t value[4];
 } dslot_t;              /* 36 bytes, parallel to dterm_t */
 
-/* TBL_SIMPLE tables: one entry per PMR in table order */
+/* TBL_SIMPLE tables: one entry per PMR, sorted by (key slot, hit word), and
+ * grouped in runs that share the slot word and the 32-bit hit-map word */
 typedef struct dsimple_s {
 	uint32_t req;
-	uint32_t slot;
 	uint32_t mask;
 	uint32_t value;
+	uint32_t idx;       /* PMR index in table order (hit-map bit) */
 } dsimple_t;            /* 16 bytes */
+
+typedef struct drun_s {
+	uint8_t  slot;
+	uint8_t  pad;
+	uint16_t word;      /* hit-map word = idx >> 5 */
+	uint16_t start;     /* first dsimple_t */
+	uint16_t count;
+} drun_t;               /* 8 bytes */
 
 #define EVAL_ALL_MAX_PMR 1024
 
@@ -134,6 +144,8 @@ typedef struct dtable_hdr_s {
 	uint32_t term_off;
 	uint32_t slot_off;   /* dslot_t[num_terms] */
 	uint32_t simple_off; /* dsimple_t[num_pmr] when TBL_SIMPLE */
+	uint32_t run_off;    /* drun_t[num_runs] when TBL_SIMPLE */
+	uint32_t num_runs;
 	uint32_t slot_mask;  /* key slots any slotted term reads */
 	uint32_t blob_bytes;
 } dtable_hdr_t;
@@ -156,6 +168,8 @@ typedef struct odpg_launch_args {
 	uint32_t slot_mask;
 	const dslot_t *slots;
 	const dsimple_t *simple;
+	const drun_t *runs;
+	uint32_t num_runs;
 	int mode;           /* 0 auto, 1 walk, 2 evaluate-all */
 	odpg_out_t *out;
 	uint16_t *mark;

@@ -255,6 +255,8 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.slot_mask = h.slot_mask;
 	a.slots = (const dslot_t *)((const uint8_t *)t->dblob + h.slot_off);
 	a.simple = (const dsimple_t *)((const uint8_t *)t->dblob + h.simple_off);
+	a.runs = (const drun_t *)((const uint8_t *)t->dblob + h.run_off);
+	a.num_runs = h.num_runs;
 	a.mode = c->kernel_mode;
 	a.out = r->out;
 	a.mark = r->mark;

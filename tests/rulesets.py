@@ -116,3 +116,51 @@ def mutate_corpus(n, seed=7, max_len=220):
             f = f + bytearray(rng.integers(0, 256, int(rng.integers(1, 64)), dtype=np.uint8))
         out.append(bytes(f))
     return out
+
+
+def plain64_corpus(n, seed=5):
+    """64-byte Eth/IPv4/UDP|TCP frames with the edge properties the register
+    fast path must reproduce: fragments, broadcast / multicast MAC and IP,
+    UDP port 4500 (IPsec NAT-T marker), zero UDP checksum, corrupted IPv4 /
+    L4 checksums, plus a share of frames that must leave the fast path
+    (short UDP length, oversize tot_len, IHL > 5, VLAN, IPv6)."""
+    rng = np.random.default_rng(seed)
+    r = rng.integers(0, 1 << 62, size=(n, 4), dtype=np.int64).astype(np.uint64)
+    src = np.uint64(gen.ip4("192.168.0.0")) + (r[:, 0] & np.uint64(0xFFFF))
+    dst = np.uint64(gen.ip4("192.168.0.0")) + (r[:, 1] & np.uint64(0xFFFF))
+    kind = rng.integers(0, 16, n)
+    dst = np.where(kind == 1, np.uint64(0xFFFFFFFF), dst)
+    dst = np.where(kind == 2, np.uint64(gen.ip4("224.0.0.5")), dst)
+    sport = (r[:, 2] & np.uint64(0xFFFF))
+    dport = (r[:, 3] & np.uint64(63))
+    dport = np.where(kind == 3, np.uint64(4500), dport)
+    udp = gen.ipv4_frames(n, 64, src, dst, gen.PROTO_UDP, sport, dport)
+    tcp = gen.ipv4_frames(n, 64, src, dst, gen.PROTO_TCP, sport, dport)
+    fr = np.where((rng.integers(0, 2, n) == 1)[:, None], tcp, udp)
+    fr[kind == 4, 20] |= 0x20                        # more-fragments bit
+    f4 = fr[kind == 4]                               # ... with a valid header checksum
+    f4[:, 24:26] = 0
+    c = gen.csum(gen.ones_sum(f4, 14, 34))
+    f4[:, 24] = (c >> 8) & 0xFF
+    f4[:, 25] = c & 0xFF
+    fr[kind == 4] = f4
+    fr[kind == 5, 0:6] = 0xFF                        # broadcast MAC
+    fr[kind == 6, 0] |= 0x01                         # multicast MAC
+    sel = (kind == 7) & (fr[:, 23] == 17)
+    fr[sel, 40:42] = 0                               # UDP checksum 0
+    fr[kind == 8, 24] ^= 0x5A                        # bad IPv4 header checksum
+    fr[kind == 9, 60] ^= 0x33                        # bad L4 checksum
+    sel = (kind == 10) & (fr[:, 23] == 17)
+    fr[sel, 38:40] = [0, 4]                          # UDP length < 8 (udp_err)
+    fr[kind == 11, 16:18] = [0, 60]                  # tot_len > frame -> ip_err
+    fr[kind == 12, 14] = 0x46                        # IHL 6 (options)
+    sel = kind == 13                                 # VLAN tag
+    fr[sel, 12:14] = [0x81, 0x00]
+    sel = kind == 14                                 # IPv6 ethertype
+    fr[sel, 12:14] = [0x86, 0xDD]
+    # keep whole waves plain too: first half of every 128 frames untouched
+    plain_wave = (np.arange(n) % 128) < 64
+    base = np.where((rng.integers(0, 2, n) == 1)[:, None], tcp, udp)
+    keep = plain_wave & (kind >= 10)
+    fr[keep] = base[keep]
+    return fr.reshape(-1)

@@ -254,3 +254,23 @@ def test_raised_limits_1024_pmr(gpu_ctx, fresh_cls):
     fr = gen.c2_frames(n)
     g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, n, stride=64, opt=ALL_CHKSUM)
     assert_same(g, o, "C4 1024 PMR")
+
+
+@pytest.mark.parametrize("opt", [0, L.PKTIN_IPV4_CHKSUM, ALL_CHKSUM])
+def test_stride64_fast_path_edges(gpu_ctx, fresh_cls, opt):
+    """64-byte stride: waves that take the register fast path and waves that
+    fall back to the generic parser, with every edge the fast path decides."""
+    p = fresh_cls.loop_pktio(pktin=opt)
+    rulesets.all_terms_rules(fresh_cls, p)
+    assert fresh_cls.pktio_start(p) == 0
+    n = 64 * 300
+    fr = rulesets.plain64_corpus(n)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, n, stride=64, opt=opt)
+    assert_same(g, o, f"fast path opt={opt}")
+    # C2 rules (TBL_SIMPLE) over the same frames
+    fresh_cls.reset()
+    p = fresh_cls.loop_pktio(pktin=opt)
+    gen.build_c2_rules(fresh_cls, p, stats=True)
+    assert fresh_cls.pktio_start(p) == 0
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, n, stride=64, opt=opt)
+    assert_same(g, o, f"fast path C2 opt={opt}")
