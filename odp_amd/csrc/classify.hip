@@ -789,6 +789,63 @@ __device__ __forceinline__ void extract_key_fast(uint32_t (&key)[KEY_SLOTS], con
 	(void)slot_mask;
 }
 
+
+/* ---- key slots on demand ------------------------------------------------
+ * The word a compiled term compares (odpg_internal.h "key slots"), fetched
+ * when a rule group needs it: from the frame registers on fast waves
+ * (uniform switch), from the LDS window otherwise. No per-packet key array
+ * is materialised (keeps register pressure and scratch at zero). */
+template <int W, bool GF>
+struct KeySrc {
+	const uint32_t *f;     /* 16 frame registers (fast waves) or nullptr */
+	const Pkt<W, GF> *v;
+	const Bases *b;
+	bool fast;
+
+	__device__ __forceinline__ uint32_t operator()(uint32_t slot) const
+	{
+		if (fast) {
+			const uint32_t (&r)[16] = *reinterpret_cast<const uint32_t (*)[16]>(f);
+			const bool l4ok = b->l4 != 0xffffu;
+
+			switch (slot) {
+			case 0: return r[0];
+			case 1: return r[1];
+			case 2: return r[2];
+			case 3: return r[3];
+			case 4: return r[4];
+			case 5: return fw<14>(r);
+			case 6: return fw<14>(r);
+			case 7: return fw<18>(r);
+			case 8: return fw<22>(r);
+			case 9: return fw<26>(r);
+			case 10: return fw<30>(r);
+			case 11: return fw<34>(r);
+			case 12: return fw<38>(r);
+			case 13: return fw<42>(r);
+			case 14: return fw<46>(r);
+			case 15: return fw<50>(r);
+			case 16: return l4ok ? fw<34>(r) : 0u;
+			case 17: return l4ok ? fw<38>(r) : 0u;
+			default: return b->len;
+			}
+		}
+		uint32_t pos;
+
+		if (slot < SLOT_VLANX)
+			pos = b->l2 + 4u * slot;
+		else if (slot == SLOT_VLANX)
+			pos = b->vlanx;
+		else if (slot < SLOT_L4)
+			pos = b->l3 + 4u * (slot - SLOT_L3);
+		else if (slot < SLOT_LEN)
+			pos = b->l4 + 4u * (slot - SLOT_L4);
+		else
+			return b->len;
+		return v->rd32(pos);
+	}
+};
+
 /* ---- evaluate-all helpers ---------------------------------------------- */
 /* extract the key slots the table reads (odpg_internal.h "key slots") */
 template <int W, bool GF>
@@ -827,7 +884,7 @@ __device__ __forceinline__ void extract_key(uint32_t (&key)[KEY_SLOTS], const Pk
 
 template <int W, bool GF>
 __device__ __forceinline__ bool term_eval(const dterm_t *__restrict__ t, const dslot_t *__restrict__ sl,
-					  const uint32_t (&key)[KEY_SLOTS], const Pkt<W, GF> &v,
+					  const KeySrc<W, GF> &key, const Pkt<W, GF> &v,
 					  const Bases &b)
 {
 	if ((b.inf_lo & t->req) != t->req)
@@ -838,7 +895,7 @@ __device__ __forceinline__ bool term_eval(const dterm_t *__restrict__ t, const d
 	const uint32_t s0 = sl->slot, nw = sl->nw;
 
 	for (uint32_t k = 0; k < nw; ++k)
-		ok = ok && ((key[s0 + k] & sl->mask[k]) == sl->value[k]);
+		ok = ok & ((key(s0 + k) & sl->mask[k]) == sl->value[k]);
 	return ok;
 }
 
@@ -846,7 +903,7 @@ __device__ __forceinline__ bool term_eval(const dterm_t *__restrict__ t, const d
 template <int W, bool GF>
 __device__ __forceinline__ bool pmr_eval(const dterm_t *__restrict__ terms,
 					 const dslot_t *__restrict__ slots, uint32_t start,
-					 uint32_t n, const uint32_t (&key)[KEY_SLOTS],
+					 uint32_t n, const KeySrc<W, GF> &key,
 					 const Pkt<W, GF> &v, const Bases &b)
 {
 	bool ok = true;
@@ -905,7 +962,7 @@ __device__ __forceinline__ int first_hit_lds(const uint32_t *hrow, uint32_t rs, 
 
 /* ----------------------------------------------------------------------- */
 template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST>
-__global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
+__global__ __launch_bounds__(BLOCK, 6) void odpg_classify_kernel(
 	const uint8_t *__restrict__ frames, const odpg_desc_t *__restrict__ desc,
 	uint32_t stride, uint32_t num, uint64_t opt, uint32_t layer, uint32_t classify,
 	const dterm_t *__restrict__ terms, const dpmr_t *__restrict__ pmrs,
@@ -913,6 +970,8 @@ __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 	int32_t error_cos, uint32_t tbl_flags, uint32_t num_pmr, uint32_t slot_mask,
 	const dslot_t *__restrict__ slots, const dsimple_t *__restrict__ simple,
 	const drun_t *__restrict__ runs, uint32_t num_runs,
+	const dhgroup_t *__restrict__ hgroups, uint32_t num_hgroups,
+	const dhent_t *__restrict__ hents_g, uint32_t num_hent,
 	odpg_out_t *__restrict__ out, uint16_t *__restrict__ mark_out,
 	odpg_meta_t *__restrict__ meta_out, uint64_t *__restrict__ pk_partial,
 	uint32_t *__restrict__ cos_partial)
@@ -923,21 +982,35 @@ __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 	/* MODE 2: per-lane PMR hit bitmap after the CoS counters */
 	const uint32_t hrw = ((num_pmr + 31u) >> 5) | 1u;
 	uint32_t *hitmap = cos_cnt + (cos_partial ? ((num_cos + 3u) & ~3u) : 0u);
+	/* exact-match hash tables, copied to LDS when small */
+	uint2 *hents_l = (uint2 *)(hitmap + (MODE == 2 ? BLOCK * hrw : 0u));
+	const bool hent_in_lds = num_hent <= HENT_LDS_MAX;
 	__shared__ unsigned long long blk_pk[4];
 
 	const uint32_t tid = threadIdx.x;
-	const uint32_t blk0 = blockIdx.x * BLOCK;
-	const uint32_t i = blk0 + tid;
-	const bool live = i < num;
 	const bool do_stats = pk_partial != nullptr;
 	const bool do_cos_stats = cos_partial != nullptr;
 	uint32_t *row = smem + tid * RW;
+	uint64_t lane_pkt = 0, lane_oct = 0, lane_err = 0, lane_disc = 0;
 
 	if (tid < 4)
 		blk_pk[tid] = 0ull;
 	if (do_cos_stats)
 		for (uint32_t c = tid; c < num_cos; c += BLOCK)
 			cos_cnt[c] = 0u;
+	if (MODE != 0 && hent_in_lds)
+		for (uint32_t k = tid; k < num_hent; k += BLOCK)
+			hents_l[k] = *(const uint2 *)(hents_g + k);
+	__syncthreads();
+	const uint2 *hents = hent_in_lds ? hents_l : (const uint2 *)hents_g;
+
+	/* persistent workgroups: tiles of BLOCK packets */
+	const uint32_t ntiles = (num + BLOCK - 1) / BLOCK;
+
+	for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+	const uint32_t blk0 = tile * BLOCK;
+	const uint32_t i = blk0 + tid;
+	const bool live = i < num;
 
 	/* ---- 1. stage the frame window in LDS ---------------------------- */
 	const uint8_t *g;
@@ -1092,42 +1165,81 @@ __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 		 * first-match walk (odp_classification.c:1599-1642) on the hit
 		 * bits. Same verdict as evaluating rules only at visited CoS:
 		 * rule evaluation has no side effects. */
-		uint32_t key[KEY_SLOTS];
 		uint64_t hits = 0ull;
 		uint32_t *hrow = hitmap + tid * hrw;
 
 		if (__ballot(active)) {
-			if (FAST && wave_fast)
-				extract_key_fast(key, f, p, slot_mask);
-			else
-				extract_key(key, v, b, slot_mask);
+			KeySrc<W, GF> key;
+
+			key.f = f;
+			key.v = &v;
+			key.b = &b;
+			key.fast = FAST && wave_fast;
 			if (tbl_flags & TBL_SIMPLE) {
 				uint32_t lo = 0u, hi = 0u;
 
 				if (MODE == 2)
 					for (uint32_t w = 0; w < hrw; ++w)
 						hrow[w] = 0u;
+				/* exact-match groups: one probe sequence each */
+				for (uint32_t gi = 0; gi < num_hgroups; ++gi) {
+					const uint4 g0 = *(const uint4 *)(hgroups + gi);
+					const uint2 g1 = *(const uint2 *)((const uint32_t *)(hgroups + gi) + 4);
+					const uint32_t hslot = __builtin_amdgcn_readfirstlane(g0.x);
+					const uint32_t hreq = __builtin_amdgcn_readfirstlane(g0.y);
+					const uint32_t hmask = __builtin_amdgcn_readfirstlane(g0.z);
+					const uint32_t lg = __builtin_amdgcn_readfirstlane(g0.w);
+					const uint32_t hoff = __builtin_amdgcn_readfirstlane(g1.x);
+					const uint32_t kvm = key(hslot) & hmask;
+
+					if ((b.inf_lo & hreq) == hreq) {
+						const uint32_t szm = (1u << lg) - 1u;
+						uint32_t h = (kvm * HASH_MUL) >> (32u - lg);
+
+						for (uint32_t pr = 0; pr <= szm; ++pr) {
+							const uint2 e = hents[hoff + h];
+
+							if (e.y == HENT_EMPTY)
+								break;
+							if (e.x == kvm) {
+								if (MODE == 1) {
+									if (e.y < 32u)
+										lo |= 1u << e.y;
+									else
+										hi |= 1u << (e.y - 32u);
+								} else {
+									hrow[e.y >> 5] |= 1u << (e.y & 31u);
+								}
+							}
+							h = (h + 1u) & szm;
+						}
+					}
+				}
 				for (uint32_t r = 0; r < num_runs; ++r) {
-					const drun_t run = runs[r];
-					const uint32_t kv = key[run.slot];
-					const dsimple_t *e = simple + run.start;
+					const uint4 run = *(const uint4 *)(runs + r);
+					const uint32_t slot = __builtin_amdgcn_readfirstlane(run.x);
+					const uint32_t word = __builtin_amdgcn_readfirstlane(run.y);
+					const uint32_t start = __builtin_amdgcn_readfirstlane(run.z);
+					const uint32_t count = __builtin_amdgcn_readfirstlane(run.w);
+					const uint32_t kv = key(slot);
+					const uint4 *e = (const uint4 *)(simple + start);
 					uint32_t acc = 0u;
 
-#pragma unroll 4
-					for (uint32_t q = 0; q < run.count; ++q) {
-						const dsimple_t x = e[q];
-						const bool ok = ((b.inf_lo & x.req) == x.req) &&
-								((kv & x.mask) == x.value);
+#pragma unroll 8
+					for (uint32_t q = 0; q < count; ++q) {
+						const uint4 x = e[q];   /* req, mask, value, idx */
+						const bool ok = ((b.inf_lo & x.x) == x.x) & ((kv & x.y) == x.z);
 
-						acc |= ok ? (1u << (x.idx & 31u)) : 0u;
+						acc |= ok ? (1u << (x.w & 31u)) : 0u;
 					}
+					const drun_t run_s = {slot, word, start, count};
 					if (MODE == 1) {
-						if (run.word == 0)
+						if (run_s.word == 0)
 							lo |= acc;
 						else
 							hi |= acc;
 					} else {
-						hrow[run.word] |= acc;
+						hrow[run_s.word] |= acc;
 					}
 				}
 				hits = ((uint64_t)hi << 32) | lo;
@@ -1289,23 +1401,29 @@ __global__ __launch_bounds__(BLOCK) void odpg_classify_kernel(
 		}
 	}
 
-	/* ---- 5. per-workgroup counter partials ---------------------------- */
+	/* ---- 5. loopback_recv accounting (loop.c:304-374), per lane ------- */
 	if (do_stats) {
-		/* loopback_recv accounting (loop.c:304-374) */
-		uint32_t is_err = (live && layer && ret != 0) ? 1u : 0u;
-		uint32_t is_disc = (live && (cret == -1 || cret == -2)) ? 1u : 0u;
-		uint32_t is_pkt = (live && ret >= 0 && cret == 0 && !(p.fl & FL_ERROR_MASK)) ? 1u : 0u;
-		uint64_t oct = is_pkt ? (uint64_t)len : 0ull;
-		uint32_t n_pkt = (uint32_t)__popcll(__ballot(is_pkt));
-		uint32_t n_err = (uint32_t)__popcll(__ballot(is_err));
-		uint32_t n_disc = (uint32_t)__popcll(__ballot(is_disc));
+		const bool is_pkt = live && ret >= 0 && cret == 0 && !(p.fl & FL_ERROR_MASK);
 
-		oct = wave_sum_u64(oct);
+		lane_err += (live && layer && ret != 0) ? 1u : 0u;
+		lane_disc += (live && (cret == -1 || cret == -2)) ? 1u : 0u;
+		lane_pkt += is_pkt ? 1u : 0u;
+		lane_oct += is_pkt ? (uint64_t)len : 0u;
+	}
+	if (COOP)
+		__syncthreads();          /* LDS rows are reused by the next tile */
+	}   /* tile loop */
+
+	/* ---- 6. per-workgroup counter partials ---------------------------- */
+	if (do_stats) {
+		uint64_t a = wave_sum_u64(lane_pkt), o = wave_sum_u64(lane_oct);
+		uint64_t e = wave_sum_u64(lane_err), d = wave_sum_u64(lane_disc);
+
 		if (__lane_id() == 0) {
-			atomicAdd(&blk_pk[0], (unsigned long long)n_pkt);
-			atomicAdd(&blk_pk[1], (unsigned long long)oct);
-			atomicAdd(&blk_pk[2], (unsigned long long)n_err);
-			atomicAdd(&blk_pk[3], (unsigned long long)n_disc);
+			atomicAdd(&blk_pk[0], (unsigned long long)a);
+			atomicAdd(&blk_pk[1], (unsigned long long)o);
+			atomicAdd(&blk_pk[2], (unsigned long long)e);
+			atomicAdd(&blk_pk[3], (unsigned long long)d);
 		}
 	}
 	if (do_stats || do_cos_stats)
@@ -1357,6 +1475,8 @@ __global__ __launch_bounds__(BLOCK) void odpg_stats_reduce_kernel(
 /* ----------------------------------------------------------------------- */
 /* host-side launch helper (called from runtime.cpp)                        */
 
+extern "C" uint32_t odpg_launch_grid(uint32_t num);
+
 template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST = false>
 static hipError_t launch_one(const odpg_launch_args &a, uint32_t grid, hipStream_t s)
 {
@@ -1366,11 +1486,14 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t grid, hipStream
 		lds += (size_t)((a.num_cos + 3u) & ~3u) * 4u;
 	if (MODE == 2)
 		lds += (size_t)BLOCK * (((a.num_pmr + 31u) >> 5) | 1u) * 4u;
+	if (MODE != 0 && a.num_hent <= HENT_LDS_MAX)
+		lds += (size_t)a.num_hent * 8u;
 	hipLaunchKernelGGL((odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST>), dim3(grid),
 			   dim3(BLOCK), lds, s, a.frames, a.desc, a.stride, a.num, a.opt, a.layer,
 			   a.classify, a.terms, a.pmrs, a.coses, a.num_cos, a.default_cos,
 			   a.error_cos, a.tbl_flags, a.num_pmr, a.slot_mask, a.slots, a.simple,
-			   a.runs, a.num_runs, a.out, a.mark, a.meta, a.pk_partial, a.cos_partial);
+			   a.runs, a.num_runs, a.hgroups, a.num_hgroups, a.hents, a.num_hent, a.out,
+			   a.mark, a.meta, a.pk_partial, a.cos_partial);
 	return hipGetLastError();
 }
 
@@ -1395,7 +1518,7 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 {
 	if (a->num == 0)
 		return 0;
-	uint32_t grid = (a->num + BLOCK - 1) / BLOCK;
+	uint32_t grid = odpg_launch_grid(a->num);
 	int mode = a->mode;
 	hipError_t e;
 
@@ -1423,7 +1546,12 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 	return 0;
 }
 
+/* persistent grid: at most MAX_GRID workgroups, each looping over tiles */
+#define MAX_GRID 2048u
+
 extern "C" uint32_t odpg_launch_grid(uint32_t num)
 {
-	return (num + BLOCK - 1) / BLOCK;
+	uint32_t tiles = (num + BLOCK - 1) / BLOCK;
+
+	return tiles < MAX_GRID ? tiles : MAX_GRID;
 }

@@ -12,6 +12,7 @@
 #include <string.h>
 #include <errno.h>
 #include <algorithm>
+#include <tuple>
 #include <vector>
 
 #include "../../include/odpg.h"
@@ -279,7 +280,7 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 
 			if (p->num_terms > ODPG_MAX_TERMS)
 				return -EINVAL;
-			dp.term_start = (uint16_t)terms.size();
+			dp.term_start = (uint32_t)terms.size();
 			for (uint32_t t = 0; t < p->num_terms; t++) {
 				int rc = lower_term(&p->terms[t], terms);
 
@@ -288,9 +289,9 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			}
 			if (terms.size() > 65535)
 				return -E2BIG;
-			dp.nterms = (uint16_t)(terms.size() - dp.term_start);
-			dp.mark = (uint16_t)p->mark;
-			dp.dst = (uint16_t)dst;
+			dp.nterms = (uint32_t)(terms.size() - dp.term_start);
+			dp.mark = p->mark & 0xffffu;
+			dp.dst = dst;
 			pmr.push_back(dp);
 			if (pmr.size() > ODPG_MAX_PMR * 4)
 				return -E2BIG;
@@ -341,6 +342,73 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		simple_slot.push_back(sl.slot);
 	}
 	std::vector<drun_t> runs;
+	std::vector<dhgroup_t> hgroups;
+	std::vector<dhent_t> hents;
+
+	if (is_simple) {
+		/* exact-match groups -> hash tables; the rest stays linear */
+		std::vector<size_t> order(simple.size());
+
+		for (size_t k = 0; k < order.size(); k++)
+			order[k] = k;
+		auto gkey = [&](size_t k) {
+			return std::make_tuple(simple_slot[k], simple[k].req, simple[k].mask);
+		};
+		std::stable_sort(order.begin(), order.end(),
+				 [&](size_t a, size_t b) { return gkey(a) < gkey(b); });
+		std::vector<bool> hashed(simple.size(), false);
+
+		for (size_t g0 = 0; g0 < order.size();) {
+			size_t g1 = g0;
+
+			while (g1 < order.size() && gkey(order[g1]) == gkey(order[g0]))
+				g1++;
+			size_t cnt = g1 - g0;
+			bool ok = cnt >= HASH_MIN;
+
+			for (size_t k = g0; k < g1 && ok; k++)
+				if (simple[order[k]].value & ~simple[order[k]].mask)
+					ok = false;   /* can never match: keep it linear */
+			if (ok) {
+				uint32_t lg = 3;
+
+				while ((1u << lg) < 2 * cnt)
+					lg++;
+				dhgroup_t hg;
+
+				memset(&hg, 0, sizeof(hg));
+				hg.slot = simple_slot[order[g0]];
+				hg.req = simple[order[g0]].req;
+				hg.mask = simple[order[g0]].mask;
+				hg.log2sz = lg;
+				hg.off = (uint32_t)hents.size();
+				hg.count = (uint32_t)cnt;
+				hents.resize(hents.size() + (1u << lg), dhent_t{0u, HENT_EMPTY});
+				for (size_t k = g0; k < g1; k++) {
+					const dsimple_t &e = simple[order[k]];
+					uint32_t h = (e.value * HASH_MUL) >> (32 - lg);
+
+					while (hents[hg.off + h].idx != HENT_EMPTY)
+						h = (h + 1) & ((1u << lg) - 1);
+					hents[hg.off + h].value = e.value;
+					hents[hg.off + h].idx = e.idx;
+					hashed[order[k]] = true;
+				}
+				hgroups.push_back(hg);
+			}
+			g0 = g1;
+		}
+		std::vector<dsimple_t> lin;
+		std::vector<uint32_t> lin_slot;
+
+		for (size_t k = 0; k < simple.size(); k++)
+			if (!hashed[k]) {
+				lin.push_back(simple[k]);
+				lin_slot.push_back(simple_slot[k]);
+			}
+		simple.swap(lin);
+		simple_slot.swap(lin_slot);
+	}
 
 	if (is_simple) {
 		/* order by (slot, hit word, index): one key-slot read and one
@@ -361,13 +429,13 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			uint32_t sl = simple_slot[ord[k]], wd = e.idx >> 5;
 
 			if (runs.empty() || runs.back().slot != sl || runs.back().word != wd ||
-			    runs.back().count == 0xffff) {
+			    runs.back().count == 0xffffu) {
 				drun_t r;
 
 				memset(&r, 0, sizeof(r));
-				r.slot = (uint8_t)sl;
-				r.word = (uint16_t)wd;
-				r.start = (uint16_t)k;
+				r.slot = sl;
+				r.word = wd;
+				r.start = (uint32_t)k;
 				runs.push_back(r);
 			}
 			runs.back().count++;
@@ -387,6 +455,8 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	if (generic)
 		h.flags |= TBL_GENERIC;
 	h.num_runs = is_simple ? (uint32_t)runs.size() : 0;
+	h.num_hgroups = is_simple ? (uint32_t)hgroups.size() : 0;
+	h.num_hent = is_simple ? (uint32_t)hents.size() : 0;
 	h.num_cos = r->num_cos;
 	h.default_cos = r->default_cos;
 	h.error_cos = r->error_cos;
@@ -407,7 +477,9 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.slot_off = align(h.term_off + (uint32_t)(terms.size() * sizeof(dterm_t)));
 	h.simple_off = align(h.slot_off + (uint32_t)(slots.size() * sizeof(dslot_t)));
 	h.run_off = align(h.simple_off + (uint32_t)(is_simple ? simple.size() * sizeof(dsimple_t) : 0));
-	h.pmr_off = align(h.run_off + (uint32_t)(is_simple ? runs.size() * sizeof(drun_t) : 0));
+	h.hgroup_off = align(h.run_off + (uint32_t)(is_simple ? runs.size() * sizeof(drun_t) : 0));
+	h.hent_off = align(h.hgroup_off + h.num_hgroups * (uint32_t)sizeof(dhgroup_t));
+	h.pmr_off = align(h.hent_off + h.num_hent * (uint32_t)sizeof(dhent_t));
 	h.cos_off = align(h.pmr_off + (uint32_t)(pmr.size() * sizeof(dpmr_t)));
 	h.blob_bytes = align(h.cos_off + (uint32_t)(cos.size() * sizeof(dcos_t)));
 	if (h.blob_bytes == 0)
@@ -417,9 +489,16 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		memcpy(blob.data() + h.term_off, terms.data(), terms.size() * sizeof(dterm_t));
 	if (!slots.empty())
 		memcpy(blob.data() + h.slot_off, slots.data(), slots.size() * sizeof(dslot_t));
-	if (is_simple && !simple.empty()) {
-		memcpy(blob.data() + h.simple_off, simple.data(), simple.size() * sizeof(dsimple_t));
-		memcpy(blob.data() + h.run_off, runs.data(), runs.size() * sizeof(drun_t));
+	if (is_simple) {
+		if (!simple.empty())
+			memcpy(blob.data() + h.simple_off, simple.data(),
+			       simple.size() * sizeof(dsimple_t));
+		if (!runs.empty())
+			memcpy(blob.data() + h.run_off, runs.data(), runs.size() * sizeof(drun_t));
+		if (!hgroups.empty())
+			memcpy(blob.data() + h.hgroup_off, hgroups.data(), hgroups.size() * sizeof(dhgroup_t));
+		if (!hents.empty())
+			memcpy(blob.data() + h.hent_off, hents.data(), hents.size() * sizeof(dhent_t));
 	}
 	if (!pmr.empty())
 		memcpy(blob.data() + h.pmr_off, pmr.data(), pmr.size() * sizeof(dpmr_t));

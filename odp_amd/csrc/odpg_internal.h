@@ -62,12 +62,14 @@ typedef struct dterm_s {
 	uint32_t value[4];
 } dterm_t;              /* 48 bytes */
 
+/* 32-bit fields throughout: wave-uniform reads of these tables become
+ * scalar (s_load) loads only when every field is dword aligned */
 typedef struct dpmr_s {
-	uint16_t term_start;
-	uint16_t nterms;    /* compiled entries, including ALT_NEXT partners */
-	uint16_t mark;
-	uint16_t dst;
-} dpmr_t;               /* 8 bytes */
+	uint32_t term_start;
+	uint32_t nterms;    /* compiled entries, including ALT_NEXT partners */
+	uint32_t mark;
+	uint32_t dst;
+} dpmr_t;               /* 16 bytes */
 
 typedef struct dcos_s {
 	uint32_t rule_start;
@@ -123,12 +125,35 @@ typedef struct dsimple_s {
 } dsimple_t;            /* 16 bytes */
 
 typedef struct drun_s {
-	uint8_t  slot;
-	uint8_t  pad;
-	uint16_t word;      /* hit-map word = idx >> 5 */
-	uint16_t start;     /* first dsimple_t */
-	uint16_t count;
-} drun_t;               /* 8 bytes */
+	uint32_t slot;
+	uint32_t word;      /* hit-map word = idx >> 5 */
+	uint32_t start;     /* first dsimple_t */
+	uint32_t count;
+} drun_t;               /* 16 bytes */
+
+/* Exact-match groups: TBL_SIMPLE entries sharing (slot, req, mask) compile to
+ * an open-addressing hash table of (value, pmr index); one probe sequence per
+ * packet replaces `count` compares. Load factor <= 1/2, linear probing,
+ * h = (key * 0x9E3779B1) >> (32 - log2sz). */
+typedef struct dhgroup_s {
+	uint32_t slot;
+	uint32_t req;
+	uint32_t mask;
+	uint32_t log2sz;
+	uint32_t off;       /* first dhent_t of this group */
+	uint32_t count;     /* real entries */
+	uint32_t pad[2];
+} dhgroup_t;            /* 32 bytes */
+
+typedef struct dhent_s {
+	uint32_t value;
+	uint32_t idx;       /* PMR index, HENT_EMPTY = free slot */
+} dhent_t;
+
+#define HENT_EMPTY    0xFFFFFFFFu
+#define HASH_MIN      6      /* smaller groups stay linear */
+#define HASH_MUL      0x9E3779B1u
+#define HENT_LDS_MAX  4096   /* entries copied to LDS per workgroup */
 
 #define EVAL_ALL_MAX_PMR 1024
 
@@ -146,6 +171,10 @@ typedef struct dtable_hdr_s {
 	uint32_t simple_off; /* dsimple_t[num_pmr] when TBL_SIMPLE */
 	uint32_t run_off;    /* drun_t[num_runs] when TBL_SIMPLE */
 	uint32_t num_runs;
+	uint32_t hgroup_off; /* dhgroup_t[num_hgroups] */
+	uint32_t num_hgroups;
+	uint32_t hent_off;   /* dhent_t[num_hent] */
+	uint32_t num_hent;
 	uint32_t slot_mask;  /* key slots any slotted term reads */
 	uint32_t blob_bytes;
 } dtable_hdr_t;
@@ -170,6 +199,10 @@ typedef struct odpg_launch_args {
 	const dsimple_t *simple;
 	const drun_t *runs;
 	uint32_t num_runs;
+	const dhgroup_t *hgroups;
+	uint32_t num_hgroups;
+	const dhent_t *hents;
+	uint32_t num_hent;
 	int mode;           /* 0 auto, 1 walk, 2 evaluate-all */
 	odpg_out_t *out;
 	uint16_t *mark;

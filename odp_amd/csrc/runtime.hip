@@ -257,6 +257,10 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.simple = (const dsimple_t *)((const uint8_t *)t->dblob + h.simple_off);
 	a.runs = (const drun_t *)((const uint8_t *)t->dblob + h.run_off);
 	a.num_runs = h.num_runs;
+	a.hgroups = (const dhgroup_t *)((const uint8_t *)t->dblob + h.hgroup_off);
+	a.num_hgroups = h.num_hgroups;
+	a.hents = (const dhent_t *)((const uint8_t *)t->dblob + h.hent_off);
+	a.num_hent = h.num_hent;
 	a.mode = c->kernel_mode;
 	a.out = r->out;
 	a.mark = r->mark;

@@ -164,3 +164,36 @@ def plain64_corpus(n, seed=5):
     keep = plain_wave & (kind >= 10)
     fr[keep] = base[keep]
     return fr.reshape(-1)
+
+
+def simple_mixed_rules(cls, pktio, stats=True):
+    """Single-compare rules only (TBL_SIMPLE): exact-match groups large enough
+    for hash tables, with duplicate values whose first-match order matters,
+    small groups that stay linear, ODP_PMR_LEN, a never-matching LD_VNI rule
+    and a rule with no terms (matches everything)."""
+    T = cls.Term
+    q = cls.queue
+    mk = lambda name, n: cls.cos_create(name, queue=q(n), stats_enable=stats)  # noqa: E731
+    default = mk("default", 0)
+    l1 = [mk(f"l1_{i}", 1 + i) for i in range(8)]
+    leaves = [mk(f"leaf_{i}", 20 + i) for i in range(40)]
+    assert cls.default_cos_set(pktio, default) == 0
+    # default: 8 UDP_DPORT rules (hash group), two share the value 7
+    dports = [7, 3, 7, 9, 11, 13, 0x3f, 1]
+    for i, d in enumerate(dports):
+        assert cls.pmr_create([T(cls.PMR_UDP_DPORT, gen.be_bytes(d, 2), b"\xff\xff")],
+                              default, l1[i], mark=100 + i)
+    # l1[0]: SIP /24 hash group (7 rules) + LEN + never + match-all, order matters
+    for i in range(5):
+        assert cls.pmr_create([T(cls.PMR_SIP_ADDR, gen.be_bytes(gen.ip4(f"192.168.{i}.0"), 4),
+                                 gen.be_bytes(0xFFFFFF00, 4))], l1[0], leaves[i])
+    assert cls.pmr_create([T(cls.PMR_LD_VNI, b"\0\0\0\1", b"\xff\xff\xff\xff")], l1[0], leaves[5])
+    assert cls.pmr_create([T(cls.PMR_LEN, (64).to_bytes(4, "little"), b"\xff\xff\xff\xff")],
+                          l1[0], leaves[6], mark=7)
+    assert cls.pmr_create([], l1[0], leaves[7], mark=8)
+    # l1[1..7]: TCP/UDP sport groups of 7 (hash) and 2 (linear)
+    for a in range(1, 8):
+        for j in range(7 if a % 2 else 2):
+            assert cls.pmr_create([T(cls.PMR_UDP_SPORT, gen.be_bytes((a * 7 + j) & 0xff, 2),
+                                     b"\x00\xff")], l1[a], leaves[(8 + a * 4 + j) % 40])
+    return {"default": default}

@@ -274,3 +274,23 @@ def test_stride64_fast_path_edges(gpu_ctx, fresh_cls, opt):
     assert fresh_cls.pktio_start(p) == 0
     g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, n, stride=64, opt=opt)
     assert_same(g, o, f"fast path C2 opt={opt}")
+
+
+@pytest.mark.parametrize("layout", ["stride64", "desc"])
+def test_simple_table_hash_groups(gpu_ctx, fresh_cls, layout):
+    """TBL_SIMPLE tables: hash groups with duplicate values, linear runs,
+    LEN / never / match-all rules; fast-path and generic waves."""
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    rulesets.simple_mixed_rules(fresh_cls, p)
+    assert fresh_cls.pktio_start(p) == 0
+    if layout == "stride64":
+        n = 64 * 200
+        fr = rulesets.plain64_corpus(n, seed=9)
+        g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, n, stride=64, opt=ALL_CHKSUM)
+    else:
+        frames = rulesets.mutate_corpus(12000, seed=21)
+        buf, desc = pack(frames)
+        g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), buf, len(frames), desc=desc,
+                    opt=ALL_CHKSUM)
+    assert_same(g, o, f"simple/hash {layout}")
+    assert len(np.unique(g["out"] & 0xFFFF)) > 8
