@@ -25,11 +25,22 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/odpg.h"
 #include "odpg_internal.h"
 
 #define BLOCK 256
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+/* streaming 16-byte load of once-read frame data (nontemporal hint) */
+__device__ __forceinline__ uint4 ld_stream(const uint4 *p)
+{
+	const u32x4 v = __builtin_nontemporal_load((const u32x4 *)p);
+
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 #define IF(x)  (1ull << (x))
 #define FB(x)  (1u << (x))
@@ -962,7 +973,7 @@ __device__ __forceinline__ int first_hit_lds(const uint32_t *hrow, uint32_t rs, 
 
 /* ----------------------------------------------------------------------- */
 template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST>
-__global__ __launch_bounds__(BLOCK, 6) void odpg_classify_kernel(
+__global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 	const uint8_t *__restrict__ frames, const odpg_desc_t *__restrict__ desc,
 	uint32_t stride, uint32_t num, uint64_t opt, uint32_t layer, uint32_t classify,
 	const dterm_t *__restrict__ terms, const dpmr_t *__restrict__ pmrs,
@@ -972,6 +983,7 @@ __global__ __launch_bounds__(BLOCK, 6) void odpg_classify_kernel(
 	const drun_t *__restrict__ runs, uint32_t num_runs,
 	const dhgroup_t *__restrict__ hgroups, uint32_t num_hgroups,
 	const dhent_t *__restrict__ hents_g, uint32_t num_hent,
+	const uint2 *__restrict__ cinfo_g, const uint32_t *__restrict__ pinfo_g,
 	odpg_out_t *__restrict__ out, uint16_t *__restrict__ mark_out,
 	odpg_meta_t *__restrict__ meta_out, uint64_t *__restrict__ pk_partial,
 	uint32_t *__restrict__ cos_partial)
@@ -985,6 +997,9 @@ __global__ __launch_bounds__(BLOCK, 6) void odpg_classify_kernel(
 	/* exact-match hash tables, copied to LDS when small */
 	uint2 *hents_l = (uint2 *)(hitmap + (MODE == 2 ? BLOCK * hrw : 0u));
 	const bool hent_in_lds = num_hent <= HENT_LDS_MAX;
+	/* per-lane CoS / PMR lookups of the first-match resolve, in LDS */
+	uint2 *cinfo = hents_l + (hent_in_lds ? num_hent : 0u);
+	uint32_t *pinfo = (uint32_t *)(cinfo + num_cos);
 	__shared__ unsigned long long blk_pk[4];
 
 	const uint32_t tid = threadIdx.x;
@@ -1001,11 +1016,40 @@ __global__ __launch_bounds__(BLOCK, 6) void odpg_classify_kernel(
 	if (MODE != 0 && hent_in_lds)
 		for (uint32_t k = tid; k < num_hent; k += BLOCK)
 			hents_l[k] = *(const uint2 *)(hents_g + k);
+	if (MODE != 0) {
+		for (uint32_t k = tid; k < num_cos; k += BLOCK)
+			cinfo[k] = cinfo_g[k];
+		for (uint32_t k = tid; k < num_pmr; k += BLOCK)
+			pinfo[k] = pinfo_g[k];
+	}
 	__syncthreads();
 	const uint2 *hents = hent_in_lds ? hents_l : (const uint2 *)hents_g;
 
 	/* persistent workgroups: tiles of BLOCK packets */
 	const uint32_t ntiles = (num + BLOCK - 1) / BLOCK;
+	uint32_t fn[16];   /* FAST: next tile's frame, prefetched one tile ahead */
+
+	if constexpr (FAST) {
+		const uint32_t i0 = blockIdx.x * BLOCK + tid;
+
+		if (blockIdx.x < ntiles && i0 < num) {
+			const uint4 *src = (const uint4 *)(frames + (size_t)i0 * 64u);
+
+#pragma unroll
+			for (int k = 0; k < 4; ++k) {
+				const uint4 x = ld_stream(src + k);
+
+				fn[4 * k + 0] = x.x;
+				fn[4 * k + 1] = x.y;
+				fn[4 * k + 2] = x.z;
+				fn[4 * k + 3] = x.w;
+			}
+		} else {
+#pragma unroll
+			for (int k = 0; k < 16; ++k)
+				fn[k] = 0u;
+		}
+	}
 
 	for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
 	const uint32_t blk0 = tile * BLOCK;
@@ -1030,17 +1074,25 @@ __global__ __launch_bounds__(BLOCK, 6) void odpg_classify_kernel(
 	bool wave_fast = false;
 
 	if constexpr (FAST) {
-		/* 64-byte frames straight into 16 registers, 4 x 16 B per lane */
-		const uint4 *src = (const uint4 *)(frames + (size_t)i * 64u);
+		/* 64-byte frames straight into 16 registers, 4 x 16 B per lane;
+		 * this tile's were prefetched, issue the next tile's now */
+#pragma unroll
+		for (int k = 0; k < 16; ++k)
+			f[k] = fn[k];
+		const uint32_t nt = tile + gridDim.x, inx = nt * BLOCK + tid;
+
+		if (nt < ntiles && inx < num) {
+			const uint4 *src = (const uint4 *)(frames + (size_t)inx * 64u);
 
 #pragma unroll
-		for (int k = 0; k < 4; ++k) {
-			uint4 x = live ? src[k] : make_uint4(0u, 0u, 0u, 0u);
+			for (int k = 0; k < 4; ++k) {
+				const uint4 x = ld_stream(src + k);
 
-			f[4 * k + 0] = x.x;
-			f[4 * k + 1] = x.y;
-			f[4 * k + 2] = x.z;
-			f[4 * k + 3] = x.w;
+				fn[4 * k + 0] = x.x;
+				fn[4 * k + 1] = x.y;
+				fn[4 * k + 2] = x.z;
+				fn[4 * k + 3] = x.w;
+			}
 		}
 		const bool plain = live && layer >= LAYER_L4 &&
 				   !(opt & (ODPG_PKTIN_DROP_IPV4_ERR | ODPG_PKTIN_DROP_IPV6_ERR |
@@ -1264,18 +1316,18 @@ __global__ __launch_bounds__(BLOCK, 6) void odpg_classify_kernel(
 			}
 		}
 		while (active) {
-			const dcos_t ce = coses[cos];
-			const int k = MODE == 1 ? first_hit64(hits, ce.rule_start, ce.nrule)
-						: first_hit_lds(hrow, ce.rule_start, ce.nrule);
+			const uint32_t ci = cinfo[cos].x;
+			const uint32_t rs = ci & 0xffffu, nr = ci >> 16;
+			const int k = MODE == 1 ? first_hit64(hits, rs, nr) : first_hit_lds(hrow, rs, nr);
 
 			if (k < 0)
 				break;
-			const dpmr_t pm = pmrs[ce.rule_start + (uint32_t)k];
+			const uint32_t pi = pinfo[rs + (uint32_t)k];
 
-			cos = pm.dst;
-			mark = pm.mark;
+			cos = pi & 0xffffu;
+			mark = pi >> 16;
 			any_match = true;
-			if (do_cos_stats && coses[cos].stats)
+			if (do_cos_stats && ((cinfo[cos].y >> 16) & 0xffu))
 				atomicAdd(&cos_cnt[cos], 1u);
 			if (++steps >= num_cos) {
 				cos = ODPG_COS_LOOP;
@@ -1339,14 +1391,15 @@ __global__ __launch_bounds__(BLOCK, 6) void odpg_classify_kernel(
 		bool err = (p.fl & FL_ERROR_MASK) != 0u;
 		bool at_done = err || !any_match;
 
-		if (do_cos_stats && at_done && cos < num_cos && coses[cos].stats)
+		if (do_cos_stats && at_done && cos < num_cos &&
+		    (MODE != 0 ? ((cinfo[cos].y >> 16) & 0xffu) : coses[cos].stats))
 			atomicAdd(&cos_cnt[cos], 1u);
 
 		if (cos == ODPG_COS_LOOP) {
 			cret = -2;
 		} else if (cos == ODPG_COS_NONE) {
 			cret = -1;
-		} else if (coses[cos].action == 1u) {
+		} else if ((MODE != 0 ? (cinfo[cos].y & 0xffu) : coses[cos].action) == 1u) {
 			cret = 1;
 		} else {
 			cret = 0;
@@ -1368,6 +1421,7 @@ __global__ __launch_bounds__(BLOCK, 6) void odpg_classify_kernel(
 		if (cret == 1)
 			w |= ODPG_OUT_CLS_DROP;
 		if (cret == 0 && want_cls && (tbl_flags & TBL_ANY_HASHQ) && coses[cos].num_queue > 1u) {
+			/* rare path (hash-queue CoS): table read from global */
 			uint32_t h = rss_hash(p, v, coses[cos].hash_proto);
 
 			w |= ((h & 31u) % coses[cos].num_queue) << 24;
@@ -1488,12 +1542,15 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t grid, hipStream
 		lds += (size_t)BLOCK * (((a.num_pmr + 31u) >> 5) | 1u) * 4u;
 	if (MODE != 0 && a.num_hent <= HENT_LDS_MAX)
 		lds += (size_t)a.num_hent * 8u;
+	if (MODE != 0)
+		lds += (size_t)a.num_cos * 8u + (size_t)a.num_pmr * 4u;
 	hipLaunchKernelGGL((odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST>), dim3(grid),
 			   dim3(BLOCK), lds, s, a.frames, a.desc, a.stride, a.num, a.opt, a.layer,
 			   a.classify, a.terms, a.pmrs, a.coses, a.num_cos, a.default_cos,
 			   a.error_cos, a.tbl_flags, a.num_pmr, a.slot_mask, a.slots, a.simple,
-			   a.runs, a.num_runs, a.hgroups, a.num_hgroups, a.hents, a.num_hent, a.out,
-			   a.mark, a.meta, a.pk_partial, a.cos_partial);
+			   a.runs, a.num_runs, a.hgroups, a.num_hgroups, a.hents, a.num_hent,
+			   (const uint2 *)a.cinfo, a.pinfo, a.out, a.mark, a.meta, a.pk_partial,
+			   a.cos_partial);
 	return hipGetLastError();
 }
 
@@ -1546,12 +1603,22 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 	return 0;
 }
 
-/* persistent grid: at most MAX_GRID workgroups, each looping over tiles */
-#define MAX_GRID 2048u
+/* Workgroups loop over tiles; the grid is capped at ODPG_GRID_CAP workgroups
+ * (environment, default below). Capping bounds the per-workgroup counter
+ * partials and the per-workgroup rule-table copy into LDS. */
+#define DEFAULT_GRID_CAP 65536u
 
 extern "C" uint32_t odpg_launch_grid(uint32_t num)
 {
+	static uint32_t cap = 0;
+
+	if (cap == 0) {
+		const char *e = getenv("ODPG_GRID_CAP");
+		long v = e ? strtol(e, nullptr, 0) : 0;
+
+		cap = v > 0 ? (uint32_t)v : DEFAULT_GRID_CAP;
+	}
 	uint32_t tiles = (num + BLOCK - 1) / BLOCK;
 
-	return tiles < MAX_GRID ? tiles : MAX_GRID;
+	return tiles < cap ? tiles : cap;
 }

@@ -246,8 +246,27 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	if (r->default_cos >= (int32_t)r->num_cos || r->error_cos >= (int32_t)r->num_cos)
 		return -EINVAL;
 
-	cos.resize(r->num_cos);
+	/* CoS slots past the last valid or referenced one can never be reached */
+	uint32_t ncos = 0;
+
 	for (uint32_t c = 0; c < r->num_cos; c++) {
+		if (r->cos[c].valid)
+			ncos = c + 1;
+		for (uint32_t i = 0; i < r->cos[c].num_rule && r->cos[c].valid; i++) {
+			uint32_t slot = r->cos[c].rule_start + i;
+
+			if (slot < r->num_slots && r->rule_dst[slot] + 1 > ncos &&
+			    r->rule_dst[slot] < r->num_cos)
+				ncos = r->rule_dst[slot] + 1;
+		}
+	}
+	if (r->default_cos >= 0 && (uint32_t)r->default_cos + 1 > ncos)
+		ncos = (uint32_t)r->default_cos + 1;
+	if (r->error_cos >= 0 && (uint32_t)r->error_cos + 1 > ncos)
+		ncos = (uint32_t)r->error_cos + 1;
+
+	cos.resize(ncos);
+	for (uint32_t c = 0; c < ncos; c++) {
 		const odpg_cos_t *ce = &r->cos[c];
 		dcos_t &d = cos[c];
 
@@ -457,7 +476,7 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.num_runs = is_simple ? (uint32_t)runs.size() : 0;
 	h.num_hgroups = is_simple ? (uint32_t)hgroups.size() : 0;
 	h.num_hent = is_simple ? (uint32_t)hents.size() : 0;
-	h.num_cos = r->num_cos;
+	h.num_cos = ncos;
 	h.default_cos = r->default_cos;
 	h.error_cos = r->error_cos;
 	h.num_pmr = (uint32_t)pmr.size();
@@ -472,6 +491,16 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			h.flags |= TBL_ANY_STATS;
 	}
 
+	std::vector<uint32_t> cinfo(2 * cos.size()), pinfo(pmr.size());
+
+	for (size_t c = 0; c < cos.size(); c++) {
+		cinfo[2 * c] = (cos[c].rule_start & 0xffffu) | ((uint32_t)cos[c].nrule << 16);
+		cinfo[2 * c + 1] = cos[c].action | ((uint32_t)cos[c].num_queue << 8) |
+				   ((uint32_t)cos[c].stats << 16) | ((uint32_t)cos[c].hash_proto << 24);
+	}
+	for (size_t k = 0; k < pmr.size(); k++)
+		pinfo[k] = (pmr[k].dst & 0xffffu) | ((pmr[k].mark & 0xffffu) << 16);
+
 	auto align = [](uint32_t x) { return (x + 63u) & ~63u; };
 	h.term_off = 0;
 	h.slot_off = align(h.term_off + (uint32_t)(terms.size() * sizeof(dterm_t)));
@@ -481,7 +510,9 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.hent_off = align(h.hgroup_off + h.num_hgroups * (uint32_t)sizeof(dhgroup_t));
 	h.pmr_off = align(h.hent_off + h.num_hent * (uint32_t)sizeof(dhent_t));
 	h.cos_off = align(h.pmr_off + (uint32_t)(pmr.size() * sizeof(dpmr_t)));
-	h.blob_bytes = align(h.cos_off + (uint32_t)(cos.size() * sizeof(dcos_t)));
+	h.cinfo_off = align(h.cos_off + (uint32_t)(cos.size() * sizeof(dcos_t)));
+	h.pinfo_off = align(h.cinfo_off + (uint32_t)(cinfo.size() * 4u));
+	h.blob_bytes = align(h.pinfo_off + (uint32_t)(pinfo.size() * 4u));
 	if (h.blob_bytes == 0)
 		h.blob_bytes = 64;
 	blob.assign(h.blob_bytes, 0);
@@ -504,6 +535,10 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		memcpy(blob.data() + h.pmr_off, pmr.data(), pmr.size() * sizeof(dpmr_t));
 	if (!cos.empty())
 		memcpy(blob.data() + h.cos_off, cos.data(), cos.size() * sizeof(dcos_t));
+	if (!cinfo.empty())
+		memcpy(blob.data() + h.cinfo_off, cinfo.data(), cinfo.size() * 4u);
+	if (!pinfo.empty())
+		memcpy(blob.data() + h.pinfo_off, pinfo.data(), pinfo.size() * 4u);
 	*hdr_out = h;
 	return 0;
 }

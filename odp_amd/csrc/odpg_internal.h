@@ -175,9 +175,14 @@ typedef struct dtable_hdr_s {
 	uint32_t num_hgroups;
 	uint32_t hent_off;   /* dhent_t[num_hent] */
 	uint32_t num_hent;
+	uint32_t cinfo_off;  /* uint2[num_cos]: {rule_start | nrule << 16,
+	                      *  action | num_queue << 8 | stats << 16 | hash_proto << 24} */
+	uint32_t pinfo_off;  /* uint32[num_pmr]: dst | mark << 16 */
 	uint32_t slot_mask;  /* key slots any slotted term reads */
 	uint32_t blob_bytes;
 } dtable_hdr_t;
+
+typedef struct uint2_s { uint32_t x, y; } uint2_t;
 
 /* kernel launch arguments (runtime.hip -> classify.hip) */
 #include "../../include/odpg.h"
@@ -203,6 +208,8 @@ typedef struct odpg_launch_args {
 	uint32_t num_hgroups;
 	const dhent_t *hents;
 	uint32_t num_hent;
+	const uint2_t *cinfo;
+	const uint32_t *pinfo;
 	int mode;           /* 0 auto, 1 walk, 2 evaluate-all */
 	odpg_out_t *out;
 	uint16_t *mark;

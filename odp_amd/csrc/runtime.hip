@@ -261,6 +261,8 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.num_hgroups = h.num_hgroups;
 	a.hents = (const dhent_t *)((const uint8_t *)t->dblob + h.hent_off);
 	a.num_hent = h.num_hent;
+	a.cinfo = (const uint2_t *)((const uint8_t *)t->dblob + h.cinfo_off);
+	a.pinfo = (const uint32_t *)((const uint8_t *)t->dblob + h.pinfo_off);
 	a.mode = c->kernel_mode;
 	a.out = r->out;
 	a.mark = r->mark;

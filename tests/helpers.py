@@ -53,6 +53,12 @@ def assert_same(a, b, what=""):
     for k in ("out", "mark", "meta", "stats"):
         if k in a and k in b:
             x, y = a[k], b[k]
+            if k == "stats" and len(x) != len(y):
+                # the compiled table drops never-referenced trailing CoS slots
+                m = min(len(x), len(y))
+                tail = x[m:] if len(x) > m else y[m:]
+                assert not np.any(tail), f"{what}: non-zero counters past CoS {m - 4}"
+                x, y = x[:m], y[:m]
             if k == "meta":
                 x = x.view(np.uint8).reshape(len(x), -1)
                 y = y.view(np.uint8).reshape(len(y), -1)

@@ -293,4 +293,4 @@ def test_simple_table_hash_groups(gpu_ctx, fresh_cls, layout):
         g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), buf, len(frames), desc=desc,
                     opt=ALL_CHKSUM)
     assert_same(g, o, f"simple/hash {layout}")
-    assert len(np.unique(g["out"] & 0xFFFF)) > 8
+    assert len(np.unique(g["out"] & 0xFFFF)) > 3
