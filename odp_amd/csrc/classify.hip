@@ -1532,7 +1532,7 @@ __global__ __launch_bounds__(BLOCK) void odpg_stats_reduce_kernel(
 extern "C" uint32_t odpg_launch_grid(uint32_t num);
 
 template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST = false>
-static hipError_t launch_one(const odpg_launch_args &a, uint32_t grid, hipStream_t s)
+static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStream_t s)
 {
 	size_t lds = (size_t)BLOCK * (W / 4 + 1) * 4u;
 
@@ -1544,6 +1544,25 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t grid, hipStream
 		lds += (size_t)a.num_hent * 8u;
 	if (MODE != 0)
 		lds += (size_t)a.num_cos * 8u + (size_t)a.num_pmr * 4u;
+	/* persistent grid: exactly the workgroups that are resident at once
+	 * (occupancy x CUs), each looping over tiles */
+	static size_t occ_lds = (size_t)-1;
+	static uint32_t occ_grid = 0;
+
+	if (occ_lds != lds) {
+		int nb = 0, dev = 0, cus = 0;
+
+		hipGetDevice(&dev);
+		hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+			    &nb, odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST>, BLOCK, lds) !=
+		    hipSuccess || nb <= 0)
+			nb = 1;
+		occ_grid = (uint32_t)(nb * (cus > 0 ? cus : 256));
+		occ_lds = lds;
+	}
+	if (!getenv("ODPG_GRID_CAP") && grid > occ_grid)
+		grid = occ_grid;
 	hipLaunchKernelGGL((odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST>), dim3(grid),
 			   dim3(BLOCK), lds, s, a.frames, a.desc, a.stride, a.num, a.opt, a.layer,
 			   a.classify, a.terms, a.pmrs, a.coses, a.num_cos, a.default_cos,
@@ -1555,7 +1574,7 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t grid, hipStream
 }
 
 template <int MODE>
-static hipError_t launch_layout(const odpg_launch_args &a, uint32_t grid, hipStream_t s)
+static hipError_t launch_layout(const odpg_launch_args &a, uint32_t &grid, hipStream_t s)
 {
 	if (a.desc)
 		return launch_one<128, false, true, true, MODE>(a, grid, s);
@@ -1603,9 +1622,9 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 	return 0;
 }
 
-/* Workgroups loop over tiles; the grid is capped at ODPG_GRID_CAP workgroups
- * (environment, default below). Capping bounds the per-workgroup counter
- * partials and the per-workgroup rule-table copy into LDS. */
+/* Workgroups loop over tiles. The launch uses the resident grid (occupancy x
+ * CUs, launch_one) unless ODPG_GRID_CAP is set; this is the upper bound that
+ * sizes the per-workgroup counter partials. */
 #define DEFAULT_GRID_CAP 65536u
 
 extern "C" uint32_t odpg_launch_grid(uint32_t num)
