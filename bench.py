@@ -45,6 +45,10 @@ def parse_args():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-mode", type=int, default=0,
                     help="0 auto, 1 wave-cooperative walk, 2 evaluate-all")
+    ap.add_argument("--diag", default="full", choices=["full", "parse", "none"],
+                    help="diagnostic floors (not the metric): 'parse' = parse + checksum "
+                         "verdicts without CoS matching, 'none' = frame loads + result "
+                         "stores only")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-buffer path (pinned H2D + kernel + D2H)")
     return ap.parse_args()
@@ -69,7 +73,7 @@ def main():
     import numpy as np
 
     from odp_amd import _lib as L
-    from odp_amd import cls, gen, gpu
+    from odp_amd import cls, gen, gpu, shard
 
     opt = L.PKTIN_IPV4_CHKSUM | L.PKTIN_UDP_CHKSUM | L.PKTIN_TCP_CHKSUM
     cls.reset()
@@ -113,7 +117,9 @@ def main():
     nstats = 4 + tbl.num_cos
     sbuf = ctx.buffer(8 * nstats)
     sbuf.zero()
-    batches = [L.odpg_batch_t(fb.ptr, None, stride, n, opt, L.LAYER_ALL, 1) for fb in fbufs]
+    layer, do_cls = {"full": (L.LAYER_ALL, 1), "parse": (L.LAYER_ALL, 0),
+                     "none": (L.LAYER_NONE, 0)}[args.diag]
+    batches = [L.odpg_batch_t(fb.ptr, None, stride, n, opt, layer, do_cls) for fb in fbufs]
     results = [L.odpg_result_t(ob.ptr, None, None, None) for ob in obufs]
     res_stats = L.odpg_result_t(obufs[0].ptr, None, None, sbuf.ptr)
     lib = L.lib
@@ -149,15 +155,12 @@ def main():
     kernel_ms = ev_ms.value / max(args.steps, 1)
 
     stats = sbuf.download(np.uint64, nstats)
-    if dist is not None:
-        import torch
-        t = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-        st = torch.tensor(stats.astype(np.int64), device=f"cuda:{local}")
-        dist.all_reduce(st, op=dist.ReduceOp.SUM)      # CoS / pktio counters across GPUs
-        stats = st.cpu().numpy().astype(np.uint64)
-    assert int(stats[0]) == n * world, ("not every packet was delivered", stats[:4])
+    # max wall clock over ranks; CoS / pktio counters summed over GPUs (RCCL)
+    dev = f"cuda:{local}" if dist is not None else None
+    wall = shard.max_over_ranks(wall, dist, dev)
+    stats = shard.reduce_counters(stats, dist, dev)
+    if args.diag == "full":
+        assert int(stats[0]) == n * world, ("not every packet was delivered", stats[:4])
 
     ms_per_step = wall * 1e3 / max(args.steps, 1)
     total_pkts = n * world * args.steps
@@ -192,6 +195,8 @@ def main():
                        "parallelism": f"dp{world} (packet shards, no data-path collective)"},
             "roofline": roofline, "cpu_baseline": cpu,
         }
+        if args.diag != "full":
+            out["diag"] = args.diag
         if args.e2e:
             out["e2e_host_path"] = e2e(ctx, tbl, frames, n, stride, opt)
         print(json.dumps(out), flush=True)

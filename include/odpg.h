@@ -251,6 +251,14 @@ int odpg_memset_dev(odpg_ctx_t *ctx, void *dst, int value, size_t bytes);
 int odpg_event_record(odpg_ctx_t *ctx, int slot);
 int odpg_event_elapsed_ms(odpg_ctx_t *ctx, int slot_a, int slot_b, float *ms);
 
+/* Diagnostic streaming floor (not a classification entry point): read npkt
+ * 64-byte frames at src, write one u32 per frame to out, with access pattern
+ * 0 coalesced / 1 lane-per-frame / 2 coalesced-via-LDS (| 0x10 nontemporal),
+ * over `grid` workgroups (0 = one per 256 frames). Used by tools/ and
+ * DESIGN.md to state the achievable HBM floor of the launch shape. */
+int odpg_diag_stream(odpg_ctx_t *ctx, const void *src, uint32_t npkt, uint32_t *out,
+		     int pattern, uint32_t grid);
+
 #ifdef __cplusplus
 }
 #endif

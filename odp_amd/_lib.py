@@ -213,6 +213,7 @@ SIGNATURES = {
     "odpg_memset_dev": (_i32, [_vp, _vp, _i32, _sz]),
     "odpg_event_record": (_i32, [_vp, _i32]),
     "odpg_event_elapsed_ms": (_i32, [_vp, _i32, _i32, C.POINTER(C.c_float)]),
+    "odpg_diag_stream": (_i32, [_vp, _vp, _u32, _vp, _i32, _u32]),
     # include/odp_cls.h
     "odp_cls_capability": (_i32, [C.POINTER(odp_cls_capability_t)]),
     "odp_cls_cos_param_init": (None, [C.POINTER(odp_cls_cos_param_t)]),

@@ -1023,38 +1023,47 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 			pinfo[k] = pinfo_g[k];
 	}
 	__syncthreads();
-	const uint2 *hents = hent_in_lds ? hents_l : (const uint2 *)hents_g;
+	/* default CoS entry: read once, outside the tile loop */
+	const bool def_valid = default_cos >= 0 && coses[default_cos].valid;
+	const bool def_rules = def_valid && coses[default_cos].nrule != 0u;
 
 	/* persistent workgroups: tiles of BLOCK packets */
 	const uint32_t ntiles = (num + BLOCK - 1) / BLOCK;
 	uint32_t fn[16];   /* FAST: next tile's frame, prefetched one tile ahead */
 
 	if constexpr (FAST) {
-		const uint32_t i0 = blockIdx.x * BLOCK + tid;
-
-		if (blockIdx.x < ntiles && i0 < num) {
-			const uint4 *src = (const uint4 *)(frames + (size_t)i0 * 64u);
+		/* unconditional (index clamped into the batch) so the loads always
+		 * issue and the wait counts on them stay exact */
+		const uint32_t i0 = min(blockIdx.x * BLOCK + tid, num - 1u);
+		const uint4 *src = (const uint4 *)(frames + (size_t)i0 * 64u);
 
 #pragma unroll
-			for (int k = 0; k < 4; ++k) {
-				const uint4 x = ld_stream(src + k);
+		for (int k = 0; k < 4; ++k) {
+			const uint4 x = ld_stream(src + k);
 
-				fn[4 * k + 0] = x.x;
-				fn[4 * k + 1] = x.y;
-				fn[4 * k + 2] = x.z;
-				fn[4 * k + 3] = x.w;
-			}
-		} else {
-#pragma unroll
-			for (int k = 0; k < 16; ++k)
-				fn[k] = 0u;
+			fn[4 * k + 0] = x.x;
+			fn[4 * k + 1] = x.y;
+			fn[4 * k + 2] = x.z;
+			fn[4 * k + 3] = x.w;
 		}
 	}
+	/* result stores of a tile are issued at the top of the next one, before
+	 * that tile's prefetch: vector-memory counters retire in issue order, so
+	 * a store issued after the prefetch would make the next wait on the
+	 * prefetched frame wait on the store too */
+	bool pend = false;
+	uint32_t pend_i = 0u, pend_w = 0u, pend_mk = 0u;
 
 	for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
 	const uint32_t blk0 = tile * BLOCK;
 	const uint32_t i = blk0 + tid;
 	const bool live = i < num;
+
+	if (pend) {
+		out[pend_i] = pend_w;
+		if (mark_out)
+			mark_out[pend_i] = (uint16_t)pend_mk;
+	}
 
 	/* ---- 1. stage the frame window in LDS ---------------------------- */
 	const uint8_t *g;
@@ -1079,20 +1088,18 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 #pragma unroll
 		for (int k = 0; k < 16; ++k)
 			f[k] = fn[k];
-		const uint32_t nt = tile + gridDim.x, inx = nt * BLOCK + tid;
-
-		if (nt < ntiles && inx < num) {
-			const uint4 *src = (const uint4 *)(frames + (size_t)inx * 64u);
+		const uint32_t nt = tile + gridDim.x;
+		const uint32_t inx = min(nt < ntiles ? nt * BLOCK + tid : i, num - 1u);
+		const uint4 *src = (const uint4 *)(frames + (size_t)inx * 64u);
 
 #pragma unroll
-			for (int k = 0; k < 4; ++k) {
-				const uint4 x = ld_stream(src + k);
+		for (int k = 0; k < 4; ++k) {
+			const uint4 x = ld_stream(src + k);
 
-				fn[4 * k + 0] = x.x;
-				fn[4 * k + 1] = x.y;
-				fn[4 * k + 2] = x.z;
-				fn[4 * k + 3] = x.w;
-			}
+			fn[4 * k + 0] = x.x;
+			fn[4 * k + 1] = x.y;
+			fn[4 * k + 2] = x.z;
+			fn[4 * k + 3] = x.w;
 		}
 		const bool plain = live && layer >= LAYER_L4 &&
 				   !(opt & (ODPG_PKTIN_DROP_IPV4_ERR | ODPG_PKTIN_DROP_IPV6_ERR |
@@ -1194,9 +1201,9 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 	if (want_cls) {
 		if (p.fl & FL_ERROR_MASK) {
 			cos = error_cos < 0 ? ODPG_COS_NONE : (uint32_t)error_cos;
-		} else if (default_cos >= 0 && coses[default_cos].valid) {
+		} else if (def_valid) {
 			cos = (uint32_t)default_cos;
-			active = coses[default_cos].nrule != 0;
+			active = def_rules;
 		} else {
 			cos = default_cos < 0 ? ODPG_COS_NONE : (uint32_t)default_cos;
 		}
@@ -1233,7 +1240,30 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 				if (MODE == 2)
 					for (uint32_t w = 0; w < hrw; ++w)
 						hrow[w] = 0u;
-				/* exact-match groups: one probe sequence each */
+				/* exact-match groups: one probe sequence each; the
+				 * entry table is read through an LDS-typed pointer when
+				 * resident (a generic pointer would make each probe wait
+				 * on the outstanding frame prefetch) */
+				auto probe = [&](const uint2 *hents, uint32_t hoff, uint32_t h,
+						 uint32_t szm, uint32_t kvm) {
+					for (uint32_t pr = 0; pr <= szm; ++pr) {
+						const uint2 e = hents[hoff + h];
+
+						if (e.y == HENT_EMPTY)
+							break;
+						if (e.x == kvm) {
+							if (MODE == 1) {
+								const uint64_t bit = 1ull << e.y;
+
+								lo |= (uint32_t)bit;
+								hi |= (uint32_t)(bit >> 32);
+							} else {
+								hrow[e.y >> 5] |= 1u << (e.y & 31u);
+							}
+						}
+						h = (h + 1u) & szm;
+					}
+				};
 				for (uint32_t gi = 0; gi < num_hgroups; ++gi) {
 					const uint4 g0 = *(const uint4 *)(hgroups + gi);
 					const uint2 g1 = *(const uint2 *)((const uint32_t *)(hgroups + gi) + 4);
@@ -1246,25 +1276,12 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 
 					if ((b.inf_lo & hreq) == hreq) {
 						const uint32_t szm = (1u << lg) - 1u;
-						uint32_t h = (kvm * HASH_MUL) >> (32u - lg);
+						const uint32_t h = (kvm * HASH_MUL) >> (32u - lg);
 
-						for (uint32_t pr = 0; pr <= szm; ++pr) {
-							const uint2 e = hents[hoff + h];
-
-							if (e.y == HENT_EMPTY)
-								break;
-							if (e.x == kvm) {
-								if (MODE == 1) {
-									if (e.y < 32u)
-										lo |= 1u << e.y;
-									else
-										hi |= 1u << (e.y - 32u);
-								} else {
-									hrow[e.y >> 5] |= 1u << (e.y & 31u);
-								}
-							}
-							h = (h + 1u) & szm;
-						}
+						if (hent_in_lds)
+							probe(hents_l, hoff, h, szm, kvm);
+						else
+							probe((const uint2 *)hents_g, hoff, h, szm, kvm);
 					}
 				}
 				for (uint32_t r = 0; r < num_runs; ++r) {
@@ -1436,11 +1453,11 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 			w |= ODPG_OUT_MARK_VALID;
 		if (ret)
 			w |= ODPG_OUT_PARSE_ERR;
-		out[i] = w;
 		uint32_t mk = (p.inf & IF(IFL_CLS_MARK)) ? mark : 0u;
 
-		if (mark_out)
-			mark_out[i] = (uint16_t)mk;
+		pend_i = i;
+		pend_w = w;
+		pend_mk = mk;
 		if (meta_out) {
 			odpg_meta_t m;
 
@@ -1464,9 +1481,15 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 		lane_pkt += is_pkt ? 1u : 0u;
 		lane_oct += is_pkt ? (uint64_t)len : 0u;
 	}
+	pend = live;
 	if (COOP)
 		__syncthreads();          /* LDS rows are reused by the next tile */
 	}   /* tile loop */
+	if (pend) {
+		out[pend_i] = pend_w;
+		if (mark_out)
+			mark_out[pend_i] = (uint16_t)pend_mk;
+	}
 
 	/* ---- 6. per-workgroup counter partials ---------------------------- */
 	if (do_stats) {
