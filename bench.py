@@ -35,7 +35,7 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c4"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4"])
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--buffers", type=int, default=0,
                     help="rotating input batches (default: enough to exceed the 256 MiB "
@@ -91,6 +91,13 @@ def main():
         nrules = 1024
         frames_fn = gen.c2_frames
         workload = "C4: 64B IPv4/UDP x 1024 PMR (32x SIP/21 -> 32x31 UDP_DPORT), raised limits"
+    elif args.config == "c3":
+        gen.build_c3_rules(cls, pktio)
+        nrules = 256
+        frames_fn = gen.c3_frames
+        workload = ("C3: IMIX 7:4:1 64/570/1518B, 80/20 IPv4/IPv6, 50/50 UDP/TCP, ~2% "
+                    "checksum errors/zero/fragments x 256 PMR DAG over 63 CoS + error CoS, "
+                    "pktin ipv4+udp+tcp checksum verify, (offset,len) descriptors")
     else:
         gen.build_c2_rules(cls, pktio)
         nrules = 64
@@ -101,25 +108,39 @@ def main():
     rules = cls.pktio_rules(pktio)
 
     n = args.batch
-    stride = 64
     # each rank owns a distinct shard of the synthetic capture
     frames = frames_fn(n, seed=gen.C_SEED + rank)
+    desc = None
+    if isinstance(frames, tuple):            # descriptor layout (C3)
+        frames, desc = frames
+        stride = 0
+        frame_bytes = float(desc["len"].mean())
+        bytes_per_pkt = frame_bytes + 8 + 4  # frame + descriptor + verdict
+    else:
+        stride = 64
+        frame_bytes = stride
+        bytes_per_pkt = stride + 4           # frame + verdict
     ctx = gpu.Context(local)
     ctx.set_kernel_mode(args.kernel_mode)
     tbl = ctx.table(rules)
-    nbuf = args.buffers or max(2, -(-300 * (1 << 20) // (n * stride)))
-    fbufs, obufs = [], []
+    nbuf = args.buffers or max(2, -(-300 * (1 << 20) // frames.nbytes))
+    fbufs, obufs, dbufs = [], [], []
     for _ in range(nbuf):
-        fb = ctx.buffer(n * stride)
+        fb = ctx.buffer(frames.nbytes)
         fb.upload(frames)
         fbufs.append(fb)
+        if desc is not None:
+            db = ctx.buffer(desc.nbytes)
+            db.upload(desc)
+            dbufs.append(db)
         obufs.append(ctx.buffer(4 * n))
     nstats = 4 + tbl.num_cos
     sbuf = ctx.buffer(8 * nstats)
     sbuf.zero()
     layer, do_cls = {"full": (L.LAYER_ALL, 1), "parse": (L.LAYER_ALL, 0),
                      "none": (L.LAYER_NONE, 0)}[args.diag]
-    batches = [L.odpg_batch_t(fb.ptr, None, stride, n, opt, layer, do_cls) for fb in fbufs]
+    batches = [L.odpg_batch_t(fb.ptr, dbufs[k].ptr if dbufs else None, stride, n, opt, layer,
+                              do_cls) for k, fb in enumerate(fbufs)]
     results = [L.odpg_result_t(ob.ptr, None, None, None) for ob in obufs]
     res_stats = L.odpg_result_t(obufs[0].ptr, None, None, sbuf.ptr)
     lib = L.lib
@@ -165,7 +186,6 @@ def main():
     ms_per_step = wall * 1e3 / max(args.steps, 1)
     total_pkts = n * world * args.steps
     value = total_pkts / wall / 1e6
-    bytes_per_pkt = stride + 4
     achieved = bytes_per_pkt * n / (kernel_ms * 1e-3) / 1e9
 
     out = None
@@ -173,7 +193,7 @@ def main():
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": None, "kernel_ms": round(kernel_ms, 5),
-                    "bytes_per_pkt": bytes_per_pkt, "pkts_per_launch": n}
+                    "bytes_per_pkt": round(bytes_per_pkt, 2), "pkts_per_launch": n}
         tf = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
         if os.path.exists(tf):
             try:
@@ -182,14 +202,18 @@ def main():
                 pass
         cpu = None
         if not args.no_cpu and world == 1:
-            cpu = cpu_baseline(rules, frames, n, stride, opt, args)
+            cpu = cpu_baseline(rules, frames, desc, n, stride, opt, args)
         out = {
-            "metric": METRIC if args.config == "c2" else METRIC.replace("64 PMR", f"{nrules} PMR"),
+            "metric": METRIC if args.config == "c2" else (
+                METRIC.replace("64B pkts", "IMIX pkts").replace("64 PMR", f"{nrules} PMR")
+                + " + RX checksum verify" if args.config == "c3"
+                else METRIC.replace("64 PMR", f"{nrules} PMR")),
             "value": round(value, 1), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": workload, "batch_per_gpu": n, "frame_bytes": stride,
+            "config": {"workload": workload, "batch_per_gpu": n,
+                       "frame_bytes": round(frame_bytes, 2),
                        "pmr_rules": nrules, "rotating_buffers": nbuf,
                        "kernel_mode": ["auto", "walk", "evaluate-all"][args.kernel_mode],
                        "parallelism": f"dp{world} (packet shards, no data-path collective)"},
@@ -198,7 +222,7 @@ def main():
         if args.diag != "full":
             out["diag"] = args.diag
         if args.e2e:
-            out["e2e_host_path"] = e2e(ctx, tbl, frames, n, stride, opt)
+            out["e2e_host_path"] = e2e(ctx, tbl, frames, desc, n, stride, opt)
         print(json.dumps(out), flush=True)
     del tbl
     ctx.close()
@@ -206,7 +230,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(rules, frames, n, stride, opt, args):
+def cpu_baseline(rules, frames, desc, n, stride, opt, args):
     """The CPU restatement of linux-generic's classifier (oracle/, a literal
     port of the reference's per-packet path) timed on this host's cores over
     the same batch, ~cpu_seconds of work."""
@@ -220,12 +244,12 @@ def cpu_baseline(rules, frames, n, stride, opt, args):
     sub = min(n, 1 << 18)
     # single-thread calibration pass
     t = time.perf_counter()
-    oracle.classify_mt(rules, frames, sub, stride=stride, opt=opt, nthreads=1, reps=1)
+    oracle.classify_mt(rules, frames, sub, stride=stride, desc=desc, opt=opt, nthreads=1, reps=1)
     one = sub / (time.perf_counter() - t) / 1e6
     reps = max(1, int(args.cpu_seconds * one * threads * 1e6 / n * 0.8))
     t = time.perf_counter()
-    _, used = oracle.classify_mt(rules, frames, n, stride=stride, opt=opt, nthreads=threads,
-                                 reps=reps)
+    _, used = oracle.classify_mt(rules, frames, n, stride=stride, desc=desc, opt=opt,
+                                 nthreads=threads, reps=reps)
     dt = time.perf_counter() - t
     model = ""
     try:
@@ -237,11 +261,11 @@ def cpu_baseline(rules, frames, n, stride, opt, args):
         pass
     return {"value": round(n * reps / dt / 1e6, 2), "unit": "Mpps", "cores": used,
             "kind": "port", "value_1thread": round(one, 2), "cpu_model": model,
-            "sample": f"{reps} passes x {n} pkts of the same C2 batch in host DRAM "
+            "sample": f"{reps} passes x {n} pkts of the same {args.config.upper()} batch in host DRAM "
                       f"({dt:.1f} s, {used} threads)"}
 
 
-def e2e(ctx, tbl, frames, n, stride, opt):
+def e2e(ctx, tbl, frames, desc, n, stride, opt):
     """Host (pinned) buffers -> H2D -> classify -> D2H verdicts, double-buffered."""
     import ctypes as C
 
@@ -254,7 +278,13 @@ def e2e(ctx, tbl, frames, n, stride, opt):
     ho = C.c_void_p()
     L.check(lib.odpg_host_alloc_pinned(4 * n, C.byref(ho)), "pinned")
     C.memmove(hp.value, frames.ctypes.data, frames.nbytes)
-    b = L.odpg_batch_t(hp.value, None, stride, n, opt, L.LAYER_ALL, 1)
+    dptr = None
+    if desc is not None:
+        hd = C.c_void_p()
+        L.check(lib.odpg_host_alloc_pinned(desc.nbytes, C.byref(hd)), "pinned")
+        C.memmove(hd.value, desc.ctypes.data, desc.nbytes)
+        dptr = hd.value
+    b = L.odpg_batch_t(hp.value, dptr, stride, n, opt, L.LAYER_ALL, 1)
     r = L.odpg_result_t(ho.value, None, None, None)
     res = {}
     for chunk in (1 << 16, 1 << 18):
@@ -265,8 +295,10 @@ def e2e(ctx, tbl, frames, n, stride, opt):
             L.check(lib.odpg_classify_host(ctx.h, tbl.h, C.byref(b), C.byref(r), chunk), "host")
         dt = (time.perf_counter() - t) / reps
         res[f"chunk_{chunk}"] = {"mpps": round(n / dt / 1e6, 1),
-                                 "gbps_h2d": round(n * stride / dt / 1e9, 2)}
+                                 "gbps_h2d": round(frames.nbytes / dt / 1e9, 2)}
     lib.odpg_host_free_pinned(hp.value)
+    if dptr:
+        lib.odpg_host_free_pinned(dptr)
     lib.odpg_host_free_pinned(ho.value)
     del np
     return res

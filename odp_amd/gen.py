@@ -267,3 +267,129 @@ def build_c4_rules(cls, pktio, n_l1=32, per_l1=31):
     assert default and all(l1) and all(pmrs)
     assert cls.default_cos_set(pktio, default) == 0
     return {"default": default, "l1": l1, "pmrs": pmrs}
+
+
+# ---- C3: IMIX + 256 PMR DAG + RX checksum verify ----------------------------
+IMIX_SIZES = (64, 570, 1518)       # 7:4:1, mean 353.83 B
+
+
+def c3_frames(n, seed=C_SEED, align=64):
+    """C3 traffic: IMIX 7:4:1 of 64/570/1518 B, 80 % IPv4 /
+    20 % IPv6, 50/50 UDP/TCP (64 B IPv6 frames are UDP: a TCP header does not
+    fit), valid checksums except: 0.5 % bad IPv4 header checksum, 0.5 % bad
+    L4 checksum, 0.5 % IPv4/UDP checksum 0, 0.5 % IPv4 fragments (MF set).
+    Returns (buf u8, desc DESC_DT[n]); frames start `align`-aligned."""
+    r = xorshift64(seed ^ 0xC3C3, n)
+    r2 = xorshift64(seed ^ 0x5A5A3C3, n)
+    sz_i = (r % np.uint64(12)).astype(np.int64)
+    size = np.where(sz_i < 7, 64, np.where(sz_i < 11, 570, 1518))
+    v6 = ((r >> np.uint64(8)) % np.uint64(5)) == 0
+    tcp = (((r >> np.uint64(12)) & np.uint64(1)) == 1) & ~(v6 & (size == 64))
+    m16 = np.uint64(0xFFFF)
+    src = np.uint64(ip4("10.0.0.0")) + ((r >> np.uint64(16)) & m16)
+    dst = np.uint64(ip4("10.1.0.0")) + ((r >> np.uint64(32)) & m16)
+    sport = (r2 & m16).astype(np.int64)
+    dport = ((r2 >> np.uint64(16)) & np.uint64(63)).astype(np.int64)
+    special = ((r2 >> np.uint64(24)) % np.uint64(1000)).astype(np.int64)
+
+    alen = (size + align - 1) // align * align
+    offs = np.zeros(n, np.int64)
+    if n:
+        offs[1:] = np.cumsum(alen)[:-1]
+    total = int(alen.sum()) if n else 0
+    buf = np.zeros(total + 64, np.uint8)
+    desc = np.zeros(n, DESC_DT)
+    desc["offset"] = offs
+    desc["len"] = size
+    for length in IMIX_SIZES:
+        for is6 in (False, True):
+            for is_tcp in (False, True):
+                idx = np.nonzero((size == length) & (v6 == is6) & (tcp == is_tcp))[0]
+                if len(idx) == 0:
+                    continue
+                proto = PROTO_TCP if is_tcp else PROTO_UDP
+                if is6:
+                    a = ipv6_frames(len(idx), length, src[idx], dst[idx], proto, sport[idx],
+                                    dport[idx], payload_seed=int(idx[0]) + 11)
+                else:
+                    a = ipv4_frames(len(idx), length, src[idx], dst[idx], proto, sport[idx],
+                                    dport[idx], payload_seed=int(idx[0]) + 7)
+                    sp = special[idx]
+                    l4 = 34
+                    # fragments (MF), header checksum recomputed
+                    fr = np.nonzero((sp >= 15) & (sp < 20))[0]
+                    if len(fr):
+                        a[fr, 14 + 6] |= 0x20
+                        a[fr, 24:26] = 0
+                        c = csum(ones_sum(a[fr], 14, 34))
+                        a[fr, 24] = (c >> 8) & 0xFF
+                        a[fr, 25] = c & 0xFF
+                    if not is_tcp:
+                        z = np.nonzero((sp >= 10) & (sp < 15))[0]
+                        a[z, l4 + 6:l4 + 8] = 0
+                    bad3 = np.nonzero(sp < 5)[0]
+                    a[bad3, 25] ^= 0x01
+                bad4 = np.nonzero((special[idx] >= 5) & (special[idx] < 10))[0]
+                a[bad4, length - 1] ^= 0x5A
+                rows = offs[idx][:, None] + np.arange(length)[None, :]
+                buf[rows] = a
+    return buf, desc
+
+
+def c3_term_menu(cls, k, h):
+    """The k-th PMR's terms for the C3 DAG (h: a per-PMR hash). Values are
+    drawn from the C3 traffic distributions so every kind both hits and
+    misses; the mix covers the slotted, exact-match and generic compare
+    paths."""
+    T = cls.Term
+    x = h & 15
+    kind = k % 11
+    if kind == 0:
+        return [T(cls.PMR_SIP_ADDR, be_bytes(ip4("10.0.0.0") | (x << 12), 4),
+                  be_bytes(0xFFFFF000, 4))]
+    if kind == 1:
+        return [T(cls.PMR_DIP_ADDR, be_bytes(ip4("10.1.0.0") | (x << 12), 4),
+                  be_bytes(0xFFFFF000, 4))]
+    if kind == 2:
+        return [T(cls.PMR_UDP_DPORT, be_bytes(h & 63, 2), b"\xff\xff")]
+    if kind == 3:
+        return [T(cls.PMR_TCP_DPORT, be_bytes(h & 63, 2), b"\xff\xff")]
+    if kind == 4:
+        return [T(cls.PMR_IPPROTO, bytes([PROTO_TCP if h & 1 else PROTO_UDP]), b"\xff")]
+    if kind == 5:
+        return [T(cls.PMR_SIP6_ADDR, bytes(12) + be_bytes(x, 4),
+                  bytes(12) + be_bytes(0xF, 4))]
+    if kind == 6:
+        return [T(cls.PMR_ETHTYPE_0, be_bytes(ETH_IPV6 if h & 1 else ETH_IPV4, 2), b"\xff\xff")]
+    if kind == 7:
+        return [T(cls.PMR_LEN, int(IMIX_SIZES[h % 3]).to_bytes(4, "little"), b"\xff\xff\xff\xff")]
+    if kind == 8:
+        return [T(cls.PMR_IP_DSCP, bytes([0]), bytes([0x3F]))]
+    if kind == 9:
+        return [T(cls.PMR_SIP_ADDR, be_bytes(ip4("10.0.0.0") | (x << 8), 4),
+                  be_bytes(0xFFFF0F00, 4)),
+                T(cls.PMR_UDP_DPORT, be_bytes(h & 7, 2), be_bytes(7, 2))]
+    return [T(cls.PMR_CUSTOM_L3, bytes([PROTO_UDP]), b"\xff", offset=9, val_sz=1)]
+
+
+def build_c3_rules(cls, pktio, stats=False, seed=0xC3):
+    """C3: 256 PMRs as a DAG over 63 CoS (8 PMRs on each
+    of CoS 0..31, destination index > source index), CoS 0 the default, CoS
+    63 the error CoS (checksum / header errors). Mixed term kinds."""
+    coses = [cls.cos_create(f"c3_{i}", queue=cls.queue(i), stats_enable=stats)
+             for i in range(63)]
+    err = cls.cos_create("c3_error", queue=cls.queue(63), stats_enable=stats)
+    assert all(coses) and err
+    assert cls.default_cos_set(pktio, coses[0]) == 0
+    assert cls.error_cos_set(pktio, err) == 0
+    hs = xorshift64(seed, 256)
+    pmrs = []
+    for c in range(32):
+        for j in range(8):
+            k = c * 8 + j
+            h = int(hs[k] >> np.uint64(8))
+            d = c + 1 + (h >> 12) % (62 - c)
+            p = cls.pmr_create(c3_term_menu(cls, k, h), coses[c], coses[d], mark=(k + 1) & 0xFFFF)
+            assert p, ("pmr", k)
+            pmrs.append(p)
+    return {"coses": coses, "error": err, "pmrs": pmrs}

@@ -294,3 +294,32 @@ def test_simple_table_hash_groups(gpu_ctx, fresh_cls, layout):
                     opt=ALL_CHKSUM)
     assert_same(g, o, f"simple/hash {layout}")
     assert len(np.unique(g["out"] & 0xFFFF)) > 3
+
+
+@pytest.mark.parametrize("n", [1, 257, 1 << 15])
+def test_c3_imix_dag(gpu_ctx, fresh_cls, n):
+    """C3: IMIX 64/570/1518 B, IPv4/IPv6, UDP/TCP, checksum errors / zero /
+    fragments, 256-PMR DAG with mixed term kinds, error CoS, descriptors."""
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    gen.build_c3_rules(fresh_cls, p, stats=True)
+    assert fresh_cls.pktio_start(p) == 0
+    buf, desc = gen.c3_frames(n)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), buf, n, desc=desc, opt=ALL_CHKSUM)
+    assert_same(g, o, "c3")
+
+
+def test_c3_host_path(gpu_ctx, fresh_cls):
+    """C3 through the pinned-host path (chunked H2D of variable-length frames)."""
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    gen.build_c3_rules(fresh_cls, p, stats=True)
+    assert fresh_cls.pktio_start(p) == 0
+    n = 20000
+    buf, desc = gen.c3_frames(n, seed=99)
+    rules = fresh_cls.pktio_rules(p)
+    tbl = gpu_ctx.table(rules)
+    h = gpu_ctx.classify_host(tbl, buf, n, desc=desc, opt=ALL_CHKSUM, chunk=3000,
+                              want_mark=True)
+    o = oracle.classify(rules, buf, n, desc=desc, opt=ALL_CHKSUM)
+    np.testing.assert_array_equal(h["out"], o["out"])
+    np.testing.assert_array_equal(h["mark"], o["mark"])
+    np.testing.assert_array_equal(h["stats"], o["stats"])

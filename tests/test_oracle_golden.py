@@ -124,3 +124,29 @@ def test_crc32c_known_answer():
     # RFC 3720 B.4: CRC32C of 32 zero bytes = 0x8A9136AA (with ~init/~final)
     assert (~oracle.crc32c(bytes(32), 0xFFFFFFFF)) & 0xFFFFFFFF == 0x8A9136AA
     assert (~oracle.crc32c(bytes([0xFF] * 32), 0xFFFFFFFF)) & 0xFFFFFFFF == 0x62A8AB43
+
+
+def test_c3_traffic_shape(fresh_cls):
+    """The C3 generator's mix as the oracle sees it: IMIX mean near 353.8 B,
+    ~20 % IPv6 (L3 checksum UNKNOWN), ~0.5 % bad L3 / ~0.5 % bad L4
+    checksums (all routed to the error CoS), several CoS of the DAG hit."""
+    from odp_amd import _lib as L
+    from odp_amd import gen
+    opt = L.PKTIN_IPV4_CHKSUM | L.PKTIN_UDP_CHKSUM | L.PKTIN_TCP_CHKSUM
+    p = fresh_cls.loop_pktio(pktin=opt)
+    r = gen.build_c3_rules(fresh_cls, p, stats=True)
+    assert len(r["pmrs"]) == 256
+    assert fresh_cls.pktio_start(p) == 0
+    n = 40000
+    buf, desc = gen.c3_frames(n)
+    assert abs(desc["len"].mean() - 353.83) < 8
+    assert (desc["offset"] % 16 == 0).all()
+    o = oracle.classify(fresh_cls.pktio_rules(p), buf, n, desc=desc, opt=opt)
+    out = o["out"]
+    l3 = (out >> 16) & 3
+    l4 = (out >> 18) & 3
+    assert 0.15 < (l3 == 0).mean() < 0.25
+    assert 0.002 < (l3 == 2).mean() < 0.01 and 0.002 < (l4 == 2).mean() < 0.01
+    err = (out >> 20) & 1
+    assert ((out & 0xFFFF)[err == 1] == 63).all()       # error CoS
+    assert len(np.unique(out & 0xFFFF)) > 8
