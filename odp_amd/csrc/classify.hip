@@ -159,17 +159,35 @@ __device__ uint32_t sum_range(const Pkt<W, GF> &v, uint32_t a, uint32_t b)
 				x &= (1u << (8u * (b & 3u))) - 1u;
 			s = oc_add(s, x);
 		}
-		while (w + 4u <= w1) {
+		/* whole 16-byte chunks: 64-bit accumulation (one add per word),
+		 * four loads in flight per step; folded end-around below, which
+		 * keeps the residue mod 0xffff (0xffffffff = 0xffff * 0x10001) */
+		uint64_t acc = 0ull;
+
+		if (w == w0 && (a & 3u) && w + 4u <= w1) {
 			uint4 q = *(const uint4 *)(v.g + 4u * w);
 
-			if (w == w0 && (a & 3u))
-				q.x &= 0xffff0000u;
-			s = oc_add(s, q.x);
-			s = oc_add(s, q.y);
-			s = oc_add(s, q.z);
-			s = oc_add(s, q.w);
+			acc += (uint64_t)(q.x & 0xffff0000u) + q.y + q.z + q.w;
 			w += 4u;
 		}
+		while (w + 16u <= w1) {
+			const uint4 *gp = (const uint4 *)(v.g + 4u * w);
+			const uint4 q0 = gp[0], q1 = gp[1], q2 = gp[2], q3 = gp[3];
+
+			acc += (uint64_t)q0.x + q0.y + q0.z + q0.w;
+			acc += (uint64_t)q1.x + q1.y + q1.z + q1.w;
+			acc += (uint64_t)q2.x + q2.y + q2.z + q2.w;
+			acc += (uint64_t)q3.x + q3.y + q3.z + q3.w;
+			w += 16u;
+		}
+		while (w + 4u <= w1) {
+			const uint4 q = *(const uint4 *)(v.g + 4u * w);
+
+			acc += (uint64_t)q.x + q.y + q.z + q.w;
+			w += 4u;
+		}
+		acc = (acc & 0xffffffffull) + (acc >> 32);
+		s = oc_add(oc_add(s, (uint32_t)acc), (uint32_t)(acc >> 32));
 		for (; w <= w1; ++w) {
 			uint32_t x = v.word(w);
 
@@ -972,7 +990,11 @@ __device__ __forceinline__ int first_hit_lds(const uint32_t *hrow, uint32_t rs, 
 }
 
 /* ----------------------------------------------------------------------- */
-template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST>
+/* LEAN: launch-time specialisation for the common production shape, a
+ * TBL_SIMPLE table without hash-queue CoS, verdict words only (no marks,
+ * metadata or counters): the unused paths compile out, which frees the
+ * scalar registers the general kernel spills. Results are identical. */
+template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST, bool LEAN>
 __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 	const uint8_t *__restrict__ frames, const odpg_desc_t *__restrict__ desc,
 	uint32_t stride, uint32_t num, uint64_t opt, uint32_t layer, uint32_t classify,
@@ -1003,6 +1025,13 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 	__shared__ unsigned long long blk_pk[4];
 
 	const uint32_t tid = threadIdx.x;
+	if constexpr (LEAN) {
+		mark_out = nullptr;
+		meta_out = nullptr;
+		pk_partial = nullptr;
+		cos_partial = nullptr;
+		tbl_flags = (tbl_flags | TBL_SIMPLE) & ~(TBL_GENERIC | TBL_ANY_HASHQ);
+	}
 	const bool do_stats = pk_partial != nullptr;
 	const bool do_cos_stats = cos_partial != nullptr;
 	uint32_t *row = smem + tid * RW;
@@ -1554,7 +1583,7 @@ __global__ __launch_bounds__(BLOCK) void odpg_stats_reduce_kernel(
 
 extern "C" uint32_t odpg_launch_grid(uint32_t num);
 
-template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST = false>
+template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST = false, bool LEAN = false>
 static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStream_t s)
 {
 	size_t lds = (size_t)BLOCK * (W / 4 + 1) * 4u;
@@ -1578,7 +1607,7 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 		hipGetDevice(&dev);
 		hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
 		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-			    &nb, odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST>, BLOCK, lds) !=
+			    &nb, odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST, LEAN>, BLOCK, lds) !=
 		    hipSuccess || nb <= 0)
 			nb = 1;
 		occ_grid = (uint32_t)(nb * (cus > 0 ? cus : 256));
@@ -1586,7 +1615,7 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 	}
 	if (!getenv("ODPG_GRID_CAP") && grid > occ_grid)
 		grid = occ_grid;
-	hipLaunchKernelGGL((odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST>), dim3(grid),
+	hipLaunchKernelGGL((odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST, LEAN>), dim3(grid),
 			   dim3(BLOCK), lds, s, a.frames, a.desc, a.stride, a.num, a.opt, a.layer,
 			   a.classify, a.terms, a.pmrs, a.coses, a.num_cos, a.default_cos,
 			   a.error_cos, a.tbl_flags, a.num_pmr, a.slot_mask, a.slots, a.simple,
@@ -1602,6 +1631,12 @@ static hipError_t launch_layout(const odpg_launch_args &a, uint32_t &grid, hipSt
 	if (a.desc)
 		return launch_one<128, false, true, true, MODE>(a, grid, s);
 	if (a.stride == 64) {
+		const bool lean = (a.tbl_flags & TBL_SIMPLE) &&
+				  !(a.tbl_flags & (TBL_GENERIC | TBL_ANY_HASHQ)) && !a.mark &&
+				  !a.meta && !a.stats;
+
+		if (MODE == 1 && lean)
+			return launch_one<64, false, false, false, 1, true, true>(a, grid, s);
 		if (MODE != 0)   /* register fast path for plain frames */
 			return launch_one<64, false, false, false, MODE, true>(a, grid, s);
 		return launch_one<64, true, false, false, MODE>(a, grid, s);
