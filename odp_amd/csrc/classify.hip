@@ -34,12 +34,13 @@
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-/* streaming 16-byte load of once-read frame data (nontemporal hint) */
+/* 16-byte load of once-read frame data. Lane-per-frame loads (lanes 64 B
+ * apart) use the default cache policy: with the nontemporal hint the same
+ * pattern streams at 3.7 TB/s instead of 5.5 (tools/diag_stream.py,
+ * patterns 1 vs 17). */
 __device__ __forceinline__ uint4 ld_stream(const uint4 *p)
 {
-	const u32x4 v = __builtin_nontemporal_load((const u32x4 *)p);
-
-	return make_uint4(v.x, v.y, v.z, v.w);
+	return *p;
 }
 
 #define IF(x)  (1ull << (x))

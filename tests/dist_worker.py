@@ -40,7 +40,8 @@ def main():
     mine = np.ascontiguousarray(frames[start:start + count])
     if a.engine == "gpu":
         from odp_amd import gpu
-        ctx = gpu.Context(int(os.environ.get("LOCAL_RANK", "0")))
+        ndev = max(1, L.lib.odpg_device_count())     # ranks may share one GPU
+        ctx = gpu.Context(int(os.environ.get("LOCAL_RANK", "0")) % ndev)
         tbl = ctx.table(rules)
         res = ctx.classify(tbl, mine, count, stride=64, opt=opt)
         out, stats = res["out"], res["stats"]
