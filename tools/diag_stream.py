@@ -48,7 +48,7 @@ def main():
             ms = C.c_float(0)
             L.check(lib.odpg_event_elapsed_ms(ctx.h, 0, 1, C.byref(ms)), "event")
             us = ms.value * 1e3 / a.steps
-            print(json.dumps({"pattern": pat, "grid": grid, "us": round(us, 2),
+            print(json.dumps({"npkt": n, "pattern": pat, "grid": grid, "us": round(us, 2),
                               "GBps": round(68 * n / (us * 1e-6) / 1e9, 1),
                               "Mpps": round(n / us, 1)}), flush=True)
 
