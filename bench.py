@@ -45,7 +45,8 @@ def parse_args():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-mode", type=int, default=0,
                     help="0 auto, 1 wave-cooperative walk, 2 evaluate-all")
-    ap.add_argument("--diag", default="full", choices=["full", "parse", "none"],
+    ap.add_argument("--diag", default="full",
+                    choices=["full", "parse", "parse-nochk", "l3", "none"],
                     help="diagnostic floors (not the metric): 'parse' = parse + checksum "
                          "verdicts without CoS matching, 'none' = frame loads + result "
                          "stores only")
@@ -138,7 +139,10 @@ def main():
     sbuf = ctx.buffer(8 * nstats)
     sbuf.zero()
     layer, do_cls = {"full": (L.LAYER_ALL, 1), "parse": (L.LAYER_ALL, 0),
+                     "parse-nochk": (L.LAYER_ALL, 0), "l3": (L.LAYER_L3, 0),
                      "none": (L.LAYER_NONE, 0)}[args.diag]
+    if args.diag in ("parse-nochk", "l3"):
+        opt = 0
     batches = [L.odpg_batch_t(fb.ptr, dbufs[k].ptr if dbufs else None, stride, n, opt, layer,
                               do_cls) for k, fb in enumerate(fbufs)]
     results = [L.odpg_result_t(ob.ptr, None, None, None) for ob in obufs]

@@ -210,8 +210,9 @@ int         odpg_device_count(void);
 int  odpg_ctx_create(int device, void *stream, odpg_ctx_t **ctx);
 void odpg_ctx_destroy(odpg_ctx_t *ctx);
 void *odpg_ctx_stream(odpg_ctx_t *ctx);
-/* Kernel strategy: 0 = auto (evaluate-all for tables up to 1024 compiled
- * PMRs, wave-cooperative walk above), 1 = walk, 2 = evaluate-all. All
+/* Kernel strategy: 0 = auto (evaluate-all for tables of single-word compares
+ * up to 1024 PMRs, which compile to exact-match groups; the wave-cooperative
+ * walk otherwise), 1 = walk, 2 = evaluate-all. All
  * strategies produce identical results; this only selects the code path. */
 int  odpg_ctx_set_kernel_mode(odpg_ctx_t *ctx, int mode);
 int  odpg_ctx_sync(odpg_ctx_t *ctx);

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libodpg.so")
+# ODPG_LIB selects another build of the same library (A/B kernel experiments)
+LIB_PATH = os.environ.get("ODPG_LIB") or os.path.join(_HERE, "lib", "libodpg.so")
 
 # ---- constants mirrored from include/odpg.h -------------------------------
 ODPG_COS_NONE = 0xFFFF

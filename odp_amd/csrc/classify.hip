@@ -369,10 +369,25 @@ __device__ __forceinline__ uint32_t parse_ipv6(Prs &p, const Pkt<W, GF> &v, uint
 	return next_hdr;
 }
 
+/* UDP / TCP checksum of a frame longer than the LDS window, left for the
+ * wave-cooperative tail pass (coop_tail_sums): the partial sum of the
+ * pseudo header + window bytes and the byte range [a, b) still to add */
+struct L4Pend {
+	uint32_t kind;      /* 0 none, 1 UDP, 2 TCP */
+	uint32_t sum;
+	uint32_t a, b;
+};
+
+#define PARSE_PEND 2
+
 /* _odp_packet_parse_common (odp_parse_internal.h:80-112) incl. the L3/L4
- * switch (odp_parse.c:360-475) and _odp_packet_l4_chksum (odp_packet.c:1906-1984) */
+ * switch (odp_parse.c:360-475) and _odp_packet_l4_chksum (odp_packet.c:1906-1984).
+ * With a non-null `pend` (global-tail kernels) the UDP/TCP checksum of a frame
+ * longer than the window returns PARSE_PEND instead; finish_l4() applies the
+ * verdict once the tail sum is known. */
 template <int W, bool GF>
-__device__ int parse_common(Prs &p, const Pkt<W, GF> &v, uint32_t layer, uint64_t opt)
+__device__ int parse_common(Prs &p, const Pkt<W, GF> &v, uint32_t layer, uint64_t opt,
+			    L4Pend *pend = nullptr)
 {
 	uint32_t off = 0, len = v.len, seg_end = v.len;
 	uint32_t l4sum = 0;
@@ -503,6 +518,16 @@ __device__ int parse_common(Prs &p, const Pkt<W, GF> &v, uint32_t layer, uint64_
 	/* _odp_packet_l4_chksum (odp_packet.c:1906-1984) */
 	uint64_t inf = p.inf;
 
+	if (GF && pend && len > (uint32_t)W &&
+	    (((opt & ODPG_PKTIN_UDP_CHKSUM) && (inf & IF(IFL_UDP)) && !(inf & IF(IFL_IPFRAG)) &&
+	      !(inf & IF(IFL_UDP_CHKSUM_ZERO))) ||
+	     ((opt & ODPG_PKTIN_TCP_CHKSUM) && (inf & IF(IFL_TCP)) && !(inf & IF(IFL_IPFRAG))))) {
+		pend->kind = (inf & IF(IFL_UDP)) ? 1u : 2u;
+		pend->sum = oc_add(l4sum, sum_range(v, p.l4, (uint32_t)W));
+		pend->a = p.l4 > (uint32_t)W ? p.l4 : (uint32_t)W;
+		pend->b = len;
+		return PARSE_PEND;
+	}
 	if ((opt & ODPG_PKTIN_UDP_CHKSUM) && (inf & IF(IFL_UDP)) && !(inf & IF(IFL_IPFRAG)) &&
 	    !(inf & IF(IFL_UDP_CHKSUM_ZERO))) {
 		uint32_t s = oc_add(l4sum, sum_range(v, p.l4, len));
@@ -537,34 +562,175 @@ __device__ int parse_common(Prs &p, const Pkt<W, GF> &v, uint32_t layer, uint64_
 	return (p.fl & FL_ERROR_MASK) != 0u;
 }
 
+/* verdict of a PARSE_PEND checksum (the UDP / TCP steps of
+ * _odp_packet_l4_chksum, odp_packet.c:1927-1964) given the tail sum */
+__device__ __forceinline__ int finish_l4(Prs &p, const L4Pend &pd, uint32_t tail, uint64_t opt)
+{
+	const uint32_t s = oc_add(pd.sum, tail);
+
+	p.inf |= IF(IFL_L4_CHKSUM_DONE);
+	if (oc_fold(s) != 0xffffu) {
+		if (pd.kind == 1u) {
+			p.fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_UDP_ERR);
+			if (opt & ODPG_PKTIN_DROP_UDP_ERR)
+				return -1;
+		} else {
+			p.fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_TCP_ERR);
+			if (opt & ODPG_PKTIN_DROP_TCP_ERR)
+				return -1;
+		}
+	}
+	return (p.fl & FL_ERROR_MASK) != 0u;
+}
+
+/* one's-complement sum over the 64 lanes (DPP row prefix, then the four
+ * row totals); every lane must be active */
+__device__ __forceinline__ uint32_t wave_oc_sum(uint32_t x)
+{
+	x = oc_add(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true));
+	x = oc_add(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true));
+	x = oc_add(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true));
+	x = oc_add(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true));
+	uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+
+	r = oc_add(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 31));
+	r = oc_add(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 47));
+	return oc_add(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 63));
+}
+
+/* 16 frame bytes at gp + off restricted to [a, b), summed as LE words */
+__device__ __forceinline__ uint64_t chunk_sum(const uint8_t *gp, uint32_t off, uint32_t a,
+					      uint32_t b)
+{
+	if (off >= b || off + 16u <= a)
+		return 0ull;
+	uint4 q = *(const uint4 *)(gp + off);
+	uint32_t w[4] = {q.x, q.y, q.z, q.w};
+	uint64_t acc = 0ull;
+
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		const int lo = (int)a - (int)(off + 4u * k), hi = (int)b - (int)(off + 4u * k);
+		uint32_t m = 0xffffffffu;
+
+		if (hi < 4)
+			m = hi <= 0 ? 0u : (1u << (8 * hi)) - 1u;
+		if (lo > 0)
+			m &= lo >= 4 ? 0u : ~((1u << (8 * lo)) - 1u);
+		acc += w[k] & m;
+	}
+	return acc;
+}
+
+/* Wave-cooperative sums of the frame tails [a, b) of the lanes in `m`: the
+ * whole wave reads one frame's tail with coalesced 16-byte loads (1 KiB per
+ * wave instruction), four frames at a time so their loads overlap, and
+ * reduces each across lanes. Lane j receives the sum of its own tail. */
+#ifndef COOP_BATCH
+#define COOP_BATCH 4
+#endif
+__device__ __forceinline__ uint32_t coop_tail_sums(uint64_t m, const uint8_t *g, const L4Pend &pd)
+{
+	const uint32_t lane = __lane_id();
+	uint32_t mine = 0u;
+
+#ifdef ODPG_EXP_NOTAIL      /* experiment builds only: cost without the tail reads */
+	return 0u;
+#endif
+	while (m) {
+		int jj[COOP_BATCH];
+		uint32_t cnt = 0;
+
+#pragma unroll
+		for (int k = 0; k < COOP_BATCH; ++k) {
+			jj[k] = m ? __builtin_ctzll(m) : -1;
+			if (m) {
+				m &= m - 1ull;
+				++cnt;
+			}
+		}
+		uint64_t acc[COOP_BATCH];
+
+#pragma unroll
+		for (int k = 0; k < COOP_BATCH; ++k) {
+			acc[k] = 0ull;
+			if (jj[k] >= 0) {
+				const uint64_t gv = (uint64_t)(uintptr_t)g;
+				const uint32_t glo = __builtin_amdgcn_readlane((int)(uint32_t)gv, jj[k]);
+				const uint32_t ghi = __builtin_amdgcn_readlane((int)(uint32_t)(gv >> 32), jj[k]);
+				const uint8_t *gp = (const uint8_t *)(uintptr_t)(((uint64_t)ghi << 32) | glo);
+				const uint32_t a = __builtin_amdgcn_readlane((int)pd.a, jj[k]);
+				const uint32_t b = __builtin_amdgcn_readlane((int)pd.b, jj[k]);
+				const uint32_t c0 = (a & ~15u) + 16u * lane;
+
+				acc[k] = chunk_sum(gp, c0, a, b) + chunk_sum(gp, c0 + 1024u, a, b);
+				for (uint32_t c = c0 + 2048u; c < b; c += 1024u)   /* jumbo frames */
+					acc[k] += chunk_sum(gp, c, a, b);
+			}
+		}
+#pragma unroll
+		for (int k = 0; k < COOP_BATCH; ++k) {
+			if (jj[k] >= 0) {
+				uint64_t x = (acc[k] & 0xffffffffull) + (acc[k] >> 32);
+				const uint32_t t = wave_oc_sum(oc_add((uint32_t)x, (uint32_t)(x >> 32)));
+
+				if (lane == (uint32_t)jj[k])
+					mine = t;
+			}
+		}
+		(void)cnt;
+	}
+	return mine;
+}
+
 /* ----------------------------------------------------------------------- */
 /* compiled term evaluation (odp_classification.c:1338-1490 via cls_compile) */
 struct Bases {
 	uint32_t l2, l3, l4, vlanx, len, inf_lo;
 };
 
+/* byte fields of the term / slot descriptors read as one dword: the
+ * wave-uniform reads then compile to scalar loads (a byte field would be a
+ * vector load, ordered behind every outstanding frame load) */
+__device__ __forceinline__ uint32_t term_hdr(const dterm_t *t)
+{
+	uint32_t x;
+
+	__builtin_memcpy(&x, t, 4);     /* kind | base << 8 | nwords << 16 | tflags << 24 */
+	return x;
+}
+
+__device__ __forceinline__ uint32_t slot_hdr(const dslot_t *sl)
+{
+	uint32_t x;
+
+	__builtin_memcpy(&x, sl, 4);    /* slot | nw << 8 */
+	return x;
+}
+
 template <int W, bool GF>
 __device__ __forceinline__ bool term_cmp(const dterm_t *__restrict__ t, const Pkt<W, GF> &v,
 					 const Bases &b)
 {
-	uint32_t kind = t->kind;
+	const uint32_t th = term_hdr(t);
+	uint32_t kind = th & 0xffu;
 
 	if (kind == DK_LEN)
 		return (b.len & t->mask[0]) == t->value[0];
 	if (kind != DK_CMP)
 		return false;
-	uint32_t base_k = t->base;
+	uint32_t base_k = (th >> 8) & 0xffu;
 	uint32_t base = base_k == DB_L3 ? b.l3 : base_k == DB_L4 ? b.l4 :
 			base_k == DB_L2 ? b.l2 : base_k == DB_VLANX ? b.vlanx : 0u;
 	uint32_t pos = base + (uint32_t)t->off;
 
-	if ((t->tflags & DT_GUARD) && !(b.len > pos + t->size))
+	if (((th >> 24) & DT_GUARD) && !(b.len > pos + t->size))
 		return false;
 	bool ok = true;
-	uint32_t nw = t->nwords;
+	uint32_t nw = (th >> 16) & 0xffu;
 
 	for (uint32_t k = 0; k < nw; ++k)
-		ok = ok && ((v.rd32(pos + 4u * k) & t->mask[k]) == t->value[k]);
+		ok = ok & ((v.rd32(pos + 4u * k) & t->mask[k]) == t->value[k]);
 	return ok;
 }
 
@@ -575,23 +741,26 @@ __device__ __forceinline__ bool pmr_match(const dterm_t *__restrict__ terms, uin
 	bool ok = true;
 	uint32_t end = start + n;
 
-	for (uint32_t ti = start; ti < end;) {
+	/* term indices stay wave-uniform (scalar loads of the term table): an
+	 * IPv4/IPv6 alternative pair is evaluated on both sides and selected
+	 * per lane, never by a per-lane pointer */
+	for (uint32_t ti = __builtin_amdgcn_readfirstlane(start); ti < end;) {
 		const dterm_t *t = terms + ti;
 		bool r;
 
-		if (t->tflags & DT_ALT_NEXT) {
+		if ((term_hdr(t) >> 24) & DT_ALT_NEXT) {
 			const dterm_t *t2 = t + 1;
+			const bool first = (b.inf_lo & t->req) == t->req;
+			const bool r1 = term_cmp(t, v, b);
+			const bool r2 = ((b.inf_lo & t2->req) == t2->req) & term_cmp(t2, v, b);
 
-			if ((b.inf_lo & t->req) == t->req)
-				r = term_cmp(t, v, b);
-			else
-				r = ((b.inf_lo & t2->req) == t2->req) && term_cmp(t2, v, b);
+			r = first ? r1 : r2;
 			ti += 2;
 		} else {
-			r = ((b.inf_lo & t->req) == t->req) && term_cmp(t, v, b);
+			r = ((b.inf_lo & t->req) == t->req) & term_cmp(t, v, b);
 			ti += 1;
 		}
-		ok = ok && r;
+		ok = ok & r;
 	}
 	return ok;
 }
@@ -917,12 +1086,14 @@ __device__ __forceinline__ bool term_eval(const dterm_t *__restrict__ t, const d
 					  const KeySrc<W, GF> &key, const Pkt<W, GF> &v,
 					  const Bases &b)
 {
-	if ((b.inf_lo & t->req) != t->req)
-		return false;
-	if (sl->slot == SLOT_NONE)
-		return term_cmp(t, v, b);
-	bool ok = true;
-	const uint32_t s0 = sl->slot, nw = sl->nw;
+	const bool req_ok = (b.inf_lo & t->req) == t->req;
+
+	const uint32_t sh = slot_hdr(sl);
+
+	if ((sh & 0xffu) == SLOT_NONE)
+		return req_ok & term_cmp(t, v, b);
+	bool ok = req_ok;
+	const uint32_t s0 = sh & 0xffu, nw = (sh >> 8) & 0xffu;
 
 	for (uint32_t k = 0; k < nw; ++k)
 		ok = ok & ((key(s0 + k) & sl->mask[k]) == sl->value[k]);
@@ -939,21 +1110,23 @@ __device__ __forceinline__ bool pmr_eval(const dterm_t *__restrict__ terms,
 	bool ok = true;
 	const uint32_t end = start + n;
 
-	for (uint32_t ti = start; ti < end;) {
+	/* wave-uniform term index (see pmr_match) */
+	for (uint32_t ti = __builtin_amdgcn_readfirstlane(start); ti < end;) {
 		const dterm_t *t = terms + ti;
 		bool r;
 
-		if (t->tflags & DT_ALT_NEXT) {
-			if ((b.inf_lo & t->req) == t->req)
-				r = term_eval(t, slots + ti, key, v, b);
-			else
-				r = term_eval(t + 1, slots + ti + 1, key, v, b);
+		if ((term_hdr(t) >> 24) & DT_ALT_NEXT) {
+			const bool first = (b.inf_lo & t->req) == t->req;
+			const bool r1 = term_eval(t, slots + ti, key, v, b);
+			const bool r2 = term_eval(t + 1, slots + ti + 1, key, v, b);
+
+			r = first ? r1 : r2;
 			ti += 2;
 		} else {
 			r = term_eval(t, slots + ti, key, v, b);
 			ti += 1;
 		}
-		ok = ok && r;
+		ok = ok & r;
 	}
 	return ok;
 }
@@ -1056,6 +1229,13 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 	/* default CoS entry: read once, outside the tile loop */
 	const bool def_valid = default_cos >= 0 && coses[default_cos].valid;
 	const bool def_rules = def_valid && coses[default_cos].nrule != 0u;
+	/* per-lane CoS info: LDS copy in the evaluate-all kernels, global otherwise */
+	auto cinfo_at = [&](uint32_t c) -> uint2 {
+		if constexpr (MODE != 0)
+			return cinfo[c];
+		else
+			return cinfo_g[c];
+	};
 
 	/* persistent workgroups: tiles of BLOCK packets */
 	const uint32_t ntiles = (num + BLOCK - 1) / BLOCK;
@@ -1211,12 +1391,28 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 	p.fl = 0u;
 	p.l2 = p.l3 = p.l4 = 0xffffu;
 	int ret = 0;
+	L4Pend pd = {0u, 0u, 0u, 0u};
 
 	if (FAST && wave_fast) {
 		if (live)
 			ret = parse_fast(p, f, opt);
 	} else if (live && layer) {
-		ret = parse_common(p, v, layer, opt);
+		if constexpr (GF)
+			ret = parse_common(p, v, layer, opt, &pd);
+		else
+			ret = parse_common(p, v, layer, opt);
+	}
+	if constexpr (GF) {
+		/* long UDP / TCP frames: tails summed by the whole wave (all 64
+		 * lanes active here, as the cooperative loads and DPP need) */
+		const uint64_t pm = __ballot(ret == PARSE_PEND);
+
+		if (pm) {
+			const uint32_t tail = coop_tail_sums(pm, g, pd);
+
+			if (ret == PARSE_PEND)
+				ret = finish_l4(p, pd, tail, opt);
+		}
 	}
 
 	/* ---- 3. CoS walk ------------------------------------------------- */
@@ -1389,8 +1585,8 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 			const uint32_t c = __builtin_amdgcn_readfirstlane(cos);
 
 			if (cos == c) {
-				const dcos_t *ce = coses + c;
-				const uint32_t rs = ce->rule_start, nr = ce->nrule;
+				const uint32_t cx = cinfo_g[c].x;   /* uniform: scalar load */
+				const uint32_t rs = cx & 0xffffu, nr = cx >> 16;
 				bool hit = false;
 				uint32_t nd = 0u, nmark = 0u;
 
@@ -1405,7 +1601,7 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 						nd = pm.dst;
 						nmark = pm.mark;
 					}
-					if (do_cos_stats && coses[pm.dst].stats) {
+					if (do_cos_stats && ((cinfo_g[pm.dst].y >> 16) & 0xffu)) {
 						uint64_t bm = __ballot(ok);
 
 						if (bm && (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(true))))
@@ -1421,7 +1617,7 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 					if (++steps >= num_cos) {
 						cos = ODPG_COS_LOOP;
 						active = false;
-					} else if (coses[nd].nrule == 0) {
+					} else if ((cinfo_g[nd].x >> 16) == 0u) {
 						active = false;
 					}
 				} else {
@@ -1439,14 +1635,14 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 		bool at_done = err || !any_match;
 
 		if (do_cos_stats && at_done && cos < num_cos &&
-		    (MODE != 0 ? ((cinfo[cos].y >> 16) & 0xffu) : coses[cos].stats))
+		    ((cinfo_at(cos).y >> 16) & 0xffu))
 			atomicAdd(&cos_cnt[cos], 1u);
 
 		if (cos == ODPG_COS_LOOP) {
 			cret = -2;
 		} else if (cos == ODPG_COS_NONE) {
 			cret = -1;
-		} else if ((MODE != 0 ? (cinfo[cos].y & 0xffu) : coses[cos].action) == 1u) {
+		} else if ((cinfo_at(cos).y & 0xffu) == 1u) {
 			cret = 1;
 		} else {
 			cret = 0;
@@ -1467,11 +1663,13 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 
 		if (cret == 1)
 			w |= ODPG_OUT_CLS_DROP;
-		if (cret == 0 && want_cls && (tbl_flags & TBL_ANY_HASHQ) && coses[cos].num_queue > 1u) {
+		if (cret == 0 && want_cls && (tbl_flags & TBL_ANY_HASHQ) &&
+		    ((cinfo_at(cos).y >> 8) & 0xffu) > 1u) {
 			/* rare path (hash-queue CoS): table read from global */
-			uint32_t h = rss_hash(p, v, coses[cos].hash_proto);
+			const uint32_t cy = cinfo_at(cos).y;
+			uint32_t h = rss_hash(p, v, cy >> 24);
 
-			w |= ((h & 31u) % coses[cos].num_queue) << 24;
+			w |= ((h & 31u) % ((cy >> 8) & 0xffu)) << 24;
 		}
 		if (p.inf & IF(IFL_L3_CHKSUM_DONE))
 			w |= (p.fl & FB(FL_L3_CHKSUM_ERR) ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 16;
@@ -1657,8 +1855,12 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 	int mode = a->mode;
 	hipError_t e;
 
+	/* auto: evaluate-all when the table compiles to exact-match groups
+	 * (cost per packet ~ number of groups); otherwise the walk, which only
+	 * evaluates the rules of the CoS a packet visits (C3: 4x faster than
+	 * evaluating all 256 generic PMRs per packet) */
 	if (mode == 0)
-		mode = a->num_pmr <= EVAL_ALL_MAX_PMR ? 2 : 1;
+		mode = (a->tbl_flags & TBL_SIMPLE) && a->num_pmr <= EVAL_ALL_MAX_PMR ? 2 : 1;
 	if (mode == 2 && a->num_pmr > EVAL_ALL_MAX_PMR)
 		mode = 1;
 	if (mode == 1)
