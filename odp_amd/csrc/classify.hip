@@ -583,102 +583,115 @@ __device__ __forceinline__ int finish_l4(Prs &p, const L4Pend &pd, uint32_t tail
 	return (p.fl & FL_ERROR_MASK) != 0u;
 }
 
-/* one's-complement sum over the 64 lanes (DPP row prefix, then the four
- * row totals); every lane must be active */
-__device__ __forceinline__ uint32_t wave_oc_sum(uint32_t x)
+/* plain u32 sum over the 64 lanes: DPP row prefix sums, then the four row
+ * totals; every lane must be active */
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x)
 {
-	x = oc_add(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true));
-	x = oc_add(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true));
-	x = oc_add(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true));
-	x = oc_add(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true));
-	uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
-
-	r = oc_add(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 31));
-	r = oc_add(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 47));
-	return oc_add(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 63));
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+	return (uint32_t)__builtin_amdgcn_readlane((int)x, 15) +
+	       (uint32_t)__builtin_amdgcn_readlane((int)x, 31) +
+	       (uint32_t)__builtin_amdgcn_readlane((int)x, 47) +
+	       (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
-/* 16 frame bytes at gp + off restricted to [a, b), summed as LE words */
-__device__ __forceinline__ uint64_t chunk_sum(const uint8_t *gp, uint32_t off, uint32_t a,
-					      uint32_t b)
+/* mask of the first `n` bytes (0..4) of a little-endian word */
+__device__ __forceinline__ uint32_t byte_mask(int n)
 {
-	if (off >= b || off + 16u <= a)
-		return 0ull;
-	uint4 q = *(const uint4 *)(gp + off);
-	uint32_t w[4] = {q.x, q.y, q.z, q.w};
+	n = n < 0 ? 0 : n > 4 ? 4 : n;
+	return (uint32_t)((1ull << (8 * n)) - 1ull);
+}
+
+/* this lane's share of frame j's tail [a, b): 16-byte chunks c0 + 16 * idx,
+ * idx = lane, lane + 64, ...; only the chunk holding byte b - 1 (and the
+ * first one when a is not 16-aligned) is masked, with wave-uniform masks.
+ * Returns the share folded to 16 bits (residue mod 0xffff). */
+__device__ __forceinline__ uint32_t tail_share(const uint8_t *gp, uint32_t a, uint32_t b,
+					       uint32_t lane)
+{
+	const uint32_t c0 = a & ~15u;
+	const uint32_t last = (b - 1u - c0) >> 4;          /* uniform */
+	const int rem = (int)(((b - 1u) & 15u) + 1u);       /* bytes of the last chunk */
+	const uint32_t e0 = byte_mask(rem), e1 = byte_mask(rem - 4), e2 = byte_mask(rem - 8),
+		       e3 = byte_mask(rem - 12);
+	const int lead = (int)(a & 15u);                    /* bytes to drop at the start */
+	const uint32_t s0 = ~byte_mask(lead), s1 = ~byte_mask(lead - 4),
+		       s2 = ~byte_mask(lead - 8), s3 = ~byte_mask(lead - 12);
 	uint64_t acc = 0ull;
 
-#pragma unroll
-	for (int k = 0; k < 4; ++k) {
-		const int lo = (int)a - (int)(off + 4u * k), hi = (int)b - (int)(off + 4u * k);
-		uint32_t m = 0xffffffffu;
+	for (uint32_t base = 0; base <= last; base += 64u) {   /* uniform: 1-2 passes for IMIX */
+		const uint32_t idx = base + lane;
 
-		if (hi < 4)
-			m = hi <= 0 ? 0u : (1u << (8 * hi)) - 1u;
-		if (lo > 0)
-			m &= lo >= 4 ? 0u : ~((1u << (8 * lo)) - 1u);
-		acc += w[k] & m;
+		if (idx <= last) {
+			const uint4 q = *(const uint4 *)(gp + c0 + 16u * idx);
+			const bool end = idx == last, start = idx == 0u;
+			const uint32_t w0 = q.x & (end ? e0 : ~0u) & (start ? s0 : ~0u);
+			const uint32_t w1 = q.y & (end ? e1 : ~0u) & (start ? s1 : ~0u);
+			const uint32_t w2 = q.z & (end ? e2 : ~0u) & (start ? s2 : ~0u);
+			const uint32_t w3 = q.w & (end ? e3 : ~0u) & (start ? s3 : ~0u);
+
+			acc += (uint64_t)w0 + w1 + w2 + w3;
+		}
 	}
-	return acc;
+	const uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
+
+	return oc_fold(oc_add(lo, hi));
 }
 
-/* Wave-cooperative sums of the frame tails [a, b) of the lanes in `m`: the
- * whole wave reads one frame's tail with coalesced 16-byte loads (1 KiB per
- * wave instruction), four frames at a time so their loads overlap, and
- * reduces each across lanes. Lane j receives the sum of its own tail. */
 #ifndef COOP_BATCH
 #define COOP_BATCH 4
 #endif
+/* Wave-cooperative sums of the frame tails [a, b) of the lanes in `m`: the
+ * whole wave reads one frame's tail with coalesced 16-byte loads (1 KiB per
+ * wave instruction), COOP_BATCH pairs of frames at a time so their loads
+ * overlap. Each lane folds its share to 16 bits; two frames travel packed in
+ * one lane reduction (64 x 0xffff < 2^22 per half). Lane j receives its own
+ * tail sum. */
 __device__ __forceinline__ uint32_t coop_tail_sums(uint64_t m, const uint8_t *g, const L4Pend &pd)
 {
 	const uint32_t lane = __lane_id();
+	const uint64_t gv = (uint64_t)(uintptr_t)g;
 	uint32_t mine = 0u;
 
 #ifdef ODPG_EXP_NOTAIL      /* experiment builds only: cost without the tail reads */
 	return 0u;
 #endif
 	while (m) {
-		int jj[COOP_BATCH];
-		uint32_t cnt = 0;
+		int jj[2 * COOP_BATCH];
+		uint32_t sh[2 * COOP_BATCH];
 
 #pragma unroll
-		for (int k = 0; k < COOP_BATCH; ++k) {
+		for (int k = 0; k < 2 * COOP_BATCH; ++k) {
 			jj[k] = m ? __builtin_ctzll(m) : -1;
-			if (m) {
-				m &= m - 1ull;
-				++cnt;
-			}
+			m &= m - 1ull;
 		}
-		uint64_t acc[COOP_BATCH];
-
 #pragma unroll
-		for (int k = 0; k < COOP_BATCH; ++k) {
-			acc[k] = 0ull;
+		for (int k = 0; k < 2 * COOP_BATCH; ++k) {
+			sh[k] = 0u;
 			if (jj[k] >= 0) {
-				const uint64_t gv = (uint64_t)(uintptr_t)g;
 				const uint32_t glo = __builtin_amdgcn_readlane((int)(uint32_t)gv, jj[k]);
 				const uint32_t ghi = __builtin_amdgcn_readlane((int)(uint32_t)(gv >> 32), jj[k]);
 				const uint8_t *gp = (const uint8_t *)(uintptr_t)(((uint64_t)ghi << 32) | glo);
 				const uint32_t a = __builtin_amdgcn_readlane((int)pd.a, jj[k]);
 				const uint32_t b = __builtin_amdgcn_readlane((int)pd.b, jj[k]);
-				const uint32_t c0 = (a & ~15u) + 16u * lane;
 
-				acc[k] = chunk_sum(gp, c0, a, b) + chunk_sum(gp, c0 + 1024u, a, b);
-				for (uint32_t c = c0 + 2048u; c < b; c += 1024u)   /* jumbo frames */
-					acc[k] += chunk_sum(gp, c, a, b);
+				sh[k] = tail_share(gp, a, b, lane);
 			}
 		}
 #pragma unroll
 		for (int k = 0; k < COOP_BATCH; ++k) {
-			if (jj[k] >= 0) {
-				uint64_t x = (acc[k] & 0xffffffffull) + (acc[k] >> 32);
-				const uint32_t t = wave_oc_sum(oc_add((uint32_t)x, (uint32_t)(x >> 32)));
+			if (jj[2 * k] >= 0) {
+				const uint32_t t0 = wave_sum_u32(sh[2 * k]);
+				const uint32_t t1 = jj[2 * k + 1] >= 0 ? wave_sum_u32(sh[2 * k + 1]) : 0u;
 
-				if (lane == (uint32_t)jj[k])
-					mine = t;
+				if (lane == (uint32_t)jj[2 * k])
+					mine = oc_fold(t0);
+				if (lane == (uint32_t)jj[2 * k + 1])
+					mine = oc_fold(t1);
 			}
 		}
-		(void)cnt;
 	}
 	return mine;
 }
@@ -1828,7 +1841,7 @@ template <int MODE>
 static hipError_t launch_layout(const odpg_launch_args &a, uint32_t &grid, hipStream_t s)
 {
 	if (a.desc)
-		return launch_one<128, false, true, true, MODE>(a, grid, s);
+		return launch_one<96, false, true, true, MODE>(a, grid, s);
 	if (a.stride == 64) {
 		const bool lean = (a.tbl_flags & TBL_SIMPLE) &&
 				  !(a.tbl_flags & (TBL_GENERIC | TBL_ANY_HASHQ)) && !a.mark &&
@@ -1844,7 +1857,7 @@ static hipError_t launch_layout(const odpg_launch_args &a, uint32_t &grid, hipSt
 		return launch_one<128, true, false, false, MODE>(a, grid, s);
 	if (a.stride < 128)
 		return launch_one<128, false, false, false, MODE>(a, grid, s);
-	return launch_one<128, false, true, false, MODE>(a, grid, s);
+	return launch_one<96, false, true, false, MODE>(a, grid, s);
 }
 
 extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
