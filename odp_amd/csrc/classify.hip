@@ -30,671 +30,7 @@
 #include "../../include/odpg.h"
 #include "odpg_internal.h"
 
-#define BLOCK 256
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-/* 16-byte load of once-read frame data. Lane-per-frame loads (lanes 64 B
- * apart) use the default cache policy: with the nontemporal hint the same
- * pattern streams at 3.7 TB/s instead of 5.5 (tools/diag_stream.py,
- * patterns 1 vs 17). */
-__device__ __forceinline__ uint4 ld_stream(const uint4 *p)
-{
-	return *p;
-}
-
-#define IF(x)  (1ull << (x))
-#define FB(x)  (1u << (x))
-
-/* ----------------------------------------------------------------------- */
-/* packet byte access: LDS window, optional global tail, zero past frame    */
-template <int W, bool GF>
-struct Pkt {
-	const uint32_t *row;   /* LDS, W/4 dwords of the frame start */
-	const uint8_t  *g;     /* global frame start (16-byte aligned) */
-	uint32_t        len;
-
-	__device__ __forceinline__ uint32_t word(uint32_t w) const
-	{
-		if (w < (uint32_t)(W / 4))
-			return row[w];
-		if (GF) {
-			uint32_t nw = (len + 3u) >> 2;
-
-			if (w < nw) {
-				uint32_t x = *(const uint32_t *)(g + 4u * w);
-				uint32_t rem = len - 4u * w;
-
-				if (rem < 4u)
-					x &= (1u << (8u * rem)) - 1u;
-				return x;
-			}
-		}
-		return 0u;
-	}
-
-	/* little-endian u32 of bytes [pos, pos + 4) */
-	__device__ __forceinline__ uint32_t rd32(uint32_t pos) const
-	{
-		uint32_t w = pos >> 2;
-		uint32_t lo = word(w);
-
-		if ((pos & 3u) == 0u)
-			return lo;
-		uint32_t hi = word(w + 1u);
-
-		return __builtin_amdgcn_alignbyte(hi, lo, pos & 3u);
-	}
-
-	__device__ __forceinline__ uint32_t u8(uint32_t pos) const
-	{
-		return (word(pos >> 2) >> (8u * (pos & 3u))) & 0xffu;
-	}
-
-	/* network-order 16-bit field */
-	__device__ __forceinline__ uint32_t be16(uint32_t pos) const
-	{
-		uint32_t x = rd32(pos);
-
-		return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu);
-	}
-
-	/* raw little-endian 16-bit load (what the reference's u16 reads see) */
-	__device__ __forceinline__ uint32_t raw16(uint32_t pos) const
-	{
-		return rd32(pos) & 0xffffu;
-	}
-};
-
-/* one's-complement accumulate (end-around carry): keeps the residue mod
- * 0xffff of the reference's 64-bit sum of little-endian words
- * (chksum_partial, odp_chksum_internal.h:60-196) and is zero only when every
- * added word is zero, so the folded verdict is identical. */
-__device__ __forceinline__ uint32_t oc_add(uint32_t s, uint32_t x)
-{
-	uint32_t r = s + x;
-
-	return r + (r < x ? 1u : 0u);
-}
-
-/* chksum_finalize (odp_chksum_internal.h:22-31) of a one's-complement sum */
-__device__ __forceinline__ uint32_t oc_fold(uint32_t s)
-{
-	s = (s >> 16) + (s & 0xffffu);
-	s = (s >> 16) + (s & 0xffffu);
-	return s;
-}
-
-/* sum of bytes [a, b) of the frame, a even, bytes past the frame zero */
-template <int W, bool GF>
-__device__ uint32_t sum_range(const Pkt<W, GF> &v, uint32_t a, uint32_t b)
-{
-	if (b > v.len)
-		b = v.len;
-	if (b <= a)
-		return 0u;
-	uint32_t w0 = a >> 2, w1 = (b - 1u) >> 2;
-	uint32_t s = 0;
-	uint32_t lim = w1 < (uint32_t)(W / 4 - 1) ? w1 : (uint32_t)(W / 4 - 1);
-	uint32_t w = w0;
-
-	/* part inside the LDS window */
-	for (; w <= lim; ++w) {
-		uint32_t x = v.row[w];
-
-		if (w == w0 && (a & 3u))
-			x &= 0xffff0000u;
-		if (w == w1 && (b & 3u))
-			x &= (1u << (8u * (b & 3u))) - 1u;
-		s = oc_add(s, x);
-	}
-	if (GF && w <= w1) {
-		/* tail beyond the window, straight from HBM: 16 B per load once
-		 * the word index is 16-byte aligned */
-		for (; w <= w1 && (w & 3u); ++w) {
-			uint32_t x = v.word(w);
-
-			if (w == w0 && (a & 3u))
-				x &= 0xffff0000u;
-			if (w == w1 && (b & 3u))
-				x &= (1u << (8u * (b & 3u))) - 1u;
-			s = oc_add(s, x);
-		}
-		/* whole 16-byte chunks: 64-bit accumulation (one add per word),
-		 * four loads in flight per step; folded end-around below, which
-		 * keeps the residue mod 0xffff (0xffffffff = 0xffff * 0x10001) */
-		uint64_t acc = 0ull;
-
-		if (w == w0 && (a & 3u) && w + 4u <= w1) {
-			uint4 q = *(const uint4 *)(v.g + 4u * w);
-
-			acc += (uint64_t)(q.x & 0xffff0000u) + q.y + q.z + q.w;
-			w += 4u;
-		}
-		while (w + 16u <= w1) {
-			const uint4 *gp = (const uint4 *)(v.g + 4u * w);
-			const uint4 q0 = gp[0], q1 = gp[1], q2 = gp[2], q3 = gp[3];
-
-			acc += (uint64_t)q0.x + q0.y + q0.z + q0.w;
-			acc += (uint64_t)q1.x + q1.y + q1.z + q1.w;
-			acc += (uint64_t)q2.x + q2.y + q2.z + q2.w;
-			acc += (uint64_t)q3.x + q3.y + q3.z + q3.w;
-			w += 16u;
-		}
-		while (w + 4u <= w1) {
-			const uint4 q = *(const uint4 *)(v.g + 4u * w);
-
-			acc += (uint64_t)q.x + q.y + q.z + q.w;
-			w += 4u;
-		}
-		acc = (acc & 0xffffffffull) + (acc >> 32);
-		s = oc_add(oc_add(s, (uint32_t)acc), (uint32_t)(acc >> 32));
-		for (; w <= w1; ++w) {
-			uint32_t x = v.word(w);
-
-			if (w == w0 && (a & 3u))
-				x &= 0xffff0000u;
-			if (w == w1 && (b & 3u))
-				x &= (1u << (8u * (b & 3u))) - 1u;
-			s = oc_add(s, x);
-		}
-	}
-	return s;
-}
-
-/* CRC32C (reflected Castagnoli, no final xor: arch/default/odp_hash_crc32.c) */
-__device__ __forceinline__ uint32_t crc32c_byte(uint32_t crc, uint32_t b)
-{
-	crc ^= b;
-#pragma unroll
-	for (int k = 0; k < 8; ++k)
-		crc = (crc >> 1) ^ (0x82F63B78u & (0u - (crc & 1u)));
-	return crc;
-}
-
-template <int W, bool GF>
-__device__ uint32_t crc32c_range(const Pkt<W, GF> &v, uint32_t off, uint32_t len, uint32_t crc)
-{
-	for (uint32_t i = 0; i < len; ++i)
-		crc = crc32c_byte(crc, v.u8(off + i));
-	return crc;
-}
-
-/* ----------------------------------------------------------------------- */
-struct Prs {
-	uint64_t inf;
-	uint32_t fl;
-	uint32_t l2, l3, l4;
-};
-
-enum { LAYER_NONE = 0, LAYER_L2, LAYER_L3, LAYER_L4, LAYER_ALL };
-
-/* _odp_parse_eth (odp_parse.c:23-106) */
-template <int W, bool GF>
-__device__ __forceinline__ uint32_t parse_eth(Prs &p, const Pkt<W, GF> &v, uint32_t &off)
-{
-	uint64_t inf = IF(IFL_L2) | IF(IFL_ETH);
-	uint32_t len = v.len;
-	uint32_t w0 = v.word(0), w1 = v.word(1), w3 = v.word(3);
-	uint32_t mac0 = ((w0 & 0xffu) << 8) | ((w0 >> 8) & 0xffu);
-	uint32_t ethtype = ((w3 & 0xffu) << 8) | ((w3 >> 8) & 0xffu);
-
-	if (len - off > 1514u)
-		inf |= IF(IFL_JUMBO);
-	if (mac0 & 0x0100u)
-		inf |= IF(IFL_ETH_MCAST);
-	if (mac0 == 0xffffu && (w0 >> 16) == 0xffffu && (w1 & 0xffffu) == 0xffffu)
-		inf |= IF(IFL_ETH_BCAST);
-	off += 14u;
-
-	if (ethtype < 1514u) {
-		inf |= IF(IFL_SNAP);
-		if (ethtype > len - off) {
-			p.fl |= FB(FL_SNAP_LEN_ERR);
-			p.inf |= inf;
-			return 0u;
-		}
-		ethtype = v.be16(off + 6u);
-		off += 8u;
-	}
-	if (ethtype == 0x88A8u) {
-		inf |= IF(IFL_VLAN_QINQ) | IF(IFL_VLAN);
-		ethtype = v.be16(off + 2u);
-		off += 4u;
-	}
-	if (ethtype == 0x8100u) {
-		inf |= IF(IFL_VLAN);
-		ethtype = v.be16(off + 2u);
-		off += 4u;
-	}
-	if (off > len) {
-		inf = IF(IFL_L2);
-		ethtype = 0u;
-	}
-	p.inf |= inf;
-	return ethtype;
-}
-
-/* parse_ipv4 (odp_parse.c:113-169); returns proto, accumulates pseudo header */
-template <int W, bool GF>
-__device__ __forceinline__ uint32_t parse_ipv4(Prs &p, const Pkt<W, GF> &v, uint32_t &off,
-					       uint64_t opt, uint32_t &l4sum)
-{
-	uint32_t o = off;
-	uint32_t len = v.len;
-	uint32_t h0 = v.rd32(o);            /* ver_ihl tos tot_len */
-	uint32_t h1 = v.rd32(o + 4u);       /* id frag_offset */
-	uint32_t h2 = v.rd32(o + 8u);       /* ttl proto chksum */
-	uint32_t dst = v.rd32(o + 16u);     /* raw */
-	uint32_t ver = (h0 & 0xf0u) >> 4, ihl = h0 & 0x0fu;
-	uint32_t l3_len = ((h0 >> 8) & 0xff00u) | (h0 >> 24);
-	uint32_t frag = ((h1 >> 8) & 0xff00u) | (h1 >> 24);
-	uint32_t dst_be = __builtin_bswap32(dst);
-
-	if ((p.fl & FB(FL_L3_CHKSUM_ERR)) || ihl < 5u || ver != 4u || 20u > len - o ||
-	    l3_len > len - o) {
-		p.fl |= FB(FL_IP_ERR);
-		return 0u;
-	}
-	if (opt & ODPG_PKTIN_IPV4_CHKSUM) {
-		p.inf |= IF(IFL_L3_CHKSUM_DONE);
-		if (oc_fold(sum_range(v, o, o + ihl * 4u)) != 0xffffu) {
-			p.fl |= FB(FL_IP_ERR) | FB(FL_L3_CHKSUM_ERR);
-			return 0u;
-		}
-	}
-	off += ihl * 4u;
-	if (opt & (ODPG_PKTIN_UDP_CHKSUM | ODPG_PKTIN_TCP_CHKSUM))
-		l4sum = sum_range(v, o + 12u, o + 20u);
-	if (ihl > 5u)
-		p.inf |= IF(IFL_IPOPT);
-	if (frag & 0x3fffu)
-		p.inf |= IF(IFL_IPFRAG);
-	if (dst_be == 0xffffffffu)
-		p.inf |= IF(IFL_IP_BCAST);
-	if ((dst_be >> 28) == 0xeu)
-		p.inf |= IF(IFL_IP_MCAST);
-	return (h2 >> 8) & 0xffu;
-}
-
-/* parse_ipv6 (odp_parse.c:179-245) */
-template <int W, bool GF>
-__device__ __forceinline__ uint32_t parse_ipv6(Prs &p, const Pkt<W, GF> &v, uint32_t &off,
-					       uint32_t seg_end, uint64_t opt, uint32_t &l4sum)
-{
-	uint32_t o = off;
-	uint32_t len = v.len;
-	uint32_t h0 = v.rd32(o);            /* ver_tc_flow */
-	uint32_t h1 = v.rd32(o + 4u);       /* payload_len next_hdr hop_limit */
-	uint32_t vtf = __builtin_bswap32(h0);
-	uint32_t payload_len = ((h1 & 0xffu) << 8) | ((h1 >> 8) & 0xffu);
-	uint32_t next_hdr = (h1 >> 16) & 0xffu;
-	uint32_t dst0 = v.u8(o + 24u);
-
-	if ((p.fl & FB(FL_L3_CHKSUM_ERR)) || (vtf >> 28) != 6u || 40u > len - o ||
-	    payload_len + 40u > len - o) {
-		p.fl |= FB(FL_IP_ERR);
-		return 0u;
-	}
-	if (dst0 == 0xffu)
-		p.inf |= IF(IFL_IP_MCAST);
-	else
-		p.inf &= ~IF(IFL_IP_MCAST);
-	p.inf &= ~IF(IFL_IP_BCAST);
-	off += 40u;
-	if (opt & (ODPG_PKTIN_UDP_CHKSUM | ODPG_PKTIN_TCP_CHKSUM))
-		l4sum = sum_range(v, o + 8u, o + 40u);
-
-	if (next_hdr == 0x00u || next_hdr == 0x2Bu) {
-		uint32_t ext_next;
-
-		p.inf |= IF(IFL_IPOPT);
-		do {
-			uint32_t e = off;
-
-			ext_next = v.u8(e);
-			off += 8u + v.u8(e + 1u) * 8u;
-		} while ((ext_next == 0x00u || ext_next == 0x2Bu) && off < seg_end);
-
-		if (off >= p.l3 + payload_len) {
-			p.fl |= FB(FL_IP_ERR);
-			return 0u;
-		}
-		if (ext_next == 0x2Cu)
-			p.inf |= IF(IFL_IPFRAG);
-		return ext_next;
-	}
-	if (next_hdr == 0x2Cu)
-		p.inf |= IF(IFL_IPOPT) | IF(IFL_IPFRAG);
-	return next_hdr;
-}
-
-/* UDP / TCP checksum of a frame longer than the LDS window, left for the
- * wave-cooperative tail pass (coop_tail_sums): the partial sum of the
- * pseudo header + window bytes and the byte range [a, b) still to add */
-struct L4Pend {
-	uint32_t kind;      /* 0 none, 1 UDP, 2 TCP */
-	uint32_t sum;
-	uint32_t a, b;
-};
-
-#define PARSE_PEND 2
-
-/* _odp_packet_parse_common (odp_parse_internal.h:80-112) incl. the L3/L4
- * switch (odp_parse.c:360-475) and _odp_packet_l4_chksum (odp_packet.c:1906-1984).
- * With a non-null `pend` (global-tail kernels) the UDP/TCP checksum of a frame
- * longer than the window returns PARSE_PEND instead; finish_l4() applies the
- * verdict once the tail sum is known. */
-template <int W, bool GF>
-__device__ int parse_common(Prs &p, const Pkt<W, GF> &v, uint32_t layer, uint64_t opt,
-			    L4Pend *pend = nullptr)
-{
-	uint32_t off = 0, len = v.len, seg_end = v.len;
-	uint32_t l4sum = 0;
-	uint32_t sctp_crc = 0;
-	uint32_t ip_proto;
-
-	if (layer == LAYER_NONE)
-		return 0;
-	p.l2 = 0;
-	uint32_t ethtype = parse_eth(p, v, off);
-
-	/* _odp_packet_parse_common_l3_l4 */
-	p.l3 = off;
-	if (layer <= LAYER_L2)
-		return (p.fl & FL_ERROR_MASK) != 0u;
-	p.inf |= IF(IFL_L3);
-	if (ethtype == 0x0800u) {
-		p.inf |= IF(IFL_IPV4);
-		ip_proto = parse_ipv4(p, v, off, opt, l4sum);
-		if (!(p.fl & FB(FL_IP_ERR)))
-			p.l4 = off;
-		else if (opt & ODPG_PKTIN_DROP_IPV4_ERR)
-			return -1;
-	} else if (ethtype == 0x86ddu) {
-		p.inf |= IF(IFL_IPV6);
-		ip_proto = parse_ipv6(p, v, off, seg_end, opt, l4sum);
-		if (!(p.fl & FB(FL_IP_ERR)))
-			p.l4 = off;
-		else if (opt & ODPG_PKTIN_DROP_IPV6_ERR)
-			return -1;
-	} else if (ethtype == 0x0806u) {
-		p.inf |= IF(IFL_ARP);
-		ip_proto = 255u;
-	} else {
-		p.inf &= ~IF(IFL_L3);
-		ip_proto = 255u;
-	}
-	if (layer == LAYER_L3)
-		return (p.fl & FL_ERROR_MASK) != 0u;
-
-	p.inf |= IF(IFL_L4);
-	bool frag = (p.inf & IF(IFL_IPFRAG)) != 0;
-
-	switch (ip_proto) {
-	case 0x01u:
-	case 0x3Au:
-		p.inf |= IF(IFL_ICMP);
-		break;
-	case 0x04u:
-		break;
-	case 0x06u: {                                       /* parse_tcp :252-274 */
-		if (off + 20u > seg_end)
-			return -1;
-		p.inf |= IF(IFL_TCP);
-		if ((v.u8(off + 12u) >> 4) < 5u)
-			p.fl |= FB(FL_TCP_ERR);
-		if ((opt & ODPG_PKTIN_TCP_CHKSUM) && !frag) {
-			uint32_t tl = (len - p.l4) & 0xffffu;
-
-			l4sum = oc_add(l4sum, ((tl >> 8) | (tl << 8)) & 0xffffu);
-			l4sum = oc_add(l4sum, 0x06u << 8);
-		}
-		if ((p.fl & FB(FL_TCP_ERR)) && (opt & ODPG_PKTIN_DROP_TCP_ERR))
-			return -1;
-		break;
-	}
-	case 0x11u: {                                       /* parse_udp :281-322 */
-		if (off + 8u > seg_end)
-			return -1;
-		p.inf |= IF(IFL_UDP);
-		uint32_t u1 = v.rd32(off + 4u);            /* length chksum */
-		uint32_t ulen_raw = u1 & 0xffffu, csum_raw = u1 >> 16;
-		uint32_t udplen = ((ulen_raw & 0xffu) << 8) | (ulen_raw >> 8);
-
-		if (udplen < 8u) {
-			p.fl |= FB(FL_UDP_ERR);
-		} else {
-			if ((opt & ODPG_PKTIN_UDP_CHKSUM) && !frag) {
-				if (csum_raw == 0u) {
-					p.inf |= IF(IFL_L4_CHKSUM_DONE) | IF(IFL_UDP_CHKSUM_ZERO);
-					if (!(p.inf & IF(IFL_IPV4)))
-						p.fl |= FB(FL_L4_CHKSUM_ERR);
-				} else {
-					l4sum = oc_add(l4sum, ulen_raw);
-					l4sum = oc_add(l4sum, 0x11u << 8);
-				}
-			}
-			if (v.be16(off + 2u) == 4500u && udplen > 4u && v.rd32(off + 8u) != 0u)
-				p.inf |= IF(IFL_IPSEC) | IF(IFL_IPSEC_UDP);
-		}
-		if ((p.fl & FB(FL_UDP_ERR)) && (opt & ODPG_PKTIN_DROP_UDP_ERR))
-			return -1;
-		break;
-	}
-	case 0x33u:
-		p.inf |= IF(IFL_IPSEC) | IF(IFL_IPSEC_AH);
-		break;
-	case 0x32u:
-		p.inf |= IF(IFL_IPSEC) | IF(IFL_IPSEC_ESP);
-		break;
-	case 0x84u: {                                       /* parse_sctp :329-352 */
-		p.inf |= IF(IFL_SCTP);
-		if (((len - p.l4) & 0xffffu) < 12u) {
-			p.fl |= FB(FL_SCTP_ERR);
-		} else if ((opt & ODPG_PKTIN_SCTP_CHKSUM) && !frag) {
-			uint32_t crc = crc32c_range(v, off, 8u, 0xffffffffu);
-
-			for (int k = 0; k < 4; ++k)
-				crc = crc32c_byte(crc, 0u);
-			sctp_crc = crc;
-		}
-		if ((p.fl & FB(FL_SCTP_ERR)) && (opt & ODPG_PKTIN_DROP_SCTP_ERR))
-			return -1;
-		break;
-	}
-	case 0x3Bu:
-		p.inf |= IF(IFL_NO_NEXT_HDR);
-		break;
-	default:
-		p.inf &= ~IF(IFL_L4);
-		break;
-	}
-	if (p.fl & FL_ERROR_MASK)
-		return 1;
-	if (layer < LAYER_L4)
-		return 0;
-
-	/* _odp_packet_l4_chksum (odp_packet.c:1906-1984) */
-	uint64_t inf = p.inf;
-
-	if (GF && pend && len > (uint32_t)W &&
-	    (((opt & ODPG_PKTIN_UDP_CHKSUM) && (inf & IF(IFL_UDP)) && !(inf & IF(IFL_IPFRAG)) &&
-	      !(inf & IF(IFL_UDP_CHKSUM_ZERO))) ||
-	     ((opt & ODPG_PKTIN_TCP_CHKSUM) && (inf & IF(IFL_TCP)) && !(inf & IF(IFL_IPFRAG))))) {
-		pend->kind = (inf & IF(IFL_UDP)) ? 1u : 2u;
-		pend->sum = oc_add(l4sum, sum_range(v, p.l4, (uint32_t)W));
-		pend->a = p.l4 > (uint32_t)W ? p.l4 : (uint32_t)W;
-		pend->b = len;
-		return PARSE_PEND;
-	}
-	if ((opt & ODPG_PKTIN_UDP_CHKSUM) && (inf & IF(IFL_UDP)) && !(inf & IF(IFL_IPFRAG)) &&
-	    !(inf & IF(IFL_UDP_CHKSUM_ZERO))) {
-		uint32_t s = oc_add(l4sum, sum_range(v, p.l4, len));
-
-		p.inf |= IF(IFL_L4_CHKSUM_DONE);
-		if (oc_fold(s) != 0xffffu) {
-			p.fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_UDP_ERR);
-			if (opt & ODPG_PKTIN_DROP_UDP_ERR)
-				return -1;
-		}
-	}
-	if ((opt & ODPG_PKTIN_TCP_CHKSUM) && (inf & IF(IFL_TCP)) && !(inf & IF(IFL_IPFRAG))) {
-		uint32_t s = oc_add(l4sum, sum_range(v, p.l4, len));
-
-		p.inf |= IF(IFL_L4_CHKSUM_DONE);
-		if (oc_fold(s) != 0xffffu) {
-			p.fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_TCP_ERR);
-			if (opt & ODPG_PKTIN_DROP_TCP_ERR)
-				return -1;
-		}
-	}
-	if ((opt & ODPG_PKTIN_SCTP_CHKSUM) && (inf & IF(IFL_SCTP)) && !(inf & IF(IFL_IPFRAG))) {
-		uint32_t crc = crc32c_range(v, p.l4 + 12u, len - p.l4 - 12u, sctp_crc);
-
-		p.inf |= IF(IFL_L4_CHKSUM_DONE);
-		if (~crc != v.rd32(p.l4 + 8u)) {
-			p.fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_SCTP_ERR);
-			if (opt & ODPG_PKTIN_DROP_SCTP_ERR)
-				return -1;
-		}
-	}
-	return (p.fl & FL_ERROR_MASK) != 0u;
-}
-
-/* verdict of a PARSE_PEND checksum (the UDP / TCP steps of
- * _odp_packet_l4_chksum, odp_packet.c:1927-1964) given the tail sum */
-__device__ __forceinline__ int finish_l4(Prs &p, const L4Pend &pd, uint32_t tail, uint64_t opt)
-{
-	const uint32_t s = oc_add(pd.sum, tail);
-
-	p.inf |= IF(IFL_L4_CHKSUM_DONE);
-	if (oc_fold(s) != 0xffffu) {
-		if (pd.kind == 1u) {
-			p.fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_UDP_ERR);
-			if (opt & ODPG_PKTIN_DROP_UDP_ERR)
-				return -1;
-		} else {
-			p.fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_TCP_ERR);
-			if (opt & ODPG_PKTIN_DROP_TCP_ERR)
-				return -1;
-		}
-	}
-	return (p.fl & FL_ERROR_MASK) != 0u;
-}
-
-/* plain u32 sum over the 64 lanes: DPP row prefix sums, then the four row
- * totals; every lane must be active */
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x)
-{
-	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
-	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
-	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
-	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
-	return (uint32_t)__builtin_amdgcn_readlane((int)x, 15) +
-	       (uint32_t)__builtin_amdgcn_readlane((int)x, 31) +
-	       (uint32_t)__builtin_amdgcn_readlane((int)x, 47) +
-	       (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-}
-
-/* mask of the first `n` bytes (0..4) of a little-endian word */
-__device__ __forceinline__ uint32_t byte_mask(int n)
-{
-	n = n < 0 ? 0 : n > 4 ? 4 : n;
-	return (uint32_t)((1ull << (8 * n)) - 1ull);
-}
-
-/* this lane's share of frame j's tail [a, b): 16-byte chunks c0 + 16 * idx,
- * idx = lane, lane + 64, ...; only the chunk holding byte b - 1 (and the
- * first one when a is not 16-aligned) is masked, with wave-uniform masks.
- * Returns the share folded to 16 bits (residue mod 0xffff). */
-__device__ __forceinline__ uint32_t tail_share(const uint8_t *gp, uint32_t a, uint32_t b,
-					       uint32_t lane)
-{
-	const uint32_t c0 = a & ~15u;
-	const uint32_t last = (b - 1u - c0) >> 4;          /* uniform */
-	const int rem = (int)(((b - 1u) & 15u) + 1u);       /* bytes of the last chunk */
-	const uint32_t e0 = byte_mask(rem), e1 = byte_mask(rem - 4), e2 = byte_mask(rem - 8),
-		       e3 = byte_mask(rem - 12);
-	const int lead = (int)(a & 15u);                    /* bytes to drop at the start */
-	const uint32_t s0 = ~byte_mask(lead), s1 = ~byte_mask(lead - 4),
-		       s2 = ~byte_mask(lead - 8), s3 = ~byte_mask(lead - 12);
-	uint64_t acc = 0ull;
-
-	for (uint32_t base = 0; base <= last; base += 64u) {   /* uniform: 1-2 passes for IMIX */
-		const uint32_t idx = base + lane;
-
-		if (idx <= last) {
-			const uint4 q = *(const uint4 *)(gp + c0 + 16u * idx);
-			const bool end = idx == last, start = idx == 0u;
-			const uint32_t w0 = q.x & (end ? e0 : ~0u) & (start ? s0 : ~0u);
-			const uint32_t w1 = q.y & (end ? e1 : ~0u) & (start ? s1 : ~0u);
-			const uint32_t w2 = q.z & (end ? e2 : ~0u) & (start ? s2 : ~0u);
-			const uint32_t w3 = q.w & (end ? e3 : ~0u) & (start ? s3 : ~0u);
-
-			acc += (uint64_t)w0 + w1 + w2 + w3;
-		}
-	}
-	const uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
-
-	return oc_fold(oc_add(lo, hi));
-}
-
-#ifndef COOP_BATCH
-#define COOP_BATCH 4
-#endif
-/* Wave-cooperative sums of the frame tails [a, b) of the lanes in `m`: the
- * whole wave reads one frame's tail with coalesced 16-byte loads (1 KiB per
- * wave instruction), COOP_BATCH pairs of frames at a time so their loads
- * overlap. Each lane folds its share to 16 bits; two frames travel packed in
- * one lane reduction (64 x 0xffff < 2^22 per half). Lane j receives its own
- * tail sum. */
-__device__ __forceinline__ uint32_t coop_tail_sums(uint64_t m, const uint8_t *g, const L4Pend &pd)
-{
-	const uint32_t lane = __lane_id();
-	const uint64_t gv = (uint64_t)(uintptr_t)g;
-	uint32_t mine = 0u;
-
-#ifdef ODPG_EXP_NOTAIL      /* experiment builds only: cost without the tail reads */
-	return 0u;
-#endif
-	while (m) {
-		int jj[2 * COOP_BATCH];
-		uint32_t sh[2 * COOP_BATCH];
-
-#pragma unroll
-		for (int k = 0; k < 2 * COOP_BATCH; ++k) {
-			jj[k] = m ? __builtin_ctzll(m) : -1;
-			m &= m - 1ull;
-		}
-#pragma unroll
-		for (int k = 0; k < 2 * COOP_BATCH; ++k) {
-			sh[k] = 0u;
-			if (jj[k] >= 0) {
-				const uint32_t glo = __builtin_amdgcn_readlane((int)(uint32_t)gv, jj[k]);
-				const uint32_t ghi = __builtin_amdgcn_readlane((int)(uint32_t)(gv >> 32), jj[k]);
-				const uint8_t *gp = (const uint8_t *)(uintptr_t)(((uint64_t)ghi << 32) | glo);
-				const uint32_t a = __builtin_amdgcn_readlane((int)pd.a, jj[k]);
-				const uint32_t b = __builtin_amdgcn_readlane((int)pd.b, jj[k]);
-
-				sh[k] = tail_share(gp, a, b, lane);
-			}
-		}
-#pragma unroll
-		for (int k = 0; k < COOP_BATCH; ++k) {
-			if (jj[2 * k] >= 0) {
-				const uint32_t t0 = wave_sum_u32(sh[2 * k]);
-				const uint32_t t1 = jj[2 * k + 1] >= 0 ? wave_sum_u32(sh[2 * k + 1]) : 0u;
-
-				if (lane == (uint32_t)jj[2 * k])
-					mine = oc_fold(t0);
-				if (lane == (uint32_t)jj[2 * k + 1])
-					mine = oc_fold(t1);
-			}
-		}
-	}
-	return mine;
-}
+#include "pkt_parse.h"
 
 /* ----------------------------------------------------------------------- */
 /* compiled term evaluation (odp_classification.c:1338-1490 via cls_compile) */
@@ -848,133 +184,6 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x)
 
 
 
-/* ---- register fast path: plain 64-byte Eth/IPv4/UDP|TCP frames ----------
- * Frames whose generic parse takes the straight path (no SNAP / VLAN, IPv4
- * IHL 5, UDP length >= 8 or TCP header >= 20 B) are parsed from the 16
- * registers holding the frame with compile-time offsets (l3 = 14, l4 = 34).
- * A wave takes it only when all its live lanes qualify (ballot); results are
- * bit-identical to parse_common() for those frames. */
-template <int K>
-__device__ __forceinline__ uint32_t fw(const uint32_t (&f)[16])
-{
-	/* little-endian u32 of frame bytes [K, K + 4), K constant */
-	if constexpr ((K & 3) == 0)
-		return f[K >> 2];
-	else
-		return __builtin_amdgcn_alignbyte(f[(K >> 2) + 1], f[K >> 2], K & 3);
-}
-
-__device__ __forceinline__ uint32_t swap16(uint32_t x)
-{
-	return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu);
-}
-
-__device__ __forceinline__ bool plain_v4(const uint32_t (&f)[16])
-{
-	const uint32_t w3 = f[3];
-	const uint32_t tot_len = swap16(f[4] & 0xffffu);
-	const uint32_t proto = f[5] >> 24;
-
-	if ((w3 & 0x00ffffffu) != 0x00450008u)      /* ethtype 0x0800, ver_ihl 0x45 */
-		return false;
-	if (tot_len > 64u - 14u)
-		return false;
-	if (proto == 0x11u)
-		return swap16(f[9] >> 16) >= 8u;         /* udp length */
-	if (proto == 0x06u)
-		return ((f[11] >> 20) & 0xfu) >= 5u;     /* tcp data offset */
-	return false;
-}
-
-__device__ __forceinline__ int parse_fast(Prs &p, const uint32_t (&f)[16], uint64_t opt)
-{
-	const uint32_t len = 64u;
-	uint64_t inf = IF(IFL_L2) | IF(IFL_ETH) | IF(IFL_L3) | IF(IFL_IPV4) | IF(IFL_L4);
-	uint32_t fl = 0u;
-
-	p.l2 = 0u;
-	p.l3 = 14u;
-	if (f[0] & 0x1u)
-		inf |= IF(IFL_ETH_MCAST);
-	if (f[0] == 0xffffffffu && (f[1] & 0xffffu) == 0xffffu)
-		inf |= IF(IFL_ETH_BCAST);
-	if (opt & ODPG_PKTIN_IPV4_CHKSUM) {
-		uint32_t s = oc_add(f[3] & 0xffff0000u, f[4]);
-
-		s = oc_add(s, f[5]);
-		s = oc_add(s, f[6]);
-		s = oc_add(s, f[7]);
-		s = oc_add(s, f[8] & 0xffffu);
-		inf |= IF(IFL_L3_CHKSUM_DONE);
-		if (oc_fold(s) != 0xffffu) {
-			/* ip_err: no l4 offset, ip_proto 0 -> l4 flag cleared */
-			p.inf = inf & ~IF(IFL_L4);
-			p.fl = FB(FL_IP_ERR) | FB(FL_L3_CHKSUM_ERR);
-			p.l4 = 0xffffu;
-			return 1;
-		}
-	}
-	const bool frag = (swap16(f[5] & 0xffffu) & 0x3fffu) != 0u;
-	const uint32_t dst_be = __builtin_bswap32(fw<30>(f));
-
-	if (frag)
-		inf |= IF(IFL_IPFRAG);
-	if (dst_be == 0xffffffffu)
-		inf |= IF(IFL_IP_BCAST);
-	if ((dst_be >> 28) == 0xeu)
-		inf |= IF(IFL_IP_MCAST);
-	p.l4 = 34u;
-	uint32_t l4sum = 0u;
-
-	if (opt & (ODPG_PKTIN_UDP_CHKSUM | ODPG_PKTIN_TCP_CHKSUM))
-		l4sum = oc_add(oc_add(f[6] & 0xffff0000u, f[7]), f[8] & 0xffffu);
-	bool do_sum = false;
-
-	if ((f[5] >> 24) == 0x11u) {                 /* parse_udp */
-		const uint32_t u1 = fw<38>(f);
-		const uint32_t ulen_raw = u1 & 0xffffu, csum_raw = u1 >> 16;
-		const uint32_t udplen = swap16(ulen_raw);
-
-		inf |= IF(IFL_UDP);
-		if ((opt & ODPG_PKTIN_UDP_CHKSUM) && !frag) {
-			if (csum_raw == 0u) {
-				inf |= IF(IFL_L4_CHKSUM_DONE) | IF(IFL_UDP_CHKSUM_ZERO);
-			} else {
-				l4sum = oc_add(oc_add(l4sum, ulen_raw), 0x11u << 8);
-				do_sum = true;
-			}
-		}
-		if (swap16(f[9] & 0xffffu) == 4500u && udplen > 4u && fw<42>(f) != 0u)
-			inf |= IF(IFL_IPSEC) | IF(IFL_IPSEC_UDP);
-		if (do_sum) {
-			uint32_t s = oc_add(l4sum, f[8] & 0xffff0000u);
-
-#pragma unroll
-			for (int k = 9; k < 16; ++k)
-				s = oc_add(s, f[k]);
-			inf |= IF(IFL_L4_CHKSUM_DONE);
-			if (oc_fold(s) != 0xffffu)
-				fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_UDP_ERR);
-		}
-	} else {                                     /* parse_tcp */
-		inf |= IF(IFL_TCP);
-		if ((opt & ODPG_PKTIN_TCP_CHKSUM) && !frag) {
-			uint32_t tl = (len - 34u) & 0xffffu;
-			uint32_t s = oc_add(oc_add(l4sum, swap16(tl)), 0x06u << 8);
-
-			s = oc_add(s, f[8] & 0xffff0000u);
-#pragma unroll
-			for (int k = 9; k < 16; ++k)
-				s = oc_add(s, f[k]);
-			inf |= IF(IFL_L4_CHKSUM_DONE);
-			if (oc_fold(s) != 0xffffu)
-				fl |= FB(FL_L4_CHKSUM_ERR) | FB(FL_TCP_ERR);
-		}
-	}
-	p.inf = inf;
-	p.fl = fl;
-	return fl ? 1 : 0;
-}
 
 __device__ __forceinline__ void extract_key_fast(uint32_t (&key)[KEY_SLOTS], const uint32_t (&f)[16],
 						 const Prs &p, uint32_t slot_mask)
