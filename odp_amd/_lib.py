@@ -101,6 +101,28 @@ class odpg_result_t(C.Structure):
                 ("stats", C.c_void_p)]
 
 
+# ---- include/odpg_fwd.h -----------------------------------------------------
+FWD_HASH, FWD_LPM = 0, 1
+FWD_MAX_ROUTES = 32
+FWD_MAX_PORTS = 32
+
+
+class odpg_route_t(C.Structure):
+    _fields_ = [("addr", C.c_uint32), ("depth", C.c_uint32), ("oif_id", C.c_int32),
+                ("src_mac", C.c_uint8 * 6), ("dst_mac", C.c_uint8 * 6)]
+
+
+class odpg_fwd_param_t(C.Structure):
+    _fields_ = [("mode", C.c_uint32), ("num_ports", C.c_uint32),
+                ("port_mac", (C.c_uint8 * 6) * FWD_MAX_PORTS),
+                ("dest_mac", (C.c_uint8 * 6) * FWD_MAX_PORTS)]
+
+
+class odpg_fwd_batch_t(C.Structure):
+    _fields_ = [("frames", C.c_void_p), ("stride", C.c_uint32), ("num", C.c_uint32),
+                ("src_port", C.c_int32), ("error_check", C.c_uint32)]
+
+
 # numpy dtypes with the same layout
 def np_dtypes():
     import numpy as np
@@ -260,6 +282,11 @@ SIGNATURES = {
     "odpg_cls_generation": (_u64, []),
     "odpg_pktio_rules": (_i32, [_vp, C.POINTER(odpg_rules_t)]),
     "odpg_pktio_recv_batch": (_i32, [_vp, _vp, _vp, _vp, _u32, _u32, _i32, _vp, _vp]),
+    # include/odpg_fwd.h
+    "odpg_fwd_create": (_i32, [_vp, C.POINTER(odpg_route_t), _u32, C.POINTER(odpg_fwd_param_t),
+                               C.POINTER(_vp)]),
+    "odpg_fwd_destroy": (None, [_vp]),
+    "odpg_l3fwd": (_i32, [_vp, _vp, C.POINTER(odpg_fwd_batch_t), _vp]),
 }
 
 

@@ -393,3 +393,58 @@ def build_c3_rules(cls, pktio, stats=False, seed=0xC3):
             assert p, ("pmr", k)
             pmrs.append(p)
     return {"coses": coses, "error": err, "pmrs": pmrs}
+
+
+# ---- C5: example/l3fwd, 10 M flows over <= 32 routes ------------------------
+C5_FLOWS = 10_000_000
+
+
+def c5_routes(seed=0xC5, n=32):
+    """`n` canonical IPv4 routes (host bits zero, depth 8..28) over 10.0.0.0/8,
+    nested and overlapping so the newest-first scan order and the LPM trie's
+    quirks both matter; output ports 0..3. Returns a list of
+    (addr, depth, oif_id, src_mac, dst_mac) in add order."""
+    r = xorshift64(seed, n)
+    depths = (8, 12, 16, 18, 20, 22, 24, 26, 28)
+    out = []
+    for k in range(n):
+        h = int(r[k])
+        d = depths[h % len(depths)]
+        addr = (ip4("10.0.0.0") | ((h >> 8) & 0x00FFFFFF)) & ((0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF)
+        if k % 4 == 0:      # pin a quarter of them inside 10.1/16 so prefixes nest
+            addr = (ip4("10.1.0.0") | ((h >> 8) & 0xFFFF)) & ((0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF)
+            d = max(d, 16)
+            addr &= (0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF
+        port = (h >> 40) & 3
+        src = [0x02, 0x00, 0x00, 0x00, 0x10, port]
+        dst = [0x02, 0x00, 0x00, 0x01, k, port]
+        out.append((addr, d, port, src, dst))
+    return out
+
+
+def c5_frames(n, routes, seed=C_SEED, flows=C5_FLOWS):
+    """C5 traffic: 64 B IPv4/UDP|TCP frames, packet i carries flow i % flows
+    (distinct 5-tuples: src 172.16.0.0 + flow, sport / dport from the flow
+    index); dst inside a random route's subnet for ~97 % of packets, an
+    unrouted 192.0.2.x address otherwise. Returns the flat frame buffer."""
+    idx = np.arange(n, dtype=np.uint64) % np.uint64(flows)
+    r = xorshift64(seed ^ 0xC5C5, n)
+    nr = len(routes)
+    pick = (r % np.uint64(max(nr, 1))).astype(np.int64)
+    addr = np.array([rt[0] for rt in routes] or [0], np.uint64)
+    depth = np.array([rt[1] for rt in routes] or [32], np.uint64)
+    host = (r >> np.uint64(16)) & ((np.uint64(1) << (np.uint64(32) - depth[pick])) - np.uint64(1))
+    dst = addr[pick] | host
+    miss = ((r >> np.uint64(56)) % np.uint64(32)) == 0
+    dst = np.where(miss, np.uint64(ip4("192.0.2.0")) + (r & np.uint64(0xFF)), dst)
+    src = np.uint64(ip4("172.16.0.0")) + idx
+    sport = (idx & np.uint64(0xFFFF)).astype(np.int64)
+    dport = ((idx >> np.uint64(16)) + np.uint64(1024)).astype(np.int64) & 0xFFFF
+    tcp = ((r >> np.uint64(8)) & np.uint64(1)) == 1
+    a = np.empty((n, 64), np.uint8)
+    for is_tcp in (False, True):
+        sel = np.nonzero(tcp == is_tcp)[0]
+        if len(sel):
+            a[sel] = ipv4_frames(len(sel), 64, src[sel], dst[sel],
+                                 PROTO_TCP if is_tcp else PROTO_UDP, sport[sel], dport[sel])
+    return a.reshape(-1)

@@ -172,3 +172,65 @@ class Context:
         if stats is not None:
             res["stats"] = stats
         return res
+
+
+class Forwarder:
+    """example/l3fwd forwarding table on the device (include/odpg_fwd.h)."""
+
+    def __init__(self, ctx, routes, mode=L.FWD_HASH, port_mac=None, dest_mac=None, num_ports=4):
+        self.ctx = ctx
+        self.routes = make_routes(routes)
+        self.param = make_fwd_param(mode, num_ports, port_mac, dest_mac)
+        h = C.c_void_p()
+        L.check(lib.odpg_fwd_create(ctx.h, self.routes, len(self.routes), C.byref(self.param),
+                                    C.byref(h)), "odpg_fwd_create")
+        self.h = h.value
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib.odpg_fwd_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def run_dev(self, frames_buf, stride, num, out_buf, src_port=0, error_check=False):
+        b = L.odpg_fwd_batch_t(frames_buf.ptr, stride, num, src_port, int(bool(error_check)))
+        L.check(lib.odpg_l3fwd(self.ctx.h, self.h, C.byref(b), out_buf.ptr), "odpg_l3fwd")
+
+    def run(self, frames, stride, num, src_port=0, error_check=False):
+        """Upload, forward, download: returns (out_port int32[num], frames)."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        fb = self.ctx.buffer(frames.nbytes + 64)
+        fb.upload(frames)
+        ob = self.ctx.buffer(4 * num)
+        self.run_dev(fb, stride, num, ob, src_port, error_check)
+        self.ctx.sync()
+        out = ob.download(np.int32, num)
+        fr = fb.download(np.uint8, frames.nbytes)
+        fb.free()
+        ob.free()
+        return out, fr
+
+
+def make_routes(routes):
+    """[(addr, depth, oif_id, src_mac, dst_mac), ...] -> ctypes odpg_route_t array."""
+    arr = (L.odpg_route_t * len(routes))()
+    for k, (addr, depth, oif, smac, dmac) in enumerate(routes):
+        arr[k].addr, arr[k].depth, arr[k].oif_id = addr, depth, oif
+        for j in range(6):
+            arr[k].src_mac[j] = smac[j]
+            arr[k].dst_mac[j] = dmac[j]
+    return arr
+
+
+def make_fwd_param(mode, num_ports, port_mac=None, dest_mac=None):
+    p = L.odpg_fwd_param_t()
+    p.mode, p.num_ports = mode, num_ports
+    for i in range(L.FWD_MAX_PORTS):
+        pm = port_mac[i] if port_mac and i < len(port_mac) else [0x02, 0, 0, 0xAA, 0, i]
+        dm = dest_mac[i] if dest_mac and i < len(dest_mac) else [0x02, 0, 0, 0xBB, 0, i]
+        for j in range(6):
+            p.port_mac[i][j] = pm[j]
+            p.dest_mac[i][j] = dm[j]
+    return p

@@ -1073,3 +1073,271 @@ uint32_t oracle_thash(const uint32_t *tuple, uint32_t len)
 {
 	return thash_softrss(tuple, len);
 }
+
+/* ======================================================================
+ * example/l3fwd forwarding decision.
+ * Restated from example/l3fwd/odp_l3fwd.c, odp_l3fwd_db.c, odp_l3fwd_lpm.c.
+ * ==================================================================== */
+#include "../include/odpg_fwd.h"
+
+/* ---- 16-4-4-4-4 trie of odp_l3fwd_lpm.c, node-array form ---------------
+ * fib_node_t (:31-38) keeps {next_hop | next, valid:1, end:1, depth:6}; a
+ * node's children are 16 consecutive nodes of the sub-table pool. Every
+ * quirk of the reference builder is kept: fib_alloc_sub (:45-60) hands out
+ * the nodes at (k + 1) * 16; a split (:93-105) copies next_hop / depth to
+ * the children but leaves them invalid; a depth <= 16 route touches one
+ * first-level node (:174-200); a route ending inside a stride updates the
+ * single child at `ip >> ip_width` (:106-111); fib_update_node (:62-81)
+ * recurses only into children that are leaves. */
+#define FIB_L1    65536u
+#define FIB_POOL  16384u
+
+typedef struct {
+	uint32_t nh;        /* next hop, or first child index in the pool */
+	uint8_t valid, end, depth;
+} fnode_t;
+
+typedef struct {
+	fnode_t l1[FIB_L1];
+	fnode_t pool[FIB_POOL];
+	uint32_t nsub;
+	int overflow;
+} fib_t;
+
+static fnode_t *fib_child(fib_t *f, const fnode_t *fe, uint32_t i)
+{
+	return &f->pool[fe->nh + i];
+}
+
+static int fib_new_sub(fib_t *f, uint32_t *base)
+{
+	uint32_t b = (f->nsub + 1u) * 16u;
+
+	/* the reference resets b entries from its new table on (:52-57) */
+	if (2u * b > FIB_POOL) {
+		f->overflow = 1;
+		return -1;
+	}
+	for (uint32_t i = 0; i < b; i++) {
+		f->pool[b + i].valid = 0;
+		f->pool[b + i].end = 1;
+	}
+	f->nsub++;
+	*base = b;
+	return 0;
+}
+
+static void fib_update(fib_t *f, fnode_t *fe, uint32_t port, uint32_t depth)
+{
+	if (fe->end) {
+		if (!fe->valid) {
+			fe->depth = (uint8_t)depth;
+			fe->nh = port;
+			fe->valid = 1;
+		} else if (fe->depth <= depth) {
+			fe->nh = port;
+			fe->depth = (uint8_t)depth;
+		}
+		return;
+	}
+	for (uint32_t i = 0; i < 16u; i++) {
+		fnode_t *c = fib_child(f, fe, i);
+
+		if (c->end)
+			fib_update(f, c, port, depth);
+	}
+}
+
+static void fib_insert_sub(fib_t *f, fnode_t *fe, uint32_t ip, uint32_t port,
+			   uint32_t width, uint32_t eaten, uint32_t depth)
+{
+	for (;;) {
+		if (fe->end) {
+			uint32_t base, old = fe->nh;
+
+			if (fib_new_sub(f, &base))
+				return;
+			fe->nh = base;
+			fe->end = 0;
+			if (fe->valid)
+				for (uint32_t i = 0; i < 16u; i++) {
+					f->pool[base + i].nh = old;
+					f->pool[base + i].depth = fe->depth;
+				}
+		}
+		if (depth - eaten <= 4u) {
+			width -= depth - eaten;
+			fib_update(f, fib_child(f, fe, ip >> width), port, depth);
+			return;
+		}
+		width -= 4u;
+		fnode_t *c = fib_child(f, fe, ip >> width);
+
+		ip &= (1u << width) - 1u;
+		eaten += 4u;
+		fe = c;
+	}
+}
+
+static void fib_insert(fib_t *f, uint32_t ip, uint32_t port, uint32_t depth)
+{
+	fnode_t *fe = &f->l1[ip >> 16];
+
+	if (depth <= 16u) {
+		if (fe->end) {
+			fe->nh = port;
+			fe->depth = (uint8_t)depth;
+			fe->valid = 1;
+			return;
+		}
+		for (uint32_t i = 0; i < 16u; i++) {
+			fnode_t *c = fib_child(f, fe, i);
+
+			if (c->end)
+				fib_update(f, c, port, depth);
+			else
+				for (uint32_t j = 0; j < 16u; j++)
+					fib_update(f, fib_child(f, c, j), port, depth);
+		}
+		return;
+	}
+	fib_insert_sub(f, fe, ip & 0xffffu, port, 16u, 16u, depth);
+}
+
+static int fib_lookup(const fib_t *f, uint32_t ip, int32_t *port)
+{
+	const fnode_t *fe = &f->l1[ip >> 16];
+	uint32_t bits = 16u;
+
+	ip &= 0xffffu;
+	while (!fe->end) {
+		bits -= 4u;
+		fe = &f->pool[fe->nh + (ip >> bits)];
+		ip &= (1u << bits) - 1u;
+	}
+	*port = (int32_t)fe->nh;
+	return fe->valid ? 0 : -1;
+}
+
+/* ---- find_fwd_db_entry (odp_l3fwd_db.c:474-508): first match in the list,
+ * which create_fwd_db_entry() prepends to (:409-411), i.e. newest first */
+static int route_first_match(const odpg_route_t *r, uint32_t n, uint32_t ip)
+{
+	for (int k = (int)n - 1; k >= 0; k--) {
+		uint32_t d = r[k].depth;
+		uint32_t mask = ((1u << d) - 1u) << (32u - d);   /* d in 1..31 */
+
+		if (r[k].addr == (ip & mask))
+			return k;
+	}
+	return -1;
+}
+
+static uint32_t rd_be32(const uint8_t *p)
+{
+	return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+/* One batch through drop_err_pkts + l3fwd_pkt_hash / l3fwd_pkt_lpm
+ * (odp_l3fwd.c:182-292). frames are rewritten in place; out_port[i] = port
+ * or -1 (dropped). Returns 0, or -1 for a route set outside the supported
+ * domain (see include/odpg_fwd.h). */
+int oracle_l3fwd(const odpg_route_t *routes, uint32_t nroutes, const odpg_fwd_param_t *prm,
+		 uint8_t *frames, uint32_t stride, uint32_t num, int32_t sif, int error_check,
+		 int32_t *out_port)
+{
+	fib_t *fib = NULL;
+
+	pthread_once(&crc_once, crc_init);
+	if (nroutes > ODPG_FWD_MAX_ROUTES)
+		return -1;
+	if (prm->mode == ODPG_FWD_LPM) {
+		fib = calloc(1, sizeof(*fib));
+		if (!fib)
+			return -1;
+		for (uint32_t i = 0; i < FIB_L1; i++)
+			fib->l1[i].end = 1;               /* fib_tbl_init (:131-137) */
+		/* setup_fwd_db walks the list newest first (odp_l3fwd.c:164-175) */
+		for (int k = (int)nroutes - 1; k >= 0; k--)
+			fib_insert(fib, routes[k].addr, (uint32_t)routes[k].oif_id, routes[k].depth);
+		if (fib->overflow) {
+			free(fib);
+			return -1;
+		}
+	} else {
+		for (uint32_t k = 0; k < nroutes; k++) {
+			uint32_t d = routes[k].depth;
+
+			if (d < 1 || d > 31 || (routes[k].addr & ((1u << (32u - d)) - 1u)))
+				return -1;
+		}
+	}
+	for (uint32_t i = 0; i < num; i++) {
+		uint8_t *fr = frames + (size_t)i * stride;
+		pv_t v = { fr, stride };
+		hdr_t h;
+		int ret;
+
+		memset(&h, 0, sizeof(h));
+		h.l2_offset = h.l3_offset = h.l4_offset = OFFSET_INVALID;
+		ret = parse_common(&h, &v, stride, error_check ? LAYER_ALL : LAYER_L4, 0);
+		if (ret < 0 || (error_check && (h.flags & F_ERROR_MASK)) ||
+		    !(h.input_flags & IFB(IF_IPV4))) {
+			out_port[i] = -1;
+			continue;
+		}
+		uint8_t *ip = fr + h.l3_offset;
+		uint32_t dst = rd_be32(ip + 16);
+		int32_t dif;
+
+		/* ipv4_dec_ttl_csum_update (odp_l3fwd.c:182-193): raw LE u16 of the
+		 * checksum field, a = ~cpu_to_be_16(0x100) = 0xfffe */
+		uint16_t cs = (uint16_t)(ip[10] | (ip[11] << 8));
+
+		ip[8]--;
+		cs = cs >= 0xfffeu ? (uint16_t)(cs - 0xfffeu) : (uint16_t)(cs + 1u);
+		ip[10] = (uint8_t)cs;
+		ip[11] = (uint8_t)(cs >> 8);
+		if (prm->mode == ODPG_FWD_LPM) {
+			int32_t p;
+
+			dif = fib_lookup(fib, dst, &p) ? sif : p;
+			memcpy(fr, prm->dest_mac[dif], 6);
+			memcpy(fr + 6, prm->port_mac[dif], 6);
+		} else {
+			int k = route_first_match(routes, nroutes, dst);
+
+			if (k >= 0) {
+				memcpy(fr + 6, routes[k].src_mac, 6);
+				memcpy(fr, routes[k].dst_mac, 6);
+				dif = routes[k].oif_id;
+			} else {
+				memcpy(fr, fr + 6, 6);          /* eth->dst = eth->src */
+				dif = sif;
+			}
+		}
+		out_port[i] = dif;
+	}
+	free(fib);
+	return 0;
+}
+
+/* test hook: trie lookup of one address after building from routes[] */
+int oracle_fib_lookup(const odpg_route_t *routes, uint32_t nroutes, const uint32_t *ips,
+		      uint32_t n, int32_t *port, int32_t *valid)
+{
+	fib_t *fib = calloc(1, sizeof(*fib));
+
+	if (!fib)
+		return -1;
+	for (uint32_t i = 0; i < FIB_L1; i++)
+		fib->l1[i].end = 1;
+	for (int k = (int)nroutes - 1; k >= 0; k--)
+		fib_insert(fib, routes[k].addr, (uint32_t)routes[k].oif_id, routes[k].depth);
+	for (uint32_t i = 0; i < n; i++)
+		valid[i] = fib_lookup(fib, ips[i], &port[i]) == 0;
+	int ovf = fib->overflow;
+
+	free(fib);
+	return ovf ? -1 : 0;
+}

@@ -35,6 +35,10 @@ def _load():
     lib.oracle_crc32c.argtypes = [vp, u32, u32]
     lib.oracle_thash.restype = u32
     lib.oracle_thash.argtypes = [vp, u32]
+    lib.oracle_l3fwd.restype = i32
+    lib.oracle_l3fwd.argtypes = [vp, u32, vp, vp, u32, u32, i32, i32, vp]
+    lib.oracle_fib_lookup.restype = i32
+    lib.oracle_fib_lookup.argtypes = [vp, u32, vp, u32, vp, vp]
     return lib
 
 
@@ -91,3 +95,30 @@ def crc32c(data: bytes, init=0xFFFFFFFF) -> int:
 def thash(words) -> int:
     a = np.ascontiguousarray(words, dtype=np.uint32)
     return lib.oracle_thash(a.ctypes.data, len(a))
+
+
+def l3fwd(routes, param, frames, stride, num, src_port=0, error_check=False):
+    """example/l3fwd restatement. `routes` is a ctypes array of odpg_route_t
+    (add order), `param` an odpg_fwd_param_t. Returns (out_port, rewritten
+    frames); the input array is not modified. rc -1 = unsupported route set."""
+    fr = np.array(frames, dtype=np.uint8, copy=True)
+    out = np.zeros(num, np.int32)
+    rc = lib.oracle_l3fwd(C.cast(routes, C.c_void_p) if len(routes) else None, len(routes),
+                          C.byref(param), fr.ctypes.data, stride, num, src_port,
+                          int(bool(error_check)), out.ctypes.data)
+    if rc:
+        raise ValueError("route set outside the restated domain")
+    return out, fr
+
+
+def fib_lookup(routes, ips):
+    """Build the l3fwd LPM trie from `routes` (add order) and look up `ips`:
+    returns (port, valid) arrays, exactly as fib_tbl_lookup reports them."""
+    ips = np.ascontiguousarray(ips, dtype=np.uint32)
+    port = np.zeros(len(ips), np.int32)
+    valid = np.zeros(len(ips), np.int32)
+    rc = lib.oracle_fib_lookup(C.cast(routes, C.c_void_p) if len(routes) else None, len(routes),
+                               ips.ctypes.data, len(ips), port.ctypes.data, valid.ctypes.data)
+    if rc:
+        raise ValueError("trie pool overflow")
+    return port, valid.astype(bool)
