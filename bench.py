@@ -46,7 +46,7 @@ def parse_args():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-mode", type=int, default=0,
-                    help="0 auto, 1 wave-cooperative walk, 2 evaluate-all")
+                    help="0 auto, 1 wave-cooperative walk, 2 evaluate-all, 3 hash walk")
     ap.add_argument("--diag", default="full",
                     choices=["full", "parse", "parse-nochk", "l3", "none"],
                     help="diagnostic floors (not the metric): 'parse' = parse + checksum "
@@ -227,7 +227,7 @@ def main():
             "config": {"workload": workload, "batch_per_gpu": n,
                        "frame_bytes": round(frame_bytes, 2),
                        "pmr_rules": nrules, "rotating_buffers": nbuf,
-                       "kernel_mode": ["auto", "walk", "evaluate-all"][args.kernel_mode],
+                       "kernel_mode": ["auto", "walk", "evaluate-all", "hash-walk"][args.kernel_mode],
                        "parallelism": f"dp{world} (packet shards, no data-path collective)"},
             "roofline": roofline, "cpu_baseline": cpu,
         }

@@ -210,9 +210,10 @@ int         odpg_device_count(void);
 int  odpg_ctx_create(int device, void *stream, odpg_ctx_t **ctx);
 void odpg_ctx_destroy(odpg_ctx_t *ctx);
 void *odpg_ctx_stream(odpg_ctx_t *ctx);
-/* Kernel strategy: 0 = auto (evaluate-all for tables of single-word compares
- * up to 1024 PMRs, which compile to exact-match groups; the wave-cooperative
- * walk otherwise), 1 = walk, 2 = evaluate-all. All
+/* Kernel strategy: 0 = auto (hash walk for tables of single-word compares
+ * with at most 8 distinct (field, mask) groups; evaluate-all for other such
+ * tables up to 1024 PMRs; the wave-cooperative walk otherwise), 1 = walk,
+ * 2 = evaluate-all, 3 = hash walk (single-word tables; walk otherwise). All
  * strategies produce identical results; this only selects the code path. */
 int  odpg_ctx_set_kernel_mode(odpg_ctx_t *ctx, int mode);
 int  odpg_ctx_sync(odpg_ctx_t *ctx);

@@ -666,7 +666,74 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 	b.len = len;
 	b.inf_lo = (uint32_t)p.inf;
 
-	if constexpr (MODE != 0) {
+	if constexpr (MODE == 3) {
+		/* hash walk: match_pmr_cos (odp_classification.c:1599-1642) one
+		 * level at a time; at CoS c a packet probes each CoS-keyed walk
+		 * group once with (c, masked key word) and the lowest PMR index
+		 * found is the first match of c's rule list (odpg_internal.h).
+		 * hgroups / hents carry the walk groups in this mode. */
+		KeySrc<W, GF> key;
+
+		key.f = f;
+		key.v = &v;
+		key.b = &b;
+		key.fast = FAST && wave_fast;
+		auto probe = [&](const uint2 *ents, uint32_t off, uint32_t h, uint32_t szm,
+				 uint32_t kv, uint32_t c) -> uint32_t {
+			for (uint32_t pr = 0; pr <= szm; ++pr) {
+				const uint2 e = ents[off + h];
+
+				if (e.y == HENT_EMPTY)
+					break;
+				if (e.x == kv && (e.y & 0xffffu) == c)
+					return e.y >> 16;
+				h = (h + 1u) & szm;
+			}
+			return 0xffffffffu;
+		};
+		while (__ballot(active)) {
+			if (active) {
+				uint32_t best = 0xffffffffu;
+
+				for (uint32_t gi = 0; gi < num_hgroups; ++gi) {
+					const uint4 g0 = *(const uint4 *)(hgroups + gi);
+					const uint2 g1 = *(const uint2 *)((const uint32_t *)(hgroups + gi) + 4);
+					const uint32_t gslot = __builtin_amdgcn_readfirstlane(g0.x);
+					const uint32_t greq = __builtin_amdgcn_readfirstlane(g0.y);
+					const uint32_t gmask = __builtin_amdgcn_readfirstlane(g0.z);
+					const uint32_t lg = __builtin_amdgcn_readfirstlane(g0.w);
+					const uint32_t goff = __builtin_amdgcn_readfirstlane(g1.x);
+
+					if ((b.inf_lo & greq) == greq) {
+						const uint32_t kv = key(gslot) & gmask;
+						const uint32_t h = walk_hash(kv, cos, lg);
+						const uint32_t r = hent_in_lds
+							? probe(hents_l, goff, h, (1u << lg) - 1u, kv, cos)
+							: probe((const uint2 *)hents_g, goff, h, (1u << lg) - 1u, kv, cos);
+
+						best = r < best ? r : best;
+					}
+				}
+				if (best == 0xffffffffu) {
+					active = false;
+				} else {
+					const uint32_t pi = pinfo[best];
+
+					cos = pi & 0xffffu;
+					mark = pi >> 16;
+					any_match = true;
+					if (do_cos_stats && ((cinfo[cos].y >> 16) & 0xffu))
+						atomicAdd(&cos_cnt[cos], 1u);
+					if (++steps >= num_cos) {
+						cos = ODPG_COS_LOOP;
+						active = false;
+					} else if ((cinfo[cos].x >> 16) == 0u) {
+						active = false;       /* no rules below: done */
+					}
+				}
+			}
+		}
+	} else if constexpr (MODE != 0) {
 		/* evaluate every PMR of the table (branch-free, wave-uniform
 		 * descriptors), then resolve match_pmr_cos's depth-first
 		 * first-match walk (odp_classification.c:1599-1642) on the hit
@@ -1056,8 +1123,8 @@ static hipError_t launch_layout(const odpg_launch_args &a, uint32_t &grid, hipSt
 				  !(a.tbl_flags & (TBL_GENERIC | TBL_ANY_HASHQ)) && !a.mark &&
 				  !a.meta && !a.stats;
 
-		if (MODE == 1 && lean)
-			return launch_one<64, false, false, false, 1, true, true>(a, grid, s);
+		if ((MODE == 1 || MODE == 3) && lean)
+			return launch_one<64, false, false, false, MODE, true, true>(a, grid, s);
 		if (MODE != 0)   /* register fast path for plain frames */
 			return launch_one<64, false, false, false, MODE, true>(a, grid, s);
 		return launch_one<64, true, false, false, MODE>(a, grid, s);
@@ -1081,11 +1148,26 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 	 * (cost per packet ~ number of groups); otherwise the walk, which only
 	 * evaluates the rules of the CoS a packet visits (C3: 4x faster than
 	 * evaluating all 256 generic PMRs per packet) */
+	const bool simple = (a->tbl_flags & TBL_SIMPLE) != 0;
+
 	if (mode == 0)
-		mode = (a->tbl_flags & TBL_SIMPLE) && a->num_pmr <= EVAL_ALL_MAX_PMR ? 2 : 1;
+		mode = simple && a->num_wgroups <= WALK_MAX_GROUPS ? 3
+		       : simple && a->num_pmr <= EVAL_ALL_MAX_PMR ? 2 : 1;
 	if (mode == 2 && a->num_pmr > EVAL_ALL_MAX_PMR)
 		mode = 1;
-	if (mode == 1)
+	if (mode == 3 && !simple)
+		mode = 1;
+	if (mode == 3) {
+		/* the hash walk reads its CoS-keyed groups through the
+		 * exact-match group arguments */
+		odpg_launch_args w = *a;
+
+		w.hgroups = a->wgroups;
+		w.num_hgroups = a->num_wgroups;
+		w.hents = (const dhent_t *)a->wents;
+		w.num_hent = a->num_went;
+		e = launch_layout<3>(w, grid, s);
+	} else if (mode == 1)
 		e = launch_layout<0>(*a, grid, s);
 	else if (a->num_pmr <= 64)
 		e = launch_layout<1>(*a, grid, s);

@@ -12,6 +12,7 @@
 #include <string.h>
 #include <errno.h>
 #include <algorithm>
+#include <map>
 #include <tuple>
 #include <vector>
 
@@ -363,6 +364,61 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	std::vector<drun_t> runs;
 	std::vector<dhgroup_t> hgroups;
 	std::vector<dhent_t> hents;
+	std::vector<dhgroup_t> wgroups;
+	std::vector<dwent_t> wents;
+
+	if (is_simple) {
+		/* CoS-keyed walk groups over every PMR (odpg_internal.h) */
+		std::vector<uint32_t> src_cos(pmr.size(), 0);
+
+		for (uint32_t c = 0; c < ncos; c++)
+			for (uint32_t k = 0; k < cos[c].nrule; k++)
+				src_cos[cos[c].rule_start + k] = c;
+		std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::vector<size_t>> by_key;
+
+		for (size_t k = 0; k < simple.size(); k++)
+			by_key[std::make_tuple(simple_slot[k], simple[k].req, simple[k].mask)].push_back(k);
+		for (auto &kv : by_key) {
+			/* lowest PMR index per (cos, value); values with bits outside
+			 * the mask never match and are left out */
+			std::map<std::pair<uint32_t, uint32_t>, uint32_t> first;
+
+			for (size_t k : kv.second) {
+				const dsimple_t &e = simple[k];
+
+				if (e.value & ~e.mask)
+					continue;
+				auto key = std::make_pair(src_cos[e.idx], e.value);
+				auto it = first.find(key);
+
+				if (it == first.end() || e.idx < it->second)
+					first[key] = e.idx;
+			}
+			uint32_t lg = 1;
+
+			while ((1u << lg) < 2 * first.size())
+				lg++;
+			dhgroup_t g;
+
+			memset(&g, 0, sizeof(g));
+			g.slot = std::get<0>(kv.first);
+			g.req = std::get<1>(kv.first);
+			g.mask = std::get<2>(kv.first);
+			g.log2sz = lg;
+			g.off = (uint32_t)wents.size();
+			g.count = (uint32_t)first.size();
+			wents.resize(wents.size() + (1u << lg), dwent_t{0u, HENT_EMPTY});
+			for (auto &f : first) {
+				uint32_t hsh = walk_hash(f.first.second, f.first.first, lg);
+
+				while (wents[g.off + hsh].cos_pmr != HENT_EMPTY)
+					hsh = (hsh + 1) & ((1u << lg) - 1);
+				wents[g.off + hsh].value = f.first.second;
+				wents[g.off + hsh].cos_pmr = f.first.first | (f.second << 16);
+			}
+			wgroups.push_back(g);
+		}
+	}
 
 	if (is_simple) {
 		/* exact-match groups -> hash tables; the rest stays linear */
@@ -476,6 +532,8 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.num_runs = is_simple ? (uint32_t)runs.size() : 0;
 	h.num_hgroups = is_simple ? (uint32_t)hgroups.size() : 0;
 	h.num_hent = is_simple ? (uint32_t)hents.size() : 0;
+	h.num_wgroups = is_simple ? (uint32_t)wgroups.size() : 0;
+	h.num_went = is_simple ? (uint32_t)wents.size() : 0;
 	h.num_cos = ncos;
 	h.default_cos = r->default_cos;
 	h.error_cos = r->error_cos;
@@ -512,7 +570,9 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.cos_off = align(h.pmr_off + (uint32_t)(pmr.size() * sizeof(dpmr_t)));
 	h.cinfo_off = align(h.cos_off + (uint32_t)(cos.size() * sizeof(dcos_t)));
 	h.pinfo_off = align(h.cinfo_off + (uint32_t)(cinfo.size() * 4u));
-	h.blob_bytes = align(h.pinfo_off + (uint32_t)(pinfo.size() * 4u));
+	h.wgroup_off = align(h.pinfo_off + (uint32_t)(pinfo.size() * 4u));
+	h.went_off = align(h.wgroup_off + h.num_wgroups * (uint32_t)sizeof(dhgroup_t));
+	h.blob_bytes = align(h.went_off + h.num_went * (uint32_t)sizeof(dwent_t));
 	if (h.blob_bytes == 0)
 		h.blob_bytes = 64;
 	blob.assign(h.blob_bytes, 0);
@@ -539,6 +599,10 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		memcpy(blob.data() + h.cinfo_off, cinfo.data(), cinfo.size() * 4u);
 	if (!pinfo.empty())
 		memcpy(blob.data() + h.pinfo_off, pinfo.data(), pinfo.size() * 4u);
+	if (h.num_wgroups)
+		memcpy(blob.data() + h.wgroup_off, wgroups.data(), wgroups.size() * sizeof(dhgroup_t));
+	if (h.num_went)
+		memcpy(blob.data() + h.went_off, wents.data(), wents.size() * sizeof(dwent_t));
 	*hdr_out = h;
 	return 0;
 }

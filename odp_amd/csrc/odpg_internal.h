@@ -150,6 +150,29 @@ typedef struct dhent_s {
 	uint32_t idx;       /* PMR index, HENT_EMPTY = free slot */
 } dhent_t;
 
+/* CoS-keyed walk groups (TBL_SIMPLE tables): every single-word PMR is in the
+ * group of its (slot, req, mask); the group's open-addressing table is keyed
+ * by (source CoS, masked value) and holds the lowest PMR index for that key.
+ * A packet at CoS c probes each group once per level of the match_pmr_cos
+ * walk; the smallest PMR index found is the first match of c's rule list. */
+typedef struct dwent_s {
+	uint32_t value;
+	uint32_t cos_pmr;   /* cos | pmr << 16, HENT_EMPTY = free slot */
+} dwent_t;
+
+#define WALK_MAX_GROUPS 8    /* more groups: evaluate-all is cheaper */
+
+#if defined(__HIPCC__)
+#define ODPG_HD __host__ __device__
+#else
+#define ODPG_HD
+#endif
+/* slot of (value, cos) in a walk group of 2^lg entries (lg >= 1) */
+static inline ODPG_HD uint32_t walk_hash(uint32_t value, uint32_t cos, uint32_t lg)
+{
+	return ((value ^ (cos * 0x85EBCA6Bu)) * 0x9E3779B1u) >> (32u - lg);
+}
+
 #define HENT_EMPTY    0xFFFFFFFFu
 #define HASH_MIN      6      /* smaller groups stay linear */
 #define HASH_MUL      0x9E3779B1u
@@ -179,6 +202,10 @@ typedef struct dtable_hdr_s {
 	                      *  action | num_queue << 8 | stats << 16 | hash_proto << 24} */
 	uint32_t pinfo_off;  /* uint32[num_pmr]: dst | mark << 16 */
 	uint32_t slot_mask;  /* key slots any slotted term reads */
+	uint32_t wgroup_off; /* dhgroup_t[num_wgroups], CoS-keyed (dwent_t tables) */
+	uint32_t num_wgroups;
+	uint32_t went_off;   /* dwent_t[num_went] */
+	uint32_t num_went;
 	uint32_t blob_bytes;
 } dtable_hdr_t;
 
@@ -210,7 +237,11 @@ typedef struct odpg_launch_args {
 	uint32_t num_hent;
 	const uint2_t *cinfo;
 	const uint32_t *pinfo;
-	int mode;           /* 0 auto, 1 walk, 2 evaluate-all */
+	const dhgroup_t *wgroups;
+	uint32_t num_wgroups;
+	const dwent_t *wents;
+	uint32_t num_went;
+	int mode;           /* 0 auto, 1 walk, 2 evaluate-all, 3 hash walk */
 	odpg_out_t *out;
 	uint16_t *mark;
 	odpg_meta_t *meta;

@@ -30,7 +30,7 @@ struct odpg_ctx_s {
 	void *ws;          /* per-workgroup counter partials */
 	size_t ws_bytes;
 	hipEvent_t ev[NUM_EVENTS];
-	int kernel_mode;   /* 0 auto, 1 walk, 2 evaluate-all */
+	int kernel_mode;   /* 0 auto, 1 walk, 2 evaluate-all, 3 hash walk */
 	std::mutex lock;
 };
 
@@ -133,7 +133,7 @@ void odpg_ctx_destroy(odpg_ctx_t *c)
 
 int odpg_ctx_set_kernel_mode(odpg_ctx_t *c, int mode)
 {
-	if (!c || mode < 0 || mode > 2)
+	if (!c || mode < 0 || mode > 3)
 		return -EINVAL;
 	c->kernel_mode = mode;
 	return 0;
@@ -263,6 +263,10 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.num_hent = h.num_hent;
 	a.cinfo = (const uint2_t *)((const uint8_t *)t->dblob + h.cinfo_off);
 	a.pinfo = (const uint32_t *)((const uint8_t *)t->dblob + h.pinfo_off);
+	a.wgroups = (const dhgroup_t *)((const uint8_t *)t->dblob + h.wgroup_off);
+	a.num_wgroups = h.num_wgroups;
+	a.wents = (const dwent_t *)((const uint8_t *)t->dblob + h.went_off);
+	a.num_went = h.num_went;
 	a.mode = c->kernel_mode;
 	a.out = r->out;
 	a.mark = r->mark;

@@ -88,7 +88,7 @@ class Context:
             pass
 
     def set_kernel_mode(self, mode):
-        """0 auto, 1 wave-cooperative walk, 2 evaluate-all (same results)."""
+        """0 auto, 1 wave-cooperative walk, 2 evaluate-all, 3 hash walk (same results)."""
         L.check(lib.odpg_ctx_set_kernel_mode(self.h, mode), "odpg_ctx_set_kernel_mode")
 
     def sync(self):

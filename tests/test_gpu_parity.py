@@ -20,12 +20,13 @@ def both(ctx, rules, buf, num, stride=0, desc=None, opt=0, layer=L.LAYER_ALL, cl
     auto) and on the oracle; the strategies must agree bit for bit."""
     tbl = ctx.table(rules)
     res = {}
-    for mode in (1, 2, 0):
+    for mode in (1, 2, 3, 0):
         ctx.set_kernel_mode(mode)
         res[mode] = ctx.classify(tbl, buf, num, stride=stride, desc=desc, opt=opt,
                                  layer=layer, classify=classify)
     ctx.set_kernel_mode(0)
     assert_same(res[1], res[2], "walk vs evaluate-all")
+    assert_same(res[1], res[3], "walk vs hash walk")
     o = oracle.classify(rules, buf, num, stride=stride, desc=desc, opt=opt, layer=layer,
                         classify=classify)
     return res[0], o
