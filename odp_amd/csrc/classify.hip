@@ -1144,15 +1144,18 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 	int mode = a->mode;
 	hipError_t e;
 
-	/* auto: evaluate-all when the table compiles to exact-match groups
-	 * (cost per packet ~ number of groups); otherwise the walk, which only
-	 * evaluates the rules of the CoS a packet visits (C3: 4x faster than
-	 * evaluating all 256 generic PMRs per packet) */
+	/* auto: single-word tables take evaluate-all (one probe per exact-match
+	 * group, C2 23 vs 32 us for the hash walk) unless their groups repeat
+	 * values across CoS (C4: every probe would walk ~15 equal keys; hash
+	 * walk 38 vs 72 us); other tables take the walk, which only evaluates
+	 * the rules of the CoS a packet visits (C3: 4x faster than evaluating
+	 * all 256 generic PMRs per packet) */
 	const bool simple = (a->tbl_flags & TBL_SIMPLE) != 0;
 
 	if (mode == 0)
-		mode = simple && a->num_wgroups <= WALK_MAX_GROUPS ? 3
-		       : simple && a->num_pmr <= EVAL_ALL_MAX_PMR ? 2 : 1;
+		mode = simple && (a->tbl_flags & TBL_HASHWALK) && a->num_wgroups <= WALK_MAX_GROUPS ? 3
+		       : simple && a->num_pmr <= EVAL_ALL_MAX_PMR ? 2
+		       : simple && a->num_wgroups <= WALK_MAX_GROUPS ? 3 : 1;
 	if (mode == 2 && a->num_pmr > EVAL_ALL_MAX_PMR)
 		mode = 1;
 	if (mode == 3 && !simple)

@@ -420,6 +420,8 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		}
 	}
 
+	size_t dup_entries = 0, dup_distinct = 0;
+
 	if (is_simple) {
 		/* exact-match groups -> hash tables; the rest stays linear */
 		std::vector<size_t> order(simple.size());
@@ -445,6 +447,13 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 				if (simple[order[k]].value & ~simple[order[k]].mask)
 					ok = false;   /* can never match: keep it linear */
 			if (ok) {
+				std::vector<uint32_t> vals;
+
+				for (size_t k = g0; k < g1; k++)
+					vals.push_back(simple[order[k]].value);
+				std::sort(vals.begin(), vals.end());
+				dup_entries += cnt;
+				dup_distinct += (size_t)(std::unique(vals.begin(), vals.end()) - vals.begin());
 				uint32_t lg = 3;
 
 				while ((1u << lg) < 2 * cnt)
@@ -527,6 +536,8 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.slot_mask = slot_mask;
 	if (is_simple)
 		h.flags |= TBL_SIMPLE;
+	if (is_simple && dup_distinct && dup_entries >= 3 * dup_distinct)
+		h.flags |= TBL_HASHWALK;
 	if (generic)
 		h.flags |= TBL_GENERIC;
 	h.num_runs = is_simple ? (uint32_t)runs.size() : 0;

@@ -87,6 +87,9 @@ typedef struct dcos_s {
 #define TBL_ANY_STATS  0x4
 #define TBL_SIMPLE     0x8   /* every PMR is one single-word slotted compare */
 #define TBL_GENERIC    0x10  /* some term needs the generic (base + off) compare */
+#define TBL_HASHWALK   0x20  /* exact-match groups repeat values across CoS (mean
+			      * >= 3 entries per distinct value): per-level
+			      * CoS-keyed probes beat evaluating every entry */
 
 /* ---- per-packet key slots (evaluate-all kernels) -------------------------
  * The parser-relative 32-bit words the terms can compare, extracted once per
