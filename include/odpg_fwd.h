@@ -5,12 +5,12 @@
  *
  * Per packet the reference l3fwd worker (example/l3fwd/odp_l3fwd.c) does:
  *   drop_err_pkts()            odp_l3fwd.c:269-292   has_error (with -e) or !ipv4 -> drop
- *   l3fwd_pkt_hash()           odp_l3fwd.c:195-236   find_fwd_db_entry(): dst-IP key,
+ *   l3fwd_pkt_hash()           odp_l3fwd.c:194-234   find_fwd_db_entry(): dst-IP key,
  *                                                     first match in the LIFO route list
  *                                                     (odp_l3fwd_db.c:474-508)
- *   l3fwd_pkt_lpm()            odp_l3fwd.c:238-256   fib_tbl_lookup() on the 16-4-4-4-4
- *                                                     trie (odp_l3fwd_lpm.c:209-230)
- *   ipv4_dec_ttl_csum_update() odp_l3fwd.c:182-193   TTL - 1, incremental checksum
+ *   l3fwd_pkt_lpm()            odp_l3fwd.c:236-256   fib_tbl_lookup() on the 16-4-4-4-4
+ *                                                     trie (odp_l3fwd_lpm.c:210-230)
+ *   ipv4_dec_ttl_csum_update() odp_l3fwd.c:183-192   TTL - 1, incremental checksum
  *   MAC rewrite + output port
  * on packets parsed by the pktio at layer L4 (ALL with -e), with no RX
  * checksum options (odp_l3fwd.c:132-135). odpg_l3fwd() does all of it for a

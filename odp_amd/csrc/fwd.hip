@@ -14,9 +14,9 @@
  *   3. route: hash mode = first match of the newest-first route list
  *      (find_fwd_db_entry, odp_l3fwd_db.c:474-508; routes are wave-uniform
  *      scalar loads); LPM mode = the reference's 16-4-4-4-4 trie
- *      (fib_tbl_lookup, odp_l3fwd_lpm.c:209-230), one dependent L2-resident
+ *      (fib_tbl_lookup, odp_l3fwd_lpm.c:210-230), one dependent L2-resident
  *      load per level;
- *   4. ipv4_dec_ttl_csum_update (odp_l3fwd.c:182-193) and the MAC rewrite of
+ *   4. ipv4_dec_ttl_csum_update (odp_l3fwd.c:183-192) and the MAC rewrite of
  *      l3fwd_pkt_hash / l3fwd_pkt_lpm, written back in place (fast waves:
  *      two 16-byte stores of bytes 0..31).
  */
@@ -400,7 +400,7 @@ extern "C" int odpg_fwd_create(odpg_ctx_t *ctx, const odpg_route_t *routes, uint
 	if (param->mode == ODPG_FWD_LPM) {
 		FibTrie t;
 
-		/* setup_fwd_db inserts newest first (odp_l3fwd.c:164-175) */
+		/* setup_fwd_db inserts newest first (odp_l3fwd.c:154-176) */
 		for (int k = (int)num_routes - 1; k >= 0; k--)
 			t.add(routes[k].addr, (uint32_t)routes[k].oif_id, routes[k].depth);
 		if (t.overflow)

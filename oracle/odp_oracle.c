@@ -1083,11 +1083,11 @@ uint32_t oracle_thash(const uint32_t *tuple, uint32_t len)
 /* ---- 16-4-4-4-4 trie of odp_l3fwd_lpm.c, node-array form ---------------
  * fib_node_t (:31-38) keeps {next_hop | next, valid:1, end:1, depth:6}; a
  * node's children are 16 consecutive nodes of the sub-table pool. Every
- * quirk of the reference builder is kept: fib_alloc_sub (:45-60) hands out
- * the nodes at (k + 1) * 16; a split (:93-105) copies next_hop / depth to
+ * quirk of the reference builder is kept: fib_alloc_sub (:57-74) hands out
+ * the nodes at (k + 1) * 16; a split (:107-122) copies next_hop / depth to
  * the children but leaves them invalid; a depth <= 16 route touches one
- * first-level node (:174-200); a route ending inside a stride updates the
- * single child at `ip >> ip_width` (:106-111); fib_update_node (:62-81)
+ * first-level node (:184-201); a route ending inside a stride updates the
+ * single child at `ip >> ip_width` (:124-130); fib_update_node (:76-99)
  * recurses only into children that are leaves. */
 #define FIB_L1    65536u
 #define FIB_POOL  16384u
@@ -1220,7 +1220,7 @@ static int fib_lookup(const fib_t *f, uint32_t ip, int32_t *port)
 }
 
 /* ---- find_fwd_db_entry (odp_l3fwd_db.c:474-508): first match in the list,
- * which create_fwd_db_entry() prepends to (:409-411), i.e. newest first */
+ * which create_fwd_db_entry() prepends to (:427-428), i.e. newest first */
 static int route_first_match(const odpg_route_t *r, uint32_t n, uint32_t ip)
 {
 	for (int k = (int)n - 1; k >= 0; k--) {
@@ -1239,7 +1239,7 @@ static uint32_t rd_be32(const uint8_t *p)
 }
 
 /* One batch through drop_err_pkts + l3fwd_pkt_hash / l3fwd_pkt_lpm
- * (odp_l3fwd.c:182-292). frames are rewritten in place; out_port[i] = port
+ * (odp_l3fwd.c:183-292). frames are rewritten in place; out_port[i] = port
  * or -1 (dropped). Returns 0, or -1 for a route set outside the supported
  * domain (see include/odpg_fwd.h). */
 int oracle_l3fwd(const odpg_route_t *routes, uint32_t nroutes, const odpg_fwd_param_t *prm,
@@ -1256,8 +1256,8 @@ int oracle_l3fwd(const odpg_route_t *routes, uint32_t nroutes, const odpg_fwd_pa
 		if (!fib)
 			return -1;
 		for (uint32_t i = 0; i < FIB_L1; i++)
-			fib->l1[i].end = 1;               /* fib_tbl_init (:131-137) */
-		/* setup_fwd_db walks the list newest first (odp_l3fwd.c:164-175) */
+			fib->l1[i].end = 1;               /* fib_tbl_init (:140-172) */
+		/* setup_fwd_db walks the list newest first (odp_l3fwd.c:154-176) */
 		for (int k = (int)nroutes - 1; k >= 0; k--)
 			fib_insert(fib, routes[k].addr, (uint32_t)routes[k].oif_id, routes[k].depth);
 		if (fib->overflow) {
@@ -1290,7 +1290,7 @@ int oracle_l3fwd(const odpg_route_t *routes, uint32_t nroutes, const odpg_fwd_pa
 		uint32_t dst = rd_be32(ip + 16);
 		int32_t dif;
 
-		/* ipv4_dec_ttl_csum_update (odp_l3fwd.c:182-193): raw LE u16 of the
+		/* ipv4_dec_ttl_csum_update (odp_l3fwd.c:183-192): raw LE u16 of the
 		 * checksum field, a = ~cpu_to_be_16(0x100) = 0xfffe */
 		uint16_t cs = (uint16_t)(ip[10] | (ip[11] << 8));
 

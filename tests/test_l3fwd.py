@@ -91,7 +91,7 @@ def test_hash_rejects_cache_dependent_routes():
 
 # ---- fib_tbl_insert / fib_tbl_lookup quirks (odp_l3fwd_lpm.c) ---------------
 def test_lpm_short_prefix_sets_one_first_level_node():
-    """depth <= 16 writes only fib_rt_tbl[ip >> 16] (:174-200)."""
+    """depth <= 16 writes only fib_rt_tbl[ip >> 16] (:184-201)."""
     port, valid = oracle.fib_lookup(gpu.make_routes([R("10.0.0.0", 8, 3)]),
                                     [ip("10.0.5.5"), ip("10.1.0.1")])
     assert list(valid) == [True, False] and port[0] == 3
@@ -99,7 +99,7 @@ def test_lpm_short_prefix_sets_one_first_level_node():
 
 def test_lpm_split_children_stay_invalid():
     """A split copies next_hop / depth into the new children but not the
-    valid bit (:93-105): after /16 then /24, the /16's other addresses miss."""
+    valid bit (:107-122): after /16 then /24, the /16's other addresses miss."""
     routes = [R("10.0.1.0", 24, 2), R("10.0.0.0", 16, 1)]   # /16 inserted first (newest first)
     port, valid = oracle.fib_lookup(gpu.make_routes(routes),
                                     [ip("10.0.1.7"), ip("10.0.2.5"), ip("10.0.200.1")])
@@ -108,7 +108,7 @@ def test_lpm_split_children_stay_invalid():
 
 def test_lpm_prefix_inside_stride_updates_single_child():
     """A route ending inside a 4-bit stride updates next[ip >> ip_width]
-    only (:106-111): 10.0.64.0/18 lands on the child for bits 0001."""
+    only (:124-130): 10.0.64.0/18 lands on the child for bits 0001."""
     port, valid = oracle.fib_lookup(gpu.make_routes([R("10.0.64.0", 18, 5)]),
                                     [ip("10.0.64.1"), ip("10.0.16.1"), ip("10.0.31.255")])
     assert list(valid) == [False, True, True] and list(port[1:]) == [5, 5]
