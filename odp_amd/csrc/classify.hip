@@ -402,22 +402,29 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 	const dhgroup_t *__restrict__ hgroups, uint32_t num_hgroups,
 	const dhent_t *__restrict__ hents_g, uint32_t num_hent,
 	const uint2 *__restrict__ cinfo_g, const uint32_t *__restrict__ pinfo_g,
+	const dmgroup_t *__restrict__ mgroups, uint32_t num_mgroups,
+	const uint4 *__restrict__ ments_g, uint32_t num_ment, const uint2 *__restrict__ pinfo2_g,
 	odpg_out_t *__restrict__ out, uint16_t *__restrict__ mark_out,
 	odpg_meta_t *__restrict__ meta_out, uint64_t *__restrict__ pk_partial,
 	uint32_t *__restrict__ cos_partial)
 {
 	constexpr uint32_t RW = W / 4 + 1;       /* odd dword row stride */
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-	uint32_t *cos_cnt = smem + BLOCK * RW;
+	/* u64 hit-map kernel: mask-group entries (16 B aligned, after the rows)
+	 * and the one-read-per-level resolve table */
+	const bool use_mg = MODE == 1 && (tbl_flags & TBL_MGROUPS);
+	uint4 *ments_l = (uint4 *)(smem + BLOCK * RW);
+	uint32_t *cos_cnt = (uint32_t *)(ments_l + (use_mg ? num_ment : 0u));
 	/* MODE 2: per-lane PMR hit bitmap after the CoS counters */
 	const uint32_t hrw = ((num_pmr + 31u) >> 5) | 1u;
 	uint32_t *hitmap = cos_cnt + (cos_partial ? ((num_cos + 3u) & ~3u) : 0u);
 	/* exact-match hash tables, copied to LDS when small */
 	uint2 *hents_l = (uint2 *)(hitmap + (MODE == 2 ? BLOCK * hrw : 0u));
-	const bool hent_in_lds = num_hent <= HENT_LDS_MAX;
+	const bool hent_in_lds = !use_mg && num_hent <= HENT_LDS_MAX;
 	/* per-lane CoS / PMR lookups of the first-match resolve, in LDS */
 	uint2 *cinfo = hents_l + (hent_in_lds ? num_hent : 0u);
 	uint32_t *pinfo = (uint32_t *)(cinfo + num_cos);
+	uint2 *pinfo2 = (uint2 *)(pinfo + ((num_pmr + 1u) & ~1u));
 	__shared__ unsigned long long blk_pk[4];
 
 	const uint32_t tid = threadIdx.x;
@@ -433,6 +440,28 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 	uint32_t *row = smem + tid * RW;
 	uint64_t lane_pkt = 0, lane_oct = 0, lane_err = 0, lane_disc = 0;
 
+	/* persistent workgroups: tiles of BLOCK packets */
+	const uint32_t ntiles = (num + BLOCK - 1) / BLOCK;
+	uint32_t fn[16];   /* FAST: next tile's frame, prefetched one tile ahead */
+
+	if constexpr (FAST) {
+		/* first tile's frames are issued before the table copy below, so
+		 * the frame stream starts at once instead of behind the table
+		 * reads' round trip; unconditional (index clamped into the batch)
+		 * so the loads always issue and the wait counts stay exact */
+		const uint32_t i0 = min(blockIdx.x * BLOCK + tid, num - 1u);
+		const uint4 *src = (const uint4 *)(frames + (size_t)i0 * 64u);
+
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			const uint4 x = ld_stream(src + k);
+
+			fn[4 * k + 0] = x.x;
+			fn[4 * k + 1] = x.y;
+			fn[4 * k + 2] = x.z;
+			fn[4 * k + 3] = x.w;
+		}
+	}
 	if (tid < 4)
 		blk_pk[tid] = 0ull;
 	if (do_cos_stats)
@@ -447,6 +476,12 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 		for (uint32_t k = tid; k < num_pmr; k += BLOCK)
 			pinfo[k] = pinfo_g[k];
 	}
+	if (use_mg)
+		for (uint32_t k = tid; k < num_ment; k += BLOCK)
+			ments_l[k] = ments_g[k];
+	if (MODE == 1)
+		for (uint32_t k = tid; k < num_pmr; k += BLOCK)
+			pinfo2[k] = pinfo2_g[k];
 	__syncthreads();
 	/* default CoS entry: read once, outside the tile loop */
 	const bool def_valid = default_cos >= 0 && coses[default_cos].valid;
@@ -459,26 +494,6 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 			return cinfo_g[c];
 	};
 
-	/* persistent workgroups: tiles of BLOCK packets */
-	const uint32_t ntiles = (num + BLOCK - 1) / BLOCK;
-	uint32_t fn[16];   /* FAST: next tile's frame, prefetched one tile ahead */
-
-	if constexpr (FAST) {
-		/* unconditional (index clamped into the batch) so the loads always
-		 * issue and the wait counts on them stay exact */
-		const uint32_t i0 = min(blockIdx.x * BLOCK + tid, num - 1u);
-		const uint4 *src = (const uint4 *)(frames + (size_t)i0 * 64u);
-
-#pragma unroll
-		for (int k = 0; k < 4; ++k) {
-			const uint4 x = ld_stream(src + k);
-
-			fn[4 * k + 0] = x.x;
-			fn[4 * k + 1] = x.y;
-			fn[4 * k + 2] = x.z;
-			fn[4 * k + 3] = x.w;
-		}
-	}
 	/* result stores of a tile are issued at the top of the next one, before
 	 * that tile's prefetch: vector-memory counters retire in issue order, so
 	 * a store issued after the prefetch would make the next wait on the
@@ -749,7 +764,43 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 			key.v = &v;
 			key.b = &b;
 			key.fast = FAST && wave_fast;
-			if (tbl_flags & TBL_SIMPLE) {
+			if (use_mg) {
+				/* mask groups: both cuckoo candidates of every group
+				 * are read (independent LDS reads, no probe chain) and
+				 * the entry whose value matches ORs its PMR bits */
+				uint32_t lo = 0u, hi = 0u;
+
+				for (uint32_t gi = 0; gi < num_mgroups; ++gi) {
+					const uint4 g0 = *(const uint4 *)(mgroups + gi);
+					const uint4 g1 = *((const uint4 *)(mgroups + gi) + 1);
+					const uint32_t gslot = __builtin_amdgcn_readfirstlane(g0.x);
+					const uint32_t greq = __builtin_amdgcn_readfirstlane(g0.y);
+					const uint32_t gmask = __builtin_amdgcn_readfirstlane(g0.z);
+					const uint32_t gsh = __builtin_amdgcn_readfirstlane(g0.w);
+					const uint32_t goff = __builtin_amdgcn_readfirstlane(g1.x);
+					const uint32_t gm1 = __builtin_amdgcn_readfirstlane(g1.y);
+					const uint32_t gm2 = __builtin_amdgcn_readfirstlane(g1.z);
+					const uint32_t gcnt = __builtin_amdgcn_readfirstlane(g1.w);
+					const uint32_t kvm = key(gslot) & gmask;
+					const bool rq = (b.inf_lo & greq) == greq;
+
+					if (gcnt == 1u) {
+						/* one value: inline {value, lo, hi} = {m1, m2, off} */
+						const bool h = rq & (kvm == gm1);
+
+						lo |= h ? gm2 : 0u;
+						hi |= h ? goff : 0u;
+						continue;
+					}
+					const uint4 e1 = ments_l[goff + ((kvm * gm1) >> gsh)];
+					const uint4 e2 = ments_l[goff + ((kvm * gm2) >> gsh)];
+					const bool h1 = rq & (e1.x == kvm), h2 = rq & (e2.x == kvm);
+
+					lo |= (h1 ? e1.y : 0u) | (h2 ? e2.y : 0u);
+					hi |= (h1 ? e1.z : 0u) | (h2 ? e2.z : 0u);
+				}
+				hits = ((uint64_t)hi << 32) | lo;
+			} else if (tbl_flags & TBL_SIMPLE) {
 				uint32_t lo = 0u, hi = 0u;
 
 				if (MODE == 2)
@@ -847,10 +898,39 @@ __global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
 				}
 			}
 		}
-		while (active) {
+		/* MODE 1: pinfo2 carries the destination's rule range, so each
+		 * level costs one LDS read */
+		uint32_t rs = 0u, nr = 0u;
+
+		if (MODE == 1 && active) {
+			const uint32_t ci = cinfo[cos].x;
+
+			rs = ci & 0xffffu;
+			nr = ci >> 16;
+		}
+		while (MODE == 1 && active) {
+			const int k = first_hit64(hits, rs, nr);
+
+			if (k < 0)
+				break;
+			const uint2 pi = pinfo2[rs + (uint32_t)k];
+
+			cos = pi.x & 0xffffu;
+			mark = pi.x >> 16;
+			rs = pi.y & 0xffu;
+			nr = (pi.y >> 8) & 0xffu;
+			any_match = true;
+			if (do_cos_stats && ((cinfo[cos].y >> 16) & 0xffu))
+				atomicAdd(&cos_cnt[cos], 1u);
+			if (++steps >= num_cos) {
+				cos = ODPG_COS_LOOP;
+				break;
+			}
+		}
+		while (MODE == 2 && active) {
 			const uint32_t ci = cinfo[cos].x;
 			const uint32_t rs = ci & 0xffffu, nr = ci >> 16;
-			const int k = MODE == 1 ? first_hit64(hits, rs, nr) : first_hit_lds(hrow, rs, nr);
+			const int k = first_hit_lds(hrow, rs, nr);
 
 			if (k < 0)
 				break;
@@ -1080,8 +1160,14 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 		lds += (size_t)((a.num_cos + 3u) & ~3u) * 4u;
 	if (MODE == 2)
 		lds += (size_t)BLOCK * (((a.num_pmr + 31u) >> 5) | 1u) * 4u;
-	if (MODE != 0 && a.num_hent <= HENT_LDS_MAX)
+	const bool use_mg = MODE == 1 && (a.tbl_flags & TBL_MGROUPS);
+
+	if (MODE != 0 && !use_mg && a.num_hent <= HENT_LDS_MAX)
 		lds += (size_t)a.num_hent * 8u;
+	if (use_mg)
+		lds += (size_t)a.num_ment * 16u;
+	if (MODE == 1)
+		lds += (size_t)a.num_pmr * 8u + 4u;
 	if (MODE != 0)
 		lds += (size_t)a.num_cos * 8u + (size_t)a.num_pmr * 4u;
 	/* persistent grid: exactly the workgroups that are resident at once
@@ -1108,7 +1194,8 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 			   a.classify, a.terms, a.pmrs, a.coses, a.num_cos, a.default_cos,
 			   a.error_cos, a.tbl_flags, a.num_pmr, a.slot_mask, a.slots, a.simple,
 			   a.runs, a.num_runs, a.hgroups, a.num_hgroups, a.hents, a.num_hent,
-			   (const uint2 *)a.cinfo, a.pinfo, a.out, a.mark, a.meta, a.pk_partial,
+			   (const uint2 *)a.cinfo, a.pinfo, a.mgroups, a.num_mgroups,
+			   (const uint4 *)a.ments, a.num_ment, (const uint2 *)a.pinfo2, a.out, a.mark, a.meta, a.pk_partial,
 			   a.cos_partial);
 	return hipGetLastError();
 }

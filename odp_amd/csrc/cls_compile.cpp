@@ -236,6 +236,89 @@ dslot_t slotify(const dterm_t &t)
 
 } /* namespace */
 
+/* Two-choice cuckoo placement of one mask group's distinct values
+ * (odpg_internal.h "Mask groups"). Deterministic: multipliers come from a
+ * fixed sequence; the table doubles when no pair places every value. */
+static void build_mgroup(const std::map<uint32_t, uint64_t> &vals, dmgroup_t &g,
+			 std::vector<dment_t> &ents)
+{
+	const size_t n = vals.size();
+	uint32_t lg = 1;
+
+	if (n == 1) {
+		/* inline single value: {value, lo, hi} in {m1, m2, off}, no entries */
+		g.count = 1;
+		g.shift = 31;
+		g.m1 = vals.begin()->first;
+		g.m2 = (uint32_t)vals.begin()->second;
+		g.off = (uint32_t)(vals.begin()->second >> 32);
+		return;
+	}
+
+	while ((1u << lg) < 2 * n)
+		lg++;
+	uint64_t seed = 0x9E3779B97F4A7C15ull;
+	auto next_mul = [&]() {
+		seed ^= seed << 13;
+		seed ^= seed >> 7;
+		seed ^= seed << 17;
+		return (uint32_t)(seed >> 32) | 1u;
+	};
+	for (;; lg++) {
+		const uint32_t sz = 1u << lg, sh = 32u - lg;
+
+		for (int attempt = 0; attempt < 64; attempt++) {
+			const uint32_t m1 = next_mul(), m2 = next_mul();
+			std::vector<int> slot(sz, -1);
+			std::vector<uint32_t> key;
+			bool ok = true;
+
+			for (auto &v : vals)
+				key.push_back(v.first);
+			for (size_t k = 0; k < n && ok; k++) {
+				int cur = (int)k;
+				uint32_t pos = (key[k] * m1) >> sh;
+
+				for (int kick = 0;; kick++) {
+					if (kick > 4 * (int)sz + 16) {
+						ok = false;
+						break;
+					}
+					std::swap(cur, slot[pos]);
+					if (cur < 0)
+						break;
+					/* move the evicted value to its other slot */
+					uint32_t p1 = (key[cur] * m1) >> sh, p2 = (key[cur] * m2) >> sh;
+
+					pos = pos == p1 ? p2 : p1;
+				}
+			}
+			if (!ok)
+				continue;
+			g.shift = sh;
+			g.m1 = m1;
+			g.m2 = m2;
+			g.off = (uint32_t)ents.size();
+			g.count = (uint32_t)n;
+			ents.resize(ents.size() + sz, dment_t{0u, 0u, 0u, 0u});
+			std::vector<uint64_t> bits;
+
+			for (auto &v : vals)
+				bits.push_back(v.second);
+			for (uint32_t s = 0; s < sz; s++) {
+				if (slot[s] < 0)
+					continue;
+				dment_t &e = ents[g.off + s];
+
+				e.value = key[slot[s]];
+				e.lo = (uint32_t)bits[slot[s]];
+				e.hi = (uint32_t)(bits[slot[s]] >> 32);
+			}
+			return;
+		}
+	}
+}
+
 int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable_hdr_t *hdr_out)
 {
 	std::vector<dcos_t> cos;
@@ -420,6 +503,35 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		}
 	}
 
+	std::vector<dmgroup_t> mgroups;
+	std::vector<dment_t> ments;
+
+	if (is_simple && pmr.size() <= MGROUP_MAX_PMR) {
+		/* mask groups over every PMR, in (slot, req, mask) order */
+		std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::map<uint32_t, uint64_t>> by_key;
+
+		for (size_t k = 0; k < simple.size(); k++) {
+			const dsimple_t &e = simple[k];
+			auto &vals = by_key[std::make_tuple(simple_slot[k], e.req, e.mask)];
+
+			if (e.value & ~e.mask)
+				continue;   /* can never match: no bit anywhere */
+			vals[e.value] |= 1ull << e.idx;
+		}
+		for (auto &kv : by_key) {
+			if (kv.second.empty())
+				continue;
+			dmgroup_t g;
+
+			memset(&g, 0, sizeof(g));
+			g.slot = std::get<0>(kv.first);
+			g.req = std::get<1>(kv.first);
+			g.mask = std::get<2>(kv.first);
+			build_mgroup(kv.second, g, ments);
+			mgroups.push_back(g);
+		}
+	}
+
 	size_t dup_entries = 0, dup_distinct = 0;
 
 	if (is_simple) {
@@ -545,6 +657,11 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.num_hent = is_simple ? (uint32_t)hents.size() : 0;
 	h.num_wgroups = is_simple ? (uint32_t)wgroups.size() : 0;
 	h.num_went = is_simple ? (uint32_t)wents.size() : 0;
+	if (is_simple && pmr.size() <= MGROUP_MAX_PMR) {
+		h.flags |= TBL_MGROUPS;
+		h.num_mgroups = (uint32_t)mgroups.size();
+		h.num_ment = (uint32_t)ments.size();
+	}
 	h.num_cos = ncos;
 	h.default_cos = r->default_cos;
 	h.error_cos = r->error_cos;
@@ -569,6 +686,19 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	}
 	for (size_t k = 0; k < pmr.size(); k++)
 		pinfo[k] = (pmr[k].dst & 0xffffu) | ((pmr[k].mark & 0xffffu) << 16);
+	std::vector<uint32_t> pinfo2;
+
+	if (pmr.size() <= MGROUP_MAX_PMR) {
+		/* rule_start < 64 and nrule <= 64 fit 8 bits each */
+		pinfo2.resize(2 * pmr.size());
+		for (size_t k = 0; k < pmr.size(); k++) {
+			const dcos_t &d = cos[pmr[k].dst];
+
+			pinfo2[2 * k] = pinfo[k];
+			pinfo2[2 * k + 1] = (d.rule_start & 0xffu) | ((uint32_t)(d.nrule & 0xffu) << 8) |
+					    ((uint32_t)d.action << 16);
+		}
+	}
 
 	auto align = [](uint32_t x) { return (x + 63u) & ~63u; };
 	h.term_off = 0;
@@ -583,7 +713,10 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.pinfo_off = align(h.cinfo_off + (uint32_t)(cinfo.size() * 4u));
 	h.wgroup_off = align(h.pinfo_off + (uint32_t)(pinfo.size() * 4u));
 	h.went_off = align(h.wgroup_off + h.num_wgroups * (uint32_t)sizeof(dhgroup_t));
-	h.blob_bytes = align(h.went_off + h.num_went * (uint32_t)sizeof(dwent_t));
+	h.mgroup_off = align(h.went_off + h.num_went * (uint32_t)sizeof(dwent_t));
+	h.ment_off = align(h.mgroup_off + h.num_mgroups * (uint32_t)sizeof(dmgroup_t));
+	h.pinfo2_off = align(h.ment_off + h.num_ment * (uint32_t)sizeof(dment_t));
+	h.blob_bytes = align(h.pinfo2_off + (uint32_t)(pinfo2.size() * 4u));
 	if (h.blob_bytes == 0)
 		h.blob_bytes = 64;
 	blob.assign(h.blob_bytes, 0);
@@ -614,6 +747,12 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		memcpy(blob.data() + h.wgroup_off, wgroups.data(), wgroups.size() * sizeof(dhgroup_t));
 	if (h.num_went)
 		memcpy(blob.data() + h.went_off, wents.data(), wents.size() * sizeof(dwent_t));
+	if (h.num_mgroups)
+		memcpy(blob.data() + h.mgroup_off, mgroups.data(), mgroups.size() * sizeof(dmgroup_t));
+	if (h.num_ment)
+		memcpy(blob.data() + h.ment_off, ments.data(), ments.size() * sizeof(dment_t));
+	if (!pinfo2.empty())
+		memcpy(blob.data() + h.pinfo2_off, pinfo2.data(), pinfo2.size() * 4u);
 	*hdr_out = h;
 	return 0;
 }

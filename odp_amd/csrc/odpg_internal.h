@@ -90,6 +90,7 @@ typedef struct dcos_s {
 #define TBL_HASHWALK   0x20  /* exact-match groups repeat values across CoS (mean
 			      * >= 3 entries per distinct value): per-level
 			      * CoS-keyed probes beat evaluating every entry */
+#define TBL_MGROUPS    0x40  /* mask groups + pinfo2 built (simple, <= 64 PMRs) */
 
 /* ---- per-packet key slots (evaluate-all kernels) -------------------------
  * The parser-relative 32-bit words the terms can compare, extracted once per
@@ -165,6 +166,36 @@ typedef struct dwent_s {
 
 #define WALK_MAX_GROUPS 8    /* more groups: evaluate-all is cheaper */
 
+/* Mask groups (TBL_SIMPLE tables of <= 64 PMRs, the u64 hit-map kernel):
+ * every (slot, req, mask) group is a two-choice cuckoo table keyed by the
+ * masked value; an entry holds the OR of the hit bits of every PMR of the
+ * group that compares equal to that value. A packet reads both candidate
+ * entries of each group (two independent LDS reads, no probe sequence) and
+ * ORs the mask of the one whose value matches. Free entries have zero masks,
+ * so a false value match on a free entry adds nothing. */
+typedef struct dmgroup_s {
+	uint32_t slot;
+	uint32_t req;
+	uint32_t mask;
+	uint32_t shift;     /* 32 - log2(entries) */
+	uint32_t off;       /* first dment_t of this group */
+	uint32_t m1, m2;    /* odd multipliers: h = (key * m) >> shift */
+	uint32_t count;     /* distinct values; 1: {value, lo, hi} inline in
+			     * {m1, m2, off} and no entries */
+} dmgroup_t;            /* 32 bytes */
+
+typedef struct dment_s {
+	uint32_t value;
+	uint32_t lo, hi;    /* hit bits of the PMRs equal to value */
+	uint32_t pad;
+} dment_t;              /* 16 bytes */
+
+#define MGROUP_MAX_PMR 64
+
+/* pinfo2[num_pmr] (u64 hit-map kernel): the first-match resolve follows one
+ * LDS read per level, {dst | mark << 16, dst rule_start | dst nrule << 8 |
+ * dst action << 16} */
+
 #if defined(__HIPCC__)
 #define ODPG_HD __host__ __device__
 #else
@@ -209,6 +240,11 @@ typedef struct dtable_hdr_s {
 	uint32_t num_wgroups;
 	uint32_t went_off;   /* dwent_t[num_went] */
 	uint32_t num_went;
+	uint32_t mgroup_off; /* dmgroup_t[num_mgroups] (num_pmr <= 64, TBL_SIMPLE) */
+	uint32_t num_mgroups;
+	uint32_t ment_off;   /* dment_t[num_ment] */
+	uint32_t num_ment;
+	uint32_t pinfo2_off; /* uint2[num_pmr] when num_pmr <= 64 */
 	uint32_t blob_bytes;
 } dtable_hdr_t;
 
@@ -244,7 +280,12 @@ typedef struct odpg_launch_args {
 	uint32_t num_wgroups;
 	const dwent_t *wents;
 	uint32_t num_went;
-	int mode;           /* 0 auto, 1 walk, 2 evaluate-all, 3 hash walk */
+	const dmgroup_t *mgroups;
+	uint32_t num_mgroups;
+	const dment_t *ments;
+	uint32_t num_ment;
+	const uint2_t *pinfo2;
+	int mode;          /* 0 auto, 1 walk, 2 evaluate-all, 3 hash walk */
 	odpg_out_t *out;
 	uint16_t *mark;
 	odpg_meta_t *meta;

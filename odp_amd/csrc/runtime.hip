@@ -267,6 +267,11 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.num_wgroups = h.num_wgroups;
 	a.wents = (const dwent_t *)((const uint8_t *)t->dblob + h.went_off);
 	a.num_went = h.num_went;
+	a.mgroups = (const dmgroup_t *)((const uint8_t *)t->dblob + h.mgroup_off);
+	a.num_mgroups = h.num_mgroups;
+	a.ments = (const dment_t *)((const uint8_t *)t->dblob + h.ment_off);
+	a.num_ment = h.num_ment;
+	a.pinfo2 = (const uint2_t *)((const uint8_t *)t->dblob + h.pinfo2_off);
 	a.mode = c->kernel_mode;
 	a.out = r->out;
 	a.mark = r->mark;
