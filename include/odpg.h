@@ -216,6 +216,11 @@ void *odpg_ctx_stream(odpg_ctx_t *ctx);
  * 2 = evaluate-all, 3 = hash walk (single-word tables; walk otherwise). All
  * strategies produce identical results; this only selects the code path. */
 int  odpg_ctx_set_kernel_mode(odpg_ctx_t *ctx, int mode);
+/* Which kernel the last odpg_classify launch in this process used (a
+ * diagnostic for tests and benches): 0 the general kernel, 1 the lean
+ * 64-byte kernel that auto mode picks for fixed 64-byte strides, tables of
+ * at most 64 single-word PMRs and verdict-only results. -1 before any. */
+int  odpg_last_kernel(void);
 int  odpg_ctx_sync(odpg_ctx_t *ctx);
 
 /* Rule table: compiled, immutable snapshot of the CoS/PMR graph. The

@@ -219,6 +219,7 @@ SIGNATURES = {
     "odpg_ctx_destroy": (None, [_vp]),
     "odpg_ctx_stream": (_vp, [_vp]),
     "odpg_ctx_set_kernel_mode": (_i32, [_vp, _i32]),
+    "odpg_last_kernel": (_i32, []),
     "odpg_ctx_sync": (_i32, [_vp]),
     "odpg_table_create": (_i32, [_vp, C.POINTER(odpg_rules_t), C.POINTER(_vp)]),
     "odpg_table_destroy": (None, [_vp]),

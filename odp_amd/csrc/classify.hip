@@ -31,12 +31,10 @@
 #include "odpg_internal.h"
 
 #include "pkt_parse.h"
+#include "cls_match.h"
 
 /* ----------------------------------------------------------------------- */
 /* compiled term evaluation (odp_classification.c:1338-1490 via cls_compile) */
-struct Bases {
-	uint32_t l2, l3, l4, vlanx, len, inf_lo;
-};
 
 /* byte fields of the term / slot descriptors read as one dword: the
  * wave-uniform reads then compile to scalar loads (a byte field would be a
@@ -211,61 +209,6 @@ __device__ __forceinline__ void extract_key_fast(uint32_t (&key)[KEY_SLOTS], con
 }
 
 
-/* ---- key slots on demand ------------------------------------------------
- * The word a compiled term compares (odpg_internal.h "key slots"), fetched
- * when a rule group needs it: from the frame registers on fast waves
- * (uniform switch), from the LDS window otherwise. No per-packet key array
- * is materialised (keeps register pressure and scratch at zero). */
-template <int W, bool GF>
-struct KeySrc {
-	const uint32_t *f;     /* 16 frame registers (fast waves) or nullptr */
-	const Pkt<W, GF> *v;
-	const Bases *b;
-	bool fast;
-
-	__device__ __forceinline__ uint32_t operator()(uint32_t slot) const
-	{
-		if (fast) {
-			const uint32_t (&r)[16] = *reinterpret_cast<const uint32_t (*)[16]>(f);
-			const bool l4ok = b->l4 != 0xffffu;
-
-			switch (slot) {
-			case 0: return r[0];
-			case 1: return r[1];
-			case 2: return r[2];
-			case 3: return r[3];
-			case 4: return r[4];
-			case 5: return fw<14>(r);
-			case 6: return fw<14>(r);
-			case 7: return fw<18>(r);
-			case 8: return fw<22>(r);
-			case 9: return fw<26>(r);
-			case 10: return fw<30>(r);
-			case 11: return fw<34>(r);
-			case 12: return fw<38>(r);
-			case 13: return fw<42>(r);
-			case 14: return fw<46>(r);
-			case 15: return fw<50>(r);
-			case 16: return l4ok ? fw<34>(r) : 0u;
-			case 17: return l4ok ? fw<38>(r) : 0u;
-			default: return b->len;
-			}
-		}
-		uint32_t pos;
-
-		if (slot < SLOT_VLANX)
-			pos = b->l2 + 4u * slot;
-		else if (slot == SLOT_VLANX)
-			pos = b->vlanx;
-		else if (slot < SLOT_L4)
-			pos = b->l3 + 4u * (slot - SLOT_L3);
-		else if (slot < SLOT_LEN)
-			pos = b->l4 + 4u * (slot - SLOT_L4);
-		else
-			return b->len;
-		return v->rd32(pos);
-	}
-};
 
 /* ---- evaluate-all helpers ---------------------------------------------- */
 /* extract the key slots the table reads (odpg_internal.h "key slots") */
@@ -353,17 +296,6 @@ __device__ __forceinline__ bool pmr_eval(const dterm_t *__restrict__ terms,
 	return ok;
 }
 
-/* first set bit of the rule range [rs, rs + nr) in a per-lane hit map */
-__device__ __forceinline__ int first_hit64(uint64_t hits, uint32_t rs, uint32_t nr)
-{
-	if (nr == 0u || rs >= 64u)
-		return -1;
-	uint64_t x = hits >> rs;
-
-	if (nr < 64u)
-		x &= (1ull << nr) - 1ull;
-	return x ? (int)__builtin_ctzll(x) : -1;
-}
 
 __device__ __forceinline__ int first_hit_lds(const uint32_t *hrow, uint32_t rs, uint32_t nr)
 {
@@ -391,7 +323,10 @@ __device__ __forceinline__ int first_hit_lds(const uint32_t *hrow, uint32_t rs, 
  * metadata or counters): the unused paths compile out, which frees the
  * scalar registers the general kernel spills. Results are identical. */
 template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST, bool LEAN>
-__global__ __launch_bounds__(BLOCK, FAST ? 5 : 6) void odpg_classify_kernel(
+#ifndef LEAN_WAVES
+#define LEAN_WAVES 5
+#endif
+__global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_classify_kernel(
 	const uint8_t *__restrict__ frames, const odpg_desc_t *__restrict__ desc,
 	uint32_t stride, uint32_t num, uint64_t opt, uint32_t layer, uint32_t classify,
 	const dterm_t *__restrict__ terms, const dpmr_t *__restrict__ pmrs,
@@ -1223,10 +1158,40 @@ static hipError_t launch_layout(const odpg_launch_args &a, uint32_t &grid, hipSt
 	return launch_one<96, false, true, false, MODE>(a, grid, s);
 }
 
+extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s);
+
+/* the lean 64-byte kernel (classify64.hip) covers this launch: fixed 64-byte
+ * stride, a <= 64-PMR simple table whose gates its register parse computes,
+ * verdict words only, full parse with classification and no drop options */
+static bool lean64_ok(const odpg_launch_args &a)
+{
+	static const bool off = getenv("ODPG_NO_LEAN64") != nullptr;
+	const uint64_t drops = ODPG_PKTIN_DROP_IPV4_ERR | ODPG_PKTIN_DROP_IPV6_ERR |
+			       ODPG_PKTIN_DROP_UDP_ERR | ODPG_PKTIN_DROP_TCP_ERR |
+			       ODPG_PKTIN_DROP_SCTP_ERR;
+
+	return !off && a.mode == 0 && !a.desc && a.stride == 64 && (a.tbl_flags & TBL_LEAN64) &&
+	       !(a.tbl_flags & (TBL_GENERIC | TBL_ANY_HASHQ)) && a.num_pmr <= MGROUP_MAX_PMR &&
+	       !a.mark && !a.meta && !a.stats && a.layer >= LAYER_L4 && a.classify &&
+	       !(a.opt & drops) && !(a.opt >> 32);
+}
+
+static int g_last_kernel = -1;
+
+extern "C" int odpg_last_kernel(void)
+{
+	return __atomic_load_n(&g_last_kernel, __ATOMIC_RELAXED);
+}
+
 extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 {
 	if (a->num == 0)
 		return 0;
+	const bool lean = lean64_ok(*a);
+
+	__atomic_store_n(&g_last_kernel, lean ? 1 : 0, __ATOMIC_RELAXED);
+	if (lean)
+		return odpg_launch_cls64(a, s);
 	uint32_t grid = odpg_launch_grid(a->num);
 	int mode = a->mode;
 	hipError_t e;

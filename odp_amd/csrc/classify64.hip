@@ -1,0 +1,415 @@
+/* SPDX-License-Identifier: BSD-3-Clause
+ *
+ * Lean gfx950 classify kernel for the production receive shape: fixed
+ * 64-byte frame stride, a TBL_SIMPLE rule table of <= 64 PMRs (mask groups,
+ * odpg_internal.h), verdict words only (no marks, metadata or counters).
+ * Same per-packet semantics as odpg_classify_kernel (classify.hip), which
+ * handles every other layout / table / output; results are bit-identical
+ * (tests/test_gpu_parity.py runs both on the same inputs).
+ *
+ * Per packet: parse + RX checksum verdicts (_odp_packet_parse_common,
+ * odp_parse_internal.h:80-112, odp_packet.c:1906-1984), error-CoS selection
+ * and the match_pmr_cos first-match walk (odp_classification.c:1599-1701)
+ * over the table's PMR hit bits.
+ *
+ * Layout: one lane per packet, one wave per 64-packet tile, waves persistent
+ * over tiles (no workgroup barrier in the loop). A lane's 64 bytes arrive as
+ * 4 x 16 B loads straight into registers, issued one tile ahead. A wave
+ * whose frames are all plain Eth/IPv4/UDP|TCP takes the register parse
+ * (checksums as v_dot2_u32_u16 sums of 16-bit halves); any other wave copies
+ * its frames to LDS rows and runs the generic parse. The mask-group entries
+ * and the resolve table live in LDS.
+ */
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdint.h>
+
+#include "../../include/odpg.h"
+#include "odpg_internal.h"
+#include "pkt_parse.h"
+#include "cls_match.h"
+
+#ifndef L64_WAVES
+#define L64_WAVES 6
+#endif
+
+struct L64Args {
+	const uint4 *frames;
+	uint32_t num;
+	uint32_t opt;          /* ODPG_PKTIN_* (all defined bits are < 32) */
+	uint32_t layer;        /* >= LAYER_L4 */
+	uint32_t num_mgroups;
+	const dmgroup_t *mgroups;
+	const uint4 *ments;
+	const uint2 *pinfo2;
+	uint32_t num_ment, num_pmr, num_cos;
+	uint32_t err_cos;      /* error CoS, or ODPG_COS_NONE */
+	uint32_t err_act;      /* its action */
+	uint32_t def_cos;      /* CoS of error-free packets before the walk */
+	uint32_t def_act;
+	uint32_t def_ci;       /* default rule range rs | nr << 8 (nr 0: no walk) */
+	odpg_out_t *out;
+};
+
+/* ---- register parse of plain 64-byte frames ------------------------------ */
+typedef unsigned short l64_us2 __attribute__((ext_vector_type(2)));
+
+/* acc + w.lo * x.lo16 + w.hi * x.hi16 (one v_dot2_u32_u16) */
+__device__ __forceinline__ uint32_t d2(uint32_t x, uint32_t w, uint32_t acc)
+{
+	return __builtin_amdgcn_udot2(__builtin_bit_cast(l64_us2, x),
+				      __builtin_bit_cast(l64_us2, w), acc, false);
+}
+
+/* end-around fold of a sum of < 2^15 16-bit words (chksum_finalize,
+ * odp_chksum_internal.h:22-31): 0xffff iff the one's-complement sum is
+ * all-ones, as the reference's 64-bit word sum folds */
+__device__ __forceinline__ uint32_t d2fold(uint32_t s)
+{
+	s = d2(s, 0x00010001u, 0u);
+	return d2(s, 0x00010001u, 0u);
+}
+
+#define W11 0x00010001u   /* both halves */
+#define W10 0x00000001u   /* low half (first byte pair) */
+#define W01 0x00010000u   /* high half */
+
+/* Verdict of a plain frame (plain_v4() true): parse_fast() semantics.
+ * Returns the output word's checksum / error / parse-error bits and the
+ * low input flags the rule gates read. */
+struct FastV {
+	uint32_t wbits;   /* ODPG_OUT_* status bits */
+	uint32_t inf_lo;
+	bool err;
+};
+
+__device__ __forceinline__ FastV parse_fast64(const uint32_t (&f)[16], uint32_t opt)
+{
+	FastV r;
+	const bool udp = (f[5] >> 24) == 0x11u;
+	uint32_t inf = (uint32_t)(IF(IFL_L2) | IF(IFL_ETH) | IF(IFL_L3) | IF(IFL_IPV4) | IF(IFL_L4));
+
+	inf |= udp ? (uint32_t)IF(IFL_UDP) : (uint32_t)IF(IFL_TCP);
+	r.inf_lo = inf;
+	r.err = false;
+	uint32_t wb = 0u;
+
+	/* IPv4 header checksum over bytes 14..33 (parse_ipv4, odp_parse.c:134-141) */
+	if (opt & ODPG_PKTIN_IPV4_CHKSUM) {
+		uint32_t s = d2(f[3], W01, 0u);
+
+		s = d2(f[4], W11, s);
+		s = d2(f[5], W11, s);
+		s = d2(f[6], W11, s);
+		s = d2(f[7], W11, s);
+		s = d2(f[8], W10, s);
+		const bool bad = d2fold(s) != 0xffffu;
+
+		wb |= (bad ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 16;
+		if (bad) {
+			/* ip_err: no L4 parse, no L4 verdict */
+			r.wbits = wb | ODPG_OUT_ERROR | ODPG_OUT_PARSE_ERR;
+			r.err = true;
+			return r;
+		}
+	}
+	const bool frag = (f[5] & 0xff3fu) != 0u;          /* be16(frag) & 0x3fff */
+	/* L4 checksum over the pseudo header and bytes 34..63
+	 * (_odp_packet_l4_chksum, odp_packet.c:1906-1984; length frame_len - 34):
+	 * src + dst, proto << 8, the length field (UDP: its own raw bytes 38..39,
+	 * counted again; TCP: be16(30)), then the segment */
+	const uint32_t need = udp ? ODPG_PKTIN_UDP_CHKSUM : ODPG_PKTIN_TCP_CHKSUM;
+	const bool zero_csum = udp && (f[10] & 0xffffu) == 0u;
+	bool done = false, bad = false;
+
+	if ((opt & need) && !frag) {
+		if (zero_csum) {
+			done = true;                                 /* udp_chksum_zero, ok */
+		} else {
+			uint32_t s = udp ? 0x1100u : 0x1e00u + 0x0600u;
+
+			s = d2(f[6], W01, s);
+			s = d2(f[7], W11, s);
+			s = d2(f[8], W11, s);
+			s = d2(f[9], udp ? 0x00020001u : W11, s);
+#pragma unroll
+			for (int k = 10; k < 16; ++k)
+				s = d2(f[k], W11, s);
+			done = true;
+			bad = d2fold(s) != 0xffffu;
+		}
+	}
+	if (done)
+		wb |= (bad ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 18;
+	if (bad) {
+		wb |= ODPG_OUT_ERROR | ODPG_OUT_PARSE_ERR;
+		r.err = true;
+	}
+	r.wbits = wb;
+	return r;
+}
+
+/* ---- the kernel ------------------------------------------------------------ */
+__global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64Args A)
+{
+	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+	constexpr uint32_t RW = 17;                     /* odd dword row stride */
+	uint32_t *row = smem + threadIdx.x * RW;        /* generic-parse LDS row */
+	uint4 *ments = (uint4 *)(smem + BLOCK * RW);
+	uint2 *pinfo2 = (uint2 *)(ments + A.num_ment);
+
+	const uint32_t lane = __lane_id();
+	const uint32_t gw = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+	const uint32_t nwaves = gridDim.x * (BLOCK / 64);
+	const uint32_t ntiles = (A.num + 63u) >> 6;
+	const uint32_t num = A.num;
+	uint32_t fn[16];
+
+	/* first tile's frames issued before the table copy (index clamped into
+	 * the batch: the loads always issue, so the wait counts stay exact) */
+	{
+		const uint32_t i0 = min(gw * 64u + lane, num - 1u);
+		const uint4 *src = A.frames + (size_t)i0 * 4u;
+
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			const uint4 x = ld_stream(src + k);
+
+			fn[4 * k + 0] = x.x;
+			fn[4 * k + 1] = x.y;
+			fn[4 * k + 2] = x.z;
+			fn[4 * k + 3] = x.w;
+		}
+	}
+	for (uint32_t k = threadIdx.x; k < A.num_ment; k += BLOCK)
+		ments[k] = A.ments[k];
+	for (uint32_t k = threadIdx.x; k < A.num_pmr; k += BLOCK)
+		pinfo2[k] = A.pinfo2[k];
+	__syncthreads();
+
+	bool pend = false;
+	uint32_t pend_i = 0u, pend_w = 0u;
+
+	for (uint32_t t = gw; t < ntiles; t += nwaves) {
+		const uint32_t i = t * 64u + lane;
+		const bool live = i < num;
+
+		/* previous tile's verdict, stored before this tile's prefetch
+		 * (vector-memory counters retire in issue order) */
+		if (pend)
+			A.out[pend_i] = pend_w;
+		uint32_t f[16];
+
+#pragma unroll
+		for (int k = 0; k < 16; ++k)
+			f[k] = fn[k];
+		{
+			const uint32_t nt = t + nwaves;
+			const uint32_t inx = min(nt < ntiles ? nt * 64u + lane : i, num - 1u);
+			const uint4 *src = A.frames + (size_t)inx * 4u;
+
+#pragma unroll
+			for (int k = 0; k < 4; ++k) {
+				const uint4 x = ld_stream(src + k);
+
+				fn[4 * k + 0] = x.x;
+				fn[4 * k + 1] = x.y;
+				fn[4 * k + 2] = x.z;
+				fn[4 * k + 3] = x.w;
+			}
+		}
+		const bool fast = __ballot(live && !plain_v4(f)) == 0ull;
+
+		/* ---- parse ---------------------------------------------------- */
+		uint32_t wbits = 0u, inf_lo = 0u;
+		bool err = false, pdrop = false;
+		Bases b;
+		Pkt<64, false> v;
+
+		v.row = row;
+		v.g = (const uint8_t *)(A.frames + (size_t)i * 4u);
+		v.len = 64u;
+		b.l2 = 0u;
+		b.l3 = 14u;
+		b.l4 = 34u;
+		b.vlanx = 14u;
+		b.len = 64u;
+		if (fast) {
+			const FastV r = parse_fast64(f, A.opt);
+
+			wbits = r.wbits;
+			inf_lo = r.inf_lo;
+			err = r.err;
+		} else {
+#pragma unroll
+			for (int k = 0; k < 16; ++k)
+				row[k] = f[k];
+			Prs p;
+
+			p.inf = 0ull;
+			p.fl = 0u;
+			p.l2 = p.l3 = p.l4 = 0xffffu;
+			const int ret = live ? parse_common(p, v, A.layer, (uint64_t)A.opt) : 0;
+
+			if (p.inf & IF(IFL_L3_CHKSUM_DONE))
+				wbits |= (p.fl & FB(FL_L3_CHKSUM_ERR) ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 16;
+			if (p.inf & IF(IFL_L4_CHKSUM_DONE))
+				wbits |= (p.fl & FB(FL_L4_CHKSUM_ERR) ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 18;
+			err = (p.fl & FL_ERROR_MASK) != 0u;
+			if (err)
+				wbits |= ODPG_OUT_ERROR;
+			if (ret)
+				wbits |= ODPG_OUT_PARSE_ERR;
+			pdrop = ret < 0;
+			inf_lo = (uint32_t)p.inf;
+			b.l2 = p.l2;
+			b.l3 = p.l3;
+			b.l4 = p.l4;
+			b.vlanx = 14u + ((p.inf & IF(IFL_VLAN_QINQ)) ? 4u : 0u);
+		}
+		b.inf_lo = inf_lo;
+
+		/* ---- CoS: cls_select_cos (odp_classification.c:1669-1701) ------ */
+		uint32_t cos = err ? A.err_cos : A.def_cos;
+		uint32_t act = err ? A.err_act : A.def_act;
+		uint32_t ci = err ? 0u : A.def_ci;
+		uint32_t mark = 0u;
+		bool any_match = false;
+
+		if (__ballot(live && !pdrop && (ci >> 8) != 0u)) {
+			/* PMR hit bits from the mask groups: both cuckoo candidates
+			 * of each group, the matching entry ORs its bits */
+			KeySrc<64, false> key;
+
+			key.f = f;
+			key.v = &v;
+			key.b = &b;
+			key.fast = fast;
+			uint32_t lo = 0u, hi = 0u;
+
+			for (uint32_t gi = 0; gi < A.num_mgroups; ++gi) {
+				const uint4 g0 = *(const uint4 *)(A.mgroups + gi);
+				const uint4 g1 = *((const uint4 *)(A.mgroups + gi) + 1);
+				const uint32_t gslot = __builtin_amdgcn_readfirstlane(g0.x);
+				const uint32_t greq = __builtin_amdgcn_readfirstlane(g0.y);
+				const uint32_t gmask = __builtin_amdgcn_readfirstlane(g0.z);
+				const uint32_t gsh = __builtin_amdgcn_readfirstlane(g0.w);
+				const uint32_t goff = __builtin_amdgcn_readfirstlane(g1.x);
+				const uint32_t gm1 = __builtin_amdgcn_readfirstlane(g1.y);
+				const uint32_t gm2 = __builtin_amdgcn_readfirstlane(g1.z);
+				const uint32_t gcnt = __builtin_amdgcn_readfirstlane(g1.w);
+				const uint32_t kvm = key(gslot) & gmask;
+				const bool rq = (inf_lo & greq) == greq;
+
+				if (gcnt == 1u) {
+					const bool h = rq & (kvm == gm1);
+
+					lo |= h ? gm2 : 0u;
+					hi |= h ? goff : 0u;
+				} else {
+					const uint4 e1 = ments[goff + ((kvm * gm1) >> gsh)];
+					const uint4 e2 = ments[goff + ((kvm * gm2) >> gsh)];
+					const bool h1 = rq & (e1.x == kvm), h2 = rq & (e2.x == kvm);
+
+					lo |= (h1 ? e1.y : 0u) | (h2 ? e2.y : 0u);
+					hi |= (h1 ? e1.z : 0u) | (h2 ? e2.z : 0u);
+				}
+			}
+			const uint64_t hits = ((uint64_t)hi << 32) | lo;
+
+			/* match_pmr_cos: first hit in the current CoS's rule range,
+			 * one LDS read per level (pinfo2 carries the next range) */
+			if (live && !pdrop) {
+				uint32_t steps = 0u;
+
+				for (;;) {
+					const int k = first_hit64(hits, ci & 0xffu, (ci >> 8) & 0xffu);
+
+					if (k < 0)
+						break;
+					const uint2 pi = pinfo2[(ci & 0xffu) + (uint32_t)k];
+
+					cos = pi.x & 0xffffu;
+					mark = pi.x >> 16;
+					ci = pi.y;
+					act = (pi.y >> 16) & 0xffu;
+					any_match = true;
+					if (++steps >= A.num_cos) {
+						cos = ODPG_COS_LOOP;
+						break;
+					}
+				}
+			}
+		}
+
+		/* ---- verdict word (odpg.h) ------------------------------------ */
+		uint32_t w;
+
+		if (pdrop) {
+			w = ODPG_COS_PDROP | wbits;
+		} else {
+			w = (cos & 0xffffu) | wbits;
+			if (cos < ODPG_COS_NOCLS && act == 1u)
+				w |= ODPG_OUT_CLS_DROP;
+			if (any_match && !err && cos != ODPG_COS_LOOP && mark)
+				w |= ODPG_OUT_MARK_VALID;
+		}
+		pend = live;
+		pend_i = i;
+		pend_w = w;
+	}
+	if (pend)
+		A.out[pend_i] = pend_w;
+}
+
+/* ---- launch ----------------------------------------------------------------- */
+extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
+{
+	if (a->num == 0)
+		return 0;
+	L64Args A;
+	const dcos_t *hcos = nullptr;   /* host copies are not needed: see below */
+
+	(void)hcos;
+	A.frames = (const uint4 *)a->frames;
+	A.num = a->num;
+	A.opt = (uint32_t)a->opt;
+	A.layer = a->layer;
+	A.num_mgroups = a->num_mgroups;
+	A.mgroups = a->mgroups;
+	A.ments = (const uint4 *)a->ments;
+	A.pinfo2 = (const uint2 *)a->pinfo2;
+	A.num_ment = a->num_ment;
+	A.num_pmr = a->num_pmr;
+	A.num_cos = a->num_cos;
+	A.err_cos = a->l64_err_cos;
+	A.err_act = a->l64_err_act;
+	A.def_cos = a->l64_def_cos;
+	A.def_act = a->l64_def_act;
+	A.def_ci = a->l64_def_ci;
+	A.out = a->out;
+
+	const size_t lds = (size_t)BLOCK * 17u * 4u + (size_t)a->num_ment * 16u +
+			   (size_t)a->num_pmr * 8u;
+	static size_t occ_lds = (size_t)-1;
+	static uint32_t occ_grid = 0;
+
+	if (occ_lds != lds) {
+		int nb = 0, dev = 0, cus = 0;
+
+		hipGetDevice(&dev);
+		hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, odpg_cls64_kernel, BLOCK, lds) !=
+		    hipSuccess || nb <= 0)
+			nb = 1;
+		occ_grid = (uint32_t)(nb * (cus > 0 ? cus : 256));
+		occ_lds = lds;
+	}
+	const uint32_t ntiles = (a->num + 63u) / 64u;
+	uint32_t grid = (ntiles + 3u) / 4u;
+
+	if (grid > occ_grid)
+		grid = occ_grid;
+	hipLaunchKernelGGL(odpg_cls64_kernel, dim3(grid), dim3(BLOCK), lds, s, A);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}

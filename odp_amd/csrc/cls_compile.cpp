@@ -658,7 +658,16 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.num_wgroups = is_simple ? (uint32_t)wgroups.size() : 0;
 	h.num_went = is_simple ? (uint32_t)wents.size() : 0;
 	if (is_simple && pmr.size() <= MGROUP_MAX_PMR) {
-		h.flags |= TBL_MGROUPS;
+		const uint32_t lean_req = (1u << IFL_L2) | (1u << IFL_L3) | (1u << IFL_L4) |
+					  (1u << IFL_ETH) | (1u << IFL_VLAN) | (1u << IFL_IPV4) |
+					  (1u << IFL_IPV6) | (1u << IFL_UDP) | (1u << IFL_TCP) |
+					  (1u << IFL_IPSEC_AH) | (1u << IFL_IPSEC_ESP);
+		bool lean = true;
+
+		for (const dmgroup_t &g : mgroups)
+			if (g.req & ~lean_req)
+				lean = false;
+		h.flags |= TBL_MGROUPS | (lean ? TBL_LEAN64 : 0u);
 		h.num_mgroups = (uint32_t)mgroups.size();
 		h.num_ment = (uint32_t)ments.size();
 	}

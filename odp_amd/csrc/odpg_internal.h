@@ -91,6 +91,10 @@ typedef struct dcos_s {
 			      * >= 3 entries per distinct value): per-level
 			      * CoS-keyed probes beat evaluating every entry */
 #define TBL_MGROUPS    0x40  /* mask groups + pinfo2 built (simple, <= 64 PMRs) */
+#define TBL_LEAN64     0x80  /* TBL_MGROUPS and every group gates only on flags
+			      * the lean kernel's register parse computes
+			      * (L2, L3, L4, ETH, VLAN, IPV4, IPV6, UDP, TCP,
+			      * IPSEC_AH, IPSEC_ESP) */
 
 /* ---- per-packet key slots (evaluate-all kernels) -------------------------
  * The parser-relative 32-bit words the terms can compare, extracted once per
@@ -285,6 +289,9 @@ typedef struct odpg_launch_args {
 	const dment_t *ments;
 	uint32_t num_ment;
 	const uint2_t *pinfo2;
+	/* lean 64-byte kernel (classify64.hip): CoS start state, from the host
+	 * copy of the table */
+	uint32_t l64_err_cos, l64_err_act, l64_def_cos, l64_def_act, l64_def_ci;
 	int mode;          /* 0 auto, 1 walk, 2 evaluate-all, 3 hash walk */
 	odpg_out_t *out;
 	uint16_t *mark;

@@ -27,6 +27,12 @@ def both(ctx, rules, buf, num, stride=0, desc=None, opt=0, layer=L.LAYER_ALL, cl
     ctx.set_kernel_mode(0)
     assert_same(res[1], res[2], "walk vs evaluate-all")
     assert_same(res[1], res[3], "walk vs hash walk")
+    if stride == 64 and desc is None:
+        # verdict words only: auto mode may take the lean 64-byte kernel
+        lean = ctx.classify(tbl, buf, num, stride=stride, opt=opt, layer=layer,
+                            classify=classify, want_mark=False, want_meta=False,
+                            want_stats=False)
+        assert_same(res[1], lean, f"walk vs verdict-only (kernel {L.lib.odpg_last_kernel()})")
     o = oracle.classify(rules, buf, num, stride=stride, desc=desc, opt=opt, layer=layer,
                         classify=classify)
     return res[0], o
@@ -324,3 +330,41 @@ def test_c3_host_path(gpu_ctx, fresh_cls):
     np.testing.assert_array_equal(h["out"], o["out"])
     np.testing.assert_array_equal(h["mark"], o["mark"])
     np.testing.assert_array_equal(h["stats"], o["stats"])
+
+
+@pytest.mark.parametrize("opt", OPTS)
+@pytest.mark.parametrize("variant", ["mixed", "drop_err", "no_default"])
+def test_lean64_kernel(gpu_ctx, fresh_cls, opt, variant):
+    """The lean 64-byte kernel (auto mode, verdict words only): fast and
+    generic waves of the plain64 corpus, marks, DROP-action CoS, error CoS,
+    no default CoS; verdict words bit-exact vs the oracle, and the launch
+    really took the lean kernel."""
+    p = fresh_cls.loop_pktio(pktin=opt)
+    if variant == "mixed":
+        rulesets.simple_mixed_rules(fresh_cls, p, stats=False)
+    elif variant == "drop_err":
+        c, T = fresh_cls, fresh_cls.Term
+        d = c.cos_create("d", queue=c.queue(0))
+        q1 = c.cos_create("q1", queue=c.queue(1))
+        q2 = c.cos_create("q2", queue=c.queue(2))
+        drop = c.cos_create("drop", action=c.COS_ACTION_DROP)
+        err = c.cos_create("err", queue=c.queue(70))
+        assert c.default_cos_set(p, d) == 0 and c.error_cos_set(p, err) == 0
+        assert c.pmr_create([T(c.PMR_SIP_ADDR, gen.be_bytes(gen.ip4("192.168.0.0"), 4),
+                               gen.be_bytes(0xFFFF8000, 4))], d, q1, mark=3)
+        assert c.pmr_create([T(c.PMR_UDP_SPORT, gen.be_bytes(5, 2), b"\x00\xff")],
+                            q1, drop, mark=9)
+        assert c.pmr_create([T(c.PMR_TCP_DPORT, gen.be_bytes(7, 2), b"\xff\xff")], q1, q2)
+    else:
+        q = fresh_cls.cos_create("q", queue=fresh_cls.queue(3))
+        assert q
+    assert fresh_cls.pktio_start(p) == 0
+    rules = fresh_cls.pktio_rules(p)
+    n = 64 * 257 + 5
+    fr = rulesets.plain64_corpus(n, seed=31)
+    tbl = gpu_ctx.table(rules)
+    g = gpu_ctx.classify(tbl, fr, n, stride=64, opt=opt, want_mark=False, want_meta=False,
+                         want_stats=False)
+    assert L.lib.odpg_last_kernel() == 1
+    o = oracle.classify(rules, fr, n, stride=64, opt=opt)
+    assert_same({"out": g["out"]}, {"out": o["out"]}, f"lean64 {variant} opt={opt}")
