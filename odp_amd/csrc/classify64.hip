@@ -149,7 +149,45 @@ __device__ __forceinline__ FastV parse_fast64(const uint32_t (&f)[16], uint32_t 
 	return r;
 }
 
-/* ---- the kernel ------------------------------------------------------------ */
+/* one mask group's descriptor, wave-uniform (SGPRs) */
+struct MGd {
+	uint32_t slot, req, mask, sh, off, m1, m2, cnt;
+	uint32_t fw, fs;   /* key word of a plain frame: bytes [4 fw + fs, +4) */
+};
+
+typedef uint32_t u32x16_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ MGd load_mg(const dmgroup_t *g)
+{
+	const uint4 g0 = *(const uint4 *)g;
+	const uint4 g1 = *((const uint4 *)g + 1);
+	MGd d;
+
+	d.slot = __builtin_amdgcn_readfirstlane(g0.x);
+	d.req = __builtin_amdgcn_readfirstlane(g0.y);
+	d.mask = __builtin_amdgcn_readfirstlane(g0.z);
+	d.sh = __builtin_amdgcn_readfirstlane(g0.w);
+	d.off = __builtin_amdgcn_readfirstlane(g1.x);
+	d.m1 = __builtin_amdgcn_readfirstlane(g1.y);
+	d.m2 = __builtin_amdgcn_readfirstlane(g1.z);
+	d.cnt = __builtin_amdgcn_readfirstlane(g1.w);
+	/* frame offset of the slot word in a plain Eth/IPv4 frame (l3 14, l4 34;
+	 * the VLANX slot reads l3's word, its VLAN gate fails there) */
+	const uint32_t o = d.slot < SLOT_VLANX ? 4u * d.slot :
+			   d.slot < SLOT_L3 ? 14u :
+			   d.slot < SLOT_L4 ? 14u + 4u * (d.slot - SLOT_L3) :
+			   d.slot < SLOT_LEN ? 34u + 4u * (d.slot - SLOT_L4) : 0u;
+
+	d.fw = o >> 2;
+	d.fs = o & 3u;
+	return d;
+}
+
+/* ---- the kernel ------------------------------------------------------------
+ * NG > 0: the table has exactly NG mask groups; their descriptors are read
+ * once into scalar registers before the tile loop. NG = 0: any count, read
+ * per tile. */
+template <int NG>
 __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64Args A)
 {
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -185,6 +223,13 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		ments[k] = A.ments[k];
 	for (uint32_t k = threadIdx.x; k < A.num_pmr; k += BLOCK)
 		pinfo2[k] = A.pinfo2[k];
+	MGd mg[NG > 0 ? NG : 1];
+
+	if constexpr (NG > 0) {
+#pragma unroll
+		for (int g = 0; g < NG; ++g)
+			mg[g] = load_mg(A.mgroups + g);
+	}
 	__syncthreads();
 
 	bool pend = false;
@@ -220,27 +265,74 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		}
 		const bool fast = __ballot(live && !plain_v4(f)) == 0ull;
 
-		/* ---- parse ---------------------------------------------------- */
+		/* ---- parse + PMR hit bits -------------------------------------
+		 * hit bits: both cuckoo candidates of each mask group are read and
+		 * the entry whose value equals the packet's masked key word ORs
+		 * its PMR bits (odpg_internal.h "Mask groups") */
 		uint32_t wbits = 0u, inf_lo = 0u;
 		bool err = false, pdrop = false;
-		Bases b;
-		Pkt<64, false> v;
+		uint32_t lo = 0u, hi = 0u;
+		const bool walk = (A.def_ci >> 8) != 0u;
+		auto probe = [&](const MGd &d, uint32_t key) {
+			const uint32_t kvm = key & d.mask;
+			const bool rq = (inf_lo & d.req) == d.req;
 
-		v.row = row;
-		v.g = (const uint8_t *)(A.frames + (size_t)i * 4u);
-		v.len = 64u;
-		b.l2 = 0u;
-		b.l3 = 14u;
-		b.l4 = 34u;
-		b.vlanx = 14u;
-		b.len = 64u;
+			if (d.cnt == 1u) {
+				const bool h = rq & (kvm == d.m1);
+
+				lo |= h ? d.m2 : 0u;
+				hi |= h ? d.off : 0u;
+			} else {
+				const uint4 e1 = ments[d.off + ((kvm * d.m1) >> d.sh)];
+				const uint4 e2 = ments[d.off + ((kvm * d.m2) >> d.sh)];
+				const bool h1 = rq & (e1.x == kvm), h2 = rq & (e2.x == kvm);
+
+				lo |= (h1 ? e1.y : 0u) | (h2 ? e2.y : 0u);
+				hi |= (h1 ? e1.z : 0u) | (h2 ? e2.z : 0u);
+			}
+		};
+#ifdef L64_EXP_NOPARSE   /* experiment builds only: skeleton floor */
+		if (fast) {
+			wbits = f[3] ^ f[9];
+		} else
+#endif
 		if (fast) {
 			const FastV r = parse_fast64(f, A.opt);
 
 			wbits = r.wbits;
 			inf_lo = r.inf_lo;
 			err = r.err;
+#ifndef L64_EXP_NOMATCH
+			if (walk) {
+				/* key word at a fixed frame offset: a uniform register
+				 * index into the frame (no per-slot branches) */
+				const u32x16_t fv = {f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7],
+						     f[8], f[9], f[10], f[11], f[12], f[13], f[14], f[15]};
+				auto fast_key = [&](const MGd &d) -> uint32_t {
+					if (d.slot == SLOT_LEN)
+						return 64u;
+					return __builtin_amdgcn_alignbyte(fv[d.fw + 1u], fv[d.fw], d.fs);
+				};
+				if constexpr (NG > 0) {
+#pragma unroll
+					for (int g = 0; g < NG; ++g)
+						probe(mg[g], fast_key(mg[g]));
+				} else {
+					for (uint32_t gi = 0; gi < A.num_mgroups; ++gi) {
+						const MGd d = load_mg(A.mgroups + gi);
+
+						probe(d, fast_key(d));
+					}
+				}
+			}
+#endif
 		} else {
+			Bases b;
+			Pkt<64, false> v;
+
+			v.row = row;
+			v.g = (const uint8_t *)(A.frames + (size_t)i * 4u);
+			v.len = 64u;
 #pragma unroll
 			for (int k = 0; k < 16; ++k)
 				row[k] = f[k];
@@ -266,8 +358,30 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 			b.l3 = p.l3;
 			b.l4 = p.l4;
 			b.vlanx = 14u + ((p.inf & IF(IFL_VLAN_QINQ)) ? 4u : 0u);
+			b.len = 64u;
+			b.inf_lo = inf_lo;
+#ifndef L64_EXP_NOMATCH
+			if (walk) {
+				KeySrc<64, false> key;
+
+				key.f = f;
+				key.v = &v;
+				key.b = &b;
+				key.fast = false;
+				if constexpr (NG > 0) {
+#pragma unroll
+					for (int g = 0; g < NG; ++g)
+						probe(mg[g], key(mg[g].slot));
+				} else {
+					for (uint32_t gi = 0; gi < A.num_mgroups; ++gi) {
+						const MGd d = load_mg(A.mgroups + gi);
+
+						probe(d, key(d.slot));
+					}
+				}
+			}
+#endif
 		}
-		b.inf_lo = inf_lo;
 
 		/* ---- CoS: cls_select_cos (odp_classification.c:1669-1701) ------ */
 		uint32_t cos = err ? A.err_cos : A.def_cos;
@@ -276,45 +390,7 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		uint32_t mark = 0u;
 		bool any_match = false;
 
-		if (__ballot(live && !pdrop && (ci >> 8) != 0u)) {
-			/* PMR hit bits from the mask groups: both cuckoo candidates
-			 * of each group, the matching entry ORs its bits */
-			KeySrc<64, false> key;
-
-			key.f = f;
-			key.v = &v;
-			key.b = &b;
-			key.fast = fast;
-			uint32_t lo = 0u, hi = 0u;
-
-			for (uint32_t gi = 0; gi < A.num_mgroups; ++gi) {
-				const uint4 g0 = *(const uint4 *)(A.mgroups + gi);
-				const uint4 g1 = *((const uint4 *)(A.mgroups + gi) + 1);
-				const uint32_t gslot = __builtin_amdgcn_readfirstlane(g0.x);
-				const uint32_t greq = __builtin_amdgcn_readfirstlane(g0.y);
-				const uint32_t gmask = __builtin_amdgcn_readfirstlane(g0.z);
-				const uint32_t gsh = __builtin_amdgcn_readfirstlane(g0.w);
-				const uint32_t goff = __builtin_amdgcn_readfirstlane(g1.x);
-				const uint32_t gm1 = __builtin_amdgcn_readfirstlane(g1.y);
-				const uint32_t gm2 = __builtin_amdgcn_readfirstlane(g1.z);
-				const uint32_t gcnt = __builtin_amdgcn_readfirstlane(g1.w);
-				const uint32_t kvm = key(gslot) & gmask;
-				const bool rq = (inf_lo & greq) == greq;
-
-				if (gcnt == 1u) {
-					const bool h = rq & (kvm == gm1);
-
-					lo |= h ? gm2 : 0u;
-					hi |= h ? goff : 0u;
-				} else {
-					const uint4 e1 = ments[goff + ((kvm * gm1) >> gsh)];
-					const uint4 e2 = ments[goff + ((kvm * gm2) >> gsh)];
-					const bool h1 = rq & (e1.x == kvm), h2 = rq & (e2.x == kvm);
-
-					lo |= (h1 ? e1.y : 0u) | (h2 ? e2.y : 0u);
-					hi |= (h1 ? e1.z : 0u) | (h2 ? e2.z : 0u);
-				}
-			}
+		{
 			const uint64_t hits = ((uint64_t)hi << 32) | lo;
 
 			/* match_pmr_cos: first hit in the current CoS's rule range,
@@ -399,7 +475,7 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 
 		hipGetDevice(&dev);
 		hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, odpg_cls64_kernel, BLOCK, lds) !=
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, odpg_cls64_kernel<0>, BLOCK, lds) !=
 		    hipSuccess || nb <= 0)
 			nb = 1;
 		occ_grid = (uint32_t)(nb * (cus > 0 ? cus : 256));
@@ -410,6 +486,12 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 
 	if (grid > occ_grid)
 		grid = occ_grid;
-	hipLaunchKernelGGL(odpg_cls64_kernel, dim3(grid), dim3(BLOCK), lds, s, A);
+	switch (a->num_mgroups) {
+	case 1: hipLaunchKernelGGL(odpg_cls64_kernel<1>, dim3(grid), dim3(BLOCK), lds, s, A); break;
+	case 2: hipLaunchKernelGGL(odpg_cls64_kernel<2>, dim3(grid), dim3(BLOCK), lds, s, A); break;
+	case 3: hipLaunchKernelGGL(odpg_cls64_kernel<3>, dim3(grid), dim3(BLOCK), lds, s, A); break;
+	case 4: hipLaunchKernelGGL(odpg_cls64_kernel<4>, dim3(grid), dim3(BLOCK), lds, s, A); break;
+	default: hipLaunchKernelGGL(odpg_cls64_kernel<0>, dim3(grid), dim3(BLOCK), lds, s, A); break;
+	}
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
