@@ -32,6 +32,7 @@
 
 #include "pkt_parse.h"
 #include "cls_match.h"
+#include "stats_commit.h"
 
 /* ----------------------------------------------------------------------- */
 /* compiled term evaluation (odp_classification.c:1338-1490 via cls_compile) */
@@ -341,7 +342,7 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 	const uint4 *__restrict__ ments_g, uint32_t num_ment, const uint2 *__restrict__ pinfo2_g,
 	odpg_out_t *__restrict__ out, uint16_t *__restrict__ mark_out,
 	odpg_meta_t *__restrict__ meta_out, uint64_t *__restrict__ pk_partial,
-	uint32_t *__restrict__ cos_partial)
+	uint32_t *__restrict__ cos_partial, uint64_t *__restrict__ sred)
 {
 	constexpr uint32_t RW = W / 4 + 1;       /* odd dword row stride */
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -1028,16 +1029,21 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 		uint64_t a = wave_sum_u64(lane_pkt), o = wave_sum_u64(lane_oct);
 		uint64_t e = wave_sum_u64(lane_err), d = wave_sum_u64(lane_disc);
 
-		if (__lane_id() == 0) {
+		if (sred) {
+			/* pktio counters only: committed in-kernel (stats_commit.h) */
+			const uint64_t v[4] = {a, o, e, d};
+
+			stats_commit_wave(v, sred);
+		} else if (__lane_id() == 0) {
 			atomicAdd(&blk_pk[0], (unsigned long long)a);
 			atomicAdd(&blk_pk[1], (unsigned long long)o);
 			atomicAdd(&blk_pk[2], (unsigned long long)e);
 			atomicAdd(&blk_pk[3], (unsigned long long)d);
 		}
 	}
-	if (do_stats || do_cos_stats)
+	if ((do_stats && !sred) || do_cos_stats)
 		__syncthreads();
-	if (do_stats && tid < 4)
+	if (do_stats && !sred && tid < 4)
 		pk_partial[(size_t)blockIdx.x * 4u + tid] = blk_pk[tid];
 	if (do_cos_stats)
 		for (uint32_t c = tid; c < num_cos; c += BLOCK)
@@ -1131,7 +1137,7 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 			   a.runs, a.num_runs, a.hgroups, a.num_hgroups, a.hents, a.num_hent,
 			   (const uint2 *)a.cinfo, a.pinfo, a.mgroups, a.num_mgroups,
 			   (const uint4 *)a.ments, a.num_ment, (const uint2 *)a.pinfo2, a.out, a.mark, a.meta, a.pk_partial,
-			   a.cos_partial);
+			   a.cos_partial, a.pk_atomic ? a.sred : nullptr);
 	return hipGetLastError();
 }
 
@@ -1162,7 +1168,8 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s);
 
 /* the lean 64-byte kernel (classify64.hip) covers this launch: fixed 64-byte
  * stride, a <= 64-PMR simple table whose gates its register parse computes,
- * verdict words only, full parse with classification and no drop options */
+ * verdict words and pktio counters only (no marks, metadata, CoS counters),
+ * full parse with classification and no drop options */
 static bool lean64_ok(const odpg_launch_args &a)
 {
 	static const bool off = getenv("ODPG_NO_LEAN64") != nullptr;
@@ -1172,7 +1179,8 @@ static bool lean64_ok(const odpg_launch_args &a)
 
 	return !off && a.mode == 0 && !a.desc && a.stride == 64 && (a.tbl_flags & TBL_LEAN64) &&
 	       !(a.tbl_flags & (TBL_GENERIC | TBL_ANY_HASHQ)) && a.num_pmr <= MGROUP_MAX_PMR &&
-	       !a.mark && !a.meta && !a.stats && a.layer >= LAYER_L4 && a.classify &&
+	       !a.mark && !a.meta && !(a.stats && (a.tbl_flags & TBL_ANY_STATS)) &&
+	       a.layer >= LAYER_L4 && a.classify &&
 	       !(a.opt & drops) && !(a.opt >> 32);
 }
 
@@ -1183,6 +1191,36 @@ extern "C" int odpg_last_kernel(void)
 	return __atomic_load_n(&g_last_kernel, __ATOMIC_RELAXED);
 }
 
+/* stats_commit.h: the slot sums of one classify launch into the caller's
+ * counters (stream-ordered after it, so plain read-modify-writes), slots
+ * re-zeroed for the next launch */
+__global__ __launch_bounds__(64) void odpg_stats_fold_kernel(uint64_t *__restrict__ sred,
+							      uint64_t *__restrict__ stats)
+{
+	const uint32_t g = threadIdx.x;
+	uint64_t x[4];
+
+#pragma unroll
+	for (int w = 0; w < 4; ++w) {
+		x[w] = sred[g * 8u + w];
+		sred[g * 8u + w] = 0ull;
+	}
+#pragma unroll
+	for (int w = 0; w < 4; ++w) {
+		const uint64_t t = wave_sum_u64(x[w]);
+
+		if (g == 0u && t)
+			stats[w] += t;
+	}
+}
+
+static int fold_stats(const odpg_launch_args *a, hipStream_t s)
+{
+	static_assert(SRED_GROUPS == 64u, "one fold lane per slot group");
+	hipLaunchKernelGGL(odpg_stats_fold_kernel, dim3(1), dim3(64), 0, s, a->sred, a->pk_partial);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
 extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 {
 	if (a->num == 0)
@@ -1190,8 +1228,11 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 	const bool lean = lean64_ok(*a);
 
 	__atomic_store_n(&g_last_kernel, lean ? 1 : 0, __ATOMIC_RELAXED);
-	if (lean)
-		return odpg_launch_cls64(a, s);
+	if (lean) {
+		int rc = odpg_launch_cls64(a, s);
+
+		return rc ? rc : a->pk_atomic ? fold_stats(a, s) : 0;
+	}
 	uint32_t grid = odpg_launch_grid(a->num);
 	int mode = a->mode;
 	hipError_t e;
@@ -1230,6 +1271,8 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 		e = launch_layout<2>(*a, grid, s);
 	if (e != hipSuccess)
 		return -EIO;
+	if (a->pk_atomic)
+		return fold_stats(a, s);
 	if (a->stats && (a->pk_partial || a->cos_partial)) {
 		uint32_t nwords = 4u + (a->cos_partial ? a->num_cos : 0u);
 		uint32_t rgrid = nwords < 1024u ? nwords : 1024u;

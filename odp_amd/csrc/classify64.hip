@@ -2,7 +2,8 @@
  *
  * Lean gfx950 classify kernel for the production receive shape: fixed
  * 64-byte frame stride, a TBL_SIMPLE rule table of <= 64 PMRs (mask groups,
- * odpg_internal.h), verdict words only (no marks, metadata or counters).
+ * odpg_internal.h), verdict words plus the loopback_recv pktio counters (no
+ * marks, metadata or per-CoS counters).
  * Same per-packet semantics as odpg_classify_kernel (classify.hip), which
  * handles every other layout / table / output; results are bit-identical
  * (tests/test_gpu_parity.py runs both on the same inputs).
@@ -28,6 +29,7 @@
 #include "odpg_internal.h"
 #include "pkt_parse.h"
 #include "cls_match.h"
+#include "stats_commit.h"
 
 #ifndef L64_WAVES
 #define L64_WAVES 6
@@ -49,6 +51,8 @@ struct L64Args {
 	uint32_t def_act;
 	uint32_t def_ci;       /* default rule range rs | nr << 8 (nr 0: no walk) */
 	odpg_out_t *out;
+	uint64_t *stats;       /* pktio counters (odpg.h), or NULL */
+	uint64_t *sred;        /* stats_commit scratch */
 };
 
 /* ---- register parse of plain 64-byte frames ------------------------------ */
@@ -234,6 +238,8 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 
 	bool pend = false;
 	uint32_t pend_i = 0u, pend_w = 0u;
+	/* loopback_recv accounting (loop.c:304-374), wave-uniform counts */
+	uint32_t n_pkt = 0u, n_err = 0u, n_disc = 0u;
 
 	for (uint32_t t = gw; t < ntiles; t += nwaves) {
 		const uint32_t i = t * 64u + lane;
@@ -433,9 +439,25 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		pend = live;
 		pend_i = i;
 		pend_w = w;
+		if (A.stats) {
+			/* in_packets: delivered error-free (cls ret 0); in_errors:
+			 * parse ret != 0; in_discards: cls ret -1 (no CoS; a CoS
+			 * loop counts the same) */
+			const bool nocos = cos == ODPG_COS_NONE || cos == ODPG_COS_LOOP;
+			const bool ok = live && !pdrop && !err && !nocos && act != 1u;
+
+			n_pkt += (uint32_t)__builtin_popcountll(__ballot(ok));
+			n_err += (uint32_t)__builtin_popcountll(__ballot(live && (wbits & ODPG_OUT_PARSE_ERR)));
+			n_disc += (uint32_t)__builtin_popcountll(__ballot(live && !pdrop && nocos));
+		}
 	}
 	if (pend)
 		A.out[pend_i] = pend_w;
+	if (A.stats) {
+		const uint64_t v[4] = {n_pkt, (uint64_t)n_pkt * 64u, n_err, n_disc};
+
+		stats_commit_wave(v, A.sred);
+	}
 }
 
 /* ---- launch ----------------------------------------------------------------- */
@@ -444,9 +466,7 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	if (a->num == 0)
 		return 0;
 	L64Args A;
-	const dcos_t *hcos = nullptr;   /* host copies are not needed: see below */
 
-	(void)hcos;
 	A.frames = (const uint4 *)a->frames;
 	A.num = a->num;
 	A.opt = (uint32_t)a->opt;
@@ -464,6 +484,8 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	A.def_act = a->l64_def_act;
 	A.def_ci = a->l64_def_ci;
 	A.out = a->out;
+	A.stats = a->stats;
+	A.sred = a->sred;
 
 	const size_t lds = (size_t)BLOCK * 17u * 4u + (size_t)a->num_ment * 16u +
 			   (size_t)a->num_pmr * 8u;

@@ -298,6 +298,8 @@ typedef struct odpg_launch_args {
 	odpg_meta_t *meta;
 	uint64_t *pk_partial;
 	uint32_t *cos_partial;
+	uint32_t pk_atomic;    /* pk_partial is the caller's counters (stats_commit.h) */
+	uint64_t *sred;        /* the context's stats_commit scratch (zeroed) */
 	uint64_t *stats;
 } odpg_launch_args;
 

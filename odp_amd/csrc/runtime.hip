@@ -14,6 +14,7 @@
 
 #include "../../include/odpg.h"
 #include "odpg_internal.h"
+#include "stats_commit.h"
 #include "cls_compile.h"
 
 
@@ -28,6 +29,7 @@ struct odpg_ctx_s {
 	bool own_stream;
 	hipStream_t copy_stream;
 	void *ws;          /* per-workgroup counter partials */
+	uint64_t *sred;    /* stats_commit scratch (SRED_BYTES, kept zeroed) */
 	size_t ws_bytes;
 	hipEvent_t ev[NUM_EVENTS];
 	int kernel_mode;   /* 0 auto, 1 walk, 2 evaluate-all, 3 hash walk */
@@ -110,6 +112,11 @@ int odpg_ctx_create(int device, void *stream, odpg_ctx_t **out)
 			delete c;
 			return -EIO;
 		}
+	if (hipMalloc(&c->sred, SRED_BYTES) != hipSuccess ||
+	    hipMemset(c->sred, 0, SRED_BYTES) != hipSuccess) {
+		delete c;
+		return -EIO;
+	}
 	*out = c;
 	return 0;
 }
@@ -123,6 +130,7 @@ void odpg_ctx_destroy(odpg_ctx_t *c)
 	hipStreamSynchronize(c->copy_stream);
 	if (c->ws)
 		hipFree(c->ws);
+	hipFree(c->sred);
 	for (int k = 0; k < NUM_EVENTS; k++)
 		hipEventDestroy(c->ev[k]);
 	hipStreamDestroy(c->copy_stream);
@@ -291,10 +299,14 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.mark = r->mark;
 	a.meta = r->meta;
 	a.stats = r->stats;
-	if (r->stats) {
+	if (r->stats && !cos_stats) {
+		/* pktio counters only: workgroups add straight into them */
+		a.pk_partial = r->stats;
+		a.pk_atomic = 1u;
+		a.sred = c->sred;
+	} else if (r->stats) {
 		a.pk_partial = (uint64_t *)ws;
-		if (cos_stats)
-			a.cos_partial = (uint32_t *)((uint8_t *)ws + (size_t)grid * 32u);
+		a.cos_partial = (uint32_t *)((uint8_t *)ws + (size_t)grid * 32u);
 	}
 	return odpg_launch_classify(&a, s);
 }
@@ -303,12 +315,11 @@ static size_t ws_need(const odpg_table_t *t, uint32_t num, bool stats)
 {
 	if (!stats)
 		return 0;
+	if (!(t->hdr.flags & TBL_ANY_STATS))
+		return 0;   /* pktio counters only: added in place */
 	uint32_t grid = odpg_launch_grid(num);
-	size_t need = (size_t)grid * 32u;
 
-	if (t->hdr.flags & TBL_ANY_STATS)
-		need += (size_t)grid * t->hdr.num_cos * 4u;
-	return need;
+	return (size_t)grid * 32u + (size_t)grid * t->hdr.num_cos * 4u;
 }
 
 int odpg_classify(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t *b,

@@ -33,6 +33,10 @@ def both(ctx, rules, buf, num, stride=0, desc=None, opt=0, layer=L.LAYER_ALL, cl
                             classify=classify, want_mark=False, want_meta=False,
                             want_stats=False)
         assert_same(res[1], lean, f"walk vs verdict-only (kernel {L.lib.odpg_last_kernel()})")
+        # verdict words + pktio counters (the lean kernel's counted launch)
+        lean = ctx.classify(tbl, buf, num, stride=stride, opt=opt, layer=layer,
+                            classify=classify, want_mark=False, want_meta=False)
+        assert_same(res[1], lean, f"walk vs verdict+stats (kernel {L.lib.odpg_last_kernel()})")
     o = oracle.classify(rules, buf, num, stride=stride, desc=desc, opt=opt, layer=layer,
                         classify=classify)
     return res[0], o
@@ -368,3 +372,8 @@ def test_lean64_kernel(gpu_ctx, fresh_cls, opt, variant):
     assert L.lib.odpg_last_kernel() == 1
     o = oracle.classify(rules, fr, n, stride=64, opt=opt)
     assert_same({"out": g["out"]}, {"out": o["out"]}, f"lean64 {variant} opt={opt}")
+    # with the pktio counters (in_packets / octets / errors / discards)
+    g = gpu_ctx.classify(tbl, fr, n, stride=64, opt=opt, want_mark=False, want_meta=False)
+    assert L.lib.odpg_last_kernel() == 1
+    assert_same({"out": g["out"], "stats": g["stats"]}, {"out": o["out"], "stats": o["stats"]},
+                f"lean64+stats {variant} opt={opt}")

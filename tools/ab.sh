@@ -10,7 +10,7 @@ STEPS="${STEPS:-50}"
 for v in $VARIANTS; do
   if [ "$v" = base ]; then lib=""; else lib="$PWD/odp_amd/lib/$v/libodpg.so"; fi
   ODPG_LIB="$lib" timeout -k 10 300 python bench.py --no-cpu --config $CFG --diag $DIAG \
-    --steps $STEPS --warmup 5 > gpurun_out/ab_${CFG}_${DIAG}_$v.json 2> gpurun_out/ab_${CFG}_${DIAG}_$v.err \
-    || { tail -3 gpurun_out/ab_${CFG}_${DIAG}_$v.err; exit 3; }
-  python -c "import json;d=json.load(open('gpurun_out/ab_${CFG}_${DIAG}_$v.json'));print('$CFG $DIAG $v', d['value'], d['roofline']['kernel_ms'])"
+    --steps $STEPS --warmup 5 ${BENCH_EXTRA:-} > gpurun_out/ab_${CFG}_${DIAG}${TAG:-}_$v.json 2> gpurun_out/ab_${CFG}_${DIAG}${TAG:-}_$v.err \
+    || { tail -3 gpurun_out/ab_${CFG}_${DIAG}${TAG:-}_$v.err; exit 3; }
+  python -c "import json;d=json.load(open('gpurun_out/ab_${CFG}_${DIAG}${TAG:-}_$v.json'));print('$CFG $DIAG $v', d['value'], d['roofline']['kernel_ms'])"
 done
