@@ -1177,8 +1177,12 @@ static bool lean64_ok(const odpg_launch_args &a)
 			       ODPG_PKTIN_DROP_UDP_ERR | ODPG_PKTIN_DROP_TCP_ERR |
 			       ODPG_PKTIN_DROP_SCTP_ERR;
 
-	return !off && a.mode == 0 && !a.desc && a.stride == 64 && (a.tbl_flags & TBL_LEAN64) &&
-	       !(a.tbl_flags & (TBL_GENERIC | TBL_ANY_HASHQ)) && a.num_pmr <= MGROUP_MAX_PMR &&
+	const bool mg = (a.tbl_flags & TBL_LEAN64) && a.num_pmr <= MGROUP_MAX_PMR;
+	const bool hw = (a.tbl_flags & TBL_LEAN64HW) && a.num_cgroups >= 1u && a.num_cgroups <= 4u &&
+			a.num_cos < ODPG_COS_NOCLS;
+
+	return !off && a.mode == 0 && !a.desc && a.stride == 64 && (mg || hw) &&
+	       !(a.tbl_flags & (TBL_GENERIC | TBL_ANY_HASHQ)) &&
 	       !a.mark && !a.meta && !(a.stats && (a.tbl_flags & TBL_ANY_STATS)) &&
 	       a.layer >= LAYER_L4 && a.classify &&
 	       !(a.opt & drops) && !(a.opt >> 32);

@@ -8,6 +8,13 @@
  * handles every other layout / table / output; results are bit-identical
  * (tests/test_gpu_parity.py runs both on the same inputs).
  *
+ * Two table forms: HW = false, mask groups (<= 64 PMRs, u64 hit map, one
+ * LDS read per walk level); HW = true, CoS-keyed cuckoo groups (TBL_LEAN64HW
+ * simple tables of any size, e.g. the 1024-PMR C4 table): per level of the
+ * walk both candidates of each group holding rules of the current CoS are
+ * read at once with key (masked key word, CoS), and the lowest PMR index
+ * found is the first match (odpg_internal.h "CoS-keyed cuckoo groups").
+ *
  * Per packet: parse + RX checksum verdicts (_odp_packet_parse_common,
  * odp_parse_internal.h:80-112, odp_packet.c:1906-1984), error-CoS selection
  * and the match_pmr_cos first-match walk (odp_classification.c:1599-1701)
@@ -45,11 +52,18 @@ struct L64Args {
 	const uint4 *ments;
 	const uint2 *pinfo2;
 	uint32_t num_ment, num_pmr, num_cos;
+	/* HW kernels: cuckoo groups, their entries, pinfo3 */
+	const dmgroup_t *cgroups;
+	const uint2 *cents;
+	uint32_t num_cent;
+	const uint2 *pinfo3;
+	uint32_t def_cgmask;
 	uint32_t err_cos;      /* error CoS, or ODPG_COS_NONE */
 	uint32_t err_act;      /* its action */
 	uint32_t def_cos;      /* CoS of error-free packets before the walk */
 	uint32_t def_act;
-	uint32_t def_ci;       /* default rule range rs | nr << 8 (nr 0: no walk) */
+	uint32_t def_ci;       /* default rule range rs | nr << 8 (mask groups) */
+	uint32_t def_rules;    /* the default CoS is valid and has rules: walk */
 	odpg_out_t *out;
 	uint64_t *stats;       /* pktio counters (odpg.h), or NULL */
 	uint64_t *sred;        /* stats_commit scratch */
@@ -188,17 +202,21 @@ __device__ __forceinline__ MGd load_mg(const dmgroup_t *g)
 }
 
 /* ---- the kernel ------------------------------------------------------------
- * NG > 0: the table has exactly NG mask groups; their descriptors are read
- * once into scalar registers before the tile loop. NG = 0: any count, read
- * per tile. */
-template <int NG>
+ * NG > 0: the table has exactly NG mask groups (HW: walk groups); their
+ * descriptors are read once into scalar registers before the tile loop.
+ * NG = 0 (mask groups only): any count, read per tile. */
+template <int NG, bool HW>
 __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64Args A)
 {
+	static_assert(!HW || NG > 0, "walk groups are hoisted");
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 	constexpr uint32_t RW = 17;                     /* odd dword row stride */
 	uint32_t *row = smem + threadIdx.x * RW;        /* generic-parse LDS row */
 	uint4 *ments = (uint4 *)(smem + BLOCK * RW);
 	uint2 *pinfo2 = (uint2 *)(ments + A.num_ment);
+	/* HW: cuckoo entries, pinfo3 */
+	uint2 *cents = (uint2 *)(smem + BLOCK * RW);
+	uint2 *pinfo3 = cents + A.num_cent;
 
 	const uint32_t lane = __lane_id();
 	const uint32_t gw = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
@@ -223,16 +241,26 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 			fn[4 * k + 3] = x.w;
 		}
 	}
-	for (uint32_t k = threadIdx.x; k < A.num_ment; k += BLOCK)
-		ments[k] = A.ments[k];
-	for (uint32_t k = threadIdx.x; k < A.num_pmr; k += BLOCK)
-		pinfo2[k] = A.pinfo2[k];
 	MGd mg[NG > 0 ? NG : 1];
 
-	if constexpr (NG > 0) {
+	if constexpr (HW) {
+		for (uint32_t k = threadIdx.x; k < A.num_cent; k += BLOCK)
+			cents[k] = A.cents[k];
+		for (uint32_t k = threadIdx.x; k < A.num_pmr; k += BLOCK)
+			pinfo3[k] = A.pinfo3[k];
 #pragma unroll
 		for (int g = 0; g < NG; ++g)
-			mg[g] = load_mg(A.mgroups + g);
+			mg[g] = load_mg(A.cgroups + g);
+	} else {
+		for (uint32_t k = threadIdx.x; k < A.num_ment; k += BLOCK)
+			ments[k] = A.ments[k];
+		for (uint32_t k = threadIdx.x; k < A.num_pmr; k += BLOCK)
+			pinfo2[k] = A.pinfo2[k];
+		if constexpr (NG > 0) {
+#pragma unroll
+			for (int g = 0; g < NG; ++g)
+				mg[g] = load_mg(A.mgroups + g);
+		}
 	}
 	__syncthreads();
 
@@ -278,7 +306,10 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		uint32_t wbits = 0u, inf_lo = 0u;
 		bool err = false, pdrop = false;
 		uint32_t lo = 0u, hi = 0u;
-		const bool walk = (A.def_ci >> 8) != 0u;
+		const bool walk = A.def_rules != 0u;
+		/* HW: per walk group, the masked key word and its gate */
+		uint32_t kv[HW ? NG : 1];
+		bool krq[HW ? NG : 1];
 		auto probe = [&](const MGd &d, uint32_t key) {
 			const uint32_t kvm = key & d.mask;
 			const bool rq = (inf_lo & d.req) == d.req;
@@ -319,7 +350,13 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 						return 64u;
 					return __builtin_amdgcn_alignbyte(fv[d.fw + 1u], fv[d.fw], d.fs);
 				};
-				if constexpr (NG > 0) {
+				if constexpr (HW) {
+#pragma unroll
+					for (int g = 0; g < NG; ++g) {
+						kv[g] = fast_key(mg[g]) & mg[g].mask;
+						krq[g] = (inf_lo & mg[g].req) == mg[g].req;
+					}
+				} else if constexpr (NG > 0) {
 #pragma unroll
 					for (int g = 0; g < NG; ++g)
 						probe(mg[g], fast_key(mg[g]));
@@ -374,7 +411,13 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 				key.v = &v;
 				key.b = &b;
 				key.fast = false;
-				if constexpr (NG > 0) {
+				if constexpr (HW) {
+#pragma unroll
+					for (int g = 0; g < NG; ++g) {
+						kv[g] = key(mg[g].slot) & mg[g].mask;
+						krq[g] = (inf_lo & mg[g].req) == mg[g].req;
+					}
+				} else if constexpr (NG > 0) {
 #pragma unroll
 					for (int g = 0; g < NG; ++g)
 						probe(mg[g], key(mg[g].slot));
@@ -396,7 +439,46 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		uint32_t mark = 0u;
 		bool any_match = false;
 
-		{
+		if constexpr (HW) {
+			/* match_pmr_cos, one level per iteration: at CoS c both
+			 * candidates of each group holding a rule of c are read with
+			 * key (c, masked key word); the lowest PMR index found is c's
+			 * first matching rule */
+			bool active = live && !pdrop && !err && walk;
+			uint32_t steps = 0u, gm = A.def_cgmask;
+
+			while (active) {
+				uint32_t best = 0xffffffffu;
+
+#pragma unroll
+				for (int g = 0; g < NG; ++g) {
+					if (!krq[g] || !((gm >> g) & 1u))
+						continue;
+					const uint32_t x = cgroup_key(kv[g], cos);
+					const uint2 e1 = cents[mg[g].off + ((x * mg[g].m1) >> mg[g].sh)];
+					const uint2 e2 = cents[mg[g].off + ((x * mg[g].m2) >> mg[g].sh)];
+
+					if (e1.x == kv[g] && (e1.y & 0xffffu) == cos)
+						best = min(best, e1.y >> 16);
+					if (e2.x == kv[g] && (e2.y & 0xffffu) == cos)
+						best = min(best, e2.y >> 16);
+				}
+				if (best == 0xffffffffu)
+					break;
+				const uint2 pi = pinfo3[best];
+
+				cos = pi.x & 0xffffu;
+				mark = pi.x >> 16;
+				act = pi.y & 0xffu;
+				any_match = true;
+				if (++steps >= A.num_cos) {
+					cos = ODPG_COS_LOOP;
+					break;
+				}
+				active = (pi.y >> 8) & 1u;   /* rules below */
+				gm = pi.y >> 12;
+			}
+		} else {
 			const uint64_t hits = ((uint64_t)hi << 32) | lo;
 
 			/* match_pmr_cos: first hit in the current CoS's rule range,
@@ -483,37 +565,60 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	A.def_cos = a->l64_def_cos;
 	A.def_act = a->l64_def_act;
 	A.def_ci = a->l64_def_ci;
+	A.def_rules = a->l64_def_rules;
+	A.cgroups = a->cgroups;
+	A.cents = (const uint2 *)a->cents;
+	A.num_cent = a->num_cent;
+	A.pinfo3 = (const uint2 *)a->pinfo3;
+	A.def_cgmask = a->def_cgmask;
 	A.out = a->out;
 	A.stats = a->stats;
 	A.sred = a->sred;
 
-	const size_t lds = (size_t)BLOCK * 17u * 4u + (size_t)a->num_ment * 16u +
-			   (size_t)a->num_pmr * 8u;
-	static size_t occ_lds = (size_t)-1;
-	static uint32_t occ_grid = 0;
+	const bool hw = (a->tbl_flags & TBL_LEAN64HW) && !(a->tbl_flags & TBL_LEAN64);
+	size_t lds = (size_t)BLOCK * 17u * 4u +
+			   (hw ? (size_t)a->num_cent * 8u + (size_t)a->num_pmr * 8u
+			       : (size_t)a->num_ment * 16u + (size_t)a->num_pmr * 8u);
+#ifdef L64_LDS_PAD   /* experiment builds only: occupancy sensitivity */
+	lds += L64_LDS_PAD;
+#endif
+	static size_t occ_lds[2] = {(size_t)-1, (size_t)-1};
+	static uint32_t occ_grid[2] = {0, 0};
 
-	if (occ_lds != lds) {
+	if (occ_lds[hw] != lds) {
 		int nb = 0, dev = 0, cus = 0;
 
 		hipGetDevice(&dev);
 		hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, odpg_cls64_kernel<0>, BLOCK, lds) !=
-		    hipSuccess || nb <= 0)
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+			    &nb, hw ? odpg_cls64_kernel<1, true> : odpg_cls64_kernel<0, false>, BLOCK,
+			    lds) != hipSuccess || nb <= 0)
 			nb = 1;
-		occ_grid = (uint32_t)(nb * (cus > 0 ? cus : 256));
-		occ_lds = lds;
+		occ_grid[hw] = (uint32_t)(nb * (cus > 0 ? cus : 256));
+		occ_lds[hw] = lds;
 	}
 	const uint32_t ntiles = (a->num + 63u) / 64u;
 	uint32_t grid = (ntiles + 3u) / 4u;
 
-	if (grid > occ_grid)
-		grid = occ_grid;
-	switch (a->num_mgroups) {
-	case 1: hipLaunchKernelGGL(odpg_cls64_kernel<1>, dim3(grid), dim3(BLOCK), lds, s, A); break;
-	case 2: hipLaunchKernelGGL(odpg_cls64_kernel<2>, dim3(grid), dim3(BLOCK), lds, s, A); break;
-	case 3: hipLaunchKernelGGL(odpg_cls64_kernel<3>, dim3(grid), dim3(BLOCK), lds, s, A); break;
-	case 4: hipLaunchKernelGGL(odpg_cls64_kernel<4>, dim3(grid), dim3(BLOCK), lds, s, A); break;
-	default: hipLaunchKernelGGL(odpg_cls64_kernel<0>, dim3(grid), dim3(BLOCK), lds, s, A); break;
+	if (grid > occ_grid[hw])
+		grid = occ_grid[hw];
+#define L64_LAUNCH(ng, h) hipLaunchKernelGGL((odpg_cls64_kernel<ng, h>), dim3(grid), dim3(BLOCK), lds, s, A)
+	if (hw) {
+		switch (a->num_cgroups) {
+		case 1: L64_LAUNCH(1, true); break;
+		case 2: L64_LAUNCH(2, true); break;
+		case 3: L64_LAUNCH(3, true); break;
+		default: L64_LAUNCH(4, true); break;   /* TBL_LEAN64HW: <= 4 groups */
+		}
+	} else {
+		switch (a->num_mgroups) {
+		case 1: L64_LAUNCH(1, false); break;
+		case 2: L64_LAUNCH(2, false); break;
+		case 3: L64_LAUNCH(3, false); break;
+		case 4: L64_LAUNCH(4, false); break;
+		default: L64_LAUNCH(0, false); break;
+		}
 	}
+#undef L64_LAUNCH
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

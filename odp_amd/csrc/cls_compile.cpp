@@ -239,6 +239,71 @@ dslot_t slotify(const dterm_t &t)
 /* Two-choice cuckoo placement of one mask group's distinct values
  * (odpg_internal.h "Mask groups"). Deterministic: multipliers come from a
  * fixed sequence; the table doubles when no pair places every value. */
+/* two-choice cuckoo table of (value, cos | pmr << 16) keyed by
+ * cgroup_key(value, cos); g.shift / m1 / m2 / off / count as dmgroup_t.
+ * Free entries are {0, HENT_EMPTY}: their CoS field (0xffff) is never a
+ * packet's CoS. Returns -1 if no placement is found. */
+static int build_cgroup(const std::vector<std::pair<uint32_t, uint32_t>> &keys, dmgroup_t &g,
+			std::vector<dwent_t> &ents)
+{
+	const size_t n = keys.size();
+	uint32_t lg = 1;
+
+	while ((1u << lg) < 2 * n)
+		lg++;
+	uint64_t seed = 0xC2B2AE3D27D4EB4Full;
+	auto next_mul = [&]() {
+		seed ^= seed << 13;
+		seed ^= seed >> 7;
+		seed ^= seed << 17;
+		return (uint32_t)(seed >> 32) | 1u;
+	};
+	std::vector<uint32_t> x(n);
+
+	for (size_t k = 0; k < n; k++)
+		x[k] = cgroup_key(keys[k].first, keys[k].second & 0xffffu);
+	for (; lg <= 20; lg++) {
+		const uint32_t sz = 1u << lg, sh = 32u - lg;
+
+		for (int attempt = 0; attempt < 64; attempt++) {
+			const uint32_t m1 = next_mul(), m2 = next_mul();
+			std::vector<int> slot(sz, -1);
+			bool ok = true;
+
+			for (size_t k = 0; k < n && ok; k++) {
+				int cur = (int)k;
+				uint32_t pos = (x[k] * m1) >> sh;
+
+				for (int kick = 0;; kick++) {
+					if (kick > 4 * (int)sz + 16) {
+						ok = false;
+						break;
+					}
+					std::swap(cur, slot[pos]);
+					if (cur < 0)
+						break;
+					uint32_t p1 = (x[cur] * m1) >> sh, p2 = (x[cur] * m2) >> sh;
+
+					pos = pos == p1 ? p2 : p1;
+				}
+			}
+			if (!ok)
+				continue;
+			g.shift = sh;
+			g.m1 = m1;
+			g.m2 = m2;
+			g.off = (uint32_t)ents.size();
+			g.count = (uint32_t)n;
+			ents.resize(ents.size() + sz, dwent_t{0u, HENT_EMPTY});
+			for (uint32_t s2 = 0; s2 < sz; s2++)
+				if (slot[s2] >= 0)
+					ents[g.off + s2] = dwent_t{keys[slot[s2]].first, keys[slot[s2]].second};
+			return 0;
+		}
+	}
+	return -1;
+}
+
 static void build_mgroup(const std::map<uint32_t, uint64_t> &vals, dmgroup_t &g,
 			 std::vector<dment_t> &ents)
 {
@@ -503,6 +568,34 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		}
 	}
 
+	/* CoS-keyed cuckoo groups for the lean kernel's walk form: the same
+	 * (cos, value) -> lowest PMR index maps as the walk groups above, as
+	 * two-choice cuckoo tables (both candidates read at once, no probe
+	 * chain) */
+	std::vector<dmgroup_t> cgroups;
+	std::vector<dwent_t> cents;
+
+	for (size_t gi = 0; gi < wgroups.size() && wgroups.size() <= 4; gi++) {
+		const dhgroup_t &wg = wgroups[gi];
+		std::vector<std::pair<uint32_t, uint32_t>> keys;   /* (value, cos_pmr) */
+
+		for (uint32_t e = 0; e < (1u << wg.log2sz); e++)
+			if (wents[wg.off + e].cos_pmr != HENT_EMPTY)
+				keys.push_back({wents[wg.off + e].value, wents[wg.off + e].cos_pmr});
+		dmgroup_t g;
+
+		memset(&g, 0, sizeof(g));
+		g.slot = wg.slot;
+		g.req = wg.req;
+		g.mask = wg.mask;
+		if (build_cgroup(keys, g, cents) != 0) {
+			cgroups.clear();
+			cents.clear();
+			break;
+		}
+		cgroups.push_back(g);
+	}
+
 	std::vector<dmgroup_t> mgroups;
 	std::vector<dment_t> ments;
 
@@ -657,11 +750,25 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.num_hent = is_simple ? (uint32_t)hents.size() : 0;
 	h.num_wgroups = is_simple ? (uint32_t)wgroups.size() : 0;
 	h.num_went = is_simple ? (uint32_t)wents.size() : 0;
+	const uint32_t lean_req = (1u << IFL_L2) | (1u << IFL_L3) | (1u << IFL_L4) |
+				  (1u << IFL_ETH) | (1u << IFL_VLAN) | (1u << IFL_IPV4) |
+				  (1u << IFL_IPV6) | (1u << IFL_UDP) | (1u << IFL_TCP) |
+				  (1u << IFL_IPSEC_AH) | (1u << IFL_IPSEC_ESP);
+
+	if ((h.flags & TBL_HASHWALK) && !cgroups.empty() && cgroups.size() == wgroups.size() &&
+	    pmr.size() < 65536 && ncos < 4096) {
+		bool lean = true;
+
+		for (const dhgroup_t &g : wgroups)
+			if (g.req & ~lean_req)
+				lean = false;
+		if (lean) {
+			h.flags |= TBL_LEAN64HW;
+			h.num_cgroups = (uint32_t)cgroups.size();
+			h.num_cent = (uint32_t)cents.size();
+		}
+	}
 	if (is_simple && pmr.size() <= MGROUP_MAX_PMR) {
-		const uint32_t lean_req = (1u << IFL_L2) | (1u << IFL_L3) | (1u << IFL_L4) |
-					  (1u << IFL_ETH) | (1u << IFL_VLAN) | (1u << IFL_IPV4) |
-					  (1u << IFL_IPV6) | (1u << IFL_UDP) | (1u << IFL_TCP) |
-					  (1u << IFL_IPSEC_AH) | (1u << IFL_IPSEC_ESP);
 		bool lean = true;
 
 		for (const dmgroup_t &g : mgroups)
@@ -709,6 +816,32 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		}
 	}
 
+	std::vector<uint32_t> pinfo3;
+
+	if (h.num_cgroups) {
+		/* per PMR {dst | mark << 16, dst action | has rules << 8 | the dst's
+		 * cuckoo-group mask << 12}; cgmask[c]: groups holding a rule of c */
+		std::vector<uint32_t> cgmask(ncos, 0u);
+
+		for (size_t g = 0; g < cgroups.size(); g++)
+			for (uint32_t e = 0; e < (1u << (32u - cgroups[g].shift)); e++) {
+				const dwent_t &w = cents[cgroups[g].off + e];
+
+				if (w.cos_pmr != HENT_EMPTY)
+					cgmask[w.cos_pmr & 0xffffu] |= 1u << g;
+			}
+		pinfo3.resize(2 * pmr.size());
+		for (size_t k = 0; k < pmr.size(); k++) {
+			const uint32_t d = pmr[k].dst;
+
+			pinfo3[2 * k] = pinfo[k];
+			pinfo3[2 * k + 1] = cos[d].action | ((cos[d].nrule ? 1u : 0u) << 8) |
+					    (cgmask[d] << 12);
+		}
+		h.def_cgmask = r->default_cos >= 0 && (uint32_t)r->default_cos < ncos ?
+			       cgmask[r->default_cos] : 0u;
+	}
+
 	auto align = [](uint32_t x) { return (x + 63u) & ~63u; };
 	h.term_off = 0;
 	h.slot_off = align(h.term_off + (uint32_t)(terms.size() * sizeof(dterm_t)));
@@ -725,7 +858,10 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.mgroup_off = align(h.went_off + h.num_went * (uint32_t)sizeof(dwent_t));
 	h.ment_off = align(h.mgroup_off + h.num_mgroups * (uint32_t)sizeof(dmgroup_t));
 	h.pinfo2_off = align(h.ment_off + h.num_ment * (uint32_t)sizeof(dment_t));
-	h.blob_bytes = align(h.pinfo2_off + (uint32_t)(pinfo2.size() * 4u));
+	h.cgroup_off = align(h.pinfo2_off + (uint32_t)(pinfo2.size() * 4u));
+	h.cent_off = align(h.cgroup_off + h.num_cgroups * (uint32_t)sizeof(dmgroup_t));
+	h.pinfo3_off = align(h.cent_off + h.num_cent * (uint32_t)sizeof(dwent_t));
+	h.blob_bytes = align(h.pinfo3_off + (uint32_t)(pinfo3.size() * 4u));
 	if (h.blob_bytes == 0)
 		h.blob_bytes = 64;
 	blob.assign(h.blob_bytes, 0);
@@ -762,6 +898,11 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		memcpy(blob.data() + h.ment_off, ments.data(), ments.size() * sizeof(dment_t));
 	if (!pinfo2.empty())
 		memcpy(blob.data() + h.pinfo2_off, pinfo2.data(), pinfo2.size() * 4u);
+	if (h.num_cgroups) {
+		memcpy(blob.data() + h.cgroup_off, cgroups.data(), cgroups.size() * sizeof(dmgroup_t));
+		memcpy(blob.data() + h.cent_off, cents.data(), cents.size() * sizeof(dwent_t));
+		memcpy(blob.data() + h.pinfo3_off, pinfo3.data(), pinfo3.size() * 4u);
+	}
 	*hdr_out = h;
 	return 0;
 }

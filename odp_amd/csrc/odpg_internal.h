@@ -95,6 +95,9 @@ typedef struct dcos_s {
 			      * the lean kernel's register parse computes
 			      * (L2, L3, L4, ETH, VLAN, IPV4, IPV6, UDP, TCP,
 			      * IPSEC_AH, IPSEC_ESP) */
+#define TBL_LEAN64HW   0x100 /* TBL_HASHWALK with <= 4 walk groups whose gates
+			      * the lean kernel's register parse computes: the
+			      * lean kernel's walk-group form */
 
 /* ---- per-packet key slots (evaluate-all kernels) -------------------------
  * The parser-relative 32-bit words the terms can compare, extracted once per
@@ -205,6 +208,16 @@ typedef struct dment_s {
 #else
 #define ODPG_HD
 #endif
+/* CoS-keyed cuckoo groups (TBL_LEAN64HW): the walk groups' (cos, value)
+ * -> lowest PMR maps as two-choice cuckoo tables in dmgroup_t form (shift,
+ * m1, m2, off, count) over dwent_t entries; a key's candidates are
+ * (cgroup_key(value, cos) * m) >> shift for m = m1, m2. pinfo3[k] =
+ * {dst | mark << 16, dst action | dst has rules << 8 | dst group mask << 12}. */
+static inline ODPG_HD uint32_t cgroup_key(uint32_t value, uint32_t cos)
+{
+	return value ^ (cos * 0x85EBCA6Bu);
+}
+
 /* slot of (value, cos) in a walk group of 2^lg entries (lg >= 1) */
 static inline ODPG_HD uint32_t walk_hash(uint32_t value, uint32_t cos, uint32_t lg)
 {
@@ -249,6 +262,12 @@ typedef struct dtable_hdr_s {
 	uint32_t ment_off;   /* dment_t[num_ment] */
 	uint32_t num_ment;
 	uint32_t pinfo2_off; /* uint2[num_pmr] when num_pmr <= 64 */
+	uint32_t cgroup_off; /* dmgroup_t[num_cgroups]: CoS-keyed cuckoo groups (TBL_LEAN64HW) */
+	uint32_t num_cgroups;
+	uint32_t cent_off;   /* dwent_t[num_cent] */
+	uint32_t num_cent;
+	uint32_t pinfo3_off; /* uint2[num_pmr] (TBL_LEAN64HW) */
+	uint32_t def_cgmask; /* cuckoo groups holding a rule of the default CoS */
 	uint32_t blob_bytes;
 } dtable_hdr_t;
 
@@ -289,9 +308,15 @@ typedef struct odpg_launch_args {
 	const dment_t *ments;
 	uint32_t num_ment;
 	const uint2_t *pinfo2;
+	const dmgroup_t *cgroups;   /* TBL_LEAN64HW cuckoo groups */
+	uint32_t num_cgroups;
+	const dwent_t *cents;
+	uint32_t num_cent;
+	const uint2_t *pinfo3;
+	uint32_t def_cgmask;
 	/* lean 64-byte kernel (classify64.hip): CoS start state, from the host
 	 * copy of the table */
-	uint32_t l64_err_cos, l64_err_act, l64_def_cos, l64_def_act, l64_def_ci;
+	uint32_t l64_err_cos, l64_err_act, l64_def_cos, l64_def_act, l64_def_ci, l64_def_rules;
 	int mode;          /* 0 auto, 1 walk, 2 evaluate-all, 3 hash walk */
 	odpg_out_t *out;
 	uint16_t *mark;

@@ -280,6 +280,12 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.ments = (const dment_t *)((const uint8_t *)t->dblob + h.ment_off);
 	a.num_ment = h.num_ment;
 	a.pinfo2 = (const uint2_t *)((const uint8_t *)t->dblob + h.pinfo2_off);
+	a.cgroups = (const dmgroup_t *)((const uint8_t *)t->dblob + h.cgroup_off);
+	a.num_cgroups = h.num_cgroups;
+	a.cents = (const dwent_t *)((const uint8_t *)t->dblob + h.cent_off);
+	a.num_cent = h.num_cent;
+	a.pinfo3 = (const uint2_t *)((const uint8_t *)t->dblob + h.pinfo3_off);
+	a.def_cgmask = h.def_cgmask;
 	{
 		/* start state of cls_select_cos (odp_classification.c:1669-1701)
 		 * for the lean kernel, as classify.hip derives it per packet */
@@ -291,6 +297,7 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 		a.l64_err_act = ec >= 0 && (uint32_t)ec < h.num_cos ? hc[ec].action : 0u;
 		a.l64_def_cos = dc < 0 ? ODPG_COS_NONE : (uint32_t)dc;
 		a.l64_def_act = dc >= 0 && (uint32_t)dc < h.num_cos ? hc[dc].action : 0u;
+		a.l64_def_rules = dvalid && hc[dc].nrule;
 		a.l64_def_ci = dvalid && hc[dc].nrule ?
 			       (hc[dc].rule_start & 0xffu) | ((uint32_t)(hc[dc].nrule & 0xffu) << 8) : 0u;
 	}

@@ -377,3 +377,61 @@ def test_lean64_kernel(gpu_ctx, fresh_cls, opt, variant):
     assert L.lib.odpg_last_kernel() == 1
     assert_same({"out": g["out"], "stats": g["stats"]}, {"out": o["out"], "stats": o["stats"]},
                 f"lean64+stats {variant} opt={opt}")
+
+
+def _hashwalk_rules(c, p):
+    """A TBL_HASHWALK table (exact-match values repeated across CoS) with
+    marks, a DROP-action leaf, an error CoS and a leaf chain two levels deep:
+    the lean kernel's walk-group form."""
+    T = c.Term
+    d = c.cos_create("d", queue=c.queue(0))
+    err = c.cos_create("err", queue=c.queue(1))
+    drop = c.cos_create("drop", action=c.COS_ACTION_DROP)
+    assert c.default_cos_set(p, d) == 0 and c.error_cos_set(p, err) == 0
+    l1 = [c.cos_create(f"l1_{a}", queue=c.queue(2 + a)) for a in range(4)]
+    for a in range(4):
+        assert c.pmr_create([T(c.PMR_SIP_ADDR, gen.be_bytes(gen.ip4("10.0.0.0") | (a << 14), 4),
+                               gen.be_bytes(0xFFFFC000, 4))], d, l1[a], mark=a + 1)
+    k = 0
+    for a in range(4):
+        for j in range(6):
+            leaf = drop if (a, j) == (2, 3) else c.cos_create(f"leaf_{k}", queue=c.queue(10 + k))
+            k += 1
+            assert c.pmr_create([T(c.PMR_UDP_DPORT, gen.be_bytes(j + 1, 2), b"\xff\xff")],
+                                l1[a], leaf, mark=100 + k if j % 2 else 0)
+            if (a, j) == (1, 0):
+                # one more level below this leaf
+                deep = c.cos_create("deep", queue=c.queue(60))
+                assert c.pmr_create([T(c.PMR_UDP_SPORT, gen.be_bytes(7, 2), b"\x00\x0f")],
+                                    leaf, deep, mark=77)
+
+
+@pytest.mark.parametrize("opt", [0, L.PKTIN_IPV4_CHKSUM, ALL_CHKSUM])
+@pytest.mark.parametrize("variant", ["c4", "marks_drop"])
+def test_lean64_hashwalk(gpu_ctx, fresh_cls, opt, variant):
+    """The lean 64-byte kernel's walk-group form (TBL_LEAN64HW, auto mode,
+    verdict words and pktio counters): the 1024-PMR C4 table and a small
+    hash-walk table with marks / DROP / error CoS / a third level, on the
+    plain64 corpus (fast and generic waves) and C2 traffic; bit-exact vs the
+    oracle, and the launch really took the lean kernel."""
+    if variant == "c4":
+        assert fresh_cls.set_limits(2048, 2048, 32) == 0
+    p = fresh_cls.loop_pktio(pktin=opt)
+    if variant == "c4":
+        gen.build_c4_rules(fresh_cls, p)
+    else:
+        _hashwalk_rules(fresh_cls, p)
+    assert fresh_cls.pktio_start(p) == 0
+    rules = fresh_cls.pktio_rules(p)
+    tbl = gpu_ctx.table(rules)
+    n = 64 * 257 + 5
+    for fr in (rulesets.plain64_corpus(n, seed=37), gen.c2_frames(n, seed=41)):
+        o = oracle.classify(rules, fr, n, stride=64, opt=opt)
+        g = gpu_ctx.classify(tbl, fr, n, stride=64, opt=opt, want_mark=False, want_meta=False,
+                             want_stats=False)
+        assert L.lib.odpg_last_kernel() == 1
+        assert_same({"out": g["out"]}, {"out": o["out"]}, f"lean64 hw {variant} opt={opt}")
+        g = gpu_ctx.classify(tbl, fr, n, stride=64, opt=opt, want_mark=False, want_meta=False)
+        assert L.lib.odpg_last_kernel() == 1
+        assert_same({"out": g["out"], "stats": g["stats"]},
+                    {"out": o["out"], "stats": o["stats"]}, f"lean64 hw+stats {variant} opt={opt}")
