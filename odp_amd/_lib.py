@@ -123,6 +123,32 @@ class odpg_fwd_batch_t(C.Structure):
                 ("src_port", C.c_int32), ("error_check", C.c_uint32)]
 
 
+# ---- include/odpg_tx.h ------------------------------------------------------
+PKTOUT_IPV4_CHKSUM, PKTOUT_UDP_CHKSUM = 1 << 5, 1 << 6
+PKTOUT_TCP_CHKSUM, PKTOUT_SCTP_CHKSUM = 1 << 7, 1 << 8
+PKTOUT_LOOP_CAPA = PKTOUT_IPV4_CHKSUM | PKTOUT_UDP_CHKSUM | PKTOUT_TCP_CHKSUM | PKTOUT_SCTP_CHKSUM
+HASH_IPV4_UDP, HASH_IPV4_TCP, HASH_IPV4 = 1, 2, 4
+HASH_IPV6_UDP, HASH_IPV6_TCP, HASH_IPV6 = 8, 16, 32
+TX_L3_CHKSUM_SET, TX_L3_CHKSUM, TX_L4_CHKSUM_SET, TX_L4_CHKSUM = 1, 2, 4, 8
+TX_HAS_IPV4, TX_HAS_IPV6, TX_HAS_UDP, TX_HAS_TCP = 1 << 8, 1 << 9, 1 << 10, 1 << 11
+TX_OUT_IPV4, TX_OUT_UDP, TX_OUT_TCP, TX_OUT_SCTP = 1 << 16, 1 << 17, 1 << 18, 1 << 19
+OFFSET_INVALID = 0xFFFF
+
+
+class odpg_tx_batch_t(C.Structure):
+    _fields_ = [("frames", C.c_void_p), ("desc", C.c_void_p), ("stride", C.c_uint32),
+                ("num", C.c_uint32), ("meta", C.c_void_p)]
+
+
+class odpg_tx_cfg_t(C.Structure):
+    _fields_ = [("pktout_cfg", C.c_uint64), ("pktout_capa", C.c_uint64),
+                ("hash_proto", C.c_uint32), ("num_qs", C.c_uint32), ("index", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+TX_META_FIELDS = [("l3_offset", "<u2"), ("l4_offset", "<u2"), ("flags", "<u4")]   # 8 B
+
+
 # numpy dtypes with the same layout
 def np_dtypes():
     import numpy as np
@@ -288,6 +314,8 @@ SIGNATURES = {
                                C.POINTER(_vp)]),
     "odpg_fwd_destroy": (None, [_vp]),
     "odpg_l3fwd": (_i32, [_vp, _vp, C.POINTER(odpg_fwd_batch_t), _vp]),
+    # include/odpg_tx.h
+    "odpg_tx_prepare": (_i32, [_vp, C.POINTER(odpg_tx_batch_t), C.POINTER(odpg_tx_cfg_t), _vp]),
 }
 
 

@@ -1,0 +1,337 @@
+/* SPDX-License-Identifier: BSD-3-Clause
+ *
+ * Loop pktio transmit side on gfx950 (include/odpg_tx.h, SURVEY.md §8(f)
+ * rank 3): per packet, loopback_fix_checksums() and get_dest_queue() of
+ * loopback_send() (platform/linux-generic/pktio/loop.c:415-523), frames
+ * rewritten in place.
+ *
+ * One lane per packet. The frame's first 64 bytes are staged in the lane's
+ * LDS row for the optional parse; checksum ranges are summed from global
+ * memory as frame-aligned little-endian dwords (end-around carry), which
+ * keeps the reference's 64-bit chksum_partial residue mod 0xffff; the
+ * reference pairs bytes relative to the L3 offset (chksum_partial's odd
+ * offset swap, odp_chksum_internal.h:60-196), so an odd L3 offset swaps the
+ * folded sum. CRC32c (SCTP insert, queue hash) is table driven from LDS.
+ */
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdint.h>
+
+#include "../../include/odpg_tx.h"
+#include "odpg_internal.h"
+#include "pkt_parse.h"
+
+namespace {
+
+constexpr uint32_t TX_BLOCK = 256;
+constexpr uint32_t TX_W = 64;               /* LDS window per lane */
+constexpr uint32_t TX_RW = TX_W / 4 + 1;    /* odd dword row stride */
+
+struct TxArgs {
+	uint8_t *frames;
+	const odpg_desc_t *desc;
+	uint32_t stride, num;
+	const odpg_tx_meta_t *meta;
+	uint64_t cfg, capa;
+	uint32_t hash_proto, num_qs, index;
+	uint32_t *out;
+};
+
+/* one dword of the frame at byte 4 * w (bytes past len read as zero) */
+__device__ __forceinline__ uint32_t tx_word(const uint8_t *g, uint32_t len, uint32_t w)
+{
+	if (4u * w >= len)
+		return 0u;
+	uint32_t x;
+
+	__builtin_memcpy(&x, g + 4u * w, 4);
+	const uint32_t rem = len - 4u * w;
+
+	return rem < 4u ? x & ((1u << (8u * rem)) - 1u) : x;
+}
+
+__device__ __forceinline__ uint32_t tx_u8(const uint8_t *g, uint32_t len, uint32_t p)
+{
+	return p < len ? g[p] : 0u;
+}
+
+/* mask of bytes [lo, hi) within dword w (frame positions) */
+__device__ __forceinline__ uint32_t tx_bmask(uint32_t w, uint32_t lo, uint32_t hi)
+{
+	uint32_t m = 0u;
+
+#pragma unroll
+	for (uint32_t j = 0; j < 4; ++j) {
+		const uint32_t p = 4u * w + j;
+
+		m |= (p >= lo && p < hi) ? 0xffu << (8u * j) : 0u;
+	}
+	return m;
+}
+
+/* packet_sum_partial (odp_packet.c:1669-1692) of [off, off + n) with the
+ * bytes of [z0, z1) taken as zero: 0 when the range leaves the frame;
+ * otherwise the one's-complement residue, folded to 16 bits, of the bytes
+ * paired relative to l3 */
+__device__ uint32_t tx_sum(const uint8_t *g, uint32_t len, uint32_t l3, uint32_t off, uint32_t n,
+			   uint32_t z0 = 0u, uint32_t z1 = 0u)
+{
+	if (n == 0u || off + n > len || off + n < off)
+		return 0u;
+	const uint32_t end = off + n, w0 = off >> 2, w1 = (end - 1u) >> 2;
+	uint32_t s = 0u;
+
+	for (uint32_t w = w0; w <= w1; ++w) {
+		uint32_t x = tx_word(g, len, w);
+
+		if (w == w0 || w == w1 || (z1 > z0 && 4u * w + 4u > z0 && 4u * w < z1))
+			x &= tx_bmask(w, off, end) & ~tx_bmask(w, z0, z1);
+		s = oc_add(s, x);
+	}
+	s = oc_fold(s);
+	return (l3 & 1u) ? ((s & 0xffu) << 8) | (s >> 8) : s;
+}
+
+__device__ __forceinline__ uint32_t crc_tab(const uint32_t *tab, uint32_t crc, uint32_t b)
+{
+	return tab[(crc ^ b) & 0xffu] ^ (crc >> 8);
+}
+
+/* byte stores (frames may sit at any alignment); false when the range
+ * leaves the frame (odp_packet_copy_from_mem fails) */
+__device__ __forceinline__ bool tx_store(uint8_t *g, uint32_t len, uint32_t off, uint32_t v,
+					 uint32_t n)
+{
+	if (off + n > len)
+		return false;
+	for (uint32_t j = 0; j < n; ++j)
+		g[off + j] = (uint8_t)(v >> (8u * j));
+	return true;
+}
+
+__global__ __launch_bounds__(TX_BLOCK) void odpg_tx_kernel(const TxArgs A)
+{
+	__shared__ uint32_t tab[256];
+	__shared__ uint32_t rows[TX_BLOCK * TX_RW];
+	const uint32_t tid = threadIdx.x;
+
+	{
+		/* reflected Castagnoli table (arch/default/odp_hash_crc32.c) */
+		uint32_t c = tid;
+
+		for (int k = 0; k < 8; ++k)
+			c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+		tab[tid] = c;
+	}
+	__syncthreads();
+	const uint32_t i = blockIdx.x * TX_BLOCK + tid;
+
+	if (i >= A.num)
+		return;
+	uint8_t *g;
+	uint32_t len;
+
+	if (A.desc) {
+		const odpg_desc_t d = A.desc[i];
+
+		g = A.frames + d.offset;
+		len = d.len;
+	} else {
+		g = A.frames + (size_t)i * A.stride;
+		len = A.stride;
+	}
+	uint32_t l3, l4, fl;
+
+	if (A.meta) {
+		const odpg_tx_meta_t m = A.meta[i];
+
+		l3 = m.l3_offset;
+		l4 = m.l4_offset;
+		fl = m.flags;
+	} else {
+		/* _odp_packet_parse_common, all layers, no checksum options */
+		uint32_t *row = rows + tid * TX_RW;
+
+		for (uint32_t w = 0; w < TX_W / 4; ++w)
+			row[w] = tx_word(g, len, w);
+		Pkt<TX_W, true> v;
+		Prs p;
+
+		v.row = row;
+		v.g = g;
+		v.len = len;
+		p.inf = 0ull;
+		p.fl = 0u;
+		p.l2 = p.l3 = p.l4 = 0xffffu;
+		parse_common(p, v, LAYER_ALL, 0ull);
+		l3 = p.l3;
+		l4 = p.l4;
+		fl = ((p.inf & IF(IFL_IPV4)) ? ODPG_TX_HAS_IPV4 : 0u) |
+		     ((p.inf & IF(IFL_IPV6)) ? ODPG_TX_HAS_IPV6 : 0u) |
+		     ((p.inf & IF(IFL_UDP)) ? ODPG_TX_HAS_UDP : 0u) |
+		     ((p.inf & IF(IFL_TCP)) ? ODPG_TX_HAS_TCP : 0u);
+	}
+	uint32_t res = 0u;
+
+	/* ---- loopback_fix_checksums (loop.c:415-466) ---------------------- */
+	if (l3 != ODPG_OFFSET_INVALID && l3 < len) {
+		/* check_proto (loop.c:382-411) */
+		const uint32_t ver = tx_u8(g, len, l3) >> 4, l3_len = len - l3;
+		bool ok = false, v4 = false;
+		uint32_t l4p = 0u;
+
+		if (ver == 4u && l3_len >= 20u) {
+			const uint32_t frag = (tx_u8(g, len, l3 + 6u) << 8) | tx_u8(g, len, l3 + 7u);
+
+			ok = true;
+			v4 = true;
+			l4p = (frag & 0x3fffu) ? 255u : tx_u8(g, len, l3 + 9u);
+		} else if (ver == 6u && l3_len >= 40u) {
+			ok = true;
+			l4p = tx_u8(g, len, l3 + 6u);
+		}
+		if (ok) {
+			/* OL_TX_CHKSUM_PKT (loop.c:379-380) */
+			auto want = [&](uint64_t bit, bool proto, uint32_t set, uint32_t ovr) {
+				return (A.capa & bit) && proto && ((fl & set) ? (fl & ovr) != 0u
+									: (A.cfg & bit) != 0u);
+			};
+			const bool ip4 = want(ODPG_PKTOUT_IPV4_CHKSUM, v4, ODPG_TX_L3_CHKSUM_SET,
+					      ODPG_TX_L3_CHKSUM);
+			const bool udp = want(ODPG_PKTOUT_UDP_CHKSUM, l4p == 17u, ODPG_TX_L4_CHKSUM_SET,
+					      ODPG_TX_L4_CHKSUM);
+			const bool tcp = want(ODPG_PKTOUT_TCP_CHKSUM, l4p == 6u, ODPG_TX_L4_CHKSUM_SET,
+					      ODPG_TX_L4_CHKSUM);
+			const bool sctp = want(ODPG_PKTOUT_SCTP_CHKSUM, l4p == 132u,
+					       ODPG_TX_L4_CHKSUM_SET, ODPG_TX_L4_CHKSUM);
+
+			/* _odp_packet_ipv4_chksum_insert (odp_packet.c:1729-1787) */
+			if (ip4 && l3 + 20u <= len) {
+				const uint32_t nleft = (tx_u8(g, len, l3) & 0x0fu) * 4u;
+
+				if (nleft >= 20u && l3 + nleft <= len) {
+					const uint32_t s = tx_sum(g, len, l3, l3, nleft, l3 + 10u, l3 + 12u);
+
+					if (tx_store(g, len, l3 + 10u, ~s & 0xffffu, 2u))
+						res |= ODPG_TX_OUT_IPV4;
+				}
+			}
+			/* _odp_packet_tcp_udp_chksum_insert (odp_packet.c:1789-1862):
+			 * both write at l4 + _ODP_UDP_CSUM_OFFSET */
+			for (int pass = 0; pass < 2; ++pass) {
+				const bool is_tcp = pass == 0;
+
+				if (!(is_tcp ? tcp : udp) || l4 == ODPG_OFFSET_INVALID)
+					continue;
+				const uint32_t cs = l4 + 6u;
+				uint32_t s = (tx_u8(g, len, l3) >> 4) == 4u
+					     ? tx_sum(g, len, l3, l3 + 12u, 8u)
+					     : tx_sum(g, len, l3, l3 + 8u, 32u);
+
+				s = oc_add(s, (is_tcp ? 6u : 17u) << 8);
+				if (is_tcp) {
+					const uint32_t tl = (len - l4) & 0xffffu;
+
+					s = oc_add(s, ((tl >> 8) | (tl << 8)) & 0xffffu);
+				} else {
+					s = oc_add(s, tx_sum(g, len, l3, l4 + 4u, 2u));
+				}
+				const bool zeroed = cs + 2u <= len;   /* the zero write */
+
+				s = oc_add(s, tx_sum(g, len, l3, l4, len - l4,
+						      zeroed ? cs : 0u, zeroed ? cs + 2u : 0u));
+				uint32_t c = ~oc_fold(s) & 0xffffu;
+
+				if (!is_tcp && c == 0u)
+					c = 0xffffu;
+				if (tx_store(g, len, cs, c, 2u))
+					res |= is_tcp ? ODPG_TX_OUT_TCP : ODPG_TX_OUT_UDP;
+			}
+			/* _odp_packet_sctp_chksum_insert (odp_packet.c:1884-1898) */
+			if (sctp && l4 != ODPG_OFFSET_INVALID) {
+				const bool zeroed = l4 + 12u <= len;
+				uint32_t crc = 0xffffffffu;
+
+				if (l4 <= len)
+					for (uint32_t p = l4; p < len; ++p) {
+						const uint32_t b = (zeroed && p >= l4 + 8u && p < l4 + 12u)
+								   ? 0u : g[p];
+
+						crc = crc_tab(tab, crc, b);
+					}
+				if (tx_store(g, len, l4 + 8u, ~crc, 4u))
+					res |= ODPG_TX_OUT_SCTP;
+			}
+		}
+	}
+
+	/* ---- get_dest_queue (loop.c:468-523) ------------------------------- */
+	uint32_t q;
+
+	if (A.hash_proto == 0u) {
+		q = A.index % A.num_qs;
+	} else {
+		const uint32_t hp = A.hash_proto;
+		uint32_t crc = 0u;
+
+		if (l4 != ODPG_OFFSET_INVALID) {
+			bool ports = false;
+
+			if ((hp & (ODPG_HASH_IPV4_UDP | ODPG_HASH_IPV6_UDP)) && (fl & ODPG_TX_HAS_UDP))
+				ports = l4 + 8u <= len;
+			else if ((hp & (ODPG_HASH_IPV4_TCP | ODPG_HASH_IPV6_TCP)) &&
+				 (fl & ODPG_TX_HAS_TCP))
+				ports = l4 + 20u <= len;
+			if (ports)
+				for (uint32_t j = 0; j < 4u; ++j)
+					crc = crc_tab(tab, crc, g[l4 + j]);
+		}
+		if (l3 != ODPG_OFFSET_INVALID) {
+			uint32_t a = 0u, n = 0u;
+
+			if ((hp & ODPG_HASH_IPV4) && (fl & ODPG_TX_HAS_IPV4)) {
+				if (l3 + 20u <= len) {
+					a = l3 + 12u;
+					n = 8u;
+				}
+			} else if ((hp & ODPG_HASH_IPV6) && (fl & ODPG_TX_HAS_IPV6)) {
+				if (l3 + 40u <= len) {
+					a = l3 + 8u;
+					n = 32u;
+				}
+			}
+			for (uint32_t j = 0; j < n; ++j)
+				crc = crc_tab(tab, crc, g[a + j]);
+		}
+		q = crc % A.num_qs;
+	}
+	A.out[i] = res | (q & ODPG_TX_OUT_QUEUE_MASK);
+}
+
+} /* namespace */
+
+extern "C" int odpg_tx_prepare(odpg_ctx_t *ctx, const odpg_tx_batch_t *b,
+			       const odpg_tx_cfg_t *cfg, uint32_t *out)
+{
+	if (!ctx || !b || !cfg || cfg->num_qs == 0u || (b->num && (!b->frames || !out)) ||
+	    (!b->desc && b->num && b->stride == 0u))
+		return -EINVAL;
+	if (b->num == 0)
+		return 0;
+	TxArgs A;
+
+	A.frames = b->frames;
+	A.desc = b->desc;
+	A.stride = b->stride;
+	A.num = b->num;
+	A.meta = b->meta;
+	A.cfg = cfg->pktout_cfg;
+	A.capa = cfg->pktout_capa;
+	A.hash_proto = cfg->hash_proto;
+	A.num_qs = cfg->num_qs;
+	A.index = cfg->index;
+	A.out = out;
+	hipLaunchKernelGGL(odpg_tx_kernel, dim3((b->num + TX_BLOCK - 1) / TX_BLOCK), dim3(TX_BLOCK),
+			   0, (hipStream_t)odpg_ctx_stream(ctx), A);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}

@@ -144,6 +144,36 @@ class Context:
                 b.free()
         return res
 
+    def tx_prepare(self, frames, num, stride=0, desc=None, meta=None, pktout_cfg=0,
+                   pktout_capa=L.PKTOUT_LOOP_CAPA, hash_proto=0, num_qs=1, index=0):
+        """loopback_send()'s checksum insertion + loop queue pick on the GPU
+        (include/odpg_tx.h). Returns (out words, rewritten frames)."""
+        _, desc_dt = L.np_dtypes()
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        fb = self.buffer(frames.nbytes + 64)
+        fb.upload(frames)
+        db = mb = None
+        if desc is not None:
+            desc = np.ascontiguousarray(desc, dtype=desc_dt)
+            db = self.buffer(desc.nbytes)
+            db.upload(desc)
+        if meta is not None:
+            meta = np.ascontiguousarray(meta, dtype=np.dtype(L.TX_META_FIELDS))
+            mb = self.buffer(meta.nbytes)
+            mb.upload(meta)
+        ob = self.buffer(4 * num)
+        b = L.odpg_tx_batch_t(fb.ptr, db.ptr if db else None, stride, num,
+                              mb.ptr if mb else None)
+        c = L.odpg_tx_cfg_t(pktout_cfg, pktout_capa, hash_proto, num_qs, index, 0)
+        L.check(lib.odpg_tx_prepare(self.h, C.byref(b), C.byref(c), ob.ptr), "odpg_tx_prepare")
+        self.sync()
+        out = ob.download(np.uint32, num)
+        fr = fb.download(np.uint8, frames.nbytes)
+        for x in (fb, db, mb, ob):
+            if x:
+                x.free()
+        return out, fr
+
     def classify_host(self, table, frames, num, stride=0, desc=None, opt=0,
                       layer=L.LAYER_ALL, classify=True, chunk=0, want_mark=False,
                       want_meta=False, want_stats=True):

@@ -1341,3 +1341,244 @@ int oracle_fib_lookup(const odpg_route_t *routes, uint32_t nroutes, const uint32
 	free(fib);
 	return ovf ? -1 : 0;
 }
+
+/* ==========================================================================
+ * Loop pktio transmit side (include/odpg_tx.h):
+ * loopback_fix_checksums + get_dest_queue, per packet of loopback_send()
+ * (pktio/loop.c:525-575). Frames are rewritten in place.
+ * ========================================================================== */
+#include "../include/odpg_tx.h"
+
+typedef struct {
+	uint8_t *d;        /* writable frame */
+	uint32_t len;      /* frame_len */
+} wv_t;
+
+/* odp_packet_copy_from_mem (fails when the range leaves the frame) */
+static int tx_write(wv_t *w, uint32_t off, const void *src, uint32_t n)
+{
+	if (off + n > w->len)
+		return -1;
+	memcpy(w->d + off, src, n);
+	return 0;
+}
+
+/* packet_sum_partial (odp_packet.c:1669-1692): 0 when the range leaves the
+ * frame; `offset - l3` selects the odd-byte swap */
+static uint64_t tx_sum_partial(const wv_t *w, uint32_t l3, uint32_t off, uint32_t len)
+{
+	pv_t v = { w->d, w->len };
+
+	/* (a range whose end wraps past 2^32, only for metadata offsets beyond
+	 * the frame, is treated as leaving the frame) */
+	if (off > w->len || len > w->len - off)
+		return 0;
+	return chksum_partial(&v, off, len, off - l3);
+}
+
+/* check_proto (loop.c:382-411) */
+static int tx_check_proto(const wv_t *w, uint32_t l3, int *v4, uint8_t *l4p)
+{
+	pv_t v = { w->d, w->len };
+	uint32_t l3_len = w->len - l3;
+	uint8_t ver = (uint8_t)(B(&v, l3) >> 4);
+
+	if (ver == 4 && l3_len >= 20) {
+		*v4 = 1;
+		*l4p = (be16(&v, l3 + 6) & 0x3fff) ? 255 : B(&v, l3 + 9);
+		return 0;
+	}
+	if (ver == 6 && l3_len >= 40) {
+		*v4 = 0;
+		*l4p = B(&v, l3 + 6);
+		return 0;
+	}
+	return -1;
+}
+
+/* _odp_packet_ipv4_chksum_insert + packet_ipv4_chksum (odp_packet.c:1729-1787) */
+static int tx_ipv4_insert(wv_t *w, uint32_t l3)
+{
+	uint8_t buf[60];
+	uint32_t nleft;
+	uint16_t c;
+
+	if (l3 == OFFSET_INVALID || l3 + 20 > w->len)
+		return -1;
+	nleft = (uint32_t)(w->d[l3] & 0x0f) * 4;
+	if (nleft < 20 || l3 + nleft > w->len)
+		return -1;
+	memcpy(buf, w->d + l3, nleft);
+	buf[10] = buf[11] = 0;
+	c = (uint16_t)~chksum_finalize(chksum_partial_mem(buf, nleft, 0));
+	return tx_write(w, l3 + 10, &c, 2);
+}
+
+/* _odp_packet_tcp_udp_chksum_insert (odp_packet.c:1789-1862) */
+static int tx_tcp_udp_insert(wv_t *w, uint32_t l3, uint32_t l4, uint16_t proto)
+{
+	uint64_t sum;
+	uint32_t zero = 0, csum_off = l4 + 6;   /* _ODP_UDP_CSUM_OFFSET for both */
+	uint16_t c;
+
+	if (l3 == OFFSET_INVALID || l4 == OFFSET_INVALID)
+		return -1;
+	if ((w->d[l3] >> 4) == 4)
+		sum = tx_sum_partial(w, l3, l3 + 12, 8);
+	else
+		sum = tx_sum_partial(w, l3, l3 + 8, 32);
+	sum += (uint64_t)proto << 8;
+	if (proto == 6) {
+		uint16_t tl = (uint16_t)(w->len - l4);
+
+		sum += (uint16_t)((tl >> 8) | (tl << 8));      /* odp_cpu_to_be_16 */
+	} else {
+		sum += tx_sum_partial(w, l3, l4 + 4, 2);
+	}
+	tx_write(w, csum_off, &zero, 2);
+	sum += tx_sum_partial(w, l3, l4, w->len - l4);
+	c = (uint16_t)~chksum_finalize(sum);
+	if (proto == 17 && c == 0)
+		c = 0xffff;
+	return tx_write(w, csum_off, &c, 2);
+}
+
+/* _odp_packet_sctp_chksum_insert (odp_packet.c:1884-1898) */
+static int tx_sctp_insert(wv_t *w, uint32_t l4)
+{
+	uint32_t sum = 0;
+	pv_t v;
+
+	if (l4 == OFFSET_INVALID)
+		return -1;
+	tx_write(w, l4 + 8, &sum, 4);
+	v.d = w->d;
+	v.len = w->len;
+	sum = ~0u;
+	if (l4 <= w->len)      /* packet_sum_crc32c: init returned if out of frame */
+		sum = crc32c(&v, l4, w->len - l4, sum);
+	sum = ~sum;
+	return tx_write(w, l4 + 8, &sum, 4);
+}
+
+/* get_dest_queue (loop.c:468-523) */
+static uint32_t tx_dest_queue(const wv_t *w, uint32_t l3, uint32_t l4, uint32_t fl,
+			      const odpg_tx_cfg_t *cfg)
+{
+	const uint32_t hp = cfg->hash_proto;
+	uint8_t data[36];
+	uint32_t n = 0;
+	pv_t v = { w->d, w->len };
+
+	if (hp == 0)
+		return cfg->index % cfg->num_qs;
+	memset(data, 0, sizeof(data));
+	if (l4 != OFFSET_INVALID) {
+		if ((hp & (ODPG_HASH_IPV4_UDP | ODPG_HASH_IPV6_UDP)) && (fl & ODPG_TX_HAS_UDP)) {
+			if (l4 + 8 <= w->len) {
+				memcpy(data + n, w->d + l4, 4);       /* src_port, dst_port */
+				n += 4;
+			}
+		} else if ((hp & (ODPG_HASH_IPV4_TCP | ODPG_HASH_IPV6_TCP)) &&
+			   (fl & ODPG_TX_HAS_TCP)) {
+			if (l4 + 20 <= w->len) {
+				memcpy(data + n, w->d + l4, 4);
+				n += 4;
+			}
+		}
+	}
+	if (l3 != OFFSET_INVALID) {
+		if ((hp & ODPG_HASH_IPV4) && (fl & ODPG_TX_HAS_IPV4)) {
+			if (l3 + 20 <= w->len) {
+				memcpy(data + n, w->d + l3 + 12, 8);  /* src_addr, dst_addr */
+				n += 8;
+			}
+		} else if ((hp & ODPG_HASH_IPV6) && (fl & ODPG_TX_HAS_IPV6)) {
+			if (l3 + 40 <= w->len) {
+				memcpy(data + n, w->d + l3 + 8, 32);
+				n += 32;
+			}
+		}
+	}
+	v.d = data;
+	v.len = n;
+	return crc32c(&v, 0, n, 0) % cfg->num_qs;
+}
+
+#define OL_TX_CHKSUM_PKT(cfg, capa, proto, ovr_set, ovr) \
+	((capa) && (proto) && ((ovr_set) ? (ovr) : (cfg)))   /* loop.c:379-380 */
+
+/* loopback_fix_checksums (loop.c:415-466) + get_dest_queue for packet i */
+static uint32_t tx_one(wv_t *w, uint32_t l3, uint32_t l4, uint32_t fl, const odpg_tx_cfg_t *cfg)
+{
+	uint32_t res = 0;
+	int v4 = 0;
+	uint8_t l4p = 0;
+
+	if (l3 != OFFSET_INVALID && l3 < w->len && tx_check_proto(w, l3, &v4, &l4p) == 0) {
+		const uint64_t c = cfg->pktout_cfg, k = cfg->pktout_capa;
+		const int l3s = !!(fl & ODPG_TX_L3_CHKSUM_SET), l3o = !!(fl & ODPG_TX_L3_CHKSUM);
+		const int l4s = !!(fl & ODPG_TX_L4_CHKSUM_SET), l4o = !!(fl & ODPG_TX_L4_CHKSUM);
+		const int ip4 = OL_TX_CHKSUM_PKT(!!(c & ODPG_PKTOUT_IPV4_CHKSUM),
+						 !!(k & ODPG_PKTOUT_IPV4_CHKSUM), v4, l3s, l3o);
+		const int udp = OL_TX_CHKSUM_PKT(!!(c & ODPG_PKTOUT_UDP_CHKSUM),
+						 !!(k & ODPG_PKTOUT_UDP_CHKSUM), l4p == 17, l4s, l4o);
+		const int tcp = OL_TX_CHKSUM_PKT(!!(c & ODPG_PKTOUT_TCP_CHKSUM),
+						 !!(k & ODPG_PKTOUT_TCP_CHKSUM), l4p == 6, l4s, l4o);
+		const int sctp = OL_TX_CHKSUM_PKT(!!(c & ODPG_PKTOUT_SCTP_CHKSUM),
+						  !!(k & ODPG_PKTOUT_SCTP_CHKSUM), l4p == 132, l4s, l4o);
+
+		if (ip4 && tx_ipv4_insert(w, l3) == 0)
+			res |= ODPG_TX_OUT_IPV4;
+		if (tcp && tx_tcp_udp_insert(w, l3, l4, 6) == 0)
+			res |= ODPG_TX_OUT_TCP;
+		if (udp && tx_tcp_udp_insert(w, l3, l4, 17) == 0)
+			res |= ODPG_TX_OUT_UDP;
+		if (sctp && tx_sctp_insert(w, l4) == 0)
+			res |= ODPG_TX_OUT_SCTP;
+	}
+	return res | (tx_dest_queue(w, l3, l4, fl, cfg) & ODPG_TX_OUT_QUEUE_MASK);
+}
+
+/* Batch entry (host buffers). meta == NULL: each frame is parsed first
+ * (_odp_packet_parse_common, all layers, no checksum options). Returns 0, or
+ * -1 for num_qs == 0. */
+int oracle_tx_prepare(uint8_t *frames, const odpg_desc_t *desc, uint32_t stride, uint32_t num,
+		      const odpg_tx_meta_t *meta, const odpg_tx_cfg_t *cfg, uint32_t *out)
+{
+	if (!cfg || cfg->num_qs == 0)
+		return -1;
+	pthread_once(&crc_once, crc_init);
+	for (uint32_t i = 0; i < num; i++) {
+		wv_t w;
+		uint32_t l3, l4, fl;
+
+		if (desc) {
+			w.d = frames + desc[i].offset;
+			w.len = desc[i].len;
+		} else {
+			w.d = frames + (size_t)i * stride;
+			w.len = stride;
+		}
+		if (meta) {
+			l3 = meta[i].l3_offset;
+			l4 = meta[i].l4_offset;
+			fl = meta[i].flags;
+		} else {
+			hdr_t h;
+			pv_t v = { w.d, w.len };
+
+			memset(&h, 0, sizeof(h));
+			h.l2_offset = h.l3_offset = h.l4_offset = OFFSET_INVALID;
+			parse_common(&h, &v, v.len, LAYER_ALL, 0);
+			l3 = h.l3_offset;
+			l4 = h.l4_offset;
+			fl = ((h.input_flags & IFB(IF_IPV4)) ? ODPG_TX_HAS_IPV4 : 0u) |
+			     ((h.input_flags & IFB(IF_IPV6)) ? ODPG_TX_HAS_IPV6 : 0u) |
+			     ((h.input_flags & IFB(IF_UDP)) ? ODPG_TX_HAS_UDP : 0u) |
+			     ((h.input_flags & IFB(IF_TCP)) ? ODPG_TX_HAS_TCP : 0u);
+		}
+		out[i] = tx_one(&w, l3, l4, fl, cfg);
+	}
+	return 0;
+}

@@ -37,6 +37,8 @@ def _load():
     lib.oracle_thash.argtypes = [vp, u32]
     lib.oracle_l3fwd.restype = i32
     lib.oracle_l3fwd.argtypes = [vp, u32, vp, vp, u32, u32, i32, i32, vp]
+    lib.oracle_tx_prepare.restype = i32
+    lib.oracle_tx_prepare.argtypes = [vp, vp, u32, u32, vp, vp, vp]
     lib.oracle_fib_lookup.restype = i32
     lib.oracle_fib_lookup.argtypes = [vp, u32, vp, u32, vp, vp]
     return lib
@@ -122,3 +124,34 @@ def fib_lookup(routes, ips):
     if rc:
         raise ValueError("trie pool overflow")
     return port, valid.astype(bool)
+
+
+class TxCfg(C.Structure):
+    """odpg_tx_cfg_t (include/odpg_tx.h)"""
+    _fields_ = [("pktout_cfg", C.c_uint64), ("pktout_capa", C.c_uint64),
+                ("hash_proto", C.c_uint32), ("num_qs", C.c_uint32), ("index", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+TX_META_DT = np.dtype([("l3_offset", "<u2"), ("l4_offset", "<u2"), ("flags", "<u4")])
+PKTOUT_LOOP_CAPA = (1 << 5) | (1 << 6) | (1 << 7) | (1 << 8)
+
+
+def tx_prepare(frames, num, stride=0, desc=None, meta=None, pktout_cfg=0,
+               pktout_capa=PKTOUT_LOOP_CAPA, hash_proto=0, num_qs=1, index=0):
+    """loopback_send()'s checksum insertion + queue pick restated
+    (pktio/loop.c:415-523). Returns (out words, rewritten copy of frames)."""
+    fr = np.array(frames, dtype=np.uint8, copy=True)
+    dptr = mptr = None
+    if desc is not None:
+        desc = np.ascontiguousarray(desc, dtype=DESC_DT)
+        dptr = desc.ctypes.data
+    if meta is not None:
+        meta = np.ascontiguousarray(meta, dtype=TX_META_DT)
+        mptr = meta.ctypes.data
+    out = np.zeros(num, np.uint32)
+    cfg = TxCfg(pktout_cfg, pktout_capa, hash_proto, num_qs, index, 0)
+    if lib.oracle_tx_prepare(fr.ctypes.data, dptr, stride, num, mptr, C.byref(cfg),
+                             out.ctypes.data):
+        raise ValueError("num_qs must be >= 1")
+    return out, fr
