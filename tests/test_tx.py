@@ -186,7 +186,7 @@ def test_tx_gpu_parity(gpu_ctx, corpus, with_meta):
         bad = np.nonzero(o_out != g_out)[0]
         assert len(bad) == 0, (corpus, cfg, hp, bad[:5], o_out[bad[:5]], g_out[bad[:5]])
         assert np.array_equal(o_fr, g_fr[:len(o_fr)]), (corpus, cfg, hp)
-        assert np.any(o_fr != buf) or cfg == 0
+        assert np.any(o_out & 0xF0000) or cfg == 0   # some insert ran
 
 
 @pytest.mark.gpu
