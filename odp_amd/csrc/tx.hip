@@ -109,6 +109,115 @@ __device__ __forceinline__ bool tx_store(uint8_t *g, uint32_t len, uint32_t off,
 	return true;
 }
 
+/* acc + w.lo * x.lo16 + w.hi * x.hi16 (one v_dot2_u32_u16) */
+typedef unsigned short tx_us2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t d2(uint32_t x, uint32_t w, uint32_t acc)
+{
+	return __builtin_amdgcn_udot2(__builtin_bit_cast(tx_us2, x), __builtin_bit_cast(tx_us2, w),
+				      acc, false);
+}
+
+/* end-around fold of a sum of < 2^15 16-bit words */
+__device__ __forceinline__ uint32_t d2fold(uint32_t s)
+{
+	s = d2(s, 0x00010001u, 0u);
+	return d2(s, 0x00010001u, 0u);
+}
+
+/* the generic path's result for a plain 64-byte frame (plain_v4(f)):
+ * l3 = 14, l4 = 34, no overrides; dwords 6 (bytes 24..27, the IPv4 checksum)
+ * and 10 (bytes 40..43, the UDP checksum / the TCP write at l4 + 6) are
+ * stored back when changed */
+__device__ __forceinline__ uint32_t tx_fast64(const TxArgs &A, const uint32_t *tab,
+					      uint32_t (&f)[16], uint32_t *g)
+{
+	constexpr uint32_t W11 = 0x00010001u, W10 = 0x00000001u, W01 = 0x00010000u;
+	const uint32_t proto = f[5] >> 24;
+	const bool frag = (f[5] & 0xff3fu) != 0u;   /* be16(frag) & 0x3fff */
+	const uint32_t l4p = frag ? 255u : proto;
+	uint32_t res = 0u;
+	bool w6 = false, w10 = false;
+
+	if ((A.capa & ODPG_PKTOUT_IPV4_CHKSUM) && (A.cfg & ODPG_PKTOUT_IPV4_CHKSUM)) {
+		/* bytes 14..33, the checksum field (24..25) as zero */
+		uint32_t s = d2(f[3], W01, 0u);
+
+		s = d2(f[4], W11, s);
+		s = d2(f[5], W11, s);
+		s = d2(f[6], W01, s);
+		s = d2(f[7], W11, s);
+		s = d2(f[8], W10, s);
+		f[6] = (f[6] & 0xffff0000u) | (~d2fold(s) & 0xffffu);
+		w6 = true;
+		res |= ODPG_TX_OUT_IPV4;
+	}
+	const bool udp = l4p == 17u && (A.capa & ODPG_PKTOUT_UDP_CHKSUM) &&
+			 (A.cfg & ODPG_PKTOUT_UDP_CHKSUM);
+	const bool tcp = l4p == 6u && (A.capa & ODPG_PKTOUT_TCP_CHKSUM) &&
+			 (A.cfg & ODPG_PKTOUT_TCP_CHKSUM);
+
+	if (udp || tcp) {
+		/* addresses (26..33) + proto << 8 + (UDP: the length field again;
+		 * TCP: be16(30)) + bytes 34..63 with 40..41 as zero */
+		uint32_t s = udp ? 0x1100u : 0x0600u + 0x1e00u;
+
+		s = d2(f[6], W01, s);
+		s = d2(f[7], W11, s);
+		s = d2(f[8], W11, s);
+		s = d2(f[9], udp ? 0x00020001u : W11, s);
+		s = d2(f[10], W01, s);
+#pragma unroll
+		for (int k = 11; k < 16; ++k)
+			s = d2(f[k], W11, s);
+		uint32_t c = ~d2fold(s) & 0xffffu;
+
+		if (udp && c == 0u)
+			c = 0xffffu;
+		f[10] = (f[10] & 0xffff0000u) | c;
+		w10 = true;
+		res |= udp ? ODPG_TX_OUT_UDP : ODPG_TX_OUT_TCP;
+	}
+	if (w6)
+		g[6] = f[6];
+	if (w10)
+		g[10] = f[10];
+
+	/* get_dest_queue: ports (34..37), then the IPv4 addresses (26..33) */
+	uint32_t q;
+
+	if (A.hash_proto == 0u) {
+		q = A.index % A.num_qs;
+	} else {
+		const uint32_t hp = A.hash_proto;
+		/* plain frames are UDP or TCP: the parser's has_udp / has_tcp */
+		const bool ports = proto == 17u ? (hp & (ODPG_HASH_IPV4_UDP | ODPG_HASH_IPV6_UDP)) != 0u
+				   : (hp & (ODPG_HASH_IPV4_TCP | ODPG_HASH_IPV6_TCP)) != 0u;
+		uint32_t crc = 0u;
+
+		if (ports) {
+			const uint32_t pw = __builtin_amdgcn_alignbyte(f[9], f[8], 2);
+
+#pragma unroll
+			for (int j = 0; j < 4; ++j)
+				crc = crc_tab(tab, crc, (pw >> (8 * j)) & 0xffu);
+		}
+		if (hp & ODPG_HASH_IPV4) {
+			const uint32_t a0 = __builtin_amdgcn_alignbyte(f[7], f[6], 2);
+			const uint32_t a1 = __builtin_amdgcn_alignbyte(f[8], f[7], 2);
+
+#pragma unroll
+			for (int j = 0; j < 4; ++j)
+				crc = crc_tab(tab, crc, (a0 >> (8 * j)) & 0xffu);
+#pragma unroll
+			for (int j = 0; j < 4; ++j)
+				crc = crc_tab(tab, crc, (a1 >> (8 * j)) & 0xffu);
+		}
+		q = crc % A.num_qs;
+	}
+	return res | (q & ODPG_TX_OUT_QUEUE_MASK);
+}
+
 __global__ __launch_bounds__(TX_BLOCK) void odpg_tx_kernel(const TxArgs A)
 {
 	__shared__ uint32_t tab[256];
@@ -125,8 +234,32 @@ __global__ __launch_bounds__(TX_BLOCK) void odpg_tx_kernel(const TxArgs A)
 	}
 	__syncthreads();
 	const uint32_t i = blockIdx.x * TX_BLOCK + tid;
+	const bool live = i < A.num;
 
-	if (i >= A.num)
+	if (A.stride == 64u && !A.desc && !A.meta) {
+		/* register fast path: a wave whose frames are all plain
+		 * Eth/IPv4 (IHL 5)/UDP|TCP 64-byte frames (the parse gives l3 14,
+		 * l4 34, IPv4 + UDP|TCP) works on the 16 frame registers and
+		 * stores back only the dwords holding the checksum fields */
+		uint32_t f[16];
+		uint4 *src = (uint4 *)(A.frames + (size_t)(live ? i : A.num - 1u) * 64u);
+
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			const uint4 x = src[k];
+
+			f[4 * k + 0] = x.x;
+			f[4 * k + 1] = x.y;
+			f[4 * k + 2] = x.z;
+			f[4 * k + 3] = x.w;
+		}
+		if (__ballot(live && !plain_v4(f)) == 0ull) {
+			if (live)
+				A.out[i] = tx_fast64(A, tab, f, (uint32_t *)src);
+			return;
+		}
+	}
+	if (!live)
 		return;
 	uint8_t *g;
 	uint32_t len;
