@@ -230,12 +230,7 @@ def main():
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": None, "kernel_ms": round(kernel_ms, 5),
                     "bytes_per_pkt": round(bytes_per_pkt, 2), "pkts_per_launch": n}
-        tf = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
-        if os.path.exists(tf):
-            try:
-                roofline["traffic"] = json.load(open(tf)).get("bytes_per_launch")
-            except Exception:
-                pass
+        roofline["traffic"] = pmc_traffic(args.config)
         cpu = None
         if not args.no_cpu and world == 1:
             cpu = cpu_baseline(rules, frames, desc, n, stride, opt, args)
@@ -266,6 +261,17 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pmc_traffic(config):
+    """HBM bytes per launch of the timed kernel from the committed rocprofv3
+    PMC summary (profiles/pmc_traffic_<config>.json, tools/pmc.sh +
+    tools/pmc_summary.py: FETCH_SIZE x 2 on gfx950 + WRITE_SIZE), or None."""
+    tf = os.path.join(ROOT, "profiles", f"pmc_traffic_{config}.json")
+    try:
+        return json.load(open(tf)).get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
 
 
 def bench_tx(args, world, rank, local, dist):
@@ -356,7 +362,7 @@ def bench_tx(args, world, rank, local, dist):
                        "parallelism": f"dp{world} (packet shards, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel_ms": round(kernel_ms, 5),
+                         "traffic": pmc_traffic(args.config), "kernel_ms": round(kernel_ms, 5),
                          "bytes_per_pkt": bytes_per_pkt, "pkts_per_launch": n},
             "cpu_baseline": cpu,
         }
@@ -449,7 +455,7 @@ def bench_l3fwd(args, world, rank, local, dist):
                        "parallelism": f"dp{world} (packet shards, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel_ms": round(kernel_ms, 5),
+                         "traffic": pmc_traffic(args.config), "kernel_ms": round(kernel_ms, 5),
                          "bytes_per_pkt": bytes_per_pkt, "pkts_per_launch": n},
             "cpu_baseline": cpu,
         }

@@ -19,7 +19,7 @@ def summarize(d):
                     + glob.glob(f"{d}/pmc_*/run_counter_collection.csv")):
         per = collections.defaultdict(float)
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0]
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
             if "classify_kernel" in k:
                 k = "odpg_classify_kernel"
             per[(k, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
@@ -34,10 +34,13 @@ def summarize(d):
 
 if __name__ == "__main__":
     s = summarize(sys.argv[1])
-    # the timed kernel: the classify-family kernel with the most dispatches
-    # (the lean odpg_cls64_kernel for verdict-only C1/C2 launches, else
-    # odpg_classify_kernel; the one counter pass is the other)
-    kname = max((n for n in s if "cls64_kernel" in n or "classify_kernel" in n),
+    # the timed kernel: the odpg_* kernel with the most dispatches (the lean
+    # odpg_cls64_kernel for C1/C2/C4, odpg_classify_kernel for C3,
+    # odpg_l3fwd_kernel for C5, odpg_tx_kernel for tx), counter folds and
+    # runtime copies excluded
+    skip = ("rocclr", "stats_reduce", "stats_fold")
+    kname = max((n for n in s if "odpg_" in n and
+                 not any(x in n for x in skip)),
                 key=lambda n: s[n]["dispatches"], default="odpg_classify_kernel")
     k = s.get(kname, {})
     if "FETCH_SIZE" in k:
