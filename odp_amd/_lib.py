@@ -149,6 +149,12 @@ class odpg_tx_cfg_t(C.Structure):
 TX_META_FIELDS = [("l3_offset", "<u2"), ("l4_offset", "<u2"), ("flags", "<u4")]   # 8 B
 
 
+# ---- include/odpg_pcap.h ----------------------------------------------------
+class odpg_capture_t(C.Structure):
+    _fields_ = [("frames", C.c_void_p), ("desc", C.c_void_p), ("num", C.c_uint32),
+                ("bytes", C.c_uint64)]
+
+
 # numpy dtypes with the same layout
 def np_dtypes():
     import numpy as np
@@ -314,6 +320,9 @@ SIGNATURES = {
                                C.POINTER(_vp)]),
     "odpg_fwd_destroy": (None, [_vp]),
     "odpg_l3fwd": (_i32, [_vp, _vp, C.POINTER(odpg_fwd_batch_t), _vp]),
+    # include/odpg_pcap.h
+    "odpg_pcap_read": (_i32, [C.c_char_p, _u32, C.POINTER(odpg_capture_t)]),
+    "odpg_pcap_free": (None, [C.POINTER(odpg_capture_t)]),
     # include/odpg_tx.h
     "odpg_tx_prepare": (_i32, [_vp, C.POINTER(odpg_tx_batch_t), C.POINTER(odpg_tx_cfg_t), _vp]),
 }
