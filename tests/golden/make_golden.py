@@ -6,7 +6,9 @@ box). It copies DATA only: frame byte arrays from test/common/test_packet_*.h,
 the checksum known-answer vectors of test/validation/api/chksum/chksum.c, the
 frames of the pcap files the example tests replay, and the expectations those
 tests assert (encoded below with the file:line they come from). No reference
-source text is stored.
+source text is stored. It also copies the two capture files byte for byte
+(data files the reference's tests replay): example/classifier/udp64.pcap ->
+classifier_udp64.pcap and test/performance/udp64.pcap -> perf_udp64.pcap.
 
     python3 tests/golden/make_golden.py [/root/reference]
 """
@@ -159,6 +161,10 @@ def main():
         json.dump(data, f, indent=1, sort_keys=True)
     print(f"wrote {OUT}: {len(frames)} frames, "
           f"{sum(len(v) for v in pcaps.values())} pcap frames")
+    import shutil
+    for src, dst in (("example/classifier/udp64.pcap", "classifier_udp64.pcap"),
+                     ("test/performance/udp64.pcap", "perf_udp64.pcap")):
+        shutil.copyfile(os.path.join(REF, src), os.path.join(os.path.dirname(OUT), dst))
 
 
 if __name__ == "__main__":
