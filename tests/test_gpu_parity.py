@@ -261,7 +261,7 @@ def test_raised_limits_1024_pmr(gpu_ctx, fresh_cls):
     p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
     gen.build_c4_rules(fresh_cls, p)
     assert fresh_cls.pktio_start(p) == 0
-    n = 1 << 18
+    n = 1 << 20                      # the C4 bench batch per GPU
     fr = gen.c2_frames(n)
     g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, n, stride=64, opt=ALL_CHKSUM)
     assert_same(g, o, "C4 1024 PMR")
@@ -307,7 +307,7 @@ def test_simple_table_hash_groups(gpu_ctx, fresh_cls, layout):
     assert len(np.unique(g["out"] & 0xFFFF)) > 3
 
 
-@pytest.mark.parametrize("n", [1, 257, 1 << 15])
+@pytest.mark.parametrize("n", [1, 257, 1 << 15, 1 << 20])
 def test_c3_imix_dag(gpu_ctx, fresh_cls, n):
     """C3: IMIX 64/570/1518 B, IPv4/IPv6, UDP/TCP, checksum errors / zero /
     fragments, 256-PMR DAG with mixed term kinds, error CoS, descriptors."""

@@ -194,3 +194,17 @@ def test_gpu_example_pcap(gpu_ctx):
     assert (out == 1).all()
     o_out, o_fr = run_oracle([R("10.0.0.0", 24, 1)], buf.reshape(-1))
     np.testing.assert_array_equal(fr[:buf.nbytes], o_fr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [L.FWD_HASH, L.FWD_LPM])
+def test_gpu_c5_full_size(gpu_ctx, mode):
+    """The C5 bench launch itself: 10 M distinct flows in one batch."""
+    n = gen.C5_FLOWS
+    routes = gen.c5_routes()
+    fr = gen.c5_frames(n, routes)
+    fw = gpu.Forwarder(gpu_ctx, routes, mode=mode)
+    g_out, g_fr = fw.run(fr, 64, n)
+    o_out, o_fr = run_oracle(routes, fr, mode=mode)
+    np.testing.assert_array_equal(g_out, o_out)
+    np.testing.assert_array_equal(g_fr[:fr.nbytes], o_fr)
