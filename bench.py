@@ -502,7 +502,8 @@ def cpu_baseline(rules, frames, desc, n, stride, opt, args):
 
 
 def e2e(ctx, tbl, frames, desc, n, stride, opt):
-    """Host (pinned) buffers -> H2D -> classify -> D2H verdicts, double-buffered."""
+    """Host (pinned) buffers -> H2D -> classify -> D2H verdicts (odpg_classify_host:
+    three staging sets cycling over a copy stream and the compute stream)."""
     import ctypes as C
 
     import numpy as np
@@ -523,7 +524,7 @@ def e2e(ctx, tbl, frames, desc, n, stride, opt):
     b = L.odpg_batch_t(hp.value, dptr, stride, n, opt, L.LAYER_ALL, 1)
     r = L.odpg_result_t(ho.value, None, None, None)
     res = {}
-    for chunk in (1 << 16, 1 << 18):
+    for chunk in (1 << 16, 1 << 17, 1 << 18, 1 << 19):
         lib.odpg_classify_host(ctx.h, tbl.h, C.byref(b), C.byref(r), chunk)
         reps = 10
         t = time.perf_counter()

@@ -23,6 +23,21 @@ extern "C" uint32_t odpg_launch_grid(uint32_t num);
 
 #define NUM_EVENTS 16
 
+/* host-path staging (odpg_classify_host): NSTAGE buffer sets cycle
+ * through H2D (copy stream) -> classify + D2H (context stream); kept in the
+ * context and grown on demand, so repeated calls allocate nothing */
+#define NSTAGE 3
+
+struct Stage {
+	uint8_t *frames;
+	odpg_desc_t *desc;
+	odpg_out_t *out;
+	uint16_t *mark;
+	odpg_meta_t *meta;
+	odpg_desc_t *hdesc;    /* pinned host, chunk-relative descriptors */
+	hipEvent_t h2d_done, compute_done;
+};
+
 struct odpg_ctx_s {
 	int device;
 	hipStream_t stream;
@@ -30,11 +45,19 @@ struct odpg_ctx_s {
 	hipStream_t copy_stream;
 	void *ws;          /* per-workgroup counter partials */
 	uint64_t *sred;    /* stats_commit scratch (SRED_BYTES, kept zeroed) */
+	Stage stage[NSTAGE];
+	size_t stage_span;     /* bytes of frames per stage */
+	uint32_t stage_chunk;  /* packets per stage (out / desc / mark / meta) */
+	uint32_t stage_flags;  /* 1 desc, 2 mark, 4 meta allocated */
+	uint64_t *stage_stats;
+	uint32_t stage_nstats;
 	size_t ws_bytes;
 	hipEvent_t ev[NUM_EVENTS];
 	int kernel_mode;   /* 0 auto, 1 walk, 2 evaluate-all, 3 hash walk */
 	std::mutex lock;
 };
+
+static void free_stage(odpg_ctx_t *c);
 
 struct odpg_table_s {
 	dtable_hdr_t hdr;
@@ -117,6 +140,12 @@ int odpg_ctx_create(int device, void *stream, odpg_ctx_t **out)
 		delete c;
 		return -EIO;
 	}
+	for (int k = 0; k < NSTAGE; k++)
+		if (hipEventCreateWithFlags(&c->stage[k].h2d_done, hipEventDisableTiming) != hipSuccess ||
+		    hipEventCreateWithFlags(&c->stage[k].compute_done, hipEventDisableTiming) != hipSuccess) {
+			delete c;
+			return -EIO;
+		}
 	*out = c;
 	return 0;
 }
@@ -131,6 +160,12 @@ void odpg_ctx_destroy(odpg_ctx_t *c)
 	if (c->ws)
 		hipFree(c->ws);
 	hipFree(c->sred);
+	free_stage(c);
+	hipFree(c->stage_stats);
+	for (int k = 0; k < NSTAGE; k++) {
+		hipEventDestroy(c->stage[k].h2d_done);
+		hipEventDestroy(c->stage[k].compute_done);
+	}
 	for (int k = 0; k < NUM_EVENTS; k++)
 		hipEventDestroy(c->ev[k]);
 	hipStreamDestroy(c->copy_stream);
@@ -318,6 +353,75 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	return odpg_launch_classify(&a, s);
 }
 
+static void free_stage(odpg_ctx_t *c)
+{
+	for (int k = 0; k < NSTAGE; k++) {
+		Stage &B = c->stage[k];
+
+		hipFree(B.frames);
+		hipFree(B.desc);
+		hipFree(B.out);
+		hipFree(B.mark);
+		hipFree(B.meta);
+		if (B.hdesc)
+			hipHostFree(B.hdesc);
+		B.frames = nullptr;
+		B.desc = nullptr;
+		B.out = nullptr;
+		B.mark = nullptr;
+		B.meta = nullptr;
+		B.hdesc = nullptr;
+	}
+	c->stage_span = 0;
+	c->stage_chunk = 0;
+	c->stage_flags = 0;
+}
+
+/* grow-only staging for odpg_classify_host */
+static int ensure_stage(odpg_ctx_t *c, size_t span, uint32_t chunk, bool desc, bool mark,
+			bool meta, uint32_t nstats)
+{
+	const uint32_t want = (desc ? 1u : 0u) | (mark ? 2u : 0u) | (meta ? 4u : 0u);
+
+	if (c->stage_span < span + 16 || c->stage_chunk < chunk ||
+	    (c->stage_flags & want) != want) {
+		HIPCHK(hipStreamSynchronize(c->stream));
+		HIPCHK(hipStreamSynchronize(c->copy_stream));
+		const size_t nspan = span + 16 > c->stage_span ? span + 16 : c->stage_span;
+		const uint32_t nchunk = chunk > c->stage_chunk ? chunk : c->stage_chunk;
+		const uint32_t flags = want | c->stage_flags;
+
+		free_stage(c);
+		for (int k = 0; k < NSTAGE; k++) {
+			Stage &B = c->stage[k];
+
+			if (hipMalloc(&B.frames, nspan) != hipSuccess ||
+			    hipMalloc(&B.out, (size_t)nchunk * sizeof(odpg_out_t)) != hipSuccess ||
+			    ((flags & 1u) && (hipMalloc(&B.desc, (size_t)nchunk * sizeof(odpg_desc_t)) != hipSuccess ||
+					      hipHostMalloc(&B.hdesc, (size_t)nchunk * sizeof(odpg_desc_t),
+							    hipHostMallocDefault) != hipSuccess)) ||
+			    ((flags & 2u) && hipMalloc(&B.mark, (size_t)nchunk * 2u) != hipSuccess) ||
+			    ((flags & 4u) && hipMalloc(&B.meta, (size_t)nchunk * sizeof(odpg_meta_t)) != hipSuccess)) {
+				free_stage(c);
+				return -ENOMEM;
+			}
+		}
+		c->stage_span = nspan;
+		c->stage_chunk = nchunk;
+		c->stage_flags = flags;
+	}
+	if (nstats > c->stage_nstats) {
+		HIPCHK(hipStreamSynchronize(c->stream));
+		hipFree(c->stage_stats);
+		c->stage_stats = nullptr;
+		c->stage_nstats = 0;
+		if (hipMalloc(&c->stage_stats, nstats * 8u) != hipSuccess)
+			return -ENOMEM;
+		c->stage_nstats = nstats;
+	}
+	return 0;
+}
+
 static size_t ws_need(const odpg_table_t *t, uint32_t num, bool stats)
 {
 	if (!stats)
@@ -403,55 +507,24 @@ int odpg_classify_host(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t 
 			max_span = hi - lo;
 	}
 
-	struct Buf {
-		uint8_t *frames;
-		odpg_desc_t *desc;
-		odpg_out_t *out;
-		uint16_t *mark;
-		odpg_meta_t *meta;
-		hipEvent_t h2d_done, compute_done;
-		std::vector<odpg_desc_t> hdesc;
-	} buf[2];
-	uint64_t *dstats = nullptr;
 	uint32_t nstats = ODPG_STATS_WORDS(t->hdr.num_cos);
 	int err = 0;
 
-	memset(buf, 0, sizeof(buf[0]) * 0);
-	for (int k = 0; k < 2; k++) {
-		buf[k].frames = nullptr;
-		buf[k].desc = nullptr;
-		buf[k].out = nullptr;
-		buf[k].mark = nullptr;
-		buf[k].meta = nullptr;
-		if (hipMalloc(&buf[k].frames, max_span + 16) != hipSuccess ||
-		    hipMalloc(&buf[k].out, (size_t)chunk * sizeof(odpg_out_t)) != hipSuccess)
-			err = -ENOMEM;
-		if (b->desc && hipMalloc(&buf[k].desc, (size_t)chunk * sizeof(odpg_desc_t)) != hipSuccess)
-			err = -ENOMEM;
-		if (r->mark && hipMalloc(&buf[k].mark, (size_t)chunk * 2u) != hipSuccess)
-			err = -ENOMEM;
-		if (r->meta && hipMalloc(&buf[k].meta, (size_t)chunk * sizeof(odpg_meta_t)) != hipSuccess)
-			err = -ENOMEM;
-		hipEventCreateWithFlags(&buf[k].h2d_done, hipEventDisableTiming);
-		hipEventCreateWithFlags(&buf[k].compute_done, hipEventDisableTiming);
-		if (b->desc)
-			buf[k].hdesc.resize(chunk);
-	}
-	if (!err && r->stats) {
-		if (hipMalloc(&dstats, nstats * 8u) != hipSuccess ||
-		    hipMemsetAsync(dstats, 0, nstats * 8u, c->stream) != hipSuccess)
-			err = -ENOMEM;
-	}
-	if (!err)
-		err = ensure_ws(c, ws_need(t, chunk, r->stats != nullptr));
+	if ((err = ensure_stage(c, max_span, chunk, b->desc != nullptr, r->mark != nullptr,
+				r->meta != nullptr, r->stats ? nstats : 0u)))
+		return err;
+	if (r->stats && hipMemsetAsync(c->stage_stats, 0, nstats * 8u, c->stream) != hipSuccess)
+		return -EIO;
+	err = ensure_ws(c, ws_need(t, chunk, r->stats != nullptr));
 
 	for (uint32_t k = 0; k < nchunks && !err; k++) {
-		Buf &B = buf[k & 1];
+		Stage &B = c->stage[k % NSTAGE];
 		uint32_t first = k * chunk, n = b->num - first < chunk ? b->num - first : chunk;
 		size_t lo = span_lo[k], bytes = span_hi[k] - span_lo[k];
 
-		/* buffer reuse: wait until the chunk that used it has finished */
-		if (k >= 2 && hipStreamWaitEvent(c->copy_stream, B.compute_done, 0) != hipSuccess) {
+		/* buffer reuse: the copy stream waits until the chunk that used this
+		 * stage has been classified and its results copied back */
+		if (k >= NSTAGE && hipStreamWaitEvent(c->copy_stream, B.compute_done, 0) != hipSuccess) {
 			err = -EIO;
 			break;
 		}
@@ -461,13 +534,15 @@ int odpg_classify_host(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t 
 			break;
 		}
 		if (b->desc) {
-			if (k >= 2)
+			/* chunk-relative descriptors, staged through a pinned buffer
+			 * the host rewrites once the stage's previous chunk is done */
+			if (k >= NSTAGE)
 				hipEventSynchronize(B.compute_done);
 			for (uint32_t j = 0; j < n; j++) {
 				B.hdesc[j].offset = (uint32_t)(b->desc[first + j].offset - lo);
 				B.hdesc[j].len = b->desc[first + j].len;
 			}
-			if (hipMemcpyAsync(B.desc, B.hdesc.data(), (size_t)n * sizeof(odpg_desc_t),
+			if (hipMemcpyAsync(B.desc, B.hdesc, (size_t)n * sizeof(odpg_desc_t),
 					   hipMemcpyHostToDevice, c->copy_stream) != hipSuccess) {
 				err = -EIO;
 				break;
@@ -485,7 +560,7 @@ int odpg_classify_host(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t 
 		cr.out = B.out;
 		cr.mark = r->mark ? B.mark : nullptr;
 		cr.meta = r->meta ? B.meta : nullptr;
-		cr.stats = dstats;
+		cr.stats = r->stats ? c->stage_stats : nullptr;
 		if (classify_on(c, c->stream, t, &cb, &cr, c->ws)) {
 			err = -EIO;
 			break;
@@ -503,7 +578,7 @@ int odpg_classify_host(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t 
 	if (!err && r->stats) {
 		std::vector<uint64_t> hs(nstats);
 
-		if (hipMemcpyAsync(hs.data(), dstats, nstats * 8u, hipMemcpyDeviceToHost,
+		if (hipMemcpyAsync(hs.data(), c->stage_stats, nstats * 8u, hipMemcpyDeviceToHost,
 				   c->stream) != hipSuccess ||
 		    hipStreamSynchronize(c->stream) != hipSuccess)
 			err = -EIO;
@@ -514,17 +589,6 @@ int odpg_classify_host(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t 
 	if (hipStreamSynchronize(c->stream) != hipSuccess ||
 	    hipStreamSynchronize(c->copy_stream) != hipSuccess)
 		err = err ? err : -EIO;
-	for (int k = 0; k < 2; k++) {
-		hipFree(buf[k].frames);
-		hipFree(buf[k].desc);
-		hipFree(buf[k].out);
-		hipFree(buf[k].mark);
-		hipFree(buf[k].meta);
-		hipEventDestroy(buf[k].h2d_done);
-		hipEventDestroy(buf[k].compute_done);
-	}
-	if (dstats)
-		hipFree(dstats);
 	return err;
 }
 
