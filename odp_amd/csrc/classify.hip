@@ -342,7 +342,8 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 	const uint4 *__restrict__ ments_g, uint32_t num_ment, const uint2 *__restrict__ pinfo2_g,
 	odpg_out_t *__restrict__ out, uint16_t *__restrict__ mark_out,
 	odpg_meta_t *__restrict__ meta_out, uint64_t *__restrict__ pk_partial,
-	uint32_t *__restrict__ cos_partial, uint64_t *__restrict__ sred)
+	uint32_t *__restrict__ cos_partial, uint64_t *__restrict__ sred,
+	const uint2 *__restrict__ xcos_g, const uint32_t *__restrict__ xlist_g, uint32_t num_xlist)
 {
 	constexpr uint32_t RW = W / 4 + 1;       /* odd dword row stride */
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -361,6 +362,11 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 	uint2 *cinfo = hents_l + (hent_in_lds ? num_hent : 0u);
 	uint32_t *pinfo = (uint32_t *)(cinfo + num_cos);
 	uint2 *pinfo2 = (uint2 *)(pinfo + ((num_pmr + 1u) & ~1u));
+	/* hybrid hash walk (TBL_XWALK): per-CoS complex-rule lists in LDS, in
+	 * the place MODE 1 keeps pinfo2 */
+	const bool use_x = MODE == 3 && (tbl_flags & TBL_XWALK);
+	uint2 *xcos_l = pinfo2;
+	uint32_t *xlist_l = (uint32_t *)(xcos_l + (use_x ? num_cos : 0u));
 	__shared__ unsigned long long blk_pk[4];
 
 	const uint32_t tid = threadIdx.x;
@@ -418,6 +424,12 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 	if (MODE == 1)
 		for (uint32_t k = tid; k < num_pmr; k += BLOCK)
 			pinfo2[k] = pinfo2_g[k];
+	if (use_x) {
+		for (uint32_t k = tid; k < num_cos; k += BLOCK)
+			xcos_l[k] = xcos_g[k];
+		for (uint32_t k = tid; k < num_xlist; k += BLOCK)
+			xlist_l[k] = xlist_g[k];
+	}
 	__syncthreads();
 	/* default CoS entry: read once, outside the tile loop */
 	const bool def_valid = default_cos >= 0 && coses[default_cos].valid;
@@ -643,9 +655,21 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 			return 0xffffffffu;
 		};
 		while (__ballot(active)) {
-			if (active) {
-				uint32_t best = 0xffffffffu;
+			uint32_t best = 0xffffffffu;
+			uint32_t xs = 0u, xn = 0u;
 
+			if (active) {
+				uint32_t gm = 0xffffffffu;
+
+				if (use_x) {
+					/* complex rules of this CoS, and the walk
+					 * groups holding one of its single-word rules */
+					const uint2 xe = xcos_l[cos];
+
+					xs = xe.x & 0xffffu;
+					xn = xe.x >> 16;
+					gm = xe.y;
+				}
 				for (uint32_t gi = 0; gi < num_hgroups; ++gi) {
 					const uint4 g0 = *(const uint4 *)(hgroups + gi);
 					const uint2 g1 = *(const uint2 *)((const uint32_t *)(hgroups + gi) + 4);
@@ -655,7 +679,7 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 					const uint32_t lg = __builtin_amdgcn_readfirstlane(g0.w);
 					const uint32_t goff = __builtin_amdgcn_readfirstlane(g1.x);
 
-					if ((b.inf_lo & greq) == greq) {
+					if (((gm >> gi) & 1u) && (b.inf_lo & greq) == greq) {
 						const uint32_t kv = key(gslot) & gmask;
 						const uint32_t h = walk_hash(kv, cos, lg);
 						const uint32_t r = hent_in_lds
@@ -665,6 +689,34 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 						best = r < best ? r : best;
 					}
 				}
+			}
+			if (use_x) {
+				/* the CoS's complex rules below the best group hit, in
+				 * rule order, one PMR at a time across the wave
+				 * (uniform index: scalar term loads, as MODE 0) */
+				uint32_t xk = 0u;
+				bool xp = active && xn != 0u && xlist_l[xs] < best;
+
+				while (__ballot(xp)) {
+					if (xp) {
+						const uint32_t cand = xlist_l[xs + xk];
+						const uint32_t u = __builtin_amdgcn_readfirstlane(cand);
+
+						if (cand == u) {
+							const dpmr_t pm = pmrs[u];
+
+							if (pmr_match(terms, pm.term_start, pm.nterms, v, b)) {
+								best = u;
+								xp = false;
+							} else {
+								++xk;
+								xp = xk < xn && xlist_l[xs + xk] < best;
+							}
+						}
+					}
+				}
+			}
+			if (active) {
 				if (best == 0xffffffffu) {
 					active = false;
 				} else {
@@ -1111,6 +1163,8 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 		lds += (size_t)a.num_pmr * 8u + 4u;
 	if (MODE != 0)
 		lds += (size_t)a.num_cos * 8u + (size_t)a.num_pmr * 4u;
+	if (MODE == 3 && (a.tbl_flags & TBL_XWALK))
+		lds += (size_t)a.num_cos * 8u + (size_t)a.num_xlist * 4u + 8u;
 	/* persistent grid: exactly the workgroups that are resident at once
 	 * (occupancy x CUs), each looping over tiles */
 	static size_t occ_lds = (size_t)-1;
@@ -1137,7 +1191,8 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 			   a.runs, a.num_runs, a.hgroups, a.num_hgroups, a.hents, a.num_hent,
 			   (const uint2 *)a.cinfo, a.pinfo, a.mgroups, a.num_mgroups,
 			   (const uint4 *)a.ments, a.num_ment, (const uint2 *)a.pinfo2, a.out, a.mark, a.meta, a.pk_partial,
-			   a.cos_partial, a.pk_atomic ? a.sred : nullptr);
+			   a.cos_partial, a.pk_atomic ? a.sred : nullptr, (const uint2 *)a.xcos, a.xlist,
+			   a.num_xlist);
 	return hipGetLastError();
 }
 
@@ -1258,12 +1313,13 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 	const bool simple = (a->tbl_flags & TBL_SIMPLE) != 0;
 
 	if (mode == 0)
-		mode = simple && (a->tbl_flags & TBL_HASHWALK) && a->num_wgroups <= WALK_MAX_GROUPS ? 3
+		mode = !simple && (a->tbl_flags & TBL_XWALK) ? 3
+		       : simple && (a->tbl_flags & TBL_HASHWALK) && a->num_wgroups <= WALK_MAX_GROUPS ? 3
 		       : simple && a->num_pmr <= EVAL_ALL_MAX_PMR ? 2
 		       : simple && a->num_wgroups <= WALK_MAX_GROUPS ? 3 : 1;
 	if (mode == 2 && a->num_pmr > EVAL_ALL_MAX_PMR)
 		mode = 1;
-	if (mode == 3 && !simple)
+	if (mode == 3 && !simple && !(a->tbl_flags & TBL_XWALK))
 		mode = 1;
 	if (mode == 3) {
 		/* the hash walk reads its CoS-keyed groups through the

@@ -231,6 +231,19 @@ dslot_t slotify(const dterm_t &t)
 	}
 	s.slot = (uint8_t)(first + w0);
 	s.nw = (uint8_t)(w1 - w0 + 1);
+	/* words with zero mask and value compare equal for every packet: drop
+	 * them from both ends (a SIP6 /124 suffix becomes one word) */
+	while (s.nw > 1 && s.mask[s.nw - 1] == 0 && s.value[s.nw - 1] == 0)
+		s.nw--;
+	while (s.nw > 1 && s.mask[0] == 0 && s.value[0] == 0) {
+		for (uint32_t w = 0; w + 1 < s.nw; w++) {
+			s.mask[w] = s.mask[w + 1];
+			s.value[w] = s.value[w + 1];
+		}
+		s.mask[s.nw - 1] = s.value[s.nw - 1] = 0;
+		s.nw--;
+		s.slot++;
+	}
 	return s;
 }
 
@@ -485,6 +498,66 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	for (size_t k = 0; k < terms.size(); k++)
 		if (slots[k].slot == SLOT_NONE && terms[k].kind == DK_CMP)
 			generic = true;
+	/* every PMR's single-word form for the walk groups, or "complex" (the
+	 * hybrid hash walk evaluates those rules with the generic compare) */
+	std::vector<dsimple_t> wsimple;
+	std::vector<uint32_t> wsimple_slot;
+	std::vector<bool> complex_pmr(pmr.size(), false);
+
+	for (size_t pi = 0; pi < pmr.size(); pi++) {
+		const dpmr_t &p = pmr[pi];
+		dsimple_t e;
+
+		memset(&e, 0, sizeof(e));
+		e.idx = (uint32_t)pi;
+		if (p.nterms == 0) {
+			wsimple.push_back(e);
+			wsimple_slot.push_back(0);
+			continue;
+		}
+		const dterm_t &t = terms[p.term_start];
+		const dslot_t &sl = slots[p.term_start];
+
+		if (p.nterms == 2 && (t.tflags & DT_ALT_NEXT)) {
+			/* IPv4 / IPv6 (or AH / ESP) alternative pair: the gates
+			 * are exclusive parse results, so "first gate ? cmp1 :
+			 * gate2 && cmp2" is the disjunction of two gated compares
+			 * and the PMR goes into both of their groups */
+			const dterm_t &t2 = terms[p.term_start + 1];
+			const dslot_t &s2 = slots[p.term_start + 1];
+			const bool excl = ((t.req & RQ(IFL_IPV4)) && (t2.req & RQ(IFL_IPV6))) ||
+					  ((t.req & RQ(IFL_IPSEC_AH)) && (t2.req & RQ(IFL_IPSEC_ESP)));
+
+			if (excl && sl.slot != SLOT_NONE && sl.nw == 1 && s2.slot != SLOT_NONE &&
+			    s2.nw == 1 && !(t2.tflags & DT_ALT_NEXT)) {
+				e.req = t.req;
+				e.mask = sl.mask[0];
+				e.value = sl.value[0];
+				wsimple.push_back(e);
+				wsimple_slot.push_back(sl.slot);
+				e.req = t2.req;
+				e.mask = s2.mask[0];
+				e.value = s2.value[0];
+				wsimple.push_back(e);
+				wsimple_slot.push_back(s2.slot);
+				continue;
+			}
+		}
+		if (p.nterms != 1 || sl.slot == SLOT_NONE || sl.nw != 1 || (t.tflags & DT_ALT_NEXT)) {
+			complex_pmr[pi] = true;
+			continue;
+		}
+		e.req = t.req;
+		e.mask = sl.mask[0];
+		e.value = sl.value[0];
+		wsimple.push_back(e);
+		wsimple_slot.push_back(sl.slot);
+	}
+	size_t num_complex = 0;
+
+	for (size_t pi = 0; pi < pmr.size(); pi++)
+		num_complex += complex_pmr[pi] ? 1 : 0;
+
 	for (size_t pi = 0; pi < pmr.size(); pi++) {
 		const dpmr_t &p = pmr[pi];
 		dsimple_t e;
@@ -515,24 +588,28 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	std::vector<dhgroup_t> wgroups;
 	std::vector<dwent_t> wents;
 
-	if (is_simple) {
-		/* CoS-keyed walk groups over every PMR (odpg_internal.h) */
-		std::vector<uint32_t> src_cos(pmr.size(), 0);
+	/* hybrid hash walk (TBL_XWALK): walk groups over the single-word PMRs
+	 * of a table that also holds a few complex ones */
+	const bool xwalk = !is_simple && num_complex * 2 <= pmr.size() && pmr.size() < 65536 &&
+			   ncos < 65536;
+	std::vector<uint32_t> src_cos(pmr.size(), 0);
 
-		for (uint32_t c = 0; c < ncos; c++)
-			for (uint32_t k = 0; k < cos[c].nrule; k++)
-				src_cos[cos[c].rule_start + k] = c;
+	for (uint32_t c = 0; c < ncos; c++)
+		for (uint32_t k = 0; k < cos[c].nrule; k++)
+			src_cos[cos[c].rule_start + k] = c;
+	if (is_simple || xwalk) {
+		/* CoS-keyed walk groups over every single-word PMR (odpg_internal.h) */
 		std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::vector<size_t>> by_key;
 
-		for (size_t k = 0; k < simple.size(); k++)
-			by_key[std::make_tuple(simple_slot[k], simple[k].req, simple[k].mask)].push_back(k);
+		for (size_t k = 0; k < wsimple.size(); k++)
+			by_key[std::make_tuple(wsimple_slot[k], wsimple[k].req, wsimple[k].mask)].push_back(k);
 		for (auto &kv : by_key) {
 			/* lowest PMR index per (cos, value); values with bits outside
 			 * the mask never match and are left out */
 			std::map<std::pair<uint32_t, uint32_t>, uint32_t> first;
 
 			for (size_t k : kv.second) {
-				const dsimple_t &e = simple[k];
+				const dsimple_t &e = wsimple[k];
 
 				if (e.value & ~e.mask)
 					continue;
@@ -575,7 +652,7 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	std::vector<dmgroup_t> cgroups;
 	std::vector<dwent_t> cents;
 
-	for (size_t gi = 0; gi < wgroups.size() && wgroups.size() <= 4; gi++) {
+	for (size_t gi = 0; gi < wgroups.size() && wgroups.size() <= 4 && is_simple; gi++) {
 		const dhgroup_t &wg = wgroups[gi];
 		std::vector<std::pair<uint32_t, uint32_t>> keys;   /* (value, cos_pmr) */
 
@@ -594,6 +671,36 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			break;
 		}
 		cgroups.push_back(g);
+	}
+
+	/* TBL_XWALK: per CoS {xlist start | count << 16, walk-group mask} and
+	 * the CoS's complex PMR indices in rule order */
+	std::vector<uint32_t> xcos, xlist;
+
+	if (xwalk && wgroups.size() <= XWALK_MAX_GROUPS) {
+		std::vector<uint32_t> gm(ncos, 0u);
+
+		for (size_t g = 0; g < wgroups.size(); g++)
+			for (uint32_t e = 0; e < (1u << wgroups[g].log2sz); e++) {
+				const dwent_t &w = wents[wgroups[g].off + e];
+
+				if (w.cos_pmr != HENT_EMPTY)
+					gm[w.cos_pmr & 0xffffu] |= 1u << g;
+			}
+		xcos.resize(2 * ncos);
+		for (uint32_t c = 0; c < ncos; c++) {
+			uint32_t st = (uint32_t)xlist.size();
+
+			for (uint32_t k = 0; k < cos[c].nrule; k++)
+				if (complex_pmr[cos[c].rule_start + k])
+					xlist.push_back(cos[c].rule_start + k);
+			xcos[2 * c] = st | (((uint32_t)xlist.size() - st) << 16);
+			xcos[2 * c + 1] = gm[c];
+		}
+		if (xlist.size() > 65535) {
+			xcos.clear();
+			xlist.clear();
+		}
 	}
 
 	std::vector<dmgroup_t> mgroups;
@@ -748,8 +855,14 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.num_runs = is_simple ? (uint32_t)runs.size() : 0;
 	h.num_hgroups = is_simple ? (uint32_t)hgroups.size() : 0;
 	h.num_hent = is_simple ? (uint32_t)hents.size() : 0;
-	h.num_wgroups = is_simple ? (uint32_t)wgroups.size() : 0;
-	h.num_went = is_simple ? (uint32_t)wents.size() : 0;
+	const bool keep_w = is_simple || !xcos.empty();
+
+	h.num_wgroups = keep_w ? (uint32_t)wgroups.size() : 0;
+	h.num_went = keep_w ? (uint32_t)wents.size() : 0;
+	if (!xcos.empty()) {
+		h.flags |= TBL_XWALK;
+		h.num_xlist = (uint32_t)xlist.size();
+	}
 	const uint32_t lean_req = (1u << IFL_L2) | (1u << IFL_L3) | (1u << IFL_L4) |
 				  (1u << IFL_ETH) | (1u << IFL_VLAN) | (1u << IFL_IPV4) |
 				  (1u << IFL_IPV6) | (1u << IFL_UDP) | (1u << IFL_TCP) |
@@ -861,7 +974,9 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.cgroup_off = align(h.pinfo2_off + (uint32_t)(pinfo2.size() * 4u));
 	h.cent_off = align(h.cgroup_off + h.num_cgroups * (uint32_t)sizeof(dmgroup_t));
 	h.pinfo3_off = align(h.cent_off + h.num_cent * (uint32_t)sizeof(dwent_t));
-	h.blob_bytes = align(h.pinfo3_off + (uint32_t)(pinfo3.size() * 4u));
+	h.xcos_off = align(h.pinfo3_off + (uint32_t)(pinfo3.size() * 4u));
+	h.xlist_off = align(h.xcos_off + (uint32_t)(xcos.size() * 4u));
+	h.blob_bytes = align(h.xlist_off + (uint32_t)(xlist.size() * 4u));
 	if (h.blob_bytes == 0)
 		h.blob_bytes = 64;
 	blob.assign(h.blob_bytes, 0);
@@ -903,6 +1018,10 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		memcpy(blob.data() + h.cent_off, cents.data(), cents.size() * sizeof(dwent_t));
 		memcpy(blob.data() + h.pinfo3_off, pinfo3.data(), pinfo3.size() * 4u);
 	}
+	if (!xcos.empty())
+		memcpy(blob.data() + h.xcos_off, xcos.data(), xcos.size() * 4u);
+	if (!xlist.empty())
+		memcpy(blob.data() + h.xlist_off, xlist.data(), xlist.size() * 4u);
 	*hdr_out = h;
 	return 0;
 }

@@ -95,6 +95,8 @@ typedef struct dcos_s {
 			      * the lean kernel's register parse computes
 			      * (L2, L3, L4, ETH, VLAN, IPV4, IPV6, UDP, TCP,
 			      * IPSEC_AH, IPSEC_ESP) */
+#define TBL_XWALK      0x200 /* hybrid hash walk: walk groups over the single-word
+                              * PMRs, xcos / xlist name the complex ones per CoS */
 #define TBL_LEAN64HW   0x100 /* TBL_HASHWALK with <= 4 walk groups whose gates
 			      * the lean kernel's register parse computes: the
 			      * lean kernel's walk-group form */
@@ -172,6 +174,7 @@ typedef struct dwent_s {
 } dwent_t;
 
 #define WALK_MAX_GROUPS 8    /* more groups: evaluate-all is cheaper */
+#define XWALK_MAX_GROUPS 32  /* hybrid walk: per-CoS group mask is one word */
 
 /* Mask groups (TBL_SIMPLE tables of <= 64 PMRs, the u64 hit-map kernel):
  * every (slot, req, mask) group is a two-choice cuckoo table keyed by the
@@ -268,6 +271,10 @@ typedef struct dtable_hdr_s {
 	uint32_t num_cent;
 	uint32_t pinfo3_off; /* uint2[num_pmr] (TBL_LEAN64HW) */
 	uint32_t def_cgmask; /* cuckoo groups holding a rule of the default CoS */
+	uint32_t xcos_off;   /* uint2[num_cos] (TBL_XWALK): {xlist start | count << 16,
+	                      *  walk groups holding a single-word rule of the CoS} */
+	uint32_t xlist_off;  /* uint32[num_xlist]: complex PMR indices, per CoS in rule order */
+	uint32_t num_xlist;
 	uint32_t blob_bytes;
 } dtable_hdr_t;
 
@@ -314,6 +321,9 @@ typedef struct odpg_launch_args {
 	uint32_t num_cent;
 	const uint2_t *pinfo3;
 	uint32_t def_cgmask;
+	const uint2_t *xcos;        /* TBL_XWALK */
+	const uint32_t *xlist;
+	uint32_t num_xlist;
 	/* lean 64-byte kernel (classify64.hip): CoS start state, from the host
 	 * copy of the table */
 	uint32_t l64_err_cos, l64_err_act, l64_def_cos, l64_def_act, l64_def_ci, l64_def_rules;

@@ -321,6 +321,9 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.num_cent = h.num_cent;
 	a.pinfo3 = (const uint2_t *)((const uint8_t *)t->dblob + h.pinfo3_off);
 	a.def_cgmask = h.def_cgmask;
+	a.xcos = (const uint2_t *)((const uint8_t *)t->dblob + h.xcos_off);
+	a.xlist = (const uint32_t *)((const uint8_t *)t->dblob + h.xlist_off);
+	a.num_xlist = h.num_xlist;
 	{
 		/* start state of cls_select_cos (odp_classification.c:1669-1701)
 		 * for the lean kernel, as classify.hip derives it per packet */
