@@ -212,9 +212,11 @@ void odpg_ctx_destroy(odpg_ctx_t *ctx);
 void *odpg_ctx_stream(odpg_ctx_t *ctx);
 /* Kernel strategy: 0 = auto (hash walk for tables of single-word compares
  * with at most 8 distinct (field, mask) groups; evaluate-all for other such
- * tables up to 1024 PMRs; the wave-cooperative walk otherwise), 1 = walk,
- * 2 = evaluate-all, 3 = hash walk (single-word tables; walk otherwise). All
- * strategies produce identical results; this only selects the code path. */
+ * tables up to 1024 PMRs; the hybrid hash walk for tables where at most half
+ * the PMRs need the generic compare; the wave-cooperative walk otherwise),
+ * 1 = walk, 2 = evaluate-all, 3 = hash walk (single-word and hybrid tables;
+ * walk otherwise). All strategies produce identical results; this only
+ * selects the code path. */
 int  odpg_ctx_set_kernel_mode(odpg_ctx_t *ctx, int mode);
 /* Which kernel the last odpg_classify launch in this process used (a
  * diagnostic for tests and benches): 0 the general kernel, 1 the lean
