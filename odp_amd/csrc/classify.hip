@@ -343,7 +343,8 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 	odpg_out_t *__restrict__ out, uint16_t *__restrict__ mark_out,
 	odpg_meta_t *__restrict__ meta_out, uint64_t *__restrict__ pk_partial,
 	uint32_t *__restrict__ cos_partial, uint64_t *__restrict__ sred,
-	const uint2 *__restrict__ xcos_g, const uint32_t *__restrict__ xlist_g, uint32_t num_xlist)
+	const uint2 *__restrict__ xcos_g, const uint32_t *__restrict__ xlist_g, uint32_t num_xent,
+	uint32_t num_xwords)
 {
 	constexpr uint32_t RW = W / 4 + 1;       /* odd dword row stride */
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -366,7 +367,9 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 	 * the place MODE 1 keeps pinfo2 */
 	const bool use_x = MODE == 3 && (tbl_flags & TBL_XWALK);
 	uint2 *xcos_l = pinfo2;
-	uint32_t *xlist_l = (uint32_t *)(xcos_l + (use_x ? num_cos : 0u));
+	uint2 *xlist_l = (uint2 *)(xcos_l + (use_x ? ((num_cos + 1u) & ~1u) : 0u));
+	/* xterm records: read as uint2 pairs (the LDS carve-up is 8-byte aligned) */
+	const uint2 *xterm_l = xlist_l + ((num_xent + 1u) & ~1u);
 	__shared__ unsigned long long blk_pk[4];
 
 	const uint32_t tid = threadIdx.x;
@@ -427,8 +430,8 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 	if (use_x) {
 		for (uint32_t k = tid; k < num_cos; k += BLOCK)
 			xcos_l[k] = xcos_g[k];
-		for (uint32_t k = tid; k < num_xlist; k += BLOCK)
-			xlist_l[k] = xlist_g[k];
+		for (uint32_t k = tid; k < num_xwords; k += BLOCK)
+			((uint32_t *)xlist_l)[k] = xlist_g[k];
 	}
 	__syncthreads();
 	/* default CoS entry: read once, outside the tile loop */
@@ -654,11 +657,57 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 			}
 			return 0xffffffffu;
 		};
+		/* hybrid walk with at most XWALK_KEYS groups: the masked key
+		 * words do not depend on the CoS, so each group's key is read
+		 * once per packet (gok: groups whose gate holds), not per level */
+		constexpr uint32_t XK = XWALK_KEYS;
+		const bool xkeys = use_x && num_hgroups <= XK;
+		uint32_t kvx[XK];
+		uint32_t gok = 0u;
+
+		if (xkeys) {
+#pragma unroll
+			for (uint32_t gi = 0; gi < XK; ++gi) {
+				kvx[gi] = 0u;
+				if (gi < num_hgroups) {
+					const uint4 g0 = *(const uint4 *)(hgroups + gi);
+					const uint32_t gslot = __builtin_amdgcn_readfirstlane(g0.x);
+					const uint32_t greq = __builtin_amdgcn_readfirstlane(g0.y);
+					const uint32_t gmask = __builtin_amdgcn_readfirstlane(g0.z);
+
+					if (active && (b.inf_lo & greq) == greq) {
+						kvx[gi] = key(gslot) & gmask;
+						gok |= 1u << gi;
+					}
+				}
+			}
+		}
 		while (__ballot(active)) {
 			uint32_t best = 0xffffffffu;
 			uint32_t xs = 0u, xn = 0u;
 
-			if (active) {
+			if (active && xkeys) {
+				const uint2 xe = xcos_l[cos];
+				const uint32_t gm = xe.y & gok;
+
+				xs = xe.x & 0xffffu;
+				xn = xe.x >> 16;
+#pragma unroll
+				for (uint32_t gi = 0; gi < XK; ++gi) {
+					if (gi < num_hgroups && ((gm >> gi) & 1u)) {
+						const uint4 g0 = *(const uint4 *)(hgroups + gi);
+						const uint2 g1 = *(const uint2 *)((const uint32_t *)(hgroups + gi) + 4);
+						const uint32_t lg = __builtin_amdgcn_readfirstlane(g0.w);
+						const uint32_t goff = __builtin_amdgcn_readfirstlane(g1.x);
+						const uint32_t h = walk_hash(kvx[gi], cos, lg);
+						const uint32_t r = hent_in_lds
+							? probe(hents_l, goff, h, (1u << lg) - 1u, kvx[gi], cos)
+							: probe((const uint2 *)hents_g, goff, h, (1u << lg) - 1u, kvx[gi], cos);
+
+						best = r < best ? r : best;
+					}
+				}
+			} else if (active) {
 				uint32_t gm = 0xffffffffu;
 
 				if (use_x) {
@@ -692,25 +741,53 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_
 			}
 			if (use_x) {
 				/* the CoS's complex rules below the best group hit, in
-				 * rule order, one PMR at a time across the wave
-				 * (uniform index: scalar term loads, as MODE 0) */
+				 * rule order. Rules of single-word slot compares are
+				 * evaluated per lane from their xterm records; the others
+				 * one PMR at a time across the wave (uniform index:
+				 * scalar term loads, as MODE 0) */
 				uint32_t xk = 0u;
-				bool xp = active && xn != 0u && xlist_l[xs] < best;
+				bool xp = active && xn != 0u && xlist_l[xs].x < best;
 
 				while (__ballot(xp)) {
 					if (xp) {
-						const uint32_t cand = xlist_l[xs + xk];
-						const uint32_t u = __builtin_amdgcn_readfirstlane(cand);
+						const uint2 xe = xlist_l[xs + xk];
+						const uint32_t nt = xe.y >> 24;
+						bool hit = false, done = false;
 
-						if (cand == u) {
-							const dpmr_t pm = pmrs[u];
+						if (nt) {
+							const uint2 *tr = xterm_l + 2u * (xe.y & 0xffffffu);
 
-							if (pmr_match(terms, pm.term_start, pm.nterms, v, b)) {
-								best = u;
+							hit = true;
+							for (uint32_t t = 0; t < nt && hit; ++t) {
+								const uint2 r0 = tr[2u * t], r1 = tr[2u * t + 1u];
+								const uint4 r = make_uint4(r0.x, r0.y, r1.x, r1.y);
+								const uint32_t sl = r.w & 0xffu;
+
+								/* gate, then the CUSTOM_L3 length guard,
+								 * before the slot is read */
+								hit = (b.inf_lo & r.x) == r.x &&
+								      (!(r.w >> 31) ||
+								       b.len > b.l3 + ((r.w >> 8) & 0xffffu)) &&
+								      (key(sl) & r.y) == r.z;
+							}
+							done = true;
+						} else {
+							const uint32_t u = __builtin_amdgcn_readfirstlane(xe.x);
+
+							if (xe.x == u) {
+								const dpmr_t pm = pmrs[u];
+
+								hit = pmr_match(terms, pm.term_start, pm.nterms, v, b);
+								done = true;
+							}
+						}
+						if (done) {
+							if (hit) {
+								best = xe.x;
 								xp = false;
 							} else {
 								++xk;
-								xp = xk < xn && xlist_l[xs + xk] < best;
+								xp = xk < xn && xlist_l[xs + xk].x < best;
 							}
 						}
 					}
@@ -1164,7 +1241,7 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 	if (MODE != 0)
 		lds += (size_t)a.num_cos * 8u + (size_t)a.num_pmr * 4u;
 	if (MODE == 3 && (a.tbl_flags & TBL_XWALK))
-		lds += (size_t)a.num_cos * 8u + (size_t)a.num_xlist * 4u + 8u;
+		lds += (size_t)((a.num_cos + 1u) & ~1u) * 8u + (size_t)a.num_xwords * 4u + 16u;
 	/* persistent grid: exactly the workgroups that are resident at once
 	 * (occupancy x CUs), each looping over tiles */
 	static size_t occ_lds = (size_t)-1;
@@ -1192,7 +1269,7 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 			   (const uint2 *)a.cinfo, a.pinfo, a.mgroups, a.num_mgroups,
 			   (const uint4 *)a.ments, a.num_ment, (const uint2 *)a.pinfo2, a.out, a.mark, a.meta, a.pk_partial,
 			   a.cos_partial, a.pk_atomic ? a.sred : nullptr, (const uint2 *)a.xcos, a.xlist,
-			   a.num_xlist);
+			   a.num_xlist, a.num_xwords);
 	return hipGetLastError();
 }
 

@@ -673,9 +673,40 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		cgroups.push_back(g);
 	}
 
-	/* TBL_XWALK: per CoS {xlist start | count << 16, walk-group mask} and
-	 * the CoS's complex PMR indices in rule order */
-	std::vector<uint32_t> xcos, xlist;
+	/* TBL_XWALK: per CoS {xlist start | count << 16, walk-group mask}; per
+	 * CoS its complex PMRs in rule order as {pmr, xterm start | n << 24},
+	 * then the xterm records {req, mask, value, slot | guard end << 8 |
+	 * guarded << 31} of the complex PMRs whose terms are all single-word
+	 * slot compares (n > 0; n == 0: the generic compare) */
+	std::vector<uint32_t> xcos, xlist, xterm;
+	uint32_t num_xent = 0;
+	auto slotted_terms = [&](const dpmr_t &p, std::vector<uint32_t> &rec) -> bool {
+		for (uint32_t k = 0; k < p.nterms; k++) {
+			dterm_t t = terms[p.term_start + k];
+			uint32_t gend = 0, guarded = 0;
+
+			if (t.tflags & DT_ALT_NEXT)
+				return false;
+			if (t.tflags & DT_GUARD) {
+				/* CUSTOM_L3: frame_len > l3 + off + size (the kernel's
+				 * term_cmp guard) checked before the slot read */
+				if (t.kind != DK_CMP || t.base != DB_L3 || t.off < 0)
+					return false;
+				gend = (uint32_t)t.off + t.size;
+				guarded = 1;
+				t.tflags &= (uint8_t)~DT_GUARD;
+			}
+			const dslot_t sl = slotify(t);
+
+			if (sl.slot == SLOT_NONE || sl.nw != 1 || gend > 0xffffu)
+				return false;
+			rec.push_back(t.req);
+			rec.push_back(sl.mask[0]);
+			rec.push_back(sl.value[0]);
+			rec.push_back(sl.slot | (gend << 8) | (guarded << 31));
+		}
+		return p.nterms > 0;
+	};
 
 	if (xwalk && wgroups.size() <= XWALK_MAX_GROUPS) {
 		std::vector<uint32_t> gm(ncos, 0u);
@@ -689,17 +720,36 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			}
 		xcos.resize(2 * ncos);
 		for (uint32_t c = 0; c < ncos; c++) {
-			uint32_t st = (uint32_t)xlist.size();
+			uint32_t st = (uint32_t)(xlist.size() / 2);
 
-			for (uint32_t k = 0; k < cos[c].nrule; k++)
-				if (complex_pmr[cos[c].rule_start + k])
-					xlist.push_back(cos[c].rule_start + k);
-			xcos[2 * c] = st | (((uint32_t)xlist.size() - st) << 16);
+			for (uint32_t k = 0; k < cos[c].nrule; k++) {
+				const uint32_t pi = cos[c].rule_start + k;
+				std::vector<uint32_t> rec;
+
+				if (!complex_pmr[pi])
+					continue;
+				uint32_t xw = 0;
+
+				if (slotted_terms(pmr[pi], rec) && xterm.size() / 4 < (1u << 24)) {
+					xw = (uint32_t)(xterm.size() / 4) | ((uint32_t)pmr[pi].nterms << 24);
+					xterm.insert(xterm.end(), rec.begin(), rec.end());
+				}
+				xlist.push_back(pi);
+				xlist.push_back(xw);
+			}
+			xcos[2 * c] = st | (((uint32_t)(xlist.size() / 2) - st) << 16);
 			xcos[2 * c + 1] = gm[c];
 		}
-		if (xlist.size() > 65535) {
+		num_xent = (uint32_t)(xlist.size() / 2);
+		if (num_xent & 1u) {            /* xterm records start 16-byte aligned */
+			xlist.push_back(0u);
+			xlist.push_back(0u);
+		}
+		xlist.insert(xlist.end(), xterm.begin(), xterm.end());
+		if (num_xent > 65535 || xlist.size() > (1u << 20)) {
 			xcos.clear();
 			xlist.clear();
+			num_xent = 0;
 		}
 	}
 
@@ -861,7 +911,8 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.num_went = keep_w ? (uint32_t)wents.size() : 0;
 	if (!xcos.empty()) {
 		h.flags |= TBL_XWALK;
-		h.num_xlist = (uint32_t)xlist.size();
+		h.num_xlist = num_xent;
+		h.num_xwords = (uint32_t)xlist.size();
 	}
 	const uint32_t lean_req = (1u << IFL_L2) | (1u << IFL_L3) | (1u << IFL_L4) |
 				  (1u << IFL_ETH) | (1u << IFL_VLAN) | (1u << IFL_IPV4) |

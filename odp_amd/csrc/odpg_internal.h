@@ -175,6 +175,9 @@ typedef struct dwent_s {
 
 #define WALK_MAX_GROUPS 8    /* more groups: evaluate-all is cheaper */
 #define XWALK_MAX_GROUPS 32  /* hybrid walk: per-CoS group mask is one word */
+#ifndef XWALK_KEYS
+#define XWALK_KEYS 12        /* hybrid walk: group keys held in registers */
+#endif
 
 /* Mask groups (TBL_SIMPLE tables of <= 64 PMRs, the u64 hit-map kernel):
  * every (slot, req, mask) group is a two-choice cuckoo table keyed by the
@@ -273,8 +276,11 @@ typedef struct dtable_hdr_s {
 	uint32_t def_cgmask; /* cuckoo groups holding a rule of the default CoS */
 	uint32_t xcos_off;   /* uint2[num_cos] (TBL_XWALK): {xlist start | count << 16,
 	                      *  walk groups holding a single-word rule of the CoS} */
-	uint32_t xlist_off;  /* uint32[num_xlist]: complex PMR indices, per CoS in rule order */
+	uint32_t xlist_off;  /* uint32[num_xwords]: uint2[num_xlist] {pmr, xterm start |
+	                      *  n << 24} per CoS in rule order (padded to even), then
+	                      *  uint4 xterm records (cls_compile.cpp) */
 	uint32_t num_xlist;
+	uint32_t num_xwords;
 	uint32_t blob_bytes;
 } dtable_hdr_t;
 
@@ -323,7 +329,7 @@ typedef struct odpg_launch_args {
 	uint32_t def_cgmask;
 	const uint2_t *xcos;        /* TBL_XWALK */
 	const uint32_t *xlist;
-	uint32_t num_xlist;
+	uint32_t num_xlist, num_xwords;
 	/* lean 64-byte kernel (classify64.hip): CoS start state, from the host
 	 * copy of the table */
 	uint32_t l64_err_cos, l64_err_act, l64_def_cos, l64_def_act, l64_def_ci, l64_def_rules;

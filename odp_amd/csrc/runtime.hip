@@ -324,6 +324,7 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.xcos = (const uint2_t *)((const uint8_t *)t->dblob + h.xcos_off);
 	a.xlist = (const uint32_t *)((const uint8_t *)t->dblob + h.xlist_off);
 	a.num_xlist = h.num_xlist;
+	a.num_xwords = h.num_xwords;
 	{
 		/* start state of cls_select_cos (odp_classification.c:1669-1701)
 		 * for the lean kernel, as classify.hip derives it per packet */
