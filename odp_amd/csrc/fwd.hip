@@ -26,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/odpg_fwd.h"
@@ -38,6 +39,7 @@
 #define FN_END   0x80000000u
 #define FN_VALID 0x40000000u
 #define FN_VAL   0x00ffffffu
+#define FWD_MAX_IV (2 * ODPG_FWD_MAX_ROUTES + 1)
 
 struct odpg_fwd_s {
 	odpg_ctx_t *ctx;
@@ -46,7 +48,7 @@ struct odpg_fwd_s {
 	uint4 *d_routes;      /* newest first: {addr, mask, oif, 0} */
 	uint4 *d_rmac;        /* per route: frame bytes 0..11 after rewrite, oif */
 	uint4 *d_pmac;        /* per port (LPM): frame bytes 0..11, 3 words */
-	uint32_t *d_l1;       /* 65536 first-level nodes */
+	uint32_t *d_l1;       /* LPM: 65536 first-level nodes; hash: route intervals */
 	uint32_t *d_pool;     /* sub-table pool */
 	uint32_t num_ports;
 };
@@ -233,6 +235,8 @@ __global__ __launch_bounds__(FBLOCK) void odpg_l3fwd_kernel(
 	__shared__ uint32_t rows[FBLOCK * RW];
 	__shared__ uint4 s_rmac[ODPG_FWD_MAX_ROUTES];
 	__shared__ uint4 s_pmac[ODPG_FWD_MAX_PORTS];
+	/* hash mode: the route list as address intervals (fwd_intervals) */
+	__shared__ uint32_t s_ivb[FWD_MAX_IV], s_iva[FWD_MAX_IV];
 
 	const uint32_t tid = threadIdx.x;
 	const uint32_t i = blockIdx.x * FBLOCK + tid;
@@ -242,6 +246,12 @@ __global__ __launch_bounds__(FBLOCK) void odpg_l3fwd_kernel(
 		s_rmac[tid] = rmac[tid];
 	if (tid < ODPG_FWD_MAX_PORTS)
 		s_pmac[tid] = pmac[tid];
+	const uint32_t niv = mode != ODPG_FWD_LPM ? l1[0] : 0u;   /* uniform */
+
+	if (tid < niv) {
+		s_ivb[tid] = l1[1u + 2u * tid];
+		s_iva[tid] = l1[2u + 2u * tid];
+	}
 
 	uint8_t *fr = frames + (size_t)(live ? i : 0u) * stride;
 	uint32_t f[16];
@@ -318,14 +328,20 @@ __global__ __launch_bounds__(FBLOCK) void odpg_l3fwd_kernel(
 			dif = (int32_t)(n & FN_VAL);
 		mac = s_pmac[(uint32_t)dif & (ODPG_FWD_MAX_PORTS - 1u)];
 	} else {
-		int32_t k = -1;
+		/* first match of the newest-first route list
+		 * (find_fwd_db_entry): the interval holding dst carries it.
+		 * Branch-free binary search for the last start <= dst (the
+		 * first start is 0). */
+		uint32_t pos = 0u;
 
-		for (uint32_t r = 0; r < nroutes; ++r) {     /* newest first */
-			const uint4 rt = routes[r];
+#pragma unroll
+		for (uint32_t step = 64u; step; step >>= 1) {
+			const uint32_t q = pos + step;
 
-			if (k < 0 && (dst & rt.y) == rt.x)
-				k = (int32_t)r;
+			if (q < niv && s_ivb[q] <= dst)
+				pos = q;
 		}
+		const int32_t k = niv ? (int32_t)s_iva[pos] : -1;
 		if (k >= 0) {
 			mac = s_rmac[k];
 			dif = (int32_t)mac.w;
@@ -400,6 +416,35 @@ extern "C" int odpg_fwd_create(odpg_ctx_t *ctx, const odpg_route_t *routes, uint
 	for (uint32_t p = 0; p < ODPG_FWD_MAX_PORTS; p++)
 		pm[p] = mac_words(param->dest_mac[p], param->port_mac[p]);
 	std::vector<uint32_t> l1(FibTrie::kL1, FN_END), pool(16, FN_END);
+
+	if (param->mode == ODPG_FWD_HASH) {
+		/* fwd_intervals: the address space cut at every route's first and
+		 * one-past-last address; on each piece the newest route holding its
+		 * start (and so every address of it) is find_fwd_db_entry's answer
+		 * (odp_l3fwd_db.c:474-508). l1 = {count, {start, route | -1}...} */
+		std::vector<uint32_t> pts{0u};
+
+		for (const uint4 &r : rt) {
+			pts.push_back(r.x);
+			const uint32_t end = r.x | ~r.y;
+
+			if (end != 0xffffffffu)
+				pts.push_back(end + 1u);
+		}
+		std::sort(pts.begin(), pts.end());
+		pts.erase(std::unique(pts.begin(), pts.end()), pts.end());
+		l1.assign(1u + 2u * pts.size(), 0u);
+		l1[0] = (uint32_t)pts.size();
+		for (size_t i = 0; i < pts.size(); i++) {
+			uint32_t a = 0xffffffffu;
+
+			for (size_t k = 0; k < rt.size() && a == 0xffffffffu; k++)
+				if ((pts[i] & rt[k].y) == rt[k].x)
+					a = (uint32_t)k;
+			l1[1 + 2 * i] = pts[i];
+			l1[2 + 2 * i] = a;
+		}
+	}
 
 	if (param->mode == ODPG_FWD_LPM) {
 		FibTrie t;
