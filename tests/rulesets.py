@@ -197,3 +197,68 @@ def simple_mixed_rules(cls, pktio, stats=True):
             assert cls.pmr_create([T(cls.PMR_UDP_SPORT, gen.be_bytes((a * 7 + j) & 0xff, 2),
                                      b"\x00\xff")], l1[a], leaves[(8 + a * 4 + j) % 40])
     return {"default": default}
+
+
+def random_mixed_rules(cls, pktio, seed, n_cos=24, complex_share=0.3, stats=True):
+    """Random CoS DAG (destination index > source index, <= 8 rules per CoS)
+    over single-word terms, IPv4 / IPv6 alternative terms and complex PMRs
+    (multi-term, CUSTOM_L3 with its length guard, CUSTOM_FRAME), with values
+    drawn from mutate_corpus's frames so rules both hit and miss. Exercises
+    the hybrid hash walk (TBL_XWALK) against the walk and the oracle."""
+    rng = np.random.default_rng(seed)
+    T = cls.Term
+    ports = [0x3f, 63, 1024, 2048, 80, 9, 7, 0]
+
+    def one():
+        k = int(rng.integers(12))
+        if k == 0:
+            d = int(rng.choice([8, 16, 24, 32]))
+            return T(cls.PMR_SIP_ADDR, b"\xc0\xa8\x01\x01", (0xFFFFFFFF << (32 - d) & 0xFFFFFFFF).to_bytes(4, "big"))
+        if k == 1:
+            return T(cls.PMR_DIP_ADDR, b"\xc0\xa8\x02\x02", b"\xff\xff\xff\x00")
+        if k in (2, 3, 4, 5):
+            term = [cls.PMR_UDP_DPORT, cls.PMR_UDP_SPORT, cls.PMR_TCP_DPORT, cls.PMR_TCP_SPORT][k - 2]
+            m = b"\xff\xff" if rng.integers(2) else b"\x00\xff"
+            return T(term, int(rng.choice(ports)).to_bytes(2, "big"), m)
+        if k == 6:
+            return T(cls.PMR_IPPROTO, bytes([int(rng.choice([6, 17, 0x84]))]), b"\xff")
+        if k == 7:
+            return T(cls.PMR_IP_DSCP, bytes([int(rng.choice([0, 0x2e]))]), b"\x3f")
+        if k == 8:
+            et = int(rng.choice([0x0800, 0x86dd, 0x8100, 0x88a8]))
+            return T(cls.PMR_ETHTYPE_0, et.to_bytes(2, "big"), b"\xff\xff")
+        if k == 9:
+            return T(cls.PMR_SIP6_ADDR, bytes(15) + bytes([int(rng.integers(4))]),
+                     bytes(15) + b"\x03")
+        if k == 10:
+            return T(cls.PMR_LEN, int(rng.choice([60, 64, 80, 96, 120])).to_bytes(4, "little"),
+                     b"\xff\xff\xff\xff")
+        return T(cls.PMR_IPSEC_SPI, b"\x00\x00\x00\x7b", b"\xff\xff\xff\xff")
+
+    def complex_terms():
+        k = int(rng.integers(3))
+        if k == 0:
+            off = int(rng.integers(0, 24))
+            sz = int(rng.integers(1, 3))
+            return [T(cls.PMR_CUSTOM_L3, bytes(int(v) for v in rng.integers(0, 256, sz)) if rng.integers(3) == 0
+                      else bytes([0x40, 0x11][:sz]) if off == 8 else bytes(sz),
+                      b"\xff" * sz if rng.integers(2) else b"\x0f" * sz, offset=off, val_sz=sz)]
+        if k == 1:
+            return [T(cls.PMR_CUSTOM_FRAME, b"\x08\x00", b"\xff\xff", offset=12)]
+        return [one(), one()]
+
+    coses = [cls.cos_create(f"r{seed}_{i}", queue=cls.queue(i), stats_enable=stats)
+             for i in range(n_cos)]
+    err = cls.cos_create(f"r{seed}_err", queue=cls.queue(n_cos), stats_enable=stats)
+    assert all(coses) and err
+    assert cls.default_cos_set(pktio, coses[0]) == 0
+    assert cls.error_cos_set(pktio, err) == 0
+    pmrs = []
+    for c in range(n_cos // 2):
+        for _ in range(int(rng.integers(1, 9))):
+            d = int(rng.integers(c + 1, n_cos))
+            terms = complex_terms() if rng.random() < complex_share else [one()]
+            p = cls.pmr_create(terms, coses[c], coses[d], mark=int(rng.integers(0, 5)))
+            if p:
+                pmrs.append(p)
+    return {"coses": coses, "error": err, "pmrs": pmrs}

@@ -435,3 +435,20 @@ def test_lean64_hashwalk(gpu_ctx, fresh_cls, opt, variant):
         assert L.lib.odpg_last_kernel() == 1
         assert_same({"out": g["out"], "stats": g["stats"]},
                     {"out": o["out"], "stats": o["stats"]}, f"lean64 hw+stats {variant} opt={opt}")
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13, 14])
+def test_hybrid_walk_random_rules(gpu_ctx, fresh_cls, seed):
+    """Random DAGs mixing single-word, IPv4/IPv6-alternative and complex PMRs
+    (the hybrid hash walk's three rule forms) on the fuzz corpus: every
+    kernel strategy bit-exact with the oracle."""
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    r = rulesets.random_mixed_rules(fresh_cls, p, seed, complex_share=0.15 + 0.1 * (seed % 4))
+    assert len(r["pmrs"]) > 20
+    assert fresh_cls.pktio_start(p) == 0
+    frames = rulesets.mutate_corpus(20000, seed=seed)
+    buf, desc = pack(frames)
+    for opt in (0, ALL_CHKSUM):
+        g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), buf, len(frames), desc=desc, opt=opt)
+        assert_same(g, o, f"random rules seed={seed} opt={opt}")
+    assert len(np.unique(g["out"] & 0xFFFF)) > 3
