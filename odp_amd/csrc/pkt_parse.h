@@ -594,6 +594,15 @@ __device__ __forceinline__ uint32_t byte_mask(int n)
  * idx = lane, lane + 64, ...; only the chunk holding byte b - 1 (and the
  * first one when a is not 16-aligned) is masked, with wave-uniform masks.
  * Returns the share folded to 16 bits (residue mod 0xffff). */
+typedef unsigned short tail_us2 __attribute__((ext_vector_type(2)));
+
+/* acc + w.lo16 + w.hi16 (one v_dot2_u32_u16 against {1, 1}) */
+__device__ __forceinline__ uint32_t tail_dot2(uint32_t w, uint32_t acc)
+{
+	return __builtin_amdgcn_udot2(__builtin_bit_cast(tail_us2, w),
+				      __builtin_bit_cast(tail_us2, 0x00010001u), acc, false);
+}
+
 __device__ __forceinline__ uint32_t tail_share(const uint8_t *gp, uint32_t a, uint32_t b,
 					       uint32_t lane)
 {
@@ -605,7 +614,7 @@ __device__ __forceinline__ uint32_t tail_share(const uint8_t *gp, uint32_t a, ui
 	const int lead = (int)(a & 15u);                    /* bytes to drop at the start */
 	const uint32_t s0 = ~byte_mask(lead), s1 = ~byte_mask(lead - 4),
 		       s2 = ~byte_mask(lead - 8), s3 = ~byte_mask(lead - 12);
-	uint64_t acc = 0ull;
+	uint32_t acc = 0u;
 
 	for (uint32_t base = 0; base <= last; base += 64u) {   /* uniform: 1-2 passes for IMIX */
 		const uint32_t idx = base + lane;
@@ -618,12 +627,16 @@ __device__ __forceinline__ uint32_t tail_share(const uint8_t *gp, uint32_t a, ui
 			const uint32_t w2 = q.z & (end ? e2 : ~0u) & (start ? s2 : ~0u);
 			const uint32_t w3 = q.w & (end ? e3 : ~0u) & (start ? s3 : ~0u);
 
-			acc += (uint64_t)w0 + w1 + w2 + w3;
+			/* sums of the 16-bit halves (v_dot2_u32_u16): the same value
+			 * mod 0xffff as the 32-bit word sum; at most 8 x 0xffff per
+			 * pass, so no carry out below 8 MiB tails */
+			acc = tail_dot2(w0, acc);
+			acc = tail_dot2(w1, acc);
+			acc = tail_dot2(w2, acc);
+			acc = tail_dot2(w3, acc);
 		}
 	}
-	const uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
-
-	return oc_fold(oc_add(lo, hi));
+	return oc_fold(acc);
 }
 
 #ifndef COOP_BATCH
