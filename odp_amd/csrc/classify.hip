@@ -327,7 +327,10 @@ template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST, bool LEAN>
 #ifndef LEAN_WAVES
 #define LEAN_WAVES 5
 #endif
-__global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : 6) void odpg_classify_kernel(
+#ifndef GEN_WAVES
+#define GEN_WAVES 6
+#endif
+__global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) void odpg_classify_kernel(
 	const uint8_t *__restrict__ frames, const odpg_desc_t *__restrict__ desc,
 	uint32_t stride, uint32_t num, uint64_t opt, uint32_t layer, uint32_t classify,
 	const dterm_t *__restrict__ terms, const dpmr_t *__restrict__ pmrs,

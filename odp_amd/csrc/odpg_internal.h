@@ -233,7 +233,9 @@ static inline ODPG_HD uint32_t walk_hash(uint32_t value, uint32_t cos, uint32_t 
 #define HENT_EMPTY    0xFFFFFFFFu
 #define HASH_MIN      6      /* smaller groups stay linear */
 #define HASH_MUL      0x9E3779B1u
+#ifndef HENT_LDS_MAX
 #define HENT_LDS_MAX  4096   /* entries copied to LDS per workgroup */
+#endif
 
 #define EVAL_ALL_MAX_PMR 1024
 
