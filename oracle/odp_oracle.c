@@ -1074,6 +1074,90 @@ uint32_t oracle_thash(const uint32_t *tuple, uint32_t len)
 	return thash_softrss(tuple, len);
 }
 
+/* ---- odph_udp_tcp_chksum() (helper/chksum.c:265-353) over one contiguous
+ * frame: the application-side checksum of the helper library, which BASELINE
+ * config C3 is also checked against. It differs from the platform verify
+ * (_odp_packet_l4_chksum, odp_packet.c:1906-1984) in its length: UDP sums
+ * udp.length bytes (:127-130), TCP sums l3_len - (l4 - l3) from the IP
+ * header (:232), where the platform sums frame_len - l4_offset.
+ * op: 0 GENERATE (writes the field), 1 VERIFY, 2 RETURN (as odph_chksum_op_t).
+ * Returns <0 error (length leaves the frame, not UDP/TCP), 0 ok / generated,
+ * 1 VERIFY of a UDP packet with checksum field 0, 2 VERIFY mismatch. */
+static uint32_t helper_seg_sum(const uint8_t *p, uint32_t len)
+{
+	/* data_seg_sum (:32-90) for a single, last segment: host-order (LE)
+	 * 16-bit words, a trailing odd byte as the low byte of a word */
+	uint32_t sum = 0, i;
+
+	for (i = 0; i + 1 < len; i += 2)
+		sum += (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8);
+	if (len & 1)
+		sum += p[len - 1];
+	return sum;
+}
+
+int oracle_helper_udp_tcp_chksum(uint8_t *frame, uint32_t frame_len, uint32_t l3_off,
+				 uint32_t l4_off, int is_ipv6, int is_tcp, int op,
+				 uint16_t *chksum_out)
+{
+	uint32_t ck_off = l4_off + (is_tcp ? 16u : 6u);
+	uint32_t l3_len, l4_len, sum, ones;
+	uint16_t stored, chksum;
+	const uint8_t *addrs;
+	uint32_t addrs_len, proto;
+
+	if (ck_off + 2 > frame_len || l4_off < l3_off)
+		return -1;
+	stored = (uint16_t)(frame[ck_off] | (frame[ck_off + 1] << 8));
+	/* VERIFY of a UDP packet without checksum (:152-154) */
+	if (op == 1 && stored == 0 && !is_tcp && chksum_out == NULL)
+		return 1;
+	if (op == 0 && stored != 0) {                    /* :158-164 */
+		frame[ck_off] = 0;
+		frame[ck_off + 1] = 0;
+	}
+	if (!is_ipv6) {                                  /* odph_process_l3_hdr :198-210 */
+		if (l3_off + 20 > frame_len)
+			return -1;
+		addrs = frame + l3_off + 12;
+		addrs_len = 8;
+		proto = frame[l3_off + 9];
+		l3_len = ((uint32_t)frame[l3_off + 2] << 8) | frame[l3_off + 3];
+	} else {                                         /* :211-224 */
+		if (l3_off + 40 > frame_len)
+			return -1;
+		addrs = frame + l3_off + 8;
+		addrs_len = 32;
+		proto = frame[l3_off + 6];
+		l3_len = (((uint32_t)frame[l3_off + 4] << 8) | frame[l3_off + 5]) + 40;
+	}
+	l4_len = is_tcp ? l3_len - (l4_off - l3_off)
+			: (((uint32_t)frame[l4_off + 4] << 8) | frame[l4_off + 5]);
+	if (l4_len > frame_len - l4_off)   /* would walk past the last segment */
+		return -1;
+	sum = helper_seg_sum(addrs, addrs_len);
+	/* swap_buf {len_hi, len_lo, 0, proto} as two host-order words (:241-246) */
+	sum += ((l4_len >> 8) & 0xFF) | ((l4_len & 0xFF) << 8);
+	sum += (uint32_t)proto << 8;
+	sum += helper_seg_sum(frame + l4_off, l4_len);
+	ones = (sum & 0xFFFF) + (sum >> 16);             /* :329-331 */
+	ones = (ones & 0xFFFF) + (ones >> 16);
+	chksum = (uint16_t)(~ones & 0xFFFF);
+	if (chksum_out)
+		*chksum_out = chksum;
+	if (op == 0) {
+		frame[ck_off] = (uint8_t)chksum;
+		frame[ck_off + 1] = (uint8_t)(chksum >> 8);
+		return 0;
+	}
+	if (op == 1) {                                   /* :342-347 */
+		if (stored == 0 && !is_tcp)
+			return 1;
+		return chksum == 0 ? 0 : 2;
+	}
+	return 0;
+}
+
 /* ======================================================================
  * example/l3fwd forwarding decision.
  * Restated from example/l3fwd/odp_l3fwd.c, odp_l3fwd_db.c, odp_l3fwd_lpm.c.

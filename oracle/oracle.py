@@ -35,6 +35,8 @@ def _load():
     lib.oracle_crc32c.argtypes = [vp, u32, u32]
     lib.oracle_thash.restype = u32
     lib.oracle_thash.argtypes = [vp, u32]
+    lib.oracle_helper_udp_tcp_chksum.restype = i32
+    lib.oracle_helper_udp_tcp_chksum.argtypes = [vp, u32, u32, u32, i32, i32, i32, vp]
     lib.oracle_l3fwd.restype = i32
     lib.oracle_l3fwd.argtypes = [vp, u32, vp, vp, u32, u32, i32, i32, vp]
     lib.oracle_tx_prepare.restype = i32
@@ -92,6 +94,20 @@ def ones_comp16(data: bytes) -> int:
 def crc32c(data: bytes, init=0xFFFFFFFF) -> int:
     b = np.frombuffer(bytes(data), np.uint8)
     return lib.oracle_crc32c(b.ctypes.data if len(b) else None, len(b), init)
+
+
+HELPER_GENERATE, HELPER_VERIFY, HELPER_RETURN = 0, 1, 2
+
+
+def helper_udp_tcp_chksum(frame, l3, l4, ipv6, tcp, op=HELPER_VERIFY):
+    """odph_udp_tcp_chksum() restated (helper/chksum.c:265-353). Returns
+    (rc, checksum, frame bytes after the op)."""
+    b = np.frombuffer(bytes(frame), np.uint8).copy()
+    ck = np.zeros(1, np.uint16)
+    rc = lib.oracle_helper_udp_tcp_chksum(b.ctypes.data, len(b), l3, l4, int(bool(ipv6)),
+                                          int(bool(tcp)), op,
+                                          None if op == HELPER_VERIFY else ck.ctypes.data)
+    return rc, int(ck[0]), bytes(b)
 
 
 def thash(words) -> int:
