@@ -45,7 +45,7 @@ def parse_args():
     ap.add_argument("--buffers", type=int, default=0,
                     help="rotating input batches (default: enough to exceed the 256 MiB "
                          "Infinity Cache so every launch streams from HBM)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stats", action="store_true",
@@ -471,22 +471,29 @@ def cpu_baseline(rules, frames, desc, n, stride, opt, args):
     port of the reference's per-packet path) timed on this host's cores over
     the same batch, ~cpu_seconds of work."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import statistics
+
     import oracle
-    try:
-        ncpu = len(os.sched_getaffinity(0))
-    except AttributeError:
-        ncpu = os.cpu_count() or 1
-    threads = args.cpu_threads or max(1, min(16, ncpu))
+    cpus, share = cpu_share()
+    threads = args.cpu_threads or len(cpus)
+    cpus = (cpus * (threads // len(cpus) + 1))[:threads]
     sub = min(n, 1 << 18)
-    # single-thread calibration pass
+    # single-thread calibration pass (pinned)
     t = time.perf_counter()
-    oracle.classify_mt(rules, frames, sub, stride=stride, desc=desc, opt=opt, nthreads=1, reps=1)
+    oracle.classify_mt(rules, frames, sub, stride=stride, desc=desc, opt=opt, nthreads=1, reps=1,
+                       cpus=cpus[:1])
     one = sub / (time.perf_counter() - t) / 1e6
-    reps = max(1, int(args.cpu_seconds * one * threads * 1e6 / n * 0.8))
-    t = time.perf_counter()
-    _, used = oracle.classify_mt(rules, frames, n, stride=stride, desc=desc, opt=opt,
-                                 nthreads=threads, reps=reps)
-    dt = time.perf_counter() - t
+    # SURVEY.md §8(d): all cores of the share, pinned, median of 5 runs; each
+    # run is ~cpu_seconds / 5 of work
+    runs = 5
+    reps = max(1, int(args.cpu_seconds / runs * one * threads * 1e6 / n * 0.8))
+    rates = []
+    used = threads
+    for _ in range(runs):
+        t = time.perf_counter()
+        _, used = oracle.classify_mt(rules, frames, n, stride=stride, desc=desc, opt=opt,
+                                     nthreads=threads, reps=reps, cpus=cpus)
+        rates.append(n * reps / (time.perf_counter() - t) / 1e6)
     model = ""
     try:
         for ln in open("/proc/cpuinfo"):
@@ -495,10 +502,28 @@ def cpu_baseline(rules, frames, desc, n, stride, opt, args):
                 break
     except OSError:
         pass
-    return {"value": round(n * reps / dt / 1e6, 2), "unit": "Mpps", "cores": used,
+    return {"value": round(statistics.median(rates), 2), "unit": "Mpps", "cores": used,
             "kind": "port", "value_1thread": round(one, 2), "cpu_model": model,
-            "sample": f"{reps} passes x {n} pkts of the same {args.config.upper()} batch in host DRAM "
-                      f"({dt:.1f} s, {used} threads)"}
+            "runs_mpps": [round(r, 2) for r in rates], "core_share": share,
+            "sample": f"median of {runs} runs, each {reps} passes x {n} pkts of the same "
+                      f"{args.config.upper()} batch in host DRAM, {used} threads pinned one per "
+                      f"core ({share})"}
+
+
+def cpu_share():
+    """CPUs the CPU baseline may use: the affinity mask, capped at the host's
+    declared per-GPU share (the GPU box sets OMP_NUM_THREADS to the 16 cores
+    it grants one GPU job; its affinity mask lists the whole machine).
+    Returns (cpu list, description)."""
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = list(range(os.cpu_count() or 1))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and 0 < int(cap) < len(aff):
+        return aff[:int(cap)], (f"{int(cap)} of the {len(aff)} CPUs in the affinity mask: the "
+                                f"host's per-GPU share (OMP_NUM_THREADS={cap})")
+    return aff, f"all {len(aff)} CPUs of the affinity mask"
 
 
 def e2e(ctx, tbl, frames, desc, n, stride, opt):

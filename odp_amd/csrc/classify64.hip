@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/odpg.h"
 #include "odpg_internal.h"
@@ -264,175 +265,37 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 	}
 	__syncthreads();
 
-	bool pend = false;
-	uint32_t pend_i = 0u, pend_w = 0u;
 	/* loopback_recv accounting (loop.c:304-374), wave-uniform counts */
 	uint32_t n_pkt = 0u, n_err = 0u, n_disc = 0u;
+	const bool walk = A.def_rules != 0u;
 
-	for (uint32_t t = gw; t < ntiles; t += nwaves) {
-		const uint32_t i = t * 64u + lane;
-		const bool live = i < num;
+	/* Hit bits of one mask group: both cuckoo candidates are read and the
+	 * entry whose value equals the packet's masked key word ORs its PMR bits
+	 * (odpg_internal.h "Mask groups"). */
+	auto probe = [&](const MGd &d, uint32_t key, uint32_t inf_lo, uint32_t &lo, uint32_t &hi) {
+		const uint32_t kvm = key & d.mask;
+		const bool rq = (inf_lo & d.req) == d.req;
 
-		/* previous tile's verdict, stored before this tile's prefetch
-		 * (vector-memory counters retire in issue order) */
-		if (pend)
-			A.out[pend_i] = pend_w;
-		uint32_t f[16];
+		if (d.cnt == 1u) {
+			const bool h = rq & (kvm == d.m1);
 
-#pragma unroll
-		for (int k = 0; k < 16; ++k)
-			f[k] = fn[k];
-		{
-			const uint32_t nt = t + nwaves;
-			const uint32_t inx = min(nt < ntiles ? nt * 64u + lane : i, num - 1u);
-			const uint4 *src = A.frames + (size_t)inx * 4u;
-
-#pragma unroll
-			for (int k = 0; k < 4; ++k) {
-				const uint4 x = ld_stream(src + k);
-
-				fn[4 * k + 0] = x.x;
-				fn[4 * k + 1] = x.y;
-				fn[4 * k + 2] = x.z;
-				fn[4 * k + 3] = x.w;
-			}
-		}
-		const bool fast = __ballot(live && !plain_v4(f)) == 0ull;
-
-		/* ---- parse + PMR hit bits -------------------------------------
-		 * hit bits: both cuckoo candidates of each mask group are read and
-		 * the entry whose value equals the packet's masked key word ORs
-		 * its PMR bits (odpg_internal.h "Mask groups") */
-		uint32_t wbits = 0u, inf_lo = 0u;
-		bool err = false, pdrop = false;
-		uint32_t lo = 0u, hi = 0u;
-		const bool walk = A.def_rules != 0u;
-		/* HW: per walk group, the masked key word and its gate */
-		uint32_t kv[HW ? NG : 1];
-		bool krq[HW ? NG : 1];
-		auto probe = [&](const MGd &d, uint32_t key) {
-			const uint32_t kvm = key & d.mask;
-			const bool rq = (inf_lo & d.req) == d.req;
-
-			if (d.cnt == 1u) {
-				const bool h = rq & (kvm == d.m1);
-
-				lo |= h ? d.m2 : 0u;
-				hi |= h ? d.off : 0u;
-			} else {
-				const uint4 e1 = ments[d.off + ((kvm * d.m1) >> d.sh)];
-				const uint4 e2 = ments[d.off + ((kvm * d.m2) >> d.sh)];
-				const bool h1 = rq & (e1.x == kvm), h2 = rq & (e2.x == kvm);
-
-				lo |= (h1 ? e1.y : 0u) | (h2 ? e2.y : 0u);
-				hi |= (h1 ? e1.z : 0u) | (h2 ? e2.z : 0u);
-			}
-		};
-#ifdef L64_EXP_NOPARSE   /* experiment builds only: skeleton floor */
-		if (fast) {
-			wbits = f[3] ^ f[9];
-		} else
-#endif
-		if (fast) {
-			const FastV r = parse_fast64(f, A.opt);
-
-			wbits = r.wbits;
-			inf_lo = r.inf_lo;
-			err = r.err;
-#ifndef L64_EXP_NOMATCH
-			if (walk) {
-				/* key word at a fixed frame offset: a uniform register
-				 * index into the frame (no per-slot branches) */
-				const u32x16_t fv = {f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7],
-						     f[8], f[9], f[10], f[11], f[12], f[13], f[14], f[15]};
-				auto fast_key = [&](const MGd &d) -> uint32_t {
-					if (d.slot == SLOT_LEN)
-						return 64u;
-					return __builtin_amdgcn_alignbyte(fv[d.fw + 1u], fv[d.fw], d.fs);
-				};
-				if constexpr (HW) {
-#pragma unroll
-					for (int g = 0; g < NG; ++g) {
-						kv[g] = fast_key(mg[g]) & mg[g].mask;
-						krq[g] = (inf_lo & mg[g].req) == mg[g].req;
-					}
-				} else if constexpr (NG > 0) {
-#pragma unroll
-					for (int g = 0; g < NG; ++g)
-						probe(mg[g], fast_key(mg[g]));
-				} else {
-					for (uint32_t gi = 0; gi < A.num_mgroups; ++gi) {
-						const MGd d = load_mg(A.mgroups + gi);
-
-						probe(d, fast_key(d));
-					}
-				}
-			}
-#endif
+			lo |= h ? d.m2 : 0u;
+			hi |= h ? d.off : 0u;
 		} else {
-			Bases b;
-			Pkt<64, false> v;
+			const uint4 e1 = ments[d.off + ((kvm * d.m1) >> d.sh)];
+			const uint4 e2 = ments[d.off + ((kvm * d.m2) >> d.sh)];
+			const bool h1 = rq & (e1.x == kvm), h2 = rq & (e2.x == kvm);
 
-			v.row = row;
-			v.g = (const uint8_t *)(A.frames + (size_t)i * 4u);
-			v.len = 64u;
-#pragma unroll
-			for (int k = 0; k < 16; ++k)
-				row[k] = f[k];
-			Prs p;
-
-			p.inf = 0ull;
-			p.fl = 0u;
-			p.l2 = p.l3 = p.l4 = 0xffffu;
-			const int ret = live ? parse_common(p, v, A.layer, (uint64_t)A.opt) : 0;
-
-			if (p.inf & IF(IFL_L3_CHKSUM_DONE))
-				wbits |= (p.fl & FB(FL_L3_CHKSUM_ERR) ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 16;
-			if (p.inf & IF(IFL_L4_CHKSUM_DONE))
-				wbits |= (p.fl & FB(FL_L4_CHKSUM_ERR) ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 18;
-			err = (p.fl & FL_ERROR_MASK) != 0u;
-			if (err)
-				wbits |= ODPG_OUT_ERROR;
-			if (ret)
-				wbits |= ODPG_OUT_PARSE_ERR;
-			pdrop = ret < 0;
-			inf_lo = (uint32_t)p.inf;
-			b.l2 = p.l2;
-			b.l3 = p.l3;
-			b.l4 = p.l4;
-			b.vlanx = 14u + ((p.inf & IF(IFL_VLAN_QINQ)) ? 4u : 0u);
-			b.len = 64u;
-			b.inf_lo = inf_lo;
-#ifndef L64_EXP_NOMATCH
-			if (walk) {
-				KeySrc<64, false> key;
-
-				key.f = f;
-				key.v = &v;
-				key.b = &b;
-				key.fast = false;
-				if constexpr (HW) {
-#pragma unroll
-					for (int g = 0; g < NG; ++g) {
-						kv[g] = key(mg[g].slot) & mg[g].mask;
-						krq[g] = (inf_lo & mg[g].req) == mg[g].req;
-					}
-				} else if constexpr (NG > 0) {
-#pragma unroll
-					for (int g = 0; g < NG; ++g)
-						probe(mg[g], key(mg[g].slot));
-				} else {
-					for (uint32_t gi = 0; gi < A.num_mgroups; ++gi) {
-						const MGd d = load_mg(A.mgroups + gi);
-
-						probe(d, key(d.slot));
-					}
-				}
-			}
-#endif
+			lo |= (h1 ? e1.y : 0u) | (h2 ? e2.y : 0u);
+			hi |= (h1 ? e1.z : 0u) | (h2 ? e2.z : 0u);
 		}
+	};
 
-		/* ---- CoS: cls_select_cos (odp_classification.c:1669-1701) ------ */
+	/* cls_select_cos + match_pmr_cos (odp_classification.c:1599-1701) on the
+	 * packet's hit bits (mask groups) or masked group keys (HW), then the
+	 * verdict word (odpg.h) and the wave's pktio counts */
+	auto finish = [&](bool live, bool pdrop, bool err, uint32_t wbits, uint32_t lo, uint32_t hi,
+			  const uint32_t *kv, const bool *krq) -> uint32_t {
 		uint32_t cos = err ? A.err_cos : A.def_cos;
 		uint32_t act = err ? A.err_act : A.def_act;
 		uint32_t ci = err ? 0u : A.def_ci;
@@ -440,10 +303,9 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		bool any_match = false;
 
 		if constexpr (HW) {
-			/* match_pmr_cos, one level per iteration: at CoS c both
-			 * candidates of each group holding a rule of c are read with
-			 * key (c, masked key word); the lowest PMR index found is c's
-			 * first matching rule */
+			/* one level per iteration: at CoS c both candidates of each
+			 * group holding a rule of c are read with key (c, masked key
+			 * word); the lowest PMR index found is c's first matching rule */
 			bool active = live && !pdrop && !err && walk;
 			uint32_t steps = 0u, gm = A.def_cgmask;
 
@@ -481,8 +343,8 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		} else {
 			const uint64_t hits = ((uint64_t)hi << 32) | lo;
 
-			/* match_pmr_cos: first hit in the current CoS's rule range,
-			 * one LDS read per level (pinfo2 carries the next range) */
+			/* first hit in the current CoS's rule range, one LDS read
+			 * per level (pinfo2 carries the next range) */
 			if (live && !pdrop) {
 				uint32_t steps = 0u;
 
@@ -505,8 +367,6 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 				}
 			}
 		}
-
-		/* ---- verdict word (odpg.h) ------------------------------------ */
 		uint32_t w;
 
 		if (pdrop) {
@@ -518,13 +378,10 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 			if (any_match && !err && cos != ODPG_COS_LOOP && mark)
 				w |= ODPG_OUT_MARK_VALID;
 		}
-		pend = live;
-		pend_i = i;
-		pend_w = w;
 		if (A.stats) {
 			/* in_packets: delivered error-free (cls ret 0); in_errors:
-			 * parse ret != 0; in_discards: cls ret -1 (no CoS; a CoS
-			 * loop counts the same) */
+			 * parse ret != 0; in_discards: cls ret -1 (no CoS; a CoS loop
+			 * counts the same) */
 			const bool nocos = cos == ODPG_COS_NONE || cos == ODPG_COS_LOOP;
 			const bool ok = live && !pdrop && !err && !nocos && act != 1u;
 
@@ -532,9 +389,211 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 			n_err += (uint32_t)__builtin_popcountll(__ballot(live && (wbits & ODPG_OUT_PARSE_ERR)));
 			n_disc += (uint32_t)__builtin_popcountll(__ballot(live && !pdrop && nocos));
 		}
+		return w;
+	};
+
+	/* Tiles in chunks of up to 64 per wave. Inside a chunk only plain waves
+	 * are classified, each tile's frames prefetched one tile ahead; a tile
+	 * with any other frame is marked in `defer` and classified after the
+	 * chunk by the generic parse, with its frames re-read. The hot loop thus
+	 * stays small (instruction cache) and no prefetch registers are live
+	 * across the generic parse (register pressure); the last tile of a chunk
+	 * issues no prefetch (a wave never re-reads past its last tile). */
+	bool pend = false;
+	uint32_t pend_i = 0u, pend_w = 0u;
+	bool first = true;
+
+	for (uint32_t t0 = gw; t0 < ntiles;) {
+		const uint32_t left = (ntiles - t0 + nwaves - 1u) / nwaves;
+		const uint32_t nk = left < 64u ? left : 64u;
+		uint64_t defer = 0ull;
+
+		if (!first) {
+			const uint32_t i0 = min(t0 * 64u + lane, num - 1u);
+			const uint4 *src = A.frames + (size_t)i0 * 4u;
+
+#pragma unroll
+			for (int k = 0; k < 4; ++k) {
+				const uint4 x = ld_stream(src + k);
+
+				fn[4 * k + 0] = x.x;
+				fn[4 * k + 1] = x.y;
+				fn[4 * k + 2] = x.z;
+				fn[4 * k + 3] = x.w;
+			}
+		}
+		first = false;
+		for (uint32_t k = 0; k < nk; ++k) {
+			const uint32_t t = t0 + k * nwaves;
+			const uint32_t i = t * 64u + lane;
+			const bool live = i < num;
+
+			/* previous tile's verdict, stored before this tile's prefetch
+			 * (vector-memory counters retire in issue order) */
+			if (pend)
+				A.out[pend_i] = pend_w;
+			pend = false;
+			uint32_t f[16];
+
+#pragma unroll
+			for (int q = 0; q < 16; ++q)
+				f[q] = fn[q];
+			if (k + 1u < nk) {
+				const uint32_t inx = min((t + nwaves) * 64u + lane, num - 1u);
+				const uint4 *src = A.frames + (size_t)inx * 4u;
+
+#pragma unroll
+				for (int q = 0; q < 4; ++q) {
+					const uint4 x = ld_stream(src + q);
+
+					fn[4 * q + 0] = x.x;
+					fn[4 * q + 1] = x.y;
+					fn[4 * q + 2] = x.z;
+					fn[4 * q + 3] = x.w;
+				}
+			}
+			if (__ballot(live && !plain_v4(f)) != 0ull) {
+				defer |= 1ull << k;
+				continue;
+			}
+			/* register parse of plain frames + the table's key words at
+			 * fixed frame offsets (uniform register index, no per-slot
+			 * branches) */
+			uint32_t lo = 0u, hi = 0u;
+			uint32_t kv[HW ? NG : 1];
+			bool krq[HW ? NG : 1];
+#ifdef L64_EXP_SKELETON   /* experiment builds only: loads + stores floor */
+			const uint32_t w = f[3] ^ f[9];
+#else
+			const FastV r = parse_fast64(f, A.opt);
+
+			if (walk) {
+				const u32x16_t fv = {f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7],
+						     f[8], f[9], f[10], f[11], f[12], f[13], f[14], f[15]};
+				auto fast_key = [&](const MGd &d) -> uint32_t {
+					if (d.slot == SLOT_LEN)
+						return 64u;
+					return __builtin_amdgcn_alignbyte(fv[d.fw + 1u], fv[d.fw], d.fs);
+				};
+				if constexpr (HW) {
+#pragma unroll
+					for (int g = 0; g < NG; ++g) {
+						kv[g] = fast_key(mg[g]) & mg[g].mask;
+						krq[g] = (r.inf_lo & mg[g].req) == mg[g].req;
+					}
+				} else if constexpr (NG > 0) {
+#pragma unroll
+					for (int g = 0; g < NG; ++g)
+						probe(mg[g], fast_key(mg[g]), r.inf_lo, lo, hi);
+				} else {
+					for (uint32_t gi = 0; gi < A.num_mgroups; ++gi) {
+						const MGd d = load_mg(A.mgroups + gi);
+
+						probe(d, fast_key(d), r.inf_lo, lo, hi);
+					}
+				}
+			}
+			const uint32_t w = finish(live, false, r.err, r.wbits, lo, hi, kv, krq);
+#endif
+			pend = live;
+			pend_i = i;
+			pend_w = w;
+		}
+		if (pend)
+			A.out[pend_i] = pend_w;
+		pend = false;
+
+		/* ---- the chunk's deferred tiles: generic parse ------------------- */
+		while (defer) {
+			const uint32_t k = (uint32_t)__builtin_ctzll(defer);
+
+			defer &= defer - 1ull;
+			const uint32_t t = t0 + k * nwaves;
+			const uint32_t i = t * 64u + lane;
+			const bool live = i < num;
+			const uint4 *src = A.frames + (size_t)min(i, num - 1u) * 4u;
+			uint32_t f[16];
+
+#pragma unroll
+			for (int q = 0; q < 4; ++q) {
+				const uint4 x = ld_stream(src + q);
+
+				f[4 * q + 0] = x.x;
+				f[4 * q + 1] = x.y;
+				f[4 * q + 2] = x.z;
+				f[4 * q + 3] = x.w;
+			}
+			Bases b;
+			Pkt<64, false> v;
+
+			v.row = row;
+			v.g = (const uint8_t *)src;
+			v.len = 64u;
+#pragma unroll
+			for (int q = 0; q < 16; ++q)
+				row[q] = f[q];
+			Prs p;
+
+			p.inf = 0ull;
+			p.fl = 0u;
+			p.l2 = p.l3 = p.l4 = 0xffffu;
+			const int ret = live ? parse_common(p, v, A.layer, (uint64_t)A.opt) : 0;
+			uint32_t wbits = 0u;
+
+			if (p.inf & IF(IFL_L3_CHKSUM_DONE))
+				wbits |= (p.fl & FB(FL_L3_CHKSUM_ERR) ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 16;
+			if (p.inf & IF(IFL_L4_CHKSUM_DONE))
+				wbits |= (p.fl & FB(FL_L4_CHKSUM_ERR) ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 18;
+			const bool err = (p.fl & FL_ERROR_MASK) != 0u;
+
+			if (err)
+				wbits |= ODPG_OUT_ERROR;
+			if (ret)
+				wbits |= ODPG_OUT_PARSE_ERR;
+			const uint32_t inf_lo = (uint32_t)p.inf;
+
+			b.l2 = p.l2;
+			b.l3 = p.l3;
+			b.l4 = p.l4;
+			b.vlanx = 14u + ((p.inf & IF(IFL_VLAN_QINQ)) ? 4u : 0u);
+			b.len = 64u;
+			b.inf_lo = inf_lo;
+			uint32_t lo = 0u, hi = 0u;
+			uint32_t kv[HW ? NG : 1];
+			bool krq[HW ? NG : 1];
+
+			if (walk) {
+				KeySrc<64, false> key;
+
+				key.f = f;
+				key.v = &v;
+				key.b = &b;
+				key.fast = false;
+				if constexpr (HW) {
+#pragma unroll
+					for (int g = 0; g < NG; ++g) {
+						kv[g] = key(mg[g].slot) & mg[g].mask;
+						krq[g] = (inf_lo & mg[g].req) == mg[g].req;
+					}
+				} else if constexpr (NG > 0) {
+#pragma unroll
+					for (int g = 0; g < NG; ++g)
+						probe(mg[g], key(mg[g].slot), inf_lo, lo, hi);
+				} else {
+					for (uint32_t gi = 0; gi < A.num_mgroups; ++gi) {
+						const MGd d = load_mg(A.mgroups + gi);
+
+						probe(d, key(d.slot), inf_lo, lo, hi);
+					}
+				}
+			}
+			const uint32_t w = finish(live, ret < 0, err, wbits, lo, hi, kv, krq);
+
+			if (live)
+				A.out[i] = w;
+		}
+		t0 += nk * nwaves;
 	}
-	if (pend)
-		A.out[pend_i] = pend_w;
 	if (A.stats) {
 		const uint64_t v[4] = {n_pkt, (uint64_t)n_pkt * 64u, n_err, n_disc};
 
@@ -602,6 +661,10 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 
 	if (grid > occ_grid[hw])
 		grid = occ_grid[hw];
+#ifdef L64_EXP_GRIDENV   /* experiment builds only: ODPG_L64_GRID workgroups */
+	if (const char *ge = getenv("ODPG_L64_GRID"))
+		grid = (uint32_t)atoi(ge);
+#endif
 #define L64_LAUNCH(ng, h) hipLaunchKernelGGL((odpg_cls64_kernel<ng, h>), dim3(grid), dim3(BLOCK), lds, s, A)
 	if (hw) {
 		switch (a->num_cgroups) {

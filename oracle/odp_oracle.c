@@ -19,6 +19,7 @@
  * would read past the end of a frame (only for malformed/truncated frames)
  * read as zero here and on the GPU.
  */
+#include <sched.h>
 #include <stdint.h>
 #include <stddef.h>
 #include <string.h>
@@ -1009,12 +1010,21 @@ typedef struct {
 	uint32_t reps;
 	odpg_out_t *out;
 	uint64_t pk[4];
+	int cpu;             /* pin to this CPU, or -1 */
 } mt_arg_t;
 
 static void *mt_worker(void *p)
 {
 	mt_arg_t *a = p;
 	cls_t c = { a->rules, NULL };
+
+	if (a->cpu >= 0) {
+		cpu_set_t set;
+
+		CPU_ZERO(&set);
+		CPU_SET(a->cpu, &set);
+		pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+	}
 
 	for (uint32_t r = 0; r < a->reps; r++)
 		for (uint32_t i = a->lo; i < a->hi; i++)
@@ -1023,12 +1033,12 @@ static void *mt_worker(void *p)
 }
 
 /* Multi-threaded batch for the CPU baseline: contiguous slices per thread,
- * `reps` passes over the batch, per-CoS stats not collected. Returns the
- * number of threads used. */
+ * `reps` passes over the batch, per-CoS stats not collected; thread t is
+ * pinned to cpus[t] when cpus is given. Returns the number of threads used. */
 int oracle_classify_mt(const odpg_rules_t *rules, const uint8_t *frames,
 		       const odpg_desc_t *desc, uint32_t stride, uint32_t num,
 		       uint64_t opt, int layer, int classify, odpg_out_t *out,
-		       int nthreads, uint32_t reps)
+		       int nthreads, uint32_t reps, const int *cpus)
 {
 	pthread_t th[256];
 	mt_arg_t args[256];
@@ -1046,6 +1056,7 @@ int oracle_classify_mt(const odpg_rules_t *rules, const uint8_t *frames,
 		args[t].reps = reps;
 		args[t].out = out;
 		memset(args[t].pk, 0, sizeof(args[t].pk));
+		args[t].cpu = cpus ? cpus[t] : -1;
 		pthread_create(&th[t], NULL, mt_worker, &args[t]);
 	}
 	for (int t = 0; t < nthreads; t++)

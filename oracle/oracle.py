@@ -28,7 +28,7 @@ def _load():
     lib.oracle_classify.restype = i32
     lib.oracle_classify.argtypes = [vp, vp, vp, u32, u32, u64, i32, i32, vp, vp, vp, vp]
     lib.oracle_classify_mt.restype = i32
-    lib.oracle_classify_mt.argtypes = [vp, vp, vp, u32, u32, u64, i32, i32, vp, i32, u32]
+    lib.oracle_classify_mt.argtypes = [vp, vp, vp, u32, u32, u64, i32, i32, vp, i32, u32, vp]
     lib.oracle_chksum_ones_comp16.restype = C.c_uint16
     lib.oracle_chksum_ones_comp16.argtypes = [vp, u32]
     lib.oracle_crc32c.restype = u32
@@ -74,15 +74,21 @@ def classify(rules, frames, num, stride=0, desc=None, opt=0, layer=4, classify=T
 
 
 def classify_mt(rules, frames, num, stride=0, desc=None, opt=0, layer=4, classify=True,
-                nthreads=1, reps=1):
+                nthreads=1, reps=1, cpus=None):
+    """Threads on contiguous slices, `reps` passes; thread t pinned to cpus[t]."""
     frames = np.ascontiguousarray(frames, dtype=np.uint8)
     dptr = None
     if desc is not None:
         desc = np.ascontiguousarray(desc, dtype=DESC_DT)
         dptr = desc.ctypes.data
     out = np.zeros(num, np.uint32)
+    cp = None
+    if cpus is not None:
+        cp = np.ascontiguousarray(cpus[:nthreads], dtype=np.int32)
+        assert len(cp) == nthreads
     n = lib.oracle_classify_mt(C.byref(rules), frames.ctypes.data, dptr, stride, num, opt,
-                               layer, int(bool(classify)), out.ctypes.data, nthreads, reps)
+                               layer, int(bool(classify)), out.ctypes.data, nthreads, reps,
+                               cp.ctypes.data if cp is not None else None)
     return out, n
 
 

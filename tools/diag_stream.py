@@ -25,13 +25,21 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--grids", default="0,1024,1280,2048,4096")
     ap.add_argument("--patterns", default="0,1,2,16,17,18")
+    ap.add_argument("--fill", default="zero", choices=["zero", "c2"],
+                    help="buffer contents: zeros, or the C2 bench frames")
     a = ap.parse_args()
     ctx = gpu.Context(0)
     n = a.npkt
     nbuf = max(2, -(-300 * (1 << 20) // (n * 64)))
     src = [ctx.buffer(n * 64) for _ in range(nbuf)]
+    if a.fill == "c2":
+        from odp_amd import gen
+        fr = gen.c2_frames(n)
     for b in src:
-        b.zero()
+        if a.fill == "c2":
+            b.upload(fr)
+        else:
+            b.zero()
     outs = [ctx.buffer(4 * n) for _ in range(nbuf)]
     lib = L.lib
     for pat in [int(x) for x in a.patterns.split(",")]:
@@ -48,7 +56,8 @@ def main():
             ms = C.c_float(0)
             L.check(lib.odpg_event_elapsed_ms(ctx.h, 0, 1, C.byref(ms)), "event")
             us = ms.value * 1e3 / a.steps
-            print(json.dumps({"npkt": n, "pattern": pat, "grid": grid, "us": round(us, 2),
+            print(json.dumps({"npkt": n, "fill": a.fill, "pattern": pat, "grid": grid,
+                              "us": round(us, 2),
                               "GBps": round(68 * n / (us * 1e-6) / 1e9, 1),
                               "Mpps": round(n / us, 1)}), flush=True)
 
