@@ -24,6 +24,8 @@
  * global atomics).
  */
 #include <hip/hip_runtime.h>
+#include <mutex>
+#include <vector>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -1224,44 +1226,108 @@ __global__ __launch_bounds__(BLOCK) void odpg_stats_reduce_kernel(
 
 extern "C" uint32_t odpg_launch_grid(uint32_t num);
 
-template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST = false, bool LEAN = false>
-static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStream_t s)
+/* dynamic LDS of one odpg_classify_kernel launch (its carve-up, kernel
+ * prologue); mode 3 reads the walk groups through the hgroup / hent fields */
+static size_t lds_need(const odpg_launch_args &a, int mode, int w)
 {
-	size_t lds = (size_t)BLOCK * (W / 4 + 1) * 4u;
+	size_t lds = (size_t)BLOCK * (w / 4 + 1) * 4u;
 
 	if (a.cos_partial)
 		lds += (size_t)((a.num_cos + 3u) & ~3u) * 4u;
-	if (MODE == 2)
+	if (mode == 2)
 		lds += (size_t)BLOCK * (((a.num_pmr + 31u) >> 5) | 1u) * 4u;
-	const bool use_mg = MODE == 1 && (a.tbl_flags & TBL_MGROUPS);
+	const bool use_mg = mode == 1 && (a.tbl_flags & TBL_MGROUPS);
 
-	if (MODE != 0 && !use_mg && a.num_hent <= HENT_LDS_MAX)
+	if (mode != 0 && !use_mg && a.num_hent <= HENT_LDS_MAX)
 		lds += (size_t)a.num_hent * 8u;
 	if (use_mg)
 		lds += (size_t)a.num_ment * 16u;
-	if (MODE == 1)
+	if (mode == 1)
 		lds += (size_t)a.num_pmr * 8u + 4u;
-	if (MODE != 0)
+	if (mode != 0)
 		lds += (size_t)a.num_cos * 8u + (size_t)a.num_pmr * 4u;
-	if (MODE == 3 && (a.tbl_flags & TBL_XWALK))
+	if (mode == 3 && (a.tbl_flags & TBL_XWALK))
 		lds += (size_t)((a.num_cos + 1u) & ~1u) * 8u + (size_t)a.num_xwords * 4u + 16u;
+	return lds;
+}
+
+/* Resident grid of a kernel at a dynamic LDS size: occupancy x CUs of the
+ * current device, from hipOccupancyMaxActiveBlocksPerMultiprocessor; cached
+ * per (kernel, LDS bytes, device) under a lock (contexts on several threads
+ * and devices launch concurrently). */
+extern "C" uint32_t odpg_resident_grid(const void *kernel, size_t lds)
+{
+	struct Occ {
+		const void *k;
+		size_t lds;
+		int dev;
+		uint32_t grid;
+	};
+	static std::mutex m;
+	static std::vector<Occ> cache;
+	int dev = 0;
+
+	hipGetDevice(&dev);
+	{
+		std::lock_guard<std::mutex> g(m);
+
+		for (const Occ &o : cache)
+			if (o.k == kernel && o.lds == lds && o.dev == dev)
+				return o.grid;
+	}
+	int nb = 0, cus = 0;
+
+	hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, BLOCK, lds) != hipSuccess ||
+	    nb <= 0)
+		nb = 1;
+	const uint32_t grid = (uint32_t)(nb * (cus > 0 ? cus : 256));
+	std::lock_guard<std::mutex> g(m);
+
+	cache.push_back({kernel, lds, dev, grid});
+	return grid;
+}
+
+/* the device's LDS per workgroup (160 KiB on gfx950), per device */
+extern "C" size_t odpg_lds_limit(void)
+{
+	static size_t lim[64];
+	int dev = 0;
+
+	hipGetDevice(&dev);
+	if (dev < 0 || dev >= 64)
+		return 65536u;
+	size_t v = __atomic_load_n(&lim[dev], __ATOMIC_RELAXED);
+
+	if (!v) {
+		hipDeviceProp_t pr;
+
+		v = hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.sharedMemPerBlock ?
+		    (size_t)pr.sharedMemPerBlock : 65536u;
+		__atomic_store_n(&lim[dev], v, __ATOMIC_RELAXED);
+	}
+	return v;
+}
+
+/* frame row width a launch of this layout uses (launch_layout below) */
+static int layout_w(const odpg_launch_args &a)
+{
+	if (a.desc)
+		return 64;   /* GF_W */
+	if (a.stride == 64 || a.stride == 128)
+		return a.stride;
+	return a.stride < 128 ? 128 : 96;
+}
+
+template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST = false, bool LEAN = false>
+static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStream_t s)
+{
+	const size_t lds = lds_need(a, MODE, W);
 	/* persistent grid: exactly the workgroups that are resident at once
 	 * (occupancy x CUs), each looping over tiles */
-	static size_t occ_lds = (size_t)-1;
-	static uint32_t occ_grid = 0;
+	const uint32_t occ_grid = odpg_resident_grid(
+		(const void *)odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST, LEAN>, lds);
 
-	if (occ_lds != lds) {
-		int nb = 0, dev = 0, cus = 0;
-
-		hipGetDevice(&dev);
-		hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-			    &nb, odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST, LEAN>, BLOCK, lds) !=
-		    hipSuccess || nb <= 0)
-			nb = 1;
-		occ_grid = (uint32_t)(nb * (cus > 0 ? cus : 256));
-		occ_lds = lds;
-	}
 	if (!getenv("ODPG_GRID_CAP") && grid > occ_grid)
 		grid = occ_grid;
 	hipLaunchKernelGGL((odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST, LEAN>), dim3(grid),
@@ -1324,7 +1390,10 @@ static bool lean64_ok(const odpg_launch_args &a)
 	const bool hw = (a.tbl_flags & TBL_LEAN64HW) && a.num_cgroups >= 1u && a.num_cgroups <= 4u &&
 			a.num_cos < ODPG_COS_NOCLS;
 
+	extern size_t odpg_cls64_lds(const odpg_launch_args &a);
+
 	return !off && a.mode == 0 && !a.desc && a.stride == 64 && (mg || hw) &&
+	       odpg_cls64_lds(a) <= odpg_lds_limit() &&
 	       !(a.tbl_flags & (TBL_GENERIC | TBL_ANY_HASHQ)) &&
 	       !a.mark && !a.meta && !(a.stats && (a.tbl_flags & TBL_ANY_STATS)) &&
 	       a.layer >= LAYER_L4 && a.classify &&
@@ -1401,6 +1470,21 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 		mode = 1;
 	if (mode == 3 && !simple && !(a->tbl_flags & TBL_XWALK))
 		mode = 1;
+	{
+		/* a table too large for a strategy's LDS carve-up (a hash-walk or
+		 * hybrid-walk table near the raised limits) takes the walk, whose
+		 * rule tables stay in global memory */
+		odpg_launch_args w = *a;
+
+		if (mode == 3) {
+			w.num_hent = a->num_went;
+			w.hgroups = a->wgroups;
+		}
+		const int kmode = mode == 1 ? 0 : mode == 2 ? (a->num_pmr <= 64 ? 1 : 2) : 3;
+
+		if (kmode != 0 && lds_need(w, kmode, layout_w(*a)) > odpg_lds_limit())
+			mode = 1;
+	}
 	if (mode == 3) {
 		/* the hash walk reads its CoS-keyed groups through the
 		 * exact-match group arguments */

@@ -42,6 +42,12 @@
 #ifndef L64_WAVES
 #define L64_WAVES 6
 #endif
+#ifndef L64_BUF          /* frames / verdicts through range-checked buffer ops */
+#define L64_BUF 0
+#endif
+#ifndef L64_PP           /* two frame buffers used in turn (else one, rotated) */
+#define L64_PP 0
+#endif
 
 struct L64Args {
 	const uint4 *frames;
@@ -51,19 +57,19 @@ struct L64Args {
 	uint32_t num_mgroups;
 	const dmgroup_t *mgroups;
 	const uint4 *ments;
-	const uint2 *pinfo2;
 	uint32_t num_ment, num_pmr, num_cos;
 	/* HW kernels: cuckoo groups, their entries, pinfo3 */
 	const dmgroup_t *cgroups;
 	const uint2 *cents;
 	uint32_t num_cent;
 	const uint2 *pinfo3;
+	const uint4 *pinfo4;   /* mask groups: {dst | mark << 16, action, rule mask lo, hi} */
+	uint32_t def_mlo, def_mhi;   /* the default CoS's rule mask */
 	uint32_t def_cgmask;
 	uint32_t err_cos;      /* error CoS, or ODPG_COS_NONE */
 	uint32_t err_act;      /* its action */
 	uint32_t def_cos;      /* CoS of error-free packets before the walk */
 	uint32_t def_act;
-	uint32_t def_ci;       /* default rule range rs | nr << 8 (mask groups) */
 	uint32_t def_rules;    /* the default CoS is valid and has rules: walk */
 	odpg_out_t *out;
 	uint64_t *stats;       /* pktio counters (odpg.h), or NULL */
@@ -168,15 +174,18 @@ __device__ __forceinline__ FastV parse_fast64(const uint32_t (&f)[16], uint32_t 
 	return r;
 }
 
-/* one mask group's descriptor, wave-uniform (SGPRs) */
+/* one mask group's descriptor, wave-uniform (SGPRs): sh == 0 marks a
+ * single-value group ({value, lo, hi} in {m1, m2, off}, dmgroup_t.count 1) */
 struct MGd {
-	uint32_t slot, req, mask, sh, off, m1, m2, cnt;
-	uint32_t fw, fs;   /* key word of a plain frame: bytes [4 fw + fs, +4) */
+	uint32_t slot, o, req, mask, sh, off, m1, m2;
+	/* o: frame byte offset of the slot word in a plain Eth/IPv4 frame */
 };
 
 typedef uint32_t u32x16_t __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ MGd load_mg(const dmgroup_t *g)
+/* single: mask groups (count 1 = one inline value); cuckoo groups keep sh */
+__device__ __forceinline__ MGd load_mg(const dmgroup_t *g, bool single = true)
 {
 	const uint4 g0 = *(const uint4 *)g;
 	const uint4 g1 = *((const uint4 *)g + 1);
@@ -185,20 +194,17 @@ __device__ __forceinline__ MGd load_mg(const dmgroup_t *g)
 	d.slot = __builtin_amdgcn_readfirstlane(g0.x);
 	d.req = __builtin_amdgcn_readfirstlane(g0.y);
 	d.mask = __builtin_amdgcn_readfirstlane(g0.z);
-	d.sh = __builtin_amdgcn_readfirstlane(g0.w);
+	d.sh = single && __builtin_amdgcn_readfirstlane(g1.w) == 1u ? 0u
+								 : __builtin_amdgcn_readfirstlane(g0.w);
 	d.off = __builtin_amdgcn_readfirstlane(g1.x);
 	d.m1 = __builtin_amdgcn_readfirstlane(g1.y);
 	d.m2 = __builtin_amdgcn_readfirstlane(g1.z);
-	d.cnt = __builtin_amdgcn_readfirstlane(g1.w);
 	/* frame offset of the slot word in a plain Eth/IPv4 frame (l3 14, l4 34;
 	 * the VLANX slot reads l3's word, its VLAN gate fails there) */
-	const uint32_t o = d.slot < SLOT_VLANX ? 4u * d.slot :
-			   d.slot < SLOT_L3 ? 14u :
-			   d.slot < SLOT_L4 ? 14u + 4u * (d.slot - SLOT_L3) :
-			   d.slot < SLOT_LEN ? 34u + 4u * (d.slot - SLOT_L4) : 0u;
-
-	d.fw = o >> 2;
-	d.fs = o & 3u;
+	d.o = d.slot < SLOT_VLANX ? 4u * d.slot :
+	      d.slot < SLOT_L3 ? 14u :
+	      d.slot < SLOT_L4 ? 14u + 4u * (d.slot - SLOT_L3) :
+	      d.slot < SLOT_LEN ? 34u + 4u * (d.slot - SLOT_L4) : 0u;
 	return d;
 }
 
@@ -214,35 +220,37 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 	constexpr uint32_t RW = 17;                     /* odd dword row stride */
 	uint32_t *row = smem + threadIdx.x * RW;        /* generic-parse LDS row */
 	uint4 *ments = (uint4 *)(smem + BLOCK * RW);
-	uint2 *pinfo2 = (uint2 *)(ments + A.num_ment);
+	uint4 *pinfo4 = ments + A.num_ment;
 	/* HW: cuckoo entries, pinfo3 */
 	uint2 *cents = (uint2 *)(smem + BLOCK * RW);
 	uint2 *pinfo3 = cents + A.num_cent;
 
 	const uint32_t lane = __lane_id();
-	const uint32_t gw = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+	/* wave-uniform (readfirstlane): buffer resources are built from it */
+	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6));
 	const uint32_t nwaves = gridDim.x * (BLOCK / 64);
 	const uint32_t ntiles = (A.num + 63u) >> 6;
 	const uint32_t num = A.num;
 	uint32_t fn[16];
 
-	/* first tile's frames issued before the table copy (index clamped into
-	 * the batch: the loads always issue, so the wait counts stay exact) */
+	MGd mg[NG > 0 ? NG : 1];
+	/* the first tile's frames are issued before the table copy below */
 	{
-		const uint32_t i0 = min(gw * 64u + lane, num - 1u);
-		const uint4 *src = A.frames + (size_t)i0 * 4u;
+		const uint32_t n0 = gw < ntiles ? min(num - gw * 64u, 64u) : 0u;
+		const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+			(void *)(A.frames + (size_t)(gw < ntiles ? gw : 0u) * 256u), 0, (int)(n0 * 64u),
+			0x00020000);
 
 #pragma unroll
-		for (int k = 0; k < 4; ++k) {
-			const uint4 x = ld_stream(src + k);
+		for (int q = 0; q < 4; ++q) {
+			const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(lane * 64u + q * 16u), 0, 0);
 
-			fn[4 * k + 0] = x.x;
-			fn[4 * k + 1] = x.y;
-			fn[4 * k + 2] = x.z;
-			fn[4 * k + 3] = x.w;
+			fn[4 * q + 0] = x.x;
+			fn[4 * q + 1] = x.y;
+			fn[4 * q + 2] = x.z;
+			fn[4 * q + 3] = x.w;
 		}
 	}
-	MGd mg[NG > 0 ? NG : 1];
 
 	if constexpr (HW) {
 		for (uint32_t k = threadIdx.x; k < A.num_cent; k += BLOCK)
@@ -251,12 +259,12 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 			pinfo3[k] = A.pinfo3[k];
 #pragma unroll
 		for (int g = 0; g < NG; ++g)
-			mg[g] = load_mg(A.cgroups + g);
+			mg[g] = load_mg(A.cgroups + g, false);
 	} else {
 		for (uint32_t k = threadIdx.x; k < A.num_ment; k += BLOCK)
 			ments[k] = A.ments[k];
 		for (uint32_t k = threadIdx.x; k < A.num_pmr; k += BLOCK)
-			pinfo2[k] = A.pinfo2[k];
+			pinfo4[k] = A.pinfo4[k];
 		if constexpr (NG > 0) {
 #pragma unroll
 			for (int g = 0; g < NG; ++g)
@@ -276,7 +284,7 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		const uint32_t kvm = key & d.mask;
 		const bool rq = (inf_lo & d.req) == d.req;
 
-		if (d.cnt == 1u) {
+		if (d.sh == 0u) {
 			const bool h = rq & (kvm == d.m1);
 
 			lo |= h ? d.m2 : 0u;
@@ -298,7 +306,6 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 			  const uint32_t *kv, const bool *krq) -> uint32_t {
 		uint32_t cos = err ? A.err_cos : A.def_cos;
 		uint32_t act = err ? A.err_act : A.def_act;
-		uint32_t ci = err ? 0u : A.def_ci;
 		uint32_t mark = 0u;
 		bool any_match = false;
 
@@ -341,24 +348,28 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 				gm = pi.y >> 12;
 			}
 		} else {
-			const uint64_t hits = ((uint64_t)hi << 32) | lo;
+			/* first hit among the current CoS's rules: the hit bits AND
+			 * the CoS's rule mask, lowest set bit; one LDS read per level
+			 * (pinfo4 carries the next CoS's mask) */
+			uint32_t mlo = err ? 0u : A.def_mlo, mhi = err ? 0u : A.def_mhi;
 
-			/* first hit in the current CoS's rule range, one LDS read
-			 * per level (pinfo2 carries the next range) */
 			if (live && !pdrop) {
 				uint32_t steps = 0u;
 
 				for (;;) {
-					const int k = first_hit64(hits, ci & 0xffu, (ci >> 8) & 0xffu);
+					const uint32_t xl = lo & mlo, xh = hi & mhi;
 
-					if (k < 0)
+					if ((xl | xh) == 0u)
 						break;
-					const uint2 pi = pinfo2[(ci & 0xffu) + (uint32_t)k];
+					const uint32_t k = xl ? (uint32_t)__builtin_ctz(xl)
+							      : 32u + (uint32_t)__builtin_ctz(xh);
+					const uint4 pi = pinfo4[k];
 
 					cos = pi.x & 0xffffu;
 					mark = pi.x >> 16;
-					ci = pi.y;
-					act = (pi.y >> 16) & 0xffu;
+					act = pi.y;
+					mlo = pi.z;
+					mhi = pi.w;
 					any_match = true;
 					if (++steps >= A.num_cos) {
 						cos = ODPG_COS_LOOP;
@@ -399,8 +410,137 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 	 * stays small (instruction cache) and no prefetch registers are live
 	 * across the generic parse (register pressure); the last tile of a chunk
 	 * issues no prefetch (a wave never re-reads past its last tile). */
-	bool pend = false;
-	uint32_t pend_i = 0u, pend_w = 0u;
+	/* Frames are read and verdicts written through buffer resources built
+	 * per tile from wave-uniform values: a resource covers exactly the
+	 * tile's frames in the batch (zero bytes for NO_TILE), so loads past
+	 * the batch return zeros without touching memory and stores past it are
+	 * dropped by the range check. Every load and store below is therefore
+	 * issued unconditionally, in a fixed order, and the compiler's counted
+	 * waits leave the other buffer's loads in flight. */
+	constexpr uint32_t NO_TILE = 0xffffffffu;
+	auto tile_n = [&](uint32_t t) -> uint32_t {    /* frames of tile t in the batch */
+		return t < ntiles ? min(num - t * 64u, 64u) : 0u;
+	};
+	auto load_tile = [&](uint32_t (&dst)[16], uint32_t t) {
+#if L64_BUF
+		const uint32_t tt = t < ntiles ? t : 0u;
+		const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+			(void *)(A.frames + (size_t)tt * 256u), 0, (int)(tile_n(t) * 64u), 0x00020000);
+
+#pragma unroll
+		for (int q = 0; q < 4; ++q) {
+			const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(lane * 64u + q * 16u), 0, 0);
+
+			dst[4 * q + 0] = x.x;
+			dst[4 * q + 1] = x.y;
+			dst[4 * q + 2] = x.z;
+			dst[4 * q + 3] = x.w;
+		}
+#else
+		if (t >= ntiles)
+			return;
+		const uint4 *src = A.frames + (size_t)min(t * 64u + lane, num - 1u) * 4u;
+
+#pragma unroll
+		for (int q = 0; q < 4; ++q) {
+			const uint4 x = ld_stream(src + q);
+
+			dst[4 * q + 0] = x.x;
+			dst[4 * q + 1] = x.y;
+			dst[4 * q + 2] = x.z;
+			dst[4 * q + 3] = x.w;
+		}
+#endif
+	};
+	uint32_t pend_t = NO_TILE, pend_w = 0u;
+	auto store_pending = [&]() {
+#if L64_BUF
+		const uint32_t tt = pend_t < ntiles ? pend_t : 0u;
+		const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+			(void *)(A.out + (size_t)tt * 64u), 0, (int)(tile_n(pend_t) * 4u), 0x00020000);
+
+		__builtin_amdgcn_raw_buffer_store_b32(pend_w, r, (int)(lane * 4u), 0, 0);
+#else
+		if (lane < tile_n(pend_t))
+			A.out[pend_t * 64u + lane] = pend_w;
+#endif
+		pend_t = NO_TILE;
+	};
+
+	/* One tile from a frame buffer whose loads were issued earlier: the
+	 * previous tile's verdict is stored, then this tile is classified if
+	 * every live frame is plain (otherwise it is deferred). Returns true if
+	 * the tile was deferred. */
+	auto tile = [&](const uint32_t (&f)[16], uint32_t t) -> bool {
+		const bool live = lane < tile_n(t);
+
+		store_pending();
+		if (__ballot(live && !plain_v4(f)) != 0ull)
+			return true;
+		/* register parse of plain frames + the table's key words at fixed
+		 * frame offsets (uniform register index, no per-slot branches) */
+		uint32_t lo = 0u, hi = 0u;
+		uint32_t kv[HW ? NG : 1];
+		bool krq[HW ? NG : 1];
+#ifdef L64_EXP_SKELETON   /* experiment builds only: loads + stores floor */
+		const uint32_t w = f[3] ^ f[9];
+#else
+#ifdef L64_EXP_NOPARSE   /* experiment builds only: match without the parse */
+		FastV r;
+		r.wbits = f[2] & 0x00f00000u;
+		r.inf_lo = (uint32_t)(IF(IFL_L2) | IF(IFL_ETH) | IF(IFL_L3) | IF(IFL_IPV4) |
+				      IF(IFL_L4) | IF(IFL_UDP));
+		r.err = false;
+#else
+		const FastV r = parse_fast64(f, A.opt);
+#endif
+
+#ifdef L64_EXP_NOMATCH   /* experiment builds only: parse without the match */
+		if (false) {
+#else
+		if (walk) {
+#endif
+			const u32x16_t fv = {f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7],
+					     f[8], f[9], f[10], f[11], f[12], f[13], f[14], f[15]};
+			auto fast_key = [&](const MGd &d) -> uint32_t {
+				if (d.slot == SLOT_LEN)
+					return 64u;
+				return __builtin_amdgcn_alignbyte(fv[(d.o >> 2) + 1u], fv[d.o >> 2], d.o & 3u);
+			};
+			if constexpr (HW) {
+#pragma unroll
+				for (int g = 0; g < NG; ++g) {
+					kv[g] = fast_key(mg[g]) & mg[g].mask;
+					krq[g] = (r.inf_lo & mg[g].req) == mg[g].req;
+				}
+			} else if constexpr (NG > 0) {
+#pragma unroll
+				for (int g = 0; g < NG; ++g)
+					probe(mg[g], fast_key(mg[g]), r.inf_lo, lo, hi);
+			} else {
+				for (uint32_t gi = 0; gi < A.num_mgroups; ++gi) {
+					const MGd d = load_mg(A.mgroups + gi);
+
+					probe(d, fast_key(d), r.inf_lo, lo, hi);
+				}
+			}
+		}
+		const uint32_t w = finish(live, false, r.err, r.wbits, lo, hi, kv, krq);
+#endif
+		pend_t = t;
+		pend_w = w;
+		return false;
+	};
+
+	/* Tiles in chunks of up to 64 per wave. Inside a chunk only plain waves
+	 * are classified; frames arrive in two register buffers used in turn,
+	 * each refilled with the tile two steps ahead right after its tile is
+	 * classified, so a wave waiting for one tile has the next one in flight.
+	 * A tile with any other frame is marked in `defer` and classified after
+	 * the chunk by the generic parse, with its frames re-read: the hot loop
+	 * stays small (instruction cache) and no prefetch registers are live
+	 * across the generic parse (register pressure). */
+	uint32_t fb[16];   /* second frame buffer (ping-pong with fn) */
 	bool first = true;
 
 	for (uint32_t t0 = gw; t0 < ntiles;) {
@@ -408,100 +548,34 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		const uint32_t nk = left < 64u ? left : 64u;
 		uint64_t defer = 0ull;
 
-		if (!first) {
-			const uint32_t i0 = min(t0 * 64u + lane, num - 1u);
-			const uint4 *src = A.frames + (size_t)i0 * 4u;
-
-#pragma unroll
-			for (int k = 0; k < 4; ++k) {
-				const uint4 x = ld_stream(src + k);
-
-				fn[4 * k + 0] = x.x;
-				fn[4 * k + 1] = x.y;
-				fn[4 * k + 2] = x.z;
-				fn[4 * k + 3] = x.w;
-			}
-		}
+		if (!first)
+			load_tile(fn, t0);
 		first = false;
+#if L64_PP
+		load_tile(fb, nk > 1u ? t0 + nwaves : NO_TILE);
+		for (uint32_t k = 0; k < nk; k += 2u) {
+			const uint32_t t = t0 + k * nwaves;
+
+			if (tile(fn, t))
+				defer |= 1ull << k;
+			load_tile(fn, k + 2u < nk ? t + 2u * nwaves : NO_TILE);
+			if (tile(fb, k + 1u < nk ? t + nwaves : NO_TILE))
+				defer |= 2ull << k;
+			load_tile(fb, k + 3u < nk ? t + 3u * nwaves : NO_TILE);
+		}
+#else
 		for (uint32_t k = 0; k < nk; ++k) {
 			const uint32_t t = t0 + k * nwaves;
-			const uint32_t i = t * 64u + lane;
-			const bool live = i < num;
-
-			/* previous tile's verdict, stored before this tile's prefetch
-			 * (vector-memory counters retire in issue order) */
-			if (pend)
-				A.out[pend_i] = pend_w;
-			pend = false;
-			uint32_t f[16];
 
 #pragma unroll
 			for (int q = 0; q < 16; ++q)
-				f[q] = fn[q];
-			if (k + 1u < nk) {
-				const uint32_t inx = min((t + nwaves) * 64u + lane, num - 1u);
-				const uint4 *src = A.frames + (size_t)inx * 4u;
-
-#pragma unroll
-				for (int q = 0; q < 4; ++q) {
-					const uint4 x = ld_stream(src + q);
-
-					fn[4 * q + 0] = x.x;
-					fn[4 * q + 1] = x.y;
-					fn[4 * q + 2] = x.z;
-					fn[4 * q + 3] = x.w;
-				}
-			}
-			if (__ballot(live && !plain_v4(f)) != 0ull) {
+				fb[q] = fn[q];
+			load_tile(fn, k + 1u < nk ? t + nwaves : NO_TILE);
+			if (tile(fb, t))
 				defer |= 1ull << k;
-				continue;
-			}
-			/* register parse of plain frames + the table's key words at
-			 * fixed frame offsets (uniform register index, no per-slot
-			 * branches) */
-			uint32_t lo = 0u, hi = 0u;
-			uint32_t kv[HW ? NG : 1];
-			bool krq[HW ? NG : 1];
-#ifdef L64_EXP_SKELETON   /* experiment builds only: loads + stores floor */
-			const uint32_t w = f[3] ^ f[9];
-#else
-			const FastV r = parse_fast64(f, A.opt);
-
-			if (walk) {
-				const u32x16_t fv = {f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7],
-						     f[8], f[9], f[10], f[11], f[12], f[13], f[14], f[15]};
-				auto fast_key = [&](const MGd &d) -> uint32_t {
-					if (d.slot == SLOT_LEN)
-						return 64u;
-					return __builtin_amdgcn_alignbyte(fv[d.fw + 1u], fv[d.fw], d.fs);
-				};
-				if constexpr (HW) {
-#pragma unroll
-					for (int g = 0; g < NG; ++g) {
-						kv[g] = fast_key(mg[g]) & mg[g].mask;
-						krq[g] = (r.inf_lo & mg[g].req) == mg[g].req;
-					}
-				} else if constexpr (NG > 0) {
-#pragma unroll
-					for (int g = 0; g < NG; ++g)
-						probe(mg[g], fast_key(mg[g]), r.inf_lo, lo, hi);
-				} else {
-					for (uint32_t gi = 0; gi < A.num_mgroups; ++gi) {
-						const MGd d = load_mg(A.mgroups + gi);
-
-						probe(d, fast_key(d), r.inf_lo, lo, hi);
-					}
-				}
-			}
-			const uint32_t w = finish(live, false, r.err, r.wbits, lo, hi, kv, krq);
-#endif
-			pend = live;
-			pend_i = i;
-			pend_w = w;
 		}
-		if (pend)
-			A.out[pend_i] = pend_w;
-		pend = false;
+#endif
+		store_pending();
 
 		/* ---- the chunk's deferred tiles: generic parse ------------------- */
 		while (defer) {
@@ -602,6 +676,18 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 }
 
 /* ---- launch ----------------------------------------------------------------- */
+extern "C" uint32_t odpg_resident_grid(const void *kernel, size_t lds);
+
+/* dynamic LDS of a lean launch: generic-parse rows + the table copy */
+size_t odpg_cls64_lds(const odpg_launch_args &a)
+{
+	const bool hw = (a.tbl_flags & TBL_LEAN64HW) && !(a.tbl_flags & TBL_LEAN64);
+
+	return (size_t)BLOCK * 17u * 4u +
+	       (hw ? (size_t)a.num_cent * 8u + (size_t)a.num_pmr * 8u
+		   : (size_t)a.num_ment * 16u + (size_t)a.num_pmr * 16u);
+}
+
 extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 {
 	if (a->num == 0)
@@ -615,7 +701,6 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	A.num_mgroups = a->num_mgroups;
 	A.mgroups = a->mgroups;
 	A.ments = (const uint4 *)a->ments;
-	A.pinfo2 = (const uint2 *)a->pinfo2;
 	A.num_ment = a->num_ment;
 	A.num_pmr = a->num_pmr;
 	A.num_cos = a->num_cos;
@@ -623,44 +708,31 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	A.err_act = a->l64_err_act;
 	A.def_cos = a->l64_def_cos;
 	A.def_act = a->l64_def_act;
-	A.def_ci = a->l64_def_ci;
 	A.def_rules = a->l64_def_rules;
 	A.cgroups = a->cgroups;
 	A.cents = (const uint2 *)a->cents;
 	A.num_cent = a->num_cent;
 	A.pinfo3 = (const uint2 *)a->pinfo3;
+	A.pinfo4 = (const uint4 *)a->pinfo4;
+	A.def_mlo = a->l64_def_mlo;
+	A.def_mhi = a->l64_def_mhi;
 	A.def_cgmask = a->def_cgmask;
 	A.out = a->out;
 	A.stats = a->stats;
 	A.sred = a->sred;
 
 	const bool hw = (a->tbl_flags & TBL_LEAN64HW) && !(a->tbl_flags & TBL_LEAN64);
-	size_t lds = (size_t)BLOCK * 17u * 4u +
-			   (hw ? (size_t)a->num_cent * 8u + (size_t)a->num_pmr * 8u
-			       : (size_t)a->num_ment * 16u + (size_t)a->num_pmr * 8u);
+	size_t lds = odpg_cls64_lds(*a);
 #ifdef L64_LDS_PAD   /* experiment builds only: occupancy sensitivity */
 	lds += L64_LDS_PAD;
 #endif
-	static size_t occ_lds[2] = {(size_t)-1, (size_t)-1};
-	static uint32_t occ_grid[2] = {0, 0};
-
-	if (occ_lds[hw] != lds) {
-		int nb = 0, dev = 0, cus = 0;
-
-		hipGetDevice(&dev);
-		hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-			    &nb, hw ? odpg_cls64_kernel<1, true> : odpg_cls64_kernel<0, false>, BLOCK,
-			    lds) != hipSuccess || nb <= 0)
-			nb = 1;
-		occ_grid[hw] = (uint32_t)(nb * (cus > 0 ? cus : 256));
-		occ_lds[hw] = lds;
-	}
+	const uint32_t occ = odpg_resident_grid(
+		hw ? (const void *)odpg_cls64_kernel<1, true> : (const void *)odpg_cls64_kernel<0, false>, lds);
 	const uint32_t ntiles = (a->num + 63u) / 64u;
 	uint32_t grid = (ntiles + 3u) / 4u;
 
-	if (grid > occ_grid[hw])
-		grid = occ_grid[hw];
+	if (grid > occ)
+		grid = occ;
 #ifdef L64_EXP_GRIDENV   /* experiment builds only: ODPG_L64_GRID workgroups */
 	if (const char *ge = getenv("ODPG_L64_GRID"))
 		grid = (uint32_t)atoi(ge);

@@ -980,6 +980,21 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		}
 	}
 
+	std::vector<uint32_t> pinfo4;
+
+	if (pmr.size() <= MGROUP_MAX_PMR) {
+		pinfo4.resize(4 * pmr.size());
+		for (size_t k = 0; k < pmr.size(); k++) {
+			const dcos_t &d = cos[pmr[k].dst];
+			const uint64_t m = d.nrule ? ((d.nrule >= 64 ? ~0ull : ((1ull << d.nrule) - 1ull))
+						      << d.rule_start) : 0ull;
+
+			pinfo4[4 * k] = pinfo[k];
+			pinfo4[4 * k + 1] = d.action;
+			pinfo4[4 * k + 2] = (uint32_t)m;
+			pinfo4[4 * k + 3] = (uint32_t)(m >> 32);
+		}
+	}
 	std::vector<uint32_t> pinfo3;
 
 	if (h.num_cgroups) {
@@ -1025,7 +1040,8 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.cgroup_off = align(h.pinfo2_off + (uint32_t)(pinfo2.size() * 4u));
 	h.cent_off = align(h.cgroup_off + h.num_cgroups * (uint32_t)sizeof(dmgroup_t));
 	h.pinfo3_off = align(h.cent_off + h.num_cent * (uint32_t)sizeof(dwent_t));
-	h.xcos_off = align(h.pinfo3_off + (uint32_t)(pinfo3.size() * 4u));
+	h.pinfo4_off = align(h.pinfo3_off + (uint32_t)(pinfo3.size() * 4u));
+	h.xcos_off = align(h.pinfo4_off + (uint32_t)(pinfo4.size() * 4u));
 	h.xlist_off = align(h.xcos_off + (uint32_t)(xcos.size() * 4u));
 	h.blob_bytes = align(h.xlist_off + (uint32_t)(xlist.size() * 4u));
 	if (h.blob_bytes == 0)
@@ -1064,6 +1080,8 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		memcpy(blob.data() + h.ment_off, ments.data(), ments.size() * sizeof(dment_t));
 	if (!pinfo2.empty())
 		memcpy(blob.data() + h.pinfo2_off, pinfo2.data(), pinfo2.size() * 4u);
+	if (!pinfo4.empty())
+		memcpy(blob.data() + h.pinfo4_off, pinfo4.data(), pinfo4.size() * 4u);
 	if (h.num_cgroups) {
 		memcpy(blob.data() + h.cgroup_off, cgroups.data(), cgroups.size() * sizeof(dmgroup_t));
 		memcpy(blob.data() + h.cent_off, cents.data(), cents.size() * sizeof(dwent_t));

@@ -207,7 +207,9 @@ typedef struct dment_s {
 
 /* pinfo2[num_pmr] (u64 hit-map kernel): the first-match resolve follows one
  * LDS read per level, {dst | mark << 16, dst rule_start | dst nrule << 8 |
- * dst action << 16} */
+ * dst action << 16}. pinfo4[num_pmr] (lean kernel): {dst | mark << 16, dst
+ * action, dst rule mask lo, hi}, the mask holding the hit-map bits of the
+ * destination's rules, so a level is one AND + find-first-set. */
 
 #if defined(__HIPCC__)
 #define ODPG_HD __host__ __device__
@@ -275,6 +277,7 @@ typedef struct dtable_hdr_s {
 	uint32_t cent_off;   /* dwent_t[num_cent] */
 	uint32_t num_cent;
 	uint32_t pinfo3_off; /* uint2[num_pmr] (TBL_LEAN64HW) */
+	uint32_t pinfo4_off; /* uint4[num_pmr] when num_pmr <= 64 (lean kernel) */
 	uint32_t def_cgmask; /* cuckoo groups holding a rule of the default CoS */
 	uint32_t xcos_off;   /* uint2[num_cos] (TBL_XWALK): {xlist start | count << 16,
 	                      *  walk groups holding a single-word rule of the CoS} */
@@ -328,6 +331,7 @@ typedef struct odpg_launch_args {
 	const dwent_t *cents;
 	uint32_t num_cent;
 	const uint2_t *pinfo3;
+	const uint32_t *pinfo4;     /* uint4 entries */
 	uint32_t def_cgmask;
 	const uint2_t *xcos;        /* TBL_XWALK */
 	const uint32_t *xlist;
@@ -335,6 +339,7 @@ typedef struct odpg_launch_args {
 	/* lean 64-byte kernel (classify64.hip): CoS start state, from the host
 	 * copy of the table */
 	uint32_t l64_err_cos, l64_err_act, l64_def_cos, l64_def_act, l64_def_ci, l64_def_rules;
+	uint32_t l64_def_mlo, l64_def_mhi;   /* the default CoS's rule mask (pinfo4 form) */
 	int mode;          /* 0 auto, 1 walk, 2 evaluate-all, 3 hash walk */
 	odpg_out_t *out;
 	uint16_t *mark;

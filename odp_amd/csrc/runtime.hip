@@ -320,6 +320,7 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.cents = (const dwent_t *)((const uint8_t *)t->dblob + h.cent_off);
 	a.num_cent = h.num_cent;
 	a.pinfo3 = (const uint2_t *)((const uint8_t *)t->dblob + h.pinfo3_off);
+	a.pinfo4 = (const uint32_t *)((const uint8_t *)t->dblob + h.pinfo4_off);
 	a.def_cgmask = h.def_cgmask;
 	a.xcos = (const uint2_t *)((const uint8_t *)t->dblob + h.xcos_off);
 	a.xlist = (const uint32_t *)((const uint8_t *)t->dblob + h.xlist_off);
@@ -339,6 +340,12 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 		a.l64_def_rules = dvalid && hc[dc].nrule;
 		a.l64_def_ci = dvalid && hc[dc].nrule ?
 			       (hc[dc].rule_start & 0xffu) | ((uint32_t)(hc[dc].nrule & 0xffu) << 8) : 0u;
+		const uint64_t dm = dvalid && hc[dc].nrule && hc[dc].rule_start < 64u ?
+				    (hc[dc].nrule >= 64u ? ~0ull : ((1ull << hc[dc].nrule) - 1ull))
+				    << hc[dc].rule_start : 0ull;
+
+		a.l64_def_mlo = (uint32_t)dm;
+		a.l64_def_mhi = (uint32_t)(dm >> 32);
 	}
 	a.mode = c->kernel_mode;
 	a.out = r->out;
@@ -470,6 +477,8 @@ int odpg_classify_host(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t 
 		return -EINVAL;
 	if ((rc = validate_batch(b)))
 		return rc;
+	if (t->device != c->device)
+		return -EXDEV;
 	if (b->num == 0)
 		return 0;
 	if (chunk == 0)

@@ -452,3 +452,36 @@ def test_hybrid_walk_random_rules(gpu_ctx, fresh_cls, seed):
         g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), buf, len(frames), desc=desc, opt=opt)
         assert_same(g, o, f"random rules seed={seed} opt={opt}")
     assert len(np.unique(g["out"] & 0xFFFF)) > 3
+
+
+def test_table_larger_than_lds(gpu_ctx, fresh_cls):
+    """A hash-walk table near the raised limits (16 SIP CoS x 1000 UDP_DPORT
+    rules, 16016 PMRs): its CoS-keyed groups exceed a workgroup's LDS, so the
+    lean kernel and the LDS-resident strategies fall back to the walk instead
+    of failing the launch; every strategy stays bit-exact."""
+    c, T = fresh_cls, fresh_cls.Term
+    assert c.set_limits(2048, 16384, 1024) == 0
+    p = c.loop_pktio(pktin=ALL_CHKSUM)
+    d = c.cos_create("d", queue=c.queue(0))
+    assert c.default_cos_set(p, d) == 0
+    leaves = [c.cos_create(f"leaf{j}", queue=c.queue(100 + j)) for j in range(1000)]
+    for a in range(16):
+        l1 = c.cos_create(f"l1_{a}", queue=c.queue(10 + a))
+        assert c.pmr_create([T(c.PMR_SIP_ADDR, gen.be_bytes(gen.ip4("10.0.0.0") | (a << 12), 4),
+                               gen.be_bytes(0xFFFFF000, 4))], d, l1)
+        for j in range(1000):
+            assert c.pmr_create([T(c.PMR_UDP_DPORT, gen.be_bytes(j, 2), b"\xff\xff")], l1, leaves[j])
+    assert c.pktio_start(p) == 0
+    n = 64 * 300
+    fr = gen.c2_frames(n).reshape(n, 64).copy()
+    rng = np.random.default_rng(3)
+    src = (gen.ip4("10.0.0.0") + rng.integers(0, 1 << 17, n)).astype(np.uint64)
+    fr[:, 26:30] = np.stack([(src >> s) & 0xFF for s in (24, 16, 8, 0)], 1).astype(np.uint8)
+    dport = rng.integers(0, 1100, n)
+    fr[:, 36] = dport >> 8
+    fr[:, 37] = dport & 0xFF
+    fr = fr.reshape(-1)
+    # checksums are not verified (pktin 0): the edited frames still parse plainly
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, n, stride=64, opt=0)
+    assert_same(g, o, "16k-PMR hash walk")
+    assert len(np.unique(g["out"] & 0xFFFF)) > 500
