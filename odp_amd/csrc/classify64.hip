@@ -116,10 +116,11 @@ __device__ __forceinline__ FastV parse_fast64(const uint32_t (&f)[16], uint32_t 
 
 	inf |= udp ? (uint32_t)IF(IFL_UDP) : (uint32_t)IF(IFL_TCP);
 	r.inf_lo = inf;
-	r.err = false;
 	uint32_t wb = 0u;
+	bool l3bad = false;
 
-	/* IPv4 header checksum over bytes 14..33 (parse_ipv4, odp_parse.c:134-141) */
+	/* IPv4 header checksum over bytes 14..33 (parse_ipv4, odp_parse.c:134-141);
+	 * a bad one is ip_err: no L4 parse, no L4 verdict */
 	if (opt & ODPG_PKTIN_IPV4_CHKSUM) {
 		uint32_t s = d2(f[3], W01, 0u);
 
@@ -128,50 +129,50 @@ __device__ __forceinline__ FastV parse_fast64(const uint32_t (&f)[16], uint32_t 
 		s = d2(f[6], W11, s);
 		s = d2(f[7], W11, s);
 		s = d2(f[8], W10, s);
-		const bool bad = d2fold(s) != 0xffffu;
-
-		wb |= (bad ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 16;
-		if (bad) {
-			/* ip_err: no L4 parse, no L4 verdict */
-			r.wbits = wb | ODPG_OUT_ERROR | ODPG_OUT_PARSE_ERR;
-			r.err = true;
-			return r;
-		}
+		l3bad = d2fold(s) != 0xffffu;
+		wb = (l3bad ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 16;
 	}
-	const bool frag = (f[5] & 0xff3fu) != 0u;          /* be16(frag) & 0x3fff */
 	/* L4 checksum over the pseudo header and bytes 34..63
 	 * (_odp_packet_l4_chksum, odp_packet.c:1906-1984; length frame_len - 34):
 	 * src + dst, proto << 8, the length field (UDP: its own raw bytes 38..39,
-	 * counted again; TCP: be16(30)), then the segment */
-	const uint32_t need = udp ? ODPG_PKTIN_UDP_CHKSUM : ODPG_PKTIN_TCP_CHKSUM;
-	const bool zero_csum = udp && (f[10] & 0xffffu) == 0u;
-	bool done = false, bad = false;
+	 * counted again; TCP: be16(30)), then the segment. Branch-free per lane:
+	 * the sum is formed whenever either protocol's check is on. */
+	bool l4bad = false;
 
-	if ((opt & need) && !frag) {
-		if (zero_csum) {
-			done = true;                                 /* udp_chksum_zero, ok */
-		} else {
-			uint32_t s = udp ? 0x1100u : 0x1e00u + 0x0600u;
+	if (opt & (ODPG_PKTIN_UDP_CHKSUM | ODPG_PKTIN_TCP_CHKSUM)) {
+		const bool frag = (f[5] & 0xff3fu) != 0u;          /* be16(frag) & 0x3fff */
+		const uint32_t need = udp ? ODPG_PKTIN_UDP_CHKSUM : ODPG_PKTIN_TCP_CHKSUM;
+		const bool zero_csum = udp && (f[10] & 0xffffu) == 0u;
+		uint32_t s = udp ? 0x1100u : 0x1e00u + 0x0600u;
 
-			s = d2(f[6], W01, s);
-			s = d2(f[7], W11, s);
-			s = d2(f[8], W11, s);
-			s = d2(f[9], udp ? 0x00020001u : W11, s);
+		s = d2(f[6], W01, s);
+		s = d2(f[7], W11, s);
+		s = d2(f[8], W11, s);
+		s = d2(f[9], udp ? 0x00020001u : W11, s);
 #pragma unroll
-			for (int k = 10; k < 16; ++k)
-				s = d2(f[k], W11, s);
-			done = true;
-			bad = d2fold(s) != 0xffffu;
-		}
+		for (int k = 10; k < 16; ++k)
+			s = d2(f[k], W11, s);
+		const bool done = ((opt & need) != 0u) & !frag & !l3bad;   /* zero: udp_chksum_zero, ok */
+
+		l4bad = done & !zero_csum & (d2fold(s) != 0xffffu);
+		wb |= done ? (l4bad ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 18 : 0u;
 	}
-	if (done)
-		wb |= (bad ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 18;
-	if (bad) {
-		wb |= ODPG_OUT_ERROR | ODPG_OUT_PARSE_ERR;
-		r.err = true;
-	}
-	r.wbits = wb;
+	r.err = l3bad | l4bad;
+	r.wbits = wb | (r.err ? ODPG_OUT_ERROR | ODPG_OUT_PARSE_ERR : 0u);
 	return r;
+}
+
+/* plain_v4() (pkt_parse.h) without branches: Eth/IPv4 IHL 5 within the 64
+ * bytes, UDP with length >= 8 or TCP with data offset >= 5 */
+__device__ __forceinline__ bool plain64(const uint32_t (&f)[16])
+{
+	const uint32_t tot_len = swap16(f[4] & 0xffffu);
+	const uint32_t proto = f[5] >> 24;
+	const bool eth_ip = (f[3] & 0x00ffffffu) == 0x00450008u;   /* ethtype 0x0800, ver_ihl 0x45 */
+	const bool udp_ok = (proto == 0x11u) & (swap16(f[9] >> 16) >= 8u);
+	const bool tcp_ok = (proto == 0x06u) & (((f[11] >> 20) & 0xfu) >= 5u);
+
+	return eth_ip & (tot_len <= 64u - 14u) & (udp_ok | tcp_ok);
 }
 
 /* one mask group's descriptor, wave-uniform (SGPRs): sh == 0 marks a
@@ -475,7 +476,7 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		const bool live = lane < tile_n(t);
 
 		store_pending();
-		if (__ballot(live && !plain_v4(f)) != 0ull)
+		if (__ballot(live && !plain64(f)) != 0ull)
 			return true;
 		/* register parse of plain frames + the table's key words at fixed
 		 * frame offsets (uniform register index, no per-slot branches) */
