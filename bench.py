@@ -6,7 +6,9 @@ verdict + PMR -> CoS walk, odpg_classify) over one batch of 2^20 synthetic
 frames already resident in HBM, writing the 4-byte verdict per packet (CoS
 index + RX checksum status, the per-packet outputs the north star names). A
 second timed loop repeats the launches with the loopback_recv pktio counters
-added in every launch; it is reported as `with_pktio_counters`.
+(and the per-CoS / per-queue delivery counts) added in every launch, into the
+sharded device counters odp_pktio_stats reads; it is reported as
+`with_pktio_counters`.
 
 Launch:  python bench.py [--gpus N --steps K --warmup W --config c2]
          torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
@@ -146,9 +148,7 @@ def main():
             db.upload(desc)
             dbufs.append(db)
         obufs.append(ctx.buffer(4 * n))
-    nstats = 4 + tbl.num_cos
-    sbuf = ctx.buffer(8 * nstats)
-    sbuf.zero()
+    cnt = ctx.counters(tbl)
     layer, do_cls = {"full": (L.LAYER_ALL, 1), "parse": (L.LAYER_ALL, 0),
                      "parse-nochk": (L.LAYER_ALL, 0), "l3": (L.LAYER_L3, 0),
                      "none": (L.LAYER_NONE, 0)}[args.diag]
@@ -159,9 +159,11 @@ def main():
     # the timed launches produce what the north star names per packet: the
     # verdict word (CoS index, L3/L4 checksum status, error / drop bits). A
     # second timed loop adds the loopback_recv pktio counters (in_packets /
-    # in_octets / in_errors / in_discards, loop.c:304-374) to every launch.
-    results = [L.odpg_result_t(ob.ptr, None, None, None) for ob in obufs]
-    results_st = [L.odpg_result_t(ob.ptr, None, None, sbuf.ptr) for ob in obufs]
+    # in_octets / in_errors / in_discards, loop.c:304-374) and the per-queue
+    # delivery counts (_odp_cos_queue_stats_add) to every launch: sharded
+    # device counters (odpg.h), folded once when read.
+    results = [L.odpg_result_t(ob.ptr, None, None, None, None) for ob in obufs]
+    results_st = [L.odpg_result_t(ob.ptr, None, None, None, cnt.h) for ob in obufs]
     lib = L.lib
 
     def launch(i, res):
@@ -200,8 +202,12 @@ def main():
     if not args.no_stats:
         wall_st, kernel_ms_st = timed(results_st)
         wall_st = shard.max_over_ranks(wall_st, dist, dev)
-        # CoS / pktio counters summed over GPUs (RCCL)
-        stats = shard.reduce_counters(sbuf.download(np.uint64, nstats), dist, dev)
+        # the read-time fold, then CoS / pktio counters summed over GPUs (RCCL)
+        tf0 = time.perf_counter()
+        folded = cnt.fold()
+        fold_ms = (time.perf_counter() - tf0) * 1e3
+        stats = shard.reduce_counters(np.concatenate([folded["pktio"], folded["cos"]]),
+                                      dist, dev)
         # (experiment builds, ODPG_LIB, may skip the counter commit)
         if args.diag == "full" and not os.environ.get("ODPG_LIB"):
             # loopback_recv accounting: every packet is either delivered
@@ -216,8 +222,10 @@ def main():
         counted = {"value": round(n * world * args.steps / wall_st / 1e6, 1),
                    "ms_per_step": round(wall_st * 1e3 / max(args.steps, 1), 5),
                    "kernel_ms": round(kernel_ms_st, 5),
-                   "what": "same launches + pktio counters (in-kernel slot adds, one-wave fold "
-                           "kernel per launch)"}
+                   "fold_ms": round(fold_ms, 3),
+                   "what": "same launches + pktio and per-queue counters (per-workgroup rows of "
+                           "odpg_counters_t, no extra kernel per launch; fold_ms = the one "
+                           "read-time fold)"}
 
     ms_per_step = wall * 1e3 / max(args.steps, 1)
     total_pkts = n * world * args.steps
@@ -257,6 +265,7 @@ def main():
         if args.e2e:
             out["e2e_host_path"] = e2e(ctx, tbl, frames, desc, n, stride, opt)
         print(json.dumps(out), flush=True)
+    cnt.close()
     del tbl
     ctx.close()
     if dist is not None:

@@ -353,9 +353,16 @@ int odpg_pktio_rules(odp_pktio_t pktio, odpg_rules_t *rules);
  * pktio/loop.c:276-374) for a whole batch on the GPU: parse layer ALL when
  * the classifier is enabled (odp_packet_io.c:709-711), the pktio's pktin
  * checksum options, the current rule table (compiled and cached per
- * generation), then the pktio (in_*) and CoS / queue counters are updated.
- * device_ptrs != 0: frames/desc/out/mark are device pointers; otherwise host
- * pointers (pinned preferred) streamed through odpg_classify_host(). */
+ * generation and context), then the pktio (in_*) and CoS / queue counters are
+ * updated: the launch adds them into device-resident sharded counters
+ * (odpg.h), folded when odp_pktio_stats / odp_cls_cos_stats /
+ * odp_cls_queue_stats / odp_pktio_stats_reset read them.
+ * device_ptrs != 0: frames/desc/out/mark are device pointers and the call is
+ * asynchronous on the context stream like odpg_classify() (odpg_ctx_sync()
+ * before reading out/mark); otherwise host pointers (pinned preferred)
+ * streamed through odpg_classify_host(), synchronous. The classifier lock is
+ * not held across the GPU work: receives on different contexts or threads run
+ * concurrently. odp_pktio_close() fails while a receive is in flight. */
 int odpg_pktio_recv_batch(odp_pktio_t pktio, odpg_ctx_t *ctx,
 			  const uint8_t *frames, const odpg_desc_t *desc, uint32_t stride,
 			  uint32_t num, int device_ptrs, odpg_out_t *out, uint16_t *mark);

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define ODPG_ABI_VERSION 1
+#define ODPG_ABI_VERSION 2
 
 /* ---- limits ------------------------------------------------------------ */
 /* Reference limits (odp_classification_datamodel.h:31-46) are enforced by the
@@ -189,16 +189,37 @@ typedef struct odpg_batch_s {
  */
 #define ODPG_STATS_WORDS(num_cos) (4u + (num_cos))
 
+/* ---- opaque objects ---------------------------------------------------- */
+typedef struct odpg_ctx_s      odpg_ctx_t;
+typedef struct odpg_table_s    odpg_table_t;
+typedef struct odpg_counters_s odpg_counters_t;
+
 typedef struct odpg_result_s {
 	odpg_out_t  *out;    /* device, num words (required)             */
 	uint16_t    *mark;   /* device, num entries, or NULL             */
 	odpg_meta_t *meta;   /* device, num entries, or NULL             */
 	uint64_t    *stats;  /* device, ODPG_STATS_WORDS(num_cos), or NULL */
+	odpg_counters_t *counters;  /* sharded counters (below), or NULL; not
+				     * together with stats */
 } odpg_result_t;
 
-/* ---- opaque objects ---------------------------------------------------- */
-typedef struct odpg_ctx_s   odpg_ctx_t;
-typedef struct odpg_table_s odpg_table_t;
+/* ---- sharded counters ----------------------------------------------------
+ * The counts a launch makes (the pktio, CoS and per-queue counters the
+ * reference keeps as atomics: loop.c:304-374, odp_classification.c:1621-1622,
+ * 1697-1698, odp_classification_internal.h:64-78) accumulate in a device
+ * block with one row per workgroup of the resident grid: each workgroup adds
+ * its counts into its own row at its end (no atomics between workgroups, no
+ * extra kernel per launch). odpg_counters_fold() sums the rows, adds the
+ * totals to the caller's words and clears the rows, ordered on the context
+ * stream after every launch enqueued before it; the reference reads its
+ * counters the same way, at query time (odp_cls_cos_stats, odp_pktio_stats).
+ * A counters object belongs to one table (its CoS and queue layout) and one
+ * context. Folded layout (uint64_t words, added to):
+ *   [0..3]                    in_packets, in_octets, in_errors, in_discards
+ *   [4 + c]                   CoS c stats.packets (CoS with stats_enable)
+ *   [4 + num_cos + 32 c + q]  packets delivered to queue q of CoS c (the
+ *                             classifier returned 0: _odp_cls_enq input)  */
+#define ODPG_COUNTER_WORDS(num_cos) (4u + (num_cos) + (num_cos) * ODPG_COS_QUEUE_MAX)
 
 /* Library / device */
 int         odpg_abi_version(void);
@@ -233,6 +254,11 @@ int  odpg_table_create(odpg_ctx_t *ctx, const odpg_rules_t *rules, odpg_table_t 
 void odpg_table_destroy(odpg_table_t *tbl);
 uint32_t odpg_table_num_cos(const odpg_table_t *tbl);
 int  odpg_table_has_cycle(const odpg_table_t *tbl);
+
+int  odpg_counters_create(odpg_ctx_t *ctx, const odpg_table_t *tbl, odpg_counters_t **cnt);
+void odpg_counters_destroy(odpg_counters_t *cnt);
+/* Synchronous: words has ODPG_COUNTER_WORDS(odpg_table_num_cos(tbl)) entries. */
+int  odpg_counters_fold(odpg_counters_t *cnt, uint64_t *words);
 
 /* Device-resident batch: frames/desc/results all in HBM. Asynchronous on the
  * context stream. */

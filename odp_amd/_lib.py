@@ -14,6 +14,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ODPG_LIB") or os.path.join(_HERE, "lib", "libodpg.so")
 
 # ---- constants mirrored from include/odpg.h -------------------------------
+ABI_VERSION = 2
+COS_QUEUE_MAX = 32
 ODPG_COS_NONE = 0xFFFF
 ODPG_COS_PDROP = 0xFFFE
 ODPG_COS_LOOP = 0xFFFD
@@ -98,7 +100,7 @@ class odpg_batch_t(C.Structure):
 
 class odpg_result_t(C.Structure):
     _fields_ = [("out", C.c_void_p), ("mark", C.c_void_p), ("meta", C.c_void_p),
-                ("stats", C.c_void_p)]
+                ("stats", C.c_void_p), ("counters", C.c_void_p)]
 
 
 # ---- include/odpg_fwd.h -----------------------------------------------------
@@ -257,6 +259,9 @@ SIGNATURES = {
     "odpg_table_destroy": (None, [_vp]),
     "odpg_table_num_cos": (_u32, [_vp]),
     "odpg_table_has_cycle": (_i32, [_vp]),
+    "odpg_counters_create": (_i32, [_vp, _vp, C.POINTER(_vp)]),
+    "odpg_counters_destroy": (None, [_vp]),
+    "odpg_counters_fold": (_i32, [_vp, C.POINTER(C.c_uint64)]),
     "odpg_classify": (_i32, [_vp, _vp, C.POINTER(odpg_batch_t), C.POINTER(odpg_result_t)]),
     "odpg_classify_host": (_i32, [_vp, _vp, C.POINTER(odpg_batch_t),
                                   C.POINTER(odpg_result_t), _u32]),

@@ -201,6 +201,10 @@ def pktio_stats(pktio):
     return st
 
 
+def pktio_stats_reset(pktio):
+    return lib.odp_pktio_stats_reset(pktio)
+
+
 def default_cos_set(pktio, cos):
     return lib.odp_pktio_default_cos_set(pktio, cos)
 

@@ -349,7 +349,7 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 	odpg_meta_t *__restrict__ meta_out, uint64_t *__restrict__ pk_partial,
 	uint32_t *__restrict__ cos_partial, uint64_t *__restrict__ sred,
 	const uint2 *__restrict__ xcos_g, const uint32_t *__restrict__ xlist_g, uint32_t num_xent,
-	uint32_t num_xwords)
+	uint32_t num_xwords, const odpg_cnt_args cnt)
 {
 	constexpr uint32_t RW = W / 4 + 1;       /* odd dword row stride */
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -358,9 +358,12 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 	const bool use_mg = MODE == 1 && (tbl_flags & TBL_MGROUPS);
 	uint4 *ments_l = (uint4 *)(smem + BLOCK * RW);
 	uint32_t *cos_cnt = (uint32_t *)(ments_l + (use_mg ? num_ment : 0u));
-	/* MODE 2: per-lane PMR hit bitmap after the CoS counters */
+	/* sharded counters: per-queue delivered counts after the CoS counters */
+	const bool cos_words = cos_partial || (cnt.row && cnt.cos);
+	uint32_t *dlv = cos_cnt + (cos_words ? ((num_cos + 3u) & ~3u) : 0u);
+	/* MODE 2: per-lane PMR hit bitmap after the counters */
 	const uint32_t hrw = ((num_pmr + 31u) >> 5) | 1u;
-	uint32_t *hitmap = cos_cnt + (cos_partial ? ((num_cos + 3u) & ~3u) : 0u);
+	uint32_t *hitmap = dlv + (cnt.row ? ((cnt.ncols + 3u) & ~3u) : 0u);
 	/* exact-match hash tables, copied to LDS when small */
 	uint2 *hents_l = (uint2 *)(hitmap + (MODE == 2 ? BLOCK * hrw : 0u));
 	const bool hent_in_lds = !use_mg && num_hent <= HENT_LDS_MAX;
@@ -385,8 +388,8 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 		cos_partial = nullptr;
 		tbl_flags = (tbl_flags | TBL_SIMPLE) & ~(TBL_GENERIC | TBL_ANY_HASHQ);
 	}
-	const bool do_stats = pk_partial != nullptr;
-	const bool do_cos_stats = cos_partial != nullptr;
+	const bool do_stats = pk_partial != nullptr || cnt.row != nullptr;
+	const bool do_cos_stats = cos_partial != nullptr || (cnt.row && cnt.cos);
 	uint32_t *row = smem + tid * RW;
 	uint64_t lane_pkt = 0, lane_oct = 0, lane_err = 0, lane_disc = 0;
 
@@ -417,6 +420,9 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 	if (do_cos_stats)
 		for (uint32_t c = tid; c < num_cos; c += BLOCK)
 			cos_cnt[c] = 0u;
+	if (cnt.row)
+		for (uint32_t c = tid; c < cnt.ncols; c += BLOCK)
+			dlv[c] = 0u;
 	if (MODE != 0 && hent_in_lds)
 		for (uint32_t k = tid; k < num_hent; k += BLOCK)
 			hents_l[k] = *(const uint2 *)(hents_g + k);
@@ -1122,6 +1128,10 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 			w |= ODPG_OUT_PARSE_ERR;
 		uint32_t mk = (p.inf & IF(IFL_CLS_MARK)) ? mark : 0u;
 
+		/* packets handed to a CoS queue (_odp_cls_enq input; per-queue
+		 * counters, odp_classification_internal.h:64-78) */
+		if (cnt.row && cret == 0 && want_cls && cos < num_cos)
+			atomicAdd(&dlv[cnt.qcol[cos] + ((w >> 24) & 31u)], 1u);
 		pend_i = i;
 		pend_w = w;
 		pend_mk = mk;
@@ -1163,7 +1173,7 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 		uint64_t a = wave_sum_u64(lane_pkt), o = wave_sum_u64(lane_oct);
 		uint64_t e = wave_sum_u64(lane_err), d = wave_sum_u64(lane_disc);
 
-		if (sred) {
+		if (sred && !cnt.row) {
 			/* pktio counters only: committed in-kernel (stats_commit.h) */
 			const uint64_t v[4] = {a, o, e, d};
 
@@ -1175,8 +1185,23 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 			atomicAdd(&blk_pk[3], (unsigned long long)d);
 		}
 	}
-	if ((do_stats && !sred) || do_cos_stats)
+	if ((do_stats && (!sred || cnt.row)) || do_cos_stats)
 		__syncthreads();
+	if (cnt.row) {
+		/* this workgroup's row of the sharded counters (odpg.h) */
+		uint64_t *r = cnt.row + (size_t)blockIdx.x * cnt.words;
+
+		if (tid < 4 && blk_pk[tid])
+			r[tid] += blk_pk[tid];
+		if (do_cos_stats)
+			for (uint32_t c = tid; c < num_cos && c < cnt.ncos; c += BLOCK)
+				if (cos_cnt[c])
+					r[4u + c] += cos_cnt[c];
+		for (uint32_t c = tid; c < cnt.ncols; c += BLOCK)
+			if (dlv[c])
+				r[4u + cnt.ncos + c] += dlv[c];
+		return;
+	}
 	if (do_stats && !sred && tid < 4)
 		pk_partial[(size_t)blockIdx.x * 4u + tid] = blk_pk[tid];
 	if (do_cos_stats)
@@ -1221,6 +1246,50 @@ __global__ __launch_bounds__(BLOCK) void odpg_stats_reduce_kernel(
 	}
 }
 
+/* sharded counters (odpg.h): sum the rows into `sum` (zeroed by the caller)
+ * and clear them. Block (64 columns x 4 row lanes), blockIdx.y a band of
+ * FOLD_ROWS rows: coalesced 512-byte row segments, one atomic per column per
+ * band. Stream-ordered after the launches that wrote the rows. */
+#define FOLD_ROWS 32u
+
+__global__ __launch_bounds__(BLOCK) void odpg_counters_fold_kernel(
+	uint64_t *__restrict__ rows, uint32_t nrows, uint32_t words, uint64_t *__restrict__ sum)
+{
+	const uint32_t col = blockIdx.x * 64u + (threadIdx.x & 63u);
+	const uint32_t ty = threadIdx.x >> 6;
+	const uint32_t r0 = blockIdx.y * FOLD_ROWS;
+	__shared__ unsigned long long part[BLOCK / 64][64];
+	uint64_t s = 0;
+
+	if (col < words)
+		for (uint32_t r = r0 + ty; r < r0 + FOLD_ROWS && r < nrows; r += BLOCK / 64) {
+			uint64_t *p = rows + (size_t)r * words + col;
+			const uint64_t x = *p;
+
+			if (x) {
+				s += x;
+				*p = 0ull;
+			}
+		}
+	part[ty][threadIdx.x & 63u] = s;
+	__syncthreads();
+	if (ty == 0 && col < words) {
+		for (uint32_t k = 1; k < BLOCK / 64; ++k)
+			s += part[k][threadIdx.x];
+		if (s)
+			atomicAdd((unsigned long long *)&sum[col], (unsigned long long)s);
+	}
+}
+
+extern "C" int odpg_launch_counters_fold(uint64_t *rows, uint32_t nrows, uint32_t words,
+					 uint64_t *sum, hipStream_t s)
+{
+	const dim3 grid((words + 63u) / 64u, (nrows + FOLD_ROWS - 1u) / FOLD_ROWS);
+
+	hipLaunchKernelGGL(odpg_counters_fold_kernel, grid, dim3(BLOCK), 0, s, rows, nrows, words, sum);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
 /* ----------------------------------------------------------------------- */
 /* host-side launch helper (called from runtime.cpp)                        */
 
@@ -1232,8 +1301,10 @@ static size_t lds_need(const odpg_launch_args &a, int mode, int w)
 {
 	size_t lds = (size_t)BLOCK * (w / 4 + 1) * 4u;
 
-	if (a.cos_partial)
+	if (a.cos_partial || (a.cnt.row && a.cnt.cos))
 		lds += (size_t)((a.num_cos + 3u) & ~3u) * 4u;
+	if (a.cnt.row)
+		lds += (size_t)((a.cnt.ncols + 3u) & ~3u) * 4u;
 	if (mode == 2)
 		lds += (size_t)BLOCK * (((a.num_pmr + 31u) >> 5) | 1u) * 4u;
 	const bool use_mg = mode == 1 && (a.tbl_flags & TBL_MGROUPS);
@@ -1330,6 +1401,8 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 
 	if (!getenv("ODPG_GRID_CAP") && grid > occ_grid)
 		grid = occ_grid;
+	if (a.cnt.row && grid > a.cnt.rows)
+		grid = a.cnt.rows;   /* one counter row per workgroup */
 	hipLaunchKernelGGL((odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST, LEAN>), dim3(grid),
 			   dim3(BLOCK), lds, s, a.frames, a.desc, a.stride, a.num, a.opt, a.layer,
 			   a.classify, a.terms, a.pmrs, a.coses, a.num_cos, a.default_cos,
@@ -1338,7 +1411,7 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 			   (const uint2 *)a.cinfo, a.pinfo, a.mgroups, a.num_mgroups,
 			   (const uint4 *)a.ments, a.num_ment, (const uint2 *)a.pinfo2, a.out, a.mark, a.meta, a.pk_partial,
 			   a.cos_partial, a.pk_atomic ? a.sred : nullptr, (const uint2 *)a.xcos, a.xlist,
-			   a.num_xlist, a.num_xwords);
+			   a.num_xlist, a.num_xwords, a.cnt);
 	return hipGetLastError();
 }
 
@@ -1396,6 +1469,7 @@ static bool lean64_ok(const odpg_launch_args &a)
 	       odpg_cls64_lds(a) <= odpg_lds_limit() &&
 	       !(a.tbl_flags & (TBL_GENERIC | TBL_ANY_HASHQ)) &&
 	       !a.mark && !a.meta && !(a.stats && (a.tbl_flags & TBL_ANY_STATS)) &&
+	       !(a.cnt.row && a.cnt.cos) &&
 	       a.layer >= LAYER_L4 && a.classify &&
 	       !(a.opt & drops) && !(a.opt >> 32);
 }
@@ -1447,7 +1521,7 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 	if (lean) {
 		int rc = odpg_launch_cls64(a, s);
 
-		return rc ? rc : a->pk_atomic ? fold_stats(a, s) : 0;
+		return rc ? rc : a->pk_atomic && !a->cnt.row ? fold_stats(a, s) : 0;
 	}
 	uint32_t grid = odpg_launch_grid(a->num);
 	int mode = a->mode;
@@ -1503,6 +1577,8 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 		e = launch_layout<2>(*a, grid, s);
 	if (e != hipSuccess)
 		return -EIO;
+	if (a->cnt.row)
+		return 0;   /* folded at read time (odpg_counters_fold) */
 	if (a->pk_atomic)
 		return fold_stats(a, s);
 	if (a->stats && (a->pk_partial || a->cos_partial)) {

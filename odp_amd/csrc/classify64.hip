@@ -45,6 +45,9 @@
 #ifndef L64_BUF          /* frames / verdicts through range-checked buffer ops */
 #define L64_BUF 0
 #endif
+#ifndef L64_CNT_SPREAD   /* copies of the per-CoS delivery histogram (lane % S) */
+#define L64_CNT_SPREAD 1
+#endif
 #ifndef L64_PP           /* two frame buffers used in turn (else one, rotated) */
 #define L64_PP 0
 #endif
@@ -74,6 +77,11 @@ struct L64Args {
 	odpg_out_t *out;
 	uint64_t *stats;       /* pktio counters (odpg.h), or NULL */
 	uint64_t *sred;        /* stats_commit scratch */
+	/* sharded counters (odpg.h): this launch's rows, or NULL; per-CoS
+	 * delivered counts land in column qcol[c] (no hash queues here) */
+	uint64_t *crow;
+	const uint32_t *qcol;
+	uint32_t cwords, cncos;
 };
 
 /* ---- register parse of plain 64-byte frames ------------------------------ */
@@ -225,6 +233,9 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 	/* HW: cuckoo entries, pinfo3 */
 	uint2 *cents = (uint2 *)(smem + BLOCK * RW);
 	uint2 *pinfo3 = cents + A.num_cent;
+	/* sharded counters: per-CoS delivered packets after the table */
+	uint32_t *dlv = HW ? (uint32_t *)(pinfo3 + A.num_pmr) : (uint32_t *)(pinfo4 + A.num_pmr);
+	__shared__ uint32_t blk[4];
 
 	const uint32_t lane = __lane_id();
 	/* wave-uniform (readfirstlane): buffer resources are built from it */
@@ -271,6 +282,12 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 			for (int g = 0; g < NG; ++g)
 				mg[g] = load_mg(A.mgroups + g);
 		}
+	}
+	if (A.crow) {
+		for (uint32_t k = threadIdx.x; k < A.num_cos * L64_CNT_SPREAD; k += BLOCK)
+			dlv[k] = 0u;
+		if (threadIdx.x < 4)
+			blk[threadIdx.x] = 0u;
 	}
 	__syncthreads();
 
@@ -390,7 +407,13 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 			if (any_match && !err && cos != ODPG_COS_LOOP && mark)
 				w |= ODPG_OUT_MARK_VALID;
 		}
-		if (A.stats) {
+		if (A.crow && live && !pdrop && cos < A.num_cos && act != 1u)
+#ifndef L64_EXP_NODLV
+			atomicAdd(&dlv[cos * L64_CNT_SPREAD + lane % L64_CNT_SPREAD], 1u);   /* handed to the CoS queue (_odp_cls_enq) */
+#else
+			;
+#endif
+		if (A.stats || A.crow) {
 			/* in_packets: delivered error-free (cls ret 0); in_errors:
 			 * parse ret != 0; in_discards: cls ret -1 (no CoS; a CoS loop
 			 * counts the same) */
@@ -669,7 +692,36 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		}
 		t0 += nk * nwaves;
 	}
-	if (A.stats) {
+	if (A.crow) {
+		/* the workgroup's counts into its own row (odpg.h "sharded
+		 * counters"): plain read-modify-writes, rows are not shared */
+		if (lane == 0u) {
+			atomicAdd(&blk[0], n_pkt);
+			atomicAdd(&blk[2], n_err);
+			atomicAdd(&blk[3], n_disc);
+		}
+		__syncthreads();
+		uint64_t *r = A.crow + (size_t)blockIdx.x * A.cwords;
+
+		if (threadIdx.x < 4u && threadIdx.x != 1u) {
+			const uint32_t x = blk[threadIdx.x];
+
+			if (x) {
+				r[threadIdx.x] += x;
+				if (threadIdx.x == 0u)
+					r[1] += (uint64_t)x * 64u;
+			}
+		}
+		for (uint32_t k = threadIdx.x; k < A.num_cos && k < A.cncos; k += BLOCK) {
+			uint32_t x = 0u;
+
+#pragma unroll
+			for (uint32_t j = 0; j < L64_CNT_SPREAD; ++j)
+				x += dlv[k * L64_CNT_SPREAD + j];
+			if (x)
+				r[4u + A.cncos + A.qcol[k]] += x;
+		}
+	} else if (A.stats) {
 		const uint64_t v[4] = {n_pkt, (uint64_t)n_pkt * 64u, n_err, n_disc};
 
 		stats_commit_wave(v, A.sred);
@@ -686,7 +738,8 @@ size_t odpg_cls64_lds(const odpg_launch_args &a)
 
 	return (size_t)BLOCK * 17u * 4u +
 	       (hw ? (size_t)a.num_cent * 8u + (size_t)a.num_pmr * 8u
-		   : (size_t)a.num_ment * 16u + (size_t)a.num_pmr * 16u);
+		   : (size_t)a.num_ment * 16u + (size_t)a.num_pmr * 16u) +
+	       (a.cnt.row ? (size_t)a.num_cos * 4u * L64_CNT_SPREAD : 0u);
 }
 
 extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
@@ -721,6 +774,10 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	A.out = a->out;
 	A.stats = a->stats;
 	A.sred = a->sred;
+	A.crow = a->cnt.row;
+	A.qcol = a->cnt.qcol;
+	A.cwords = a->cnt.words;
+	A.cncos = a->cnt.ncos;
 
 	const bool hw = (a->tbl_flags & TBL_LEAN64HW) && !(a->tbl_flags & TBL_LEAN64);
 	size_t lds = odpg_cls64_lds(*a);
@@ -734,6 +791,8 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 
 	if (grid > occ)
 		grid = occ;
+	if (a->cnt.row && grid > a->cnt.rows)
+		grid = a->cnt.rows;   /* one counter row per workgroup */
 #ifdef L64_EXP_GRIDENV   /* experiment builds only: ODPG_L64_GRID workgroups */
 	if (const char *ge = getenv("ODPG_L64_GRID"))
 		grid = (uint32_t)atoi(ge);

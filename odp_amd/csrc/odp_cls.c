@@ -11,7 +11,12 @@
  * (:757-761), destroyed CoS keep their slot contents until reuse (:464-478).
  * The data plane never reads these structures: every change bumps a
  * generation and odpg_pktio_recv_batch() compiles an immutable snapshot
- * (odpg_rules_t -> device table) the first time a generation is used.
+ * (odpg_rules_t -> device table) the first time a generation is used on a
+ * context. The launches add their pktio / CoS / queue counts into the
+ * binding's device-resident sharded counters (odpg.h); the statistics calls
+ * fold them into the host totals when they are read, as the reference reads
+ * its atomics at query time. The global lock covers the object model and the
+ * binding lookup, never the GPU work of a receive.
  */
 #include <errno.h>
 #include <inttypes.h>
@@ -52,6 +57,8 @@ typedef struct {
 	uint64_t st_packets, st_discards;
 	uint64_t q_packets[COS_QUEUE_MAX], q_discards[COS_QUEUE_MAX];
 	odp_queue_t hq[COS_QUEUE_MAX];   /* implementation-created hash queues */
+	uint64_t uid;           /* creation serial: counts of an earlier CoS in
+				 * the slot are not folded into this one */
 } cos_e;
 
 typedef struct {
@@ -74,13 +81,27 @@ typedef struct {
 	int error_cos;          /* -1 = NULL */
 	uint32_t headroom;
 	odp_pktio_stats_t stats;
-	/* compiled table cache */
-	odpg_table_t *tbl;
-	odpg_ctx_t *tbl_ctx;
-	uint64_t tbl_gen;
-	uint64_t *dstats;
-	odpg_ctx_t *dstats_ctx;
+	struct bind_s *binds;   /* compiled tables, one per context in use */
 } pktio_e;
+
+/* A pktio's compiled table on one context and the sharded counters its
+ * launches add into. A binding whose generation is old is stale: it is
+ * folded and freed once no receive holds it. */
+typedef struct bind_s {
+	struct bind_s *next;
+	odpg_ctx_t *ctx;
+	odpg_table_t *tbl;
+	odpg_counters_t *cnt;
+	uint64_t gen;
+	uint32_t ncos;
+	uint64_t *cos_uid;      /* [ncos] CoS serials the table was compiled from */
+	uint64_t *words;        /* [ODPG_COUNTER_WORDS(ncos)] fold buffer */
+	uint64_t pktin_opt;
+	uint32_t layer, classify;
+	int refs;               /* receives in flight */
+	int dirty;              /* launched since the last fold */
+	int stale;
+} bind_t;
 
 static struct {
 	int init;
@@ -91,12 +112,13 @@ static struct {
 	pktio_e pktio[MAX_PKTIO];
 	uint64_t generation;
 	uintptr_t next_queue_id;
+	uint64_t next_uid;
 	/* snapshot buffers */
 	odpg_cos_t *s_cos;
 	odpg_pmr_t *s_pmr;
 	uint32_t *s_rule_pmr, *s_rule_dst;
 } g = { 0, PTHREAD_MUTEX_INITIALIZER, REF_MAX_COS, REF_MAX_PMR, REF_MAX_PMR_PER_COS,
-	NULL, NULL, {{0}}, 1, 0x40000000u, NULL, NULL, NULL, NULL };
+	NULL, NULL, {{0}}, 1, 0x40000000u, 1, NULL, NULL, NULL, NULL };
 
 static void free_tables(void)
 {
@@ -200,6 +222,91 @@ static void bump(void)
 	g.generation++;
 }
 
+/* ---- bindings and their counters --------------------------------------- */
+/* Sum a binding's device counters into the pktio's and the CoS's totals
+ * (loop.c:304-374 pktio counters, odp_classification.c:1621-1622,1697-1698
+ * CoS packets, odp_classification_internal.h:64-78 queue packets). */
+static void bind_fold_locked(pktio_e *p, bind_t *b)
+{
+	if (!b->dirty || !b->cnt)
+		return;
+	const uint32_t nw = ODPG_COUNTER_WORDS(b->ncos);
+
+	memset(b->words, 0, (size_t)nw * sizeof(uint64_t));
+	if (odpg_counters_fold(b->cnt, b->words)) {
+		ERR("counter fold failed\n");
+		return;
+	}
+	b->dirty = 0;
+	p->stats.in_packets += b->words[0];
+	p->stats.in_octets += b->words[1];
+	p->stats.in_errors += b->words[2];
+	p->stats.in_discards += b->words[3];
+	for (uint32_t c = 0; c < b->ncos && c < g.max_cos; c++) {
+		cos_e *ce = &g.cos[c];
+		const uint64_t *q = b->words + 4u + b->ncos + (size_t)c * ODPG_COS_QUEUE_MAX;
+
+		if (ce->uid != b->cos_uid[c])
+			continue;       /* the CoS was destroyed since the compile */
+		ce->st_packets += b->words[4u + c];
+		for (uint32_t k = 0; k < COS_QUEUE_MAX; k++)
+			ce->q_packets[k] += q[k];
+	}
+}
+
+static void bind_free(bind_t *b)
+{
+	odpg_counters_destroy(b->cnt);
+	odpg_table_destroy(b->tbl);
+	free(b->cos_uid);
+	free(b->words);
+	free(b);
+}
+
+/* unlink and free the pktio's bindings that match (ctx NULL = all), folding
+ * their counts first unless `drop` */
+static void binds_release_locked(pktio_e *p, const odpg_ctx_t *ctx, int drop)
+{
+	bind_t **pp = &p->binds;
+
+	while (*pp) {
+		bind_t *b = *pp;
+
+		if (ctx && b->ctx != ctx) {
+			pp = &b->next;
+			continue;
+		}
+		if (!drop)
+			bind_fold_locked(p, b);
+		*pp = b->next;
+		bind_free(b);
+	}
+}
+
+static void fold_pktio_locked(pktio_e *p)
+{
+	for (bind_t *b = p->binds; b; b = b->next)
+		bind_fold_locked(p, b);
+}
+
+static void fold_all_locked(void)
+{
+	for (int i = 0; i < MAX_PKTIO; i++)
+		if (g.pktio[i].valid)
+			fold_pktio_locked(&g.pktio[i]);
+}
+
+/* odpg_ctx_destroy() hook: nothing may keep a table or counters of a context
+ * past its end (a later context at the same address must not find them) */
+void odpg_cls_ctx_release(odpg_ctx_t *ctx)
+{
+	LOCK();
+	for (int i = 0; i < MAX_PKTIO; i++)
+		if (g.pktio[i].valid)
+			binds_release_locked(&g.pktio[i], ctx, 0);
+	UNLOCK();
+}
+
 int odpg_cls_set_limits(uint32_t max_cos, uint32_t max_pmr, uint32_t max_pmr_per_cos)
 {
 	int rc = 0;
@@ -223,12 +330,8 @@ int odpg_cls_set_limits(uint32_t max_cos, uint32_t max_pmr, uint32_t max_pmr_per
 void odpg_cls_reset(void)
 {
 	LOCK();
-	for (int i = 0; i < MAX_PKTIO; i++) {
-		if (g.pktio[i].tbl)
-			odpg_table_destroy(g.pktio[i].tbl);
-		if (g.pktio[i].dstats)
-			odpg_dev_free(g.pktio[i].dstats_ctx, g.pktio[i].dstats);
-	}
+	for (int i = 0; i < MAX_PKTIO; i++)
+		binds_release_locked(&g.pktio[i], NULL, 1);
 	memset(g.pktio, 0, sizeof(g.pktio));
 	free_tables();
 	g.init = 0;
@@ -393,6 +496,7 @@ odp_cos_t odp_cls_cos_create(const char *name, const odp_cls_cos_param_t *param_
 		c->index = i;
 		c->vector = param.vector;
 		c->stats_enable = param.stats_enable;
+		c->uid = g.next_uid++;
 		ret = cos_from_ndx(i);
 		bump();
 		break;
@@ -755,6 +859,7 @@ int odp_cls_cos_stats(odp_cos_t cos_id, odp_cls_cos_stats_t *stats)
 	}
 	memset(stats, 0, sizeof(*stats));
 	LOCK();
+	fold_all_locked();
 	stats->discards = c->st_discards;
 	stats->packets = c->st_packets;
 	UNLOCK();
@@ -793,6 +898,7 @@ int odp_cls_queue_stats(odp_cos_t cos_id, odp_queue_t queue, odp_cls_queue_stats
 	}
 	memset(stats, 0, sizeof(*stats));
 	LOCK();
+	fold_all_locked();
 	stats->discards = c->q_discards[qi];
 	stats->packets = c->q_packets[qi];
 	UNLOCK();
@@ -875,10 +981,13 @@ int odp_pktio_close(odp_pktio_t hdl)
 		UNLOCK();
 		return -1;
 	}
-	if (p->tbl)
-		odpg_table_destroy(p->tbl);
-	if (p->dstats)
-		odpg_dev_free(p->dstats_ctx, p->dstats);
+	for (bind_t *b = p->binds; b; b = b->next)
+		if (b->refs) {
+			UNLOCK();
+			ERR("pktio close during a receive\n");
+			return -1;
+		}
+	binds_release_locked(p, NULL, 0);   /* CoS counts outlive the pktio */
 	memset(p, 0, sizeof(*p));
 	bump();
 	UNLOCK();
@@ -990,6 +1099,7 @@ int odp_pktio_stats(odp_pktio_t hdl, odp_pktio_stats_t *stats)
 		UNLOCK();
 		return -1;
 	}
+	fold_pktio_locked(p);
 	*stats = p->stats;
 	UNLOCK();
 	return 0;
@@ -1004,6 +1114,7 @@ int odp_pktio_stats_reset(odp_pktio_t hdl)
 		UNLOCK();
 		return -1;
 	}
+	fold_pktio_locked(p);
 	memset(&p->stats, 0, sizeof(p->stats));
 	UNLOCK();
 	return 0;
@@ -1156,16 +1267,70 @@ int odpg_pktio_rules(odp_pktio_t hdl, odpg_rules_t *r)
 	return rc;
 }
 
+/* the pktio's current binding on `ctx`, compiled now if the rules changed
+ * since (stale bindings of the context are retired); NULL + *rc on error */
+static bind_t *bind_get_locked(pktio_e *p, odpg_ctx_t *ctx, int *rc)
+{
+	bind_t *b, **pp = &p->binds;
+	odpg_rules_t r;
+
+	for (b = p->binds; b; b = b->next)
+		if (b->ctx == ctx && !b->stale && b->gen == g.generation)
+			return b;
+	while ((b = *pp)) {
+		if (b->ctx == ctx && !b->stale)
+			b->stale = 1;
+		if (b->stale && !b->refs) {
+			bind_fold_locked(p, b);
+			*pp = b->next;
+			bind_free(b);
+		} else {
+			pp = &b->next;
+		}
+	}
+	if ((*rc = snapshot_locked(p, &r)))
+		return NULL;
+	b = calloc(1, sizeof(*b));
+	if (!b) {
+		*rc = -ENOMEM;
+		return NULL;
+	}
+	if ((*rc = odpg_table_create(ctx, &r, &b->tbl))) {
+		free(b);
+		return NULL;
+	}
+	b->ncos = odpg_table_num_cos(b->tbl);
+	b->cos_uid = calloc(b->ncos ? b->ncos : 1, sizeof(uint64_t));
+	b->words = calloc(ODPG_COUNTER_WORDS(b->ncos), sizeof(uint64_t));
+	if (!b->cos_uid || !b->words) {
+		*rc = -ENOMEM;
+		bind_free(b);
+		return NULL;
+	}
+	if ((*rc = odpg_counters_create(ctx, b->tbl, &b->cnt))) {
+		bind_free(b);
+		return NULL;
+	}
+	for (uint32_t c = 0; c < b->ncos && c < g.max_cos; c++)
+		b->cos_uid[c] = g.cos[c].valid ? g.cos[c].uid : 0;
+	b->ctx = ctx;
+	b->gen = g.generation;
+	b->pktin_opt = p->config.pktin.all_bits;
+	b->layer = (uint32_t)p->parse_layer;
+	b->classify = (uint32_t)p->cls_enabled;
+	b->next = p->binds;
+	p->binds = b;
+	return b;
+}
+
 int odpg_pktio_recv_batch(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
 			  const odpg_desc_t *desc, uint32_t stride, uint32_t num,
 			  int device_ptrs, odpg_out_t *out, uint16_t *mark)
 {
 	int rc = 0;
-	odpg_rules_t r;
 	odpg_batch_t b;
 	odpg_result_t res;
-	uint32_t nstats;
-	uint64_t *hstats = NULL;
+	bind_t *bd;
 
 	if (!ctx || !out)
 		return -EINVAL;
@@ -1173,73 +1338,44 @@ int odpg_pktio_recv_batch(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frame
 	pktio_e *p = get_pktio(hdl);
 
 	if (!p || !p->started) {
-		rc = -EINVAL;
-		goto out;
+		UNLOCK();
+		return -EINVAL;
 	}
-	if (!p->tbl || p->tbl_gen != g.generation || p->tbl_ctx != ctx) {
-		if (p->tbl)
-			odpg_table_destroy(p->tbl);
-		p->tbl = NULL;
-		if ((rc = snapshot_locked(p, &r)))
-			goto out;
-		if ((rc = odpg_table_create(ctx, &r, &p->tbl)))
-			goto out;
-		p->tbl_gen = g.generation;
-		p->tbl_ctx = ctx;
+	if (!(bd = bind_get_locked(p, ctx, &rc))) {
+		UNLOCK();
+		return rc;
 	}
-	nstats = ODPG_STATS_WORDS(g.max_cos);
-	hstats = calloc(nstats, sizeof(uint64_t));
-	if (!hstats) {
-		rc = -ENOMEM;
-		goto out;
-	}
+	bd->refs++;
+	bd->dirty = 1;
+	UNLOCK();
+
+	/* the launch: verdicts, marks and the binding's counters (no host
+	 * counting, no lock held) */
 	memset(&b, 0, sizeof(b));
 	b.frames = frames;
 	b.desc = desc;
 	b.stride = stride;
 	b.num = num;
-	b.pktin_opt = p->config.pktin.all_bits;
-	b.layer = (uint32_t)p->parse_layer;
-	b.classify = (uint32_t)p->cls_enabled;
+	b.pktin_opt = bd->pktin_opt;
+	b.layer = bd->layer;
+	b.classify = bd->classify;
+	memset(&res, 0, sizeof(res));
 	res.out = out;
 	res.mark = mark;
-	res.meta = NULL;
-	if (device_ptrs) {
-		if (!p->dstats || p->dstats_ctx != ctx) {
-			if (p->dstats)
-				odpg_dev_free(p->dstats_ctx, p->dstats);
-			p->dstats = NULL;
-			if ((rc = odpg_dev_alloc(ctx, nstats * 8u, (void **)&p->dstats)))
-				goto out;
-			p->dstats_ctx = ctx;
-		}
-		res.stats = p->dstats;
-		if ((rc = odpg_memset_dev(ctx, p->dstats, 0, nstats * 8u)) ||
-		    (rc = odpg_classify(ctx, p->tbl, &b, &res)) ||
-		    (rc = odpg_memcpy_d2h(ctx, hstats, p->dstats, nstats * 8u)))
-			goto out;
-	} else {
-		res.stats = hstats;
-		if ((rc = odpg_classify_host(ctx, p->tbl, &b, &res, 0)))
-			goto out;
-		/* per-queue enqueue counters (_odp_cos_queue_stats_add,
-		 * odp_classification_internal.h:64-78) from the verdicts */
-		for (uint32_t i = 0; i < num; i++) {
-			uint32_t w = out[i], c = ODPG_OUT_COS(w);
+	res.counters = bd->cnt;
+	rc = device_ptrs ? odpg_classify(ctx, bd->tbl, &b, &res)
+			 : odpg_classify_host(ctx, bd->tbl, &b, &res, 0);
 
-			if (c >= g.max_cos || (w & ODPG_OUT_CLS_DROP))
-				continue;
-			g.cos[c].q_packets[g.cos[c].num_queue > 1 ? ODPG_OUT_HASHQ(w) : 0]++;
-		}
+	LOCK();
+	if (--bd->refs == 0 && bd->stale) {
+		bind_t **pp = &p->binds;
+
+		while (*pp != bd)
+			pp = &(*pp)->next;
+		bind_fold_locked(p, bd);
+		*pp = bd->next;
+		bind_free(bd);
 	}
-	p->stats.in_packets += hstats[0];
-	p->stats.in_octets += hstats[1];
-	p->stats.in_errors += hstats[2];
-	p->stats.in_discards += hstats[3];
-	for (uint32_t c = 0; c < g.max_cos; c++)
-		g.cos[c].st_packets += hstats[4 + c];
-out:
-	free(hstats);
 	UNLOCK();
 	return rc;
 }

@@ -291,6 +291,24 @@ typedef struct dtable_hdr_s {
 
 typedef struct uint2_s { uint32_t x, y; } uint2_t;
 
+/* sharded counters of one launch (odpg.h "sharded counters"): row r of
+ * `words` u64 belongs to workgroup r: [4 pktio][ncos CoS stats][ncols
+ * delivered per queue column, qcol[c] + hash queue] */
+typedef struct odpg_cnt_args {
+	uint64_t *row;          /* rows base, NULL = no sharded counters */
+	const uint32_t *qcol;   /* device, queue column of each CoS (num_cos + 1) */
+	uint32_t words, rows, ncos, ncols;
+	uint32_t cos;           /* the table has CoS with stats_enable */
+	uint32_t pad;
+} odpg_cnt_args;
+
+/* odp_cls.c: drop the classifier's tables / counters bound to a context
+ * (called by odpg_ctx_destroy before the context's stream goes away) */
+#ifdef __cplusplus
+extern "C"
+#endif
+void odpg_cls_ctx_release(struct odpg_ctx_s *ctx);
+
 /* kernel launch arguments (runtime.hip -> classify.hip) */
 #include "../../include/odpg.h"
 typedef struct odpg_launch_args {
@@ -349,6 +367,7 @@ typedef struct odpg_launch_args {
 	uint32_t pk_atomic;    /* pk_partial is the caller's counters (stats_commit.h) */
 	uint64_t *sred;        /* the context's stats_commit scratch (zeroed) */
 	uint64_t *stats;
+	odpg_cnt_args cnt;
 } odpg_launch_args;
 
 #endif

@@ -65,7 +65,39 @@ struct odpg_table_s {
 	void *dblob;
 	int device;
 	int cycle;
+	uint64_t qsig;     /* counter layout: CoS count, queues and stats flags */
 };
+
+/* odpg.h "sharded counters" */
+struct odpg_counters_s {
+	odpg_ctx_t *ctx;
+	uint64_t qsig;
+	uint32_t ncos, ncols, words, rows;
+	uint32_t any_cos;              /* some CoS has stats_enable */
+	uint64_t *drows;               /* device, rows x words */
+	uint32_t *dqcol;               /* device, queue column of each CoS */
+	uint64_t *dsum;                /* device, words (fold target) */
+	uint64_t *hsum;                /* pinned host, words */
+	hipEvent_t done;
+	std::vector<uint32_t> qcol;    /* host: ncos + 1 prefix of num_queue */
+	std::vector<uint8_t> nq;
+	std::mutex lock;               /* one fold at a time */
+};
+
+/* layout signature of a table's counters: a counters object serves every
+ * table with the same CoS count, queue counts and stats flags */
+static uint64_t table_qsig(const odpg_table_t *t)
+{
+	const dcos_t *hc = (const dcos_t *)(t->blob.data() + t->hdr.cos_off);
+	uint64_t h = 1469598103934665603ull ^ t->hdr.num_cos;
+
+	for (uint32_t c = 0; c < t->hdr.num_cos; c++) {
+		const uint32_t nq = hc[c].num_queue ? hc[c].num_queue : 1u;
+
+		h = (h ^ (nq | ((uint32_t)(hc[c].stats != 0) << 8))) * 1099511628211ull;
+	}
+	return h;
+}
 
 #define HIPCHK(x)                                                              \
 	do {                                                                   \
@@ -86,7 +118,7 @@ int odpg_abi_version(void)
 
 const char *odpg_build_info(void)
 {
-	return "odpg gfx950 classifier, ABI 1";
+	return "odpg gfx950 classifier, ABI 2";
 }
 
 int odpg_device_count(void)
@@ -154,6 +186,7 @@ void odpg_ctx_destroy(odpg_ctx_t *c)
 {
 	if (!c)
 		return;
+	odpg_cls_ctx_release(c);
 	hipSetDevice(c->device);
 	hipStreamSynchronize(c->stream);
 	hipStreamSynchronize(c->copy_stream);
@@ -208,6 +241,7 @@ int odpg_table_create(odpg_ctx_t *c, const odpg_rules_t *rules, odpg_table_t **o
 	}
 	t->cycle = odpg_rules_has_cycle(t->blob, t->hdr);
 	t->device = c->device;
+	t->qsig = table_qsig(t);
 	hipSetDevice(c->device);
 	if (hipMalloc(&t->dblob, t->hdr.blob_bytes) != hipSuccess) {
 		delete t;
@@ -241,6 +275,139 @@ uint32_t odpg_table_num_cos(const odpg_table_t *t)
 int odpg_table_has_cycle(const odpg_table_t *t)
 {
 	return t ? t->cycle : 0;
+}
+
+/* ---- sharded counters ---------------------------------------------------- */
+#define CNT_ROWS_PER_CU 8u
+#define CNT_MAX_BYTES   (512ull << 20)
+#define CNT_MAX_LDS     (48u << 10)   /* LDS histograms of one workgroup */
+
+extern "C" int odpg_launch_counters_fold(uint64_t *rows, uint32_t nrows, uint32_t words,
+					 uint64_t *sum, hipStream_t s);
+
+static void counters_free(odpg_counters_t *k)
+{
+	hipFree(k->drows);
+	hipFree(k->dqcol);
+	hipFree(k->dsum);
+	if (k->hsum)
+		hipHostFree(k->hsum);
+	if (k->done)
+		hipEventDestroy(k->done);
+	delete k;
+}
+
+int odpg_counters_create(odpg_ctx_t *c, const odpg_table_t *t, odpg_counters_t **out)
+{
+	if (!c || !t || !out)
+		return -EINVAL;
+	if (t->device != c->device)
+		return -EXDEV;
+	const dtable_hdr_t &h = t->hdr;
+	const dcos_t *hc = (const dcos_t *)(t->blob.data() + h.cos_off);
+	odpg_counters_t *k = new odpg_counters_t();
+
+	k->ctx = c;
+	k->qsig = t->qsig;
+	k->ncos = h.num_cos;
+	k->qcol.resize(h.num_cos + 1u);
+	k->nq.resize(h.num_cos);
+	uint32_t col = 0;
+
+	for (uint32_t i = 0; i < h.num_cos; i++) {
+		k->qcol[i] = col;
+		k->nq[i] = (uint8_t)(hc[i].num_queue ? hc[i].num_queue : 1u);
+		col += k->nq[i];
+		k->any_cos |= hc[i].stats ? 1u : 0u;
+	}
+	k->qcol[h.num_cos] = col;
+	k->ncols = col;
+	k->words = 4u + k->ncos + k->ncols;
+	if (((size_t)k->ncos + k->ncols) * 4u > CNT_MAX_LDS) {
+		delete k;
+		return -E2BIG;
+	}
+	int cus = 0;
+
+	hipSetDevice(c->device);
+	if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
+	    cus <= 0)
+		cus = 256;
+	k->rows = (uint32_t)cus * CNT_ROWS_PER_CU;
+	while (k->rows > (uint32_t)cus && (size_t)k->rows * k->words * 8u > CNT_MAX_BYTES)
+		k->rows >>= 1;
+	if ((size_t)k->rows * k->words * 8u > CNT_MAX_BYTES) {
+		delete k;
+		return -E2BIG;
+	}
+	const size_t rb = (size_t)k->rows * k->words * 8u;
+
+	if (hipMalloc(&k->drows, rb) != hipSuccess ||
+	    hipMalloc(&k->dqcol, (size_t)(k->ncos + 1u) * 4u) != hipSuccess ||
+	    hipMalloc(&k->dsum, (size_t)k->words * 8u) != hipSuccess ||
+	    hipHostMalloc(&k->hsum, (size_t)k->words * 8u, hipHostMallocDefault) != hipSuccess ||
+	    hipEventCreateWithFlags(&k->done, hipEventDisableTiming) != hipSuccess) {
+		counters_free(k);
+		return -ENOMEM;
+	}
+	{
+		std::lock_guard<std::mutex> g(c->lock);
+
+		if (hipMemsetAsync(k->drows, 0, rb, c->stream) != hipSuccess ||
+		    hipMemsetAsync(k->dsum, 0, (size_t)k->words * 8u, c->stream) != hipSuccess ||
+		    hipMemcpyAsync(k->dqcol, k->qcol.data(), (size_t)(k->ncos + 1u) * 4u,
+				   hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+		    hipEventRecord(k->done, c->stream) != hipSuccess) {
+			counters_free(k);
+			return -EIO;
+		}
+	}
+	if (hipEventSynchronize(k->done) != hipSuccess) {
+		counters_free(k);
+		return -EIO;
+	}
+	*out = k;
+	return 0;
+}
+
+void odpg_counters_destroy(odpg_counters_t *k)
+{
+	if (!k)
+		return;
+	hipSetDevice(k->ctx->device);
+	hipStreamSynchronize(k->ctx->stream);   /* launches still adding into the rows */
+	counters_free(k);
+}
+
+int odpg_counters_fold(odpg_counters_t *k, uint64_t *words)
+{
+	if (!k || !words)
+		return -EINVAL;
+	odpg_ctx_t *c = k->ctx;
+	std::lock_guard<std::mutex> fl(k->lock);
+
+	hipSetDevice(c->device);
+	{
+		/* enqueue behind every launch already on the context stream */
+		std::lock_guard<std::mutex> g(c->lock);
+
+		if (odpg_launch_counters_fold(k->drows, k->rows, k->words, k->dsum, c->stream) ||
+		    hipMemcpyAsync(k->hsum, k->dsum, (size_t)k->words * 8u, hipMemcpyDeviceToHost,
+				   c->stream) != hipSuccess ||
+		    hipMemsetAsync(k->dsum, 0, (size_t)k->words * 8u, c->stream) != hipSuccess ||
+		    hipEventRecord(k->done, c->stream) != hipSuccess)
+			return -EIO;
+	}
+	HIPCHK(hipEventSynchronize(k->done));
+	for (uint32_t w = 0; w < 4u + k->ncos; w++)
+		words[w] += k->hsum[w];
+	const uint64_t *dl = k->hsum + 4u + k->ncos;
+	uint64_t *uq = words + 4u + k->ncos;
+
+	for (uint32_t i = 0; i < k->ncos; i++)
+		for (uint32_t q = 0; q < k->nq[i]; q++)
+			uq[(size_t)i * ODPG_COS_QUEUE_MAX + q] += dl[k->qcol[i] + q];
+	return 0;
 }
 
 static int ensure_ws(odpg_ctx_t *c, size_t bytes)
@@ -352,7 +519,17 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.mark = r->mark;
 	a.meta = r->meta;
 	a.stats = r->stats;
-	if (r->stats && !cos_stats) {
+	if (r->counters) {
+		odpg_counters_t *k = r->counters;
+
+		a.cnt.row = k->drows;
+		a.cnt.qcol = k->dqcol;
+		a.cnt.words = k->words;
+		a.cnt.rows = k->rows;
+		a.cnt.ncos = k->ncos;
+		a.cnt.ncols = k->ncols;
+		a.cnt.cos = k->any_cos;
+	} else if (r->stats && !cos_stats) {
 		/* pktio counters only: workgroups add straight into them */
 		a.pk_partial = r->stats;
 		a.pk_atomic = 1u;
@@ -444,6 +621,20 @@ static size_t ws_need(const odpg_table_t *t, uint32_t num, bool stats)
 	return (size_t)grid * 32u + (size_t)grid * t->hdr.num_cos * 4u;
 }
 
+/* a counters object serves launches on its own context (its rows are
+ * updated with plain read-modify-writes, stream-ordered) and tables of its
+ * layout; not together with the caller's stats block */
+static int check_counters(const odpg_ctx_t *c, const odpg_table_t *t, const odpg_result_t *r)
+{
+	const odpg_counters_t *k = r->counters;
+
+	if (!k)
+		return 0;
+	if (r->stats || k->ctx != c || k->qsig != t->qsig || k->ncos != t->hdr.num_cos)
+		return -EINVAL;
+	return 0;
+}
+
 int odpg_classify(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t *b,
 		  const odpg_result_t *r)
 {
@@ -455,6 +646,8 @@ int odpg_classify(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t *b,
 		return rc;
 	if (t->device != c->device)
 		return -EXDEV;
+	if ((rc = check_counters(c, t, r)))
+		return rc;
 	if (b->num == 0)
 		return 0;
 	std::lock_guard<std::mutex> g(c->lock);
@@ -479,6 +672,8 @@ int odpg_classify_host(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t 
 		return rc;
 	if (t->device != c->device)
 		return -EXDEV;
+	if ((rc = check_counters(c, t, r)))
+		return rc;
 	if (b->num == 0)
 		return 0;
 	if (chunk == 0)
@@ -574,6 +769,7 @@ int odpg_classify_host(odpg_ctx_t *c, const odpg_table_t *t, const odpg_batch_t 
 		cr.mark = r->mark ? B.mark : nullptr;
 		cr.meta = r->meta ? B.meta : nullptr;
 		cr.stats = r->stats ? c->stage_stats : nullptr;
+		cr.counters = r->counters;
 		if (classify_on(c, c->stream, t, &cb, &cr, c->ws)) {
 			err = -EIO;
 			break;

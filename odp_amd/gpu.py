@@ -66,6 +66,40 @@ class Table:
             pass
 
 
+class Counters:
+    """Sharded device counters of one table layout (odpg.h "sharded
+    counters"): launches add into per-workgroup rows; fold() sums them."""
+
+    def __init__(self, ctx, table):
+        h = C.c_void_p()
+        L.check(lib.odpg_counters_create(ctx.h, table.h, C.byref(h)), "odpg_counters_create")
+        self.h = h.value
+        self.num_cos = table.num_cos
+        self.words = 4 + self.num_cos + self.num_cos * L.COS_QUEUE_MAX
+
+    def fold(self):
+        """Counts since the last fold: {"pktio": [in_packets, in_octets,
+        in_errors, in_discards], "cos": per-CoS packets, "queue": [num_cos,
+        COS_QUEUE_MAX] delivered packets}."""
+        w = np.zeros(self.words, np.uint64)
+        L.check(lib.odpg_counters_fold(self.h, w.ctypes.data_as(C.POINTER(C.c_uint64))),
+                "odpg_counters_fold")
+        n = self.num_cos
+        return {"pktio": w[:4], "cos": w[4:4 + n],
+                "queue": w[4 + n:].reshape(n, L.COS_QUEUE_MAX)}
+
+    def close(self):
+        if self.h:
+            lib.odpg_counters_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Context:
     def __init__(self, device=0, stream=None):
         n = lib.odpg_device_count()
@@ -100,20 +134,28 @@ class Context:
     def table(self, rules):
         return Table(self, rules)
 
+    def counters(self, table):
+        return Counters(self, table)
+
     def classify_dev(self, table, frames_buf, num, stride=0, desc_buf=None, opt=0,
                      layer=L.LAYER_ALL, classify=True, out_buf=None, mark_buf=None,
-                     meta_buf=None, stats_buf=None):
+                     meta_buf=None, stats_buf=None, counters=None):
         b = L.odpg_batch_t(frames_buf.ptr, desc_buf.ptr if desc_buf else None, stride, num,
                            opt, layer, int(bool(classify)))
         r = L.odpg_result_t(out_buf.ptr if out_buf else None,
                             mark_buf.ptr if mark_buf else None,
                             meta_buf.ptr if meta_buf else None,
-                            stats_buf.ptr if stats_buf else None)
+                            stats_buf.ptr if stats_buf else None,
+                            counters.h if counters else None)
         L.check(lib.odpg_classify(self.h, table.h, C.byref(b), C.byref(r)), "odpg_classify")
 
     def classify(self, table, frames, num, stride=0, desc=None, opt=0, layer=L.LAYER_ALL,
-                 classify=True, want_mark=True, want_meta=True, want_stats=True):
-        """Upload host arrays, classify on the GPU, download results."""
+                 classify=True, want_mark=True, want_meta=True, want_stats=True,
+                 counters=None):
+        """Upload host arrays, classify on the GPU, download results. With
+        `counters` the launch adds into those (want_stats is ignored)."""
+        if counters is not None:
+            want_stats = False
         meta_dt, desc_dt = L.np_dtypes()
         frames = np.ascontiguousarray(frames, dtype=np.uint8)
         fb = self.buffer(frames.nbytes + 64)
@@ -130,7 +172,8 @@ class Context:
         sb = self.buffer(8 * nst) if want_stats else None
         if sb:
             sb.zero()
-        self.classify_dev(table, fb, num, stride, db, opt, layer, classify, ob, mb, eb, sb)
+        self.classify_dev(table, fb, num, stride, db, opt, layer, classify, ob, mb, eb, sb,
+                          counters)
         self.sync()
         res = {"out": ob.download(np.uint32, num)}
         if mb:

@@ -67,3 +67,30 @@ def assert_same(a, b, what=""):
                     if x.ndim else []
                 raise AssertionError(f"{what}: '{k}' differs at {len(bad)} entries, "
                                      f"first {bad[:8]}: {x[bad[:4]]} vs {y[bad[:4]]}")
+
+
+def expected_counters(o, num_cos):
+    """The sharded-counter fold (odpg.h) an oracle run implies: its pktio and
+    CoS counters, and per (CoS, hash queue) the packets the classifier handed
+    to a queue (ret 0: a CoS, no drop action; _odp_cls_enq ->
+    _odp_cos_queue_stats_add, odp_classification_internal.h:64-78)."""
+    out = np.asarray(o["out"], np.uint32)
+    cos = out & 0xFFFF
+    ok = (cos < num_cos) & ((out & L.ODPG_OUT_CLS_DROP) == 0)
+    q = np.zeros((num_cos, L.COS_QUEUE_MAX), np.uint64)
+    np.add.at(q, (cos[ok], (out[ok] >> 24) & 31), 1)
+    st = np.asarray(o["stats"], np.uint64)
+    cs = np.zeros(num_cos, np.uint64)
+    m = min(num_cos, len(st) - 4)
+    cs[:m] = st[4:4 + m]
+    assert not np.any(st[4 + m:]), "oracle counts a CoS past the table"
+    return {"pktio": st[:4].copy(), "cos": cs, "queue": q}
+
+
+def assert_counters(f, e, what=""):
+    for k in ("pktio", "cos", "queue"):
+        if not np.array_equal(f[k], e[k]):
+            bad = np.argwhere(f[k] != e[k])[:6]
+            raise AssertionError(f"{what}: counters '{k}' differ at {bad.tolist()}: "
+                                 f"{[int(f[k][tuple(b)]) for b in bad]} vs "
+                                 f"{[int(e[k][tuple(b)]) for b in bad]}")

@@ -6,7 +6,8 @@ import pytest
 
 import oracle
 import rulesets
-from helpers import ALL_CHKSUM, GOLDEN, assert_same, golden_frames, pack
+from helpers import (ALL_CHKSUM, GOLDEN, assert_counters, assert_same, expected_counters,
+                     golden_frames, pack)
 from odp_amd import _lib as L
 from odp_amd import gen
 
@@ -19,6 +20,8 @@ def both(ctx, rules, buf, num, stride=0, desc=None, opt=0, layer=L.LAYER_ALL, cl
     """Classify on the GPU with every kernel strategy (walk, evaluate-all,
     auto) and on the oracle; the strategies must agree bit for bit."""
     tbl = ctx.table(rules)
+    o = oracle.classify(rules, buf, num, stride=stride, desc=desc, opt=opt, layer=layer,
+                        classify=classify)
     res = {}
     for mode in (1, 2, 3, 0):
         ctx.set_kernel_mode(mode)
@@ -37,8 +40,21 @@ def both(ctx, rules, buf, num, stride=0, desc=None, opt=0, layer=L.LAYER_ALL, cl
         lean = ctx.classify(tbl, buf, num, stride=stride, opt=opt, layer=layer,
                             classify=classify, want_mark=False, want_meta=False)
         assert_same(res[1], lean, f"walk vs verdict+stats (kernel {L.lib.odpg_last_kernel()})")
-    o = oracle.classify(rules, buf, num, stride=stride, desc=desc, opt=opt, layer=layer,
-                        classify=classify)
+    # sharded counters (odpg.h): the walk and auto (lean kernel where it
+    # applies), two launches each, one fold against the oracle's counts
+    cnt = ctx.counters(tbl)
+    want = expected_counters(o, tbl.num_cos)
+    for mode in (1, 0):
+        ctx.set_kernel_mode(mode)
+        for _ in range(2):
+            g = ctx.classify(tbl, buf, num, stride=stride, desc=desc, opt=opt, layer=layer,
+                             classify=classify, want_mark=False, want_meta=False, counters=cnt)
+            assert np.array_equal(g["out"], res[1]["out"]), f"counters launch, mode {mode}"
+        f = cnt.fold()
+        assert_counters(f, {k: v * 2 for k, v in want.items()},
+                        f"mode {mode} kernel {L.lib.odpg_last_kernel()}")
+    ctx.set_kernel_mode(0)
+    cnt.close()
     return res[0], o
 
 
@@ -251,8 +267,24 @@ def test_pktio_recv_batch_counters(gpu_ctx, fresh_cls):
     ob = gpu_ctx.buffer(4 * n)
     rc = L.lib.odpg_pktio_recv_batch(p, gpu_ctx.h, fb.ptr, None, 64, n, 1, ob.ptr, None)
     assert rc == 0
+    gpu_ctx.sync()                   # the device path is asynchronous
     assert np.array_equal(ob.download(np.uint32, n), out)
+    st = fresh_cls.pktio_stats(p)
+    assert st.in_packets == 2 * n and st.in_octets == 128 * n
+    for c in [r["default"]] + r["l1"] + r["leaves"]:
+        rc, cs = fresh_cls.cos_stats(c)
+        assert rc == 0 and cs.packets == 2 * o["stats"][4 + fresh_cls.to_index(c)]
+    # queue counters after the device call: every queue of every CoS
+    want = expected_counters(o, len(o["stats"]) - 4)["queue"]
+    for c in [r["default"]] + r["l1"] + r["leaves"]:
+        rc, qs = fresh_cls.queue_stats(c, fresh_cls.cos_queue(c))
+        assert rc == 0 and qs.packets == 2 * want[fresh_cls.to_index(c), 0], c
+    # reads fold once: a second read sees the same totals
     assert fresh_cls.pktio_stats(p).in_packets == 2 * n
+    fresh_cls.pktio_stats_reset(p)
+    assert fresh_cls.pktio_stats(p).in_packets == 0
+    rc = L.lib.odpg_pktio_recv_batch(p, gpu_ctx.h, fb.ptr, None, 64, n, 1, ob.ptr, None)
+    assert rc == 0 and fresh_cls.pktio_stats(p).in_packets == n
     del C
 
 

@@ -51,5 +51,5 @@ def test_library_is_gfx950():
 
 
 def test_abi_version_without_gpu():
-    assert L.lib.odpg_abi_version() == 1
+    assert L.lib.odpg_abi_version() == L.ABI_VERSION == 2
     assert b"gfx950" in L.lib.odpg_build_info()
