@@ -251,12 +251,20 @@ int  odpg_ctx_sync(odpg_ctx_t *ctx);
  * is indeterminate", odp_classification.c:1348-1349); here each snapshot is
  * immutable and rebuilt per generation. */
 int  odpg_table_create(odpg_ctx_t *ctx, const odpg_rules_t *rules, odpg_table_t **tbl);
+/* Recompile `tbl` in place from new rules (a new generation): the upload is
+ * ordered on the context stream after the launches already enqueued with the
+ * old contents, so it needs no wait and no reallocation unless the table
+ * grew. Not concurrently with other threads' launches on the table. */
+int  odpg_table_update(odpg_ctx_t *ctx, odpg_table_t *tbl, const odpg_rules_t *rules);
 void odpg_table_destroy(odpg_table_t *tbl);
 uint32_t odpg_table_num_cos(const odpg_table_t *tbl);
 int  odpg_table_has_cycle(const odpg_table_t *tbl);
 
 int  odpg_counters_create(odpg_ctx_t *ctx, const odpg_table_t *tbl, odpg_counters_t **cnt);
 void odpg_counters_destroy(odpg_counters_t *cnt);
+/* 1 if `cnt` can count launches on `tbl` (its layout: CoS count, queues and
+ * stats flags), else 0 */
+int  odpg_counters_match(const odpg_counters_t *cnt, const odpg_table_t *tbl);
 /* Synchronous: words has ODPG_COUNTER_WORDS(odpg_table_num_cos(tbl)) entries. */
 int  odpg_counters_fold(odpg_counters_t *cnt, uint64_t *words);
 

@@ -256,11 +256,13 @@ SIGNATURES = {
     "odpg_last_kernel": (_i32, []),
     "odpg_ctx_sync": (_i32, [_vp]),
     "odpg_table_create": (_i32, [_vp, C.POINTER(odpg_rules_t), C.POINTER(_vp)]),
+    "odpg_table_update": (_i32, [_vp, _vp, C.POINTER(odpg_rules_t)]),
     "odpg_table_destroy": (None, [_vp]),
     "odpg_table_num_cos": (_u32, [_vp]),
     "odpg_table_has_cycle": (_i32, [_vp]),
     "odpg_counters_create": (_i32, [_vp, _vp, C.POINTER(_vp)]),
     "odpg_counters_destroy": (None, [_vp]),
+    "odpg_counters_match": (_i32, [_vp, _vp]),
     "odpg_counters_fold": (_i32, [_vp, C.POINTER(C.c_uint64)]),
     "odpg_classify": (_i32, [_vp, _vp, C.POINTER(odpg_batch_t), C.POINTER(odpg_result_t)]),
     "odpg_classify_host": (_i32, [_vp, _vp, C.POINTER(odpg_batch_t),

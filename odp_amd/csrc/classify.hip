@@ -1326,13 +1326,13 @@ static size_t lds_need(const odpg_launch_args &a, int mode, int w)
  * current device, from hipOccupancyMaxActiveBlocksPerMultiprocessor; cached
  * per (kernel, LDS bytes, device) under a lock (contexts on several threads
  * and devices launch concurrently). */
-extern "C" uint32_t odpg_resident_grid(const void *kernel, size_t lds)
+extern "C" uint32_t odpg_resident_grid(const void *kernel, uint32_t block, size_t lds)
 {
 	struct Occ {
 		const void *k;
 		size_t lds;
 		int dev;
-		uint32_t grid;
+		uint32_t block, grid;
 	};
 	static std::mutex m;
 	static std::vector<Occ> cache;
@@ -1343,19 +1343,19 @@ extern "C" uint32_t odpg_resident_grid(const void *kernel, size_t lds)
 		std::lock_guard<std::mutex> g(m);
 
 		for (const Occ &o : cache)
-			if (o.k == kernel && o.lds == lds && o.dev == dev)
+			if (o.k == kernel && o.lds == lds && o.dev == dev && o.block == block)
 				return o.grid;
 	}
 	int nb = 0, cus = 0;
 
 	hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, BLOCK, lds) != hipSuccess ||
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, (int)block, lds) != hipSuccess ||
 	    nb <= 0)
 		nb = 1;
 	const uint32_t grid = (uint32_t)(nb * (cus > 0 ? cus : 256));
 	std::lock_guard<std::mutex> g(m);
 
-	cache.push_back({kernel, lds, dev, grid});
+	cache.push_back({kernel, lds, dev, block, grid});
 	return grid;
 }
 
@@ -1397,7 +1397,7 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 	/* persistent grid: exactly the workgroups that are resident at once
 	 * (occupancy x CUs), each looping over tiles */
 	const uint32_t occ_grid = odpg_resident_grid(
-		(const void *)odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST, LEAN>, lds);
+		(const void *)odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST, LEAN>, BLOCK, lds);
 
 	if (!getenv("ODPG_GRID_CAP") && grid > occ_grid)
 		grid = occ_grid;

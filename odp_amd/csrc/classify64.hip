@@ -45,9 +45,10 @@
 #ifndef L64_BUF          /* frames / verdicts through range-checked buffer ops */
 #define L64_BUF 0
 #endif
-#ifndef L64_CNT_SPREAD   /* copies of the per-CoS delivery histogram (lane % S) */
-#define L64_CNT_SPREAD 1
+#ifndef L64_BLOCK        /* threads per workgroup */
+#define L64_BLOCK 256
 #endif
+#define LB L64_BLOCK
 #ifndef L64_PP           /* two frame buffers used in turn (else one, rotated) */
 #define L64_PP 0
 #endif
@@ -77,11 +78,9 @@ struct L64Args {
 	odpg_out_t *out;
 	uint64_t *stats;       /* pktio counters (odpg.h), or NULL */
 	uint64_t *sred;        /* stats_commit scratch */
-	/* sharded counters (odpg.h): this launch's rows, or NULL; per-CoS
-	 * delivered counts land in column qcol[c] (no hash queues here) */
-	uint64_t *crow;
-	const uint32_t *qcol;
-	uint32_t cwords, cncos;
+	/* sharded counters (odpg.h): their layout in device memory, read
+	 * once after the tile loop (no registers held across it) */
+	const odpg_cnt_dev *cnt;
 };
 
 /* ---- register parse of plain 64-byte frames ------------------------------ */
@@ -217,30 +216,42 @@ __device__ __forceinline__ MGd load_mg(const dmgroup_t *g, bool single = true)
 	return d;
 }
 
+/* sharded-counter histogram bins after the CoS bins (CM 2) */
+#define BIN_ERR    0u
+#define BIN_PDROP  1u
+#define BIN_NOCOS  2u
+#define BIN_DROP   3u
+#define BIN_EXTRA  4u
+
 /* ---- the kernel ------------------------------------------------------------
  * NG > 0: the table has exactly NG mask groups (HW: walk groups); their
  * descriptors are read once into scalar registers before the tile loop.
  * NG = 0 (mask groups only): any count, read per tile. */
-template <int NG, bool HW>
-__global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64Args A)
+/* CM: counters of the launch: 0 none, 1 the caller's pktio block
+ * (stats_commit.h), 2 sharded counter rows (odpg.h). CK: every hoisted
+ * group is a cuckoo group over a frame word (TBL_MG_CUCKOO): no per-group
+ * kind tests in the tile loop. */
+template <int NG, bool HW, int CM, bool CK>
+__global__ __launch_bounds__(LB, L64_WAVES * 256 / LB) void odpg_cls64_kernel(const L64Args A)
 {
 	static_assert(!HW || NG > 0, "walk groups are hoisted");
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 	constexpr uint32_t RW = 17;                     /* odd dword row stride */
 	uint32_t *row = smem + threadIdx.x * RW;        /* generic-parse LDS row */
-	uint4 *ments = (uint4 *)(smem + BLOCK * RW);
+	/* sharded counters (CM 2): the histogram right after the rows, at a
+	 * fixed offset (its adds need no base register); the table after it */
+	uint32_t *dlv = smem + LB * RW;
+	const uint32_t nbins = CM == 2 ? ((A.num_cos + BIN_EXTRA + 3u) & ~3u) : 0u;
+	uint4 *ments = (uint4 *)(dlv + nbins);
 	uint4 *pinfo4 = ments + A.num_ment;
 	/* HW: cuckoo entries, pinfo3 */
-	uint2 *cents = (uint2 *)(smem + BLOCK * RW);
+	uint2 *cents = (uint2 *)(dlv + nbins);
 	uint2 *pinfo3 = cents + A.num_cent;
-	/* sharded counters: per-CoS delivered packets after the table */
-	uint32_t *dlv = HW ? (uint32_t *)(pinfo3 + A.num_pmr) : (uint32_t *)(pinfo4 + A.num_pmr);
-	__shared__ uint32_t blk[4];
 
 	const uint32_t lane = __lane_id();
 	/* wave-uniform (readfirstlane): buffer resources are built from it */
-	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6));
-	const uint32_t nwaves = gridDim.x * (BLOCK / 64);
+	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (LB / 64) + (threadIdx.x >> 6));
+	const uint32_t nwaves = gridDim.x * (LB / 64);
 	const uint32_t ntiles = (A.num + 63u) >> 6;
 	const uint32_t num = A.num;
 	uint32_t fn[16];
@@ -265,17 +276,17 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 	}
 
 	if constexpr (HW) {
-		for (uint32_t k = threadIdx.x; k < A.num_cent; k += BLOCK)
+		for (uint32_t k = threadIdx.x; k < A.num_cent; k += LB)
 			cents[k] = A.cents[k];
-		for (uint32_t k = threadIdx.x; k < A.num_pmr; k += BLOCK)
+		for (uint32_t k = threadIdx.x; k < A.num_pmr; k += LB)
 			pinfo3[k] = A.pinfo3[k];
 #pragma unroll
 		for (int g = 0; g < NG; ++g)
 			mg[g] = load_mg(A.cgroups + g, false);
 	} else {
-		for (uint32_t k = threadIdx.x; k < A.num_ment; k += BLOCK)
+		for (uint32_t k = threadIdx.x; k < A.num_ment; k += LB)
 			ments[k] = A.ments[k];
-		for (uint32_t k = threadIdx.x; k < A.num_pmr; k += BLOCK)
+		for (uint32_t k = threadIdx.x; k < A.num_pmr; k += LB)
 			pinfo4[k] = A.pinfo4[k];
 		if constexpr (NG > 0) {
 #pragma unroll
@@ -283,11 +294,9 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 				mg[g] = load_mg(A.mgroups + g);
 		}
 	}
-	if (A.crow) {
-		for (uint32_t k = threadIdx.x; k < A.num_cos * L64_CNT_SPREAD; k += BLOCK)
+	if constexpr (CM == 2) {
+		for (uint32_t k = threadIdx.x; k < A.num_cos + BIN_EXTRA; k += LB)
 			dlv[k] = 0u;
-		if (threadIdx.x < 4)
-			blk[threadIdx.x] = 0u;
 	}
 	__syncthreads();
 
@@ -302,7 +311,7 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		const uint32_t kvm = key & d.mask;
 		const bool rq = (inf_lo & d.req) == d.req;
 
-		if (d.sh == 0u) {
+		if (!CK && d.sh == 0u) {
 			const bool h = rq & (kvm == d.m1);
 
 			lo |= h ? d.m2 : 0u;
@@ -407,13 +416,29 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 			if (any_match && !err && cos != ODPG_COS_LOOP && mark)
 				w |= ODPG_OUT_MARK_VALID;
 		}
-		if (A.crow && live && !pdrop && cos < A.num_cos && act != 1u)
-#ifndef L64_EXP_NODLV
-			atomicAdd(&dlv[cos * L64_CNT_SPREAD + lane % L64_CNT_SPREAD], 1u);   /* handed to the CoS queue (_odp_cls_enq) */
+		if constexpr (CM == 2) {
+			/* one histogram add per packet carries every counter (four
+			 * bins, then one per CoS): the CoS it is handed to
+			 * error-free (_odp_cls_enq; in_packets), an error packet (goes
+			 * to the error CoS; in_errors), a parse drop (in_errors), no
+			 * CoS or a CoS loop (in_discards), a drop CoS (no counter) */
+			const uint32_t b = pdrop ? BIN_PDROP : err ? BIN_ERR :
+					   cos >= A.num_cos ? BIN_NOCOS : act == 1u ? BIN_DROP : BIN_EXTRA + cos;
+
+#if defined(L64_EXP_BINLANE)   /* experiment builds only: conflict-free bins */
+			if (live)
+				atomicAdd(&dlv[(b & 0u) + lane], 1u);
+#elif defined(L64_EXP_BINZERO)  /* experiment builds only: one bin */
+			if (live)
+				atomicAdd(&dlv[b & 0u], 1u);
+#elif defined(L64_EXP_BINNONE)
+			if (b == 12345u)
+				atomicAdd(&dlv[0], 1u);
 #else
-			;
+			if (live)
+				atomicAdd(&dlv[b], 1u);
 #endif
-		if (A.stats || A.crow) {
+		} else if constexpr (CM == 1) {
 			/* in_packets: delivered error-free (cls ret 0); in_errors:
 			 * parse ret != 0; in_discards: cls ret -1 (no CoS; a CoS loop
 			 * counts the same) */
@@ -527,7 +552,7 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 			const u32x16_t fv = {f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7],
 					     f[8], f[9], f[10], f[11], f[12], f[13], f[14], f[15]};
 			auto fast_key = [&](const MGd &d) -> uint32_t {
-				if (d.slot == SLOT_LEN)
+				if (!CK && d.slot == SLOT_LEN)
 					return 64u;
 				return __builtin_amdgcn_alignbyte(fv[(d.o >> 2) + 1u], fv[d.o >> 2], d.o & 3u);
 			};
@@ -692,36 +717,48 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 		}
 		t0 += nk * nwaves;
 	}
-	if (A.crow) {
-		/* the workgroup's counts into its own row (odpg.h "sharded
-		 * counters"): plain read-modify-writes, rows are not shared */
-		if (lane == 0u) {
-			atomicAdd(&blk[0], n_pkt);
-			atomicAdd(&blk[2], n_err);
-			atomicAdd(&blk[3], n_disc);
-		}
+	if constexpr (CM == 2) {
+		/* the workgroup's histogram into its own counter row (odpg.h
+		 * "sharded counters"): no-return atomics, one trip to L2 at the
+		 * kernel's tail (a read-modify-write would be two) */
+#ifdef L64_EXP_NOFLUSH   /* experiment builds only */
+		if (A.num_cos != 12345u)
+			return;
+#endif
 		__syncthreads();
-		uint64_t *r = A.crow + (size_t)blockIdx.x * A.cwords;
+		const odpg_cnt_dev C = *A.cnt;
+		unsigned long long *r = (unsigned long long *)(C.rows + (size_t)blockIdx.x * C.words);
+		const uint32_t nc = A.num_cos < C.ncos ? A.num_cos : C.ncos;
+		/* without hash queues each CoS owns one column; else its first */
+		auto col = [&](uint32_t c) { return 4u + C.ncos + (C.ident ? c : C.qcol[c]); };
 
-		if (threadIdx.x < 4u && threadIdx.x != 1u) {
-			const uint32_t x = blk[threadIdx.x];
+		for (uint32_t k0 = 0; k0 < nc; k0 += LB) {
+			const uint32_t k = k0 + threadIdx.x;
+			const uint32_t x = k < nc ? dlv[BIN_EXTRA + k] : 0u;
 
-			if (x) {
-				r[threadIdx.x] += x;
-				if (threadIdx.x == 0u)
-					r[1] += (uint64_t)x * 64u;
+			if (x)
+				atomicAdd(r + col(k), (unsigned long long)x);
+			const uint32_t t = wave_sum_u32(x);     /* in_packets, in_octets */
+
+			if (lane == 0u && t) {
+				atomicAdd(r + 0, (unsigned long long)t);
+				atomicAdd(r + 1, (unsigned long long)t * 64ull);
 			}
 		}
-		for (uint32_t k = threadIdx.x; k < A.num_cos && k < A.cncos; k += BLOCK) {
-			uint32_t x = 0u;
+		if (threadIdx.x == 0u) {
+			const uint32_t ne = dlv[BIN_ERR], np = dlv[BIN_PDROP];
+			uint32_t nd = dlv[BIN_NOCOS];
 
-#pragma unroll
-			for (uint32_t j = 0; j < L64_CNT_SPREAD; ++j)
-				x += dlv[k * L64_CNT_SPREAD + j];
-			if (x)
-				r[4u + A.cncos + A.qcol[k]] += x;
+			if (ne && A.err_cos < nc && A.err_act != 1u)
+				atomicAdd(r + col(A.err_cos), (unsigned long long)ne);
+			else if (A.err_cos >= nc)
+				nd += ne;
+			if (ne + np)
+				atomicAdd(r + 2, (unsigned long long)(ne + np));
+			if (nd)
+				atomicAdd(r + 3, (unsigned long long)nd);
 		}
-	} else if (A.stats) {
+	} else if constexpr (CM == 1) {
 		const uint64_t v[4] = {n_pkt, (uint64_t)n_pkt * 64u, n_err, n_disc};
 
 		stats_commit_wave(v, A.sred);
@@ -729,17 +766,17 @@ __global__ __launch_bounds__(BLOCK, L64_WAVES) void odpg_cls64_kernel(const L64A
 }
 
 /* ---- launch ----------------------------------------------------------------- */
-extern "C" uint32_t odpg_resident_grid(const void *kernel, size_t lds);
+extern "C" uint32_t odpg_resident_grid(const void *kernel, uint32_t block, size_t lds);
 
 /* dynamic LDS of a lean launch: generic-parse rows + the table copy */
 size_t odpg_cls64_lds(const odpg_launch_args &a)
 {
 	const bool hw = (a.tbl_flags & TBL_LEAN64HW) && !(a.tbl_flags & TBL_LEAN64);
 
-	return (size_t)BLOCK * 17u * 4u +
+	return (size_t)LB * 17u * 4u +
 	       (hw ? (size_t)a.num_cent * 8u + (size_t)a.num_pmr * 8u
 		   : (size_t)a.num_ment * 16u + (size_t)a.num_pmr * 16u) +
-	       (a.cnt.row ? (size_t)a.num_cos * 4u * L64_CNT_SPREAD : 0u);
+	       (a.cnt.row ? (((size_t)a.num_cos + BIN_EXTRA + 3u) & ~(size_t)3u) * 4u : 0u);
 }
 
 extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
@@ -774,36 +811,45 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	A.out = a->out;
 	A.stats = a->stats;
 	A.sred = a->sred;
-	A.crow = a->cnt.row;
-	A.qcol = a->cnt.qcol;
-	A.cwords = a->cnt.words;
-	A.cncos = a->cnt.ncos;
+	A.cnt = a->cnt.dev;
 
 	const bool hw = (a->tbl_flags & TBL_LEAN64HW) && !(a->tbl_flags & TBL_LEAN64);
 	size_t lds = odpg_cls64_lds(*a);
 #ifdef L64_LDS_PAD   /* experiment builds only: occupancy sensitivity */
 	lds += L64_LDS_PAD;
 #endif
-	const uint32_t occ = odpg_resident_grid(
-		hw ? (const void *)odpg_cls64_kernel<1, true> : (const void *)odpg_cls64_kernel<0, false>, lds);
 	const uint32_t ntiles = (a->num + 63u) / 64u;
-	uint32_t grid = (ntiles + 3u) / 4u;
+	const uint32_t want = (ntiles + LB / 64u - 1u) / (LB / 64u);
+	const uint32_t rows = a->cnt.row ? a->cnt.rows : 0xffffffffu;
+	const int cm = a->cnt.row ? 2 : a->stats ? 1 : 0;
+	const bool ck = !hw && (a->tbl_flags & TBL_MG_CUCKOO);
 
-	if (grid > occ)
-		grid = occ;
-	if (a->cnt.row && grid > a->cnt.rows)
-		grid = a->cnt.rows;   /* one counter row per workgroup */
+	/* resident grid of the instantiation launched, at most one workgroup
+	 * per counter row */
+	auto go = [&](const void *k, auto launch) {
+		uint32_t grid = odpg_resident_grid(k, LB, lds);
+
+		grid = grid < want ? grid : want;
+		grid = grid < rows ? grid : rows;
 #ifdef L64_EXP_GRIDENV   /* experiment builds only: ODPG_L64_GRID workgroups */
-	if (const char *ge = getenv("ODPG_L64_GRID"))
-		grid = (uint32_t)atoi(ge);
+		if (const char *ge = getenv("ODPG_L64_GRID"))
+			grid = (uint32_t)atoi(ge);
 #endif
-#define L64_LAUNCH(ng, h) hipLaunchKernelGGL((odpg_cls64_kernel<ng, h>), dim3(grid), dim3(BLOCK), lds, s, A)
+		launch(grid);
+	};
+#define L64_LAUNCH_CM(ng, h, c, k)                                                           \
+	go((const void *)odpg_cls64_kernel<ng, h, c, k>, [&](uint32_t grid) {                 \
+		hipLaunchKernelGGL((odpg_cls64_kernel<ng, h, c, k>), dim3(grid), dim3(LB), lds, s, A); \
+	})
+#define L64_LAUNCH_K(ng, h, k)                                                                 \
+	(cm == 2 ? L64_LAUNCH_CM(ng, h, 2, k) : cm == 1 ? L64_LAUNCH_CM(ng, h, 1, k) : L64_LAUNCH_CM(ng, h, 0, k))
+#define L64_LAUNCH(ng, h) (ck ? L64_LAUNCH_K(ng, h, true) : L64_LAUNCH_K(ng, h, false))
 	if (hw) {
 		switch (a->num_cgroups) {
-		case 1: L64_LAUNCH(1, true); break;
-		case 2: L64_LAUNCH(2, true); break;
-		case 3: L64_LAUNCH(3, true); break;
-		default: L64_LAUNCH(4, true); break;   /* TBL_LEAN64HW: <= 4 groups */
+		case 1: L64_LAUNCH_K(1, true, false); break;
+		case 2: L64_LAUNCH_K(2, true, false); break;
+		case 3: L64_LAUNCH_K(3, true, false); break;
+		default: L64_LAUNCH_K(4, true, false); break;   /* TBL_LEAN64HW: <= 4 groups */
 		}
 	} else {
 		switch (a->num_mgroups) {
@@ -811,9 +857,11 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 		case 2: L64_LAUNCH(2, false); break;
 		case 3: L64_LAUNCH(3, false); break;
 		case 4: L64_LAUNCH(4, false); break;
-		default: L64_LAUNCH(0, false); break;
+		default: L64_LAUNCH_K(0, false, false); break;
 		}
 	}
 #undef L64_LAUNCH
+#undef L64_LAUNCH_K
+#undef L64_LAUNCH_CM
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -938,7 +938,12 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		for (const dmgroup_t &g : mgroups)
 			if (g.req & ~lean_req)
 				lean = false;
-		h.flags |= TBL_MGROUPS | (lean ? TBL_LEAN64 : 0u);
+		bool cuckoo = true;
+
+		for (const dmgroup_t &g : mgroups)
+			if (g.count <= 1u || g.slot == SLOT_LEN)
+				cuckoo = false;
+		h.flags |= TBL_MGROUPS | (lean ? TBL_LEAN64 : 0u) | (cuckoo ? TBL_MG_CUCKOO : 0u);
 		h.num_mgroups = (uint32_t)mgroups.size();
 		h.num_ment = (uint32_t)ments.size();
 	}

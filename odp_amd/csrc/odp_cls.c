@@ -1267,6 +1267,54 @@ int odpg_pktio_rules(odp_pktio_t hdl, odpg_rules_t *r)
 	return rc;
 }
 
+/* recompile an idle binding for the current generation; nonzero = build a
+ * new binding instead */
+static int bind_update_locked(pktio_e *p, bind_t *b)
+{
+	odpg_rules_t r;
+
+	if (snapshot_locked(p, &r) || odpg_table_update(b->ctx, b->tbl, &r))
+		return -1;
+	const uint32_t ncos = odpg_table_num_cos(b->tbl);
+	int same = odpg_counters_match(b->cnt, b->tbl) && ncos == b->ncos;
+
+	for (uint32_t c = 0; same && c < ncos && c < g.max_cos; c++)
+		same = b->cos_uid[c] == (g.cos[c].valid ? g.cos[c].uid : 0);
+	if (!same) {
+		/* counts so far belong to the CoS the old table named */
+		uint64_t *uid = calloc(ncos ? ncos : 1, sizeof(uint64_t));
+		uint64_t *words = calloc(ODPG_COUNTER_WORDS(ncos), sizeof(uint64_t));
+
+		if (!uid || !words) {
+			free(uid);
+			free(words);
+			return -1;
+		}
+		bind_fold_locked(p, b);
+		if (!odpg_counters_match(b->cnt, b->tbl)) {
+			odpg_counters_destroy(b->cnt);
+			b->cnt = NULL;
+			if (odpg_counters_create(b->ctx, b->tbl, &b->cnt)) {
+				free(uid);
+				free(words);
+				return -1;     /* the caller retires b */
+			}
+		}
+		free(b->cos_uid);
+		free(b->words);
+		b->cos_uid = uid;
+		b->words = words;
+		b->ncos = ncos;
+		for (uint32_t c = 0; c < ncos && c < g.max_cos; c++)
+			b->cos_uid[c] = g.cos[c].valid ? g.cos[c].uid : 0;
+	}
+	b->gen = g.generation;
+	b->pktin_opt = p->config.pktin.all_bits;
+	b->layer = (uint32_t)p->parse_layer;
+	b->classify = (uint32_t)p->cls_enabled;
+	return 0;
+}
+
 /* the pktio's current binding on `ctx`, compiled now if the rules changed
  * since (stale bindings of the context are retired); NULL + *rc on error */
 static bind_t *bind_get_locked(pktio_e *p, odpg_ctx_t *ctx, int *rc)
@@ -1277,6 +1325,13 @@ static bind_t *bind_get_locked(pktio_e *p, odpg_ctx_t *ctx, int *rc)
 	for (b = p->binds; b; b = b->next)
 		if (b->ctx == ctx && !b->stale && b->gen == g.generation)
 			return b;
+	/* an idle binding of the context is recompiled in place: no device
+	 * allocation, and its counters carry on when the CoS layout is kept */
+	for (b = p->binds; b; b = b->next)
+		if (b->ctx == ctx && !b->stale && !b->refs)
+			break;
+	if (b && !bind_update_locked(p, b))
+		return b;
 	while ((b = *pp)) {
 		if (b->ctx == ctx && !b->stale)
 			b->stale = 1;

@@ -95,6 +95,8 @@ typedef struct dcos_s {
 			      * the lean kernel's register parse computes
 			      * (L2, L3, L4, ETH, VLAN, IPV4, IPV6, UDP, TCP,
 			      * IPSEC_AH, IPSEC_ESP) */
+#define TBL_MG_CUCKOO  0x400 /* every mask group is a cuckoo group (> 1 value)
+			      * over a frame word (no frame-length slot) */
 #define TBL_XWALK      0x200 /* hybrid hash walk: walk groups over the single-word
                               * PMRs, xcos / xlist name the complex ones per CoS */
 #define TBL_LEAN64HW   0x100 /* TBL_HASHWALK with <= 4 walk groups whose gates
@@ -294,9 +296,17 @@ typedef struct uint2_s { uint32_t x, y; } uint2_t;
 /* sharded counters of one launch (odpg.h "sharded counters"): row r of
  * `words` u64 belongs to workgroup r: [4 pktio][ncos CoS stats][ncols
  * delivered per queue column, qcol[c] + hash queue] */
+typedef struct odpg_cnt_dev {
+	uint64_t *rows;
+	const uint32_t *qcol;   /* queue column of each CoS (num_cos + 1) */
+	uint32_t words, ncos, ncols;
+	uint32_t ident;         /* ncols == ncos: qcol[c] == c */
+} odpg_cnt_dev;
+
 typedef struct odpg_cnt_args {
 	uint64_t *row;          /* rows base, NULL = no sharded counters */
 	const uint32_t *qcol;   /* device, queue column of each CoS (num_cos + 1) */
+	const odpg_cnt_dev *dev;   /* device copy of this layout (lean kernel) */
 	uint32_t words, rows, ncos, ncols;
 	uint32_t cos;           /* the table has CoS with stats_enable */
 	uint32_t pad;

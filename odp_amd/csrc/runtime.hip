@@ -66,6 +66,8 @@ struct odpg_table_s {
 	int device;
 	int cycle;
 	uint64_t qsig;     /* counter layout: CoS count, queues and stats flags */
+	size_t cap;        /* bytes allocated at dblob */
+	hipEvent_t uploaded;   /* the last upload of `blob` has been consumed */
 };
 
 /* odpg.h "sharded counters" */
@@ -76,6 +78,7 @@ struct odpg_counters_s {
 	uint32_t any_cos;              /* some CoS has stats_enable */
 	uint64_t *drows;               /* device, rows x words */
 	uint32_t *dqcol;               /* device, queue column of each CoS */
+	odpg_cnt_dev *ddev;            /* device, the layout for the lean kernel */
 	uint64_t *dsum;                /* device, words (fold target) */
 	uint64_t *hsum;                /* pinned host, words */
 	hipEvent_t done;
@@ -242,11 +245,13 @@ int odpg_table_create(odpg_ctx_t *c, const odpg_rules_t *rules, odpg_table_t **o
 	t->cycle = odpg_rules_has_cycle(t->blob, t->hdr);
 	t->device = c->device;
 	t->qsig = table_qsig(t);
+	t->uploaded = nullptr;
 	hipSetDevice(c->device);
 	if (hipMalloc(&t->dblob, t->hdr.blob_bytes) != hipSuccess) {
 		delete t;
 		return -ENOMEM;
 	}
+	t->cap = t->hdr.blob_bytes;
 	if (hipMemcpyAsync(t->dblob, t->blob.data(), t->hdr.blob_bytes, hipMemcpyHostToDevice,
 			   c->stream) != hipSuccess ||
 	    hipStreamSynchronize(c->stream) != hipSuccess) {
@@ -258,11 +263,57 @@ int odpg_table_create(odpg_ctx_t *c, const odpg_rules_t *rules, odpg_table_t **o
 	return 0;
 }
 
+int odpg_table_update(odpg_ctx_t *c, odpg_table_t *t, const odpg_rules_t *rules)
+{
+	if (!c || !t || !rules)
+		return -EINVAL;
+	if (t->device != c->device)
+		return -EXDEV;
+	std::vector<uint8_t> blob;
+	dtable_hdr_t hdr;
+	int rc = odpg_compile_rules(rules, blob, &hdr);
+
+	if (rc)
+		return rc;
+	std::lock_guard<std::mutex> g(c->lock);
+
+	hipSetDevice(c->device);
+	/* the previous upload read t->blob asynchronously */
+	if (t->uploaded && hipEventSynchronize(t->uploaded) != hipSuccess)
+		return -EIO;
+	if (!t->uploaded && hipEventCreateWithFlags(&t->uploaded, hipEventDisableTiming) != hipSuccess)
+		return -EIO;
+	if (hdr.blob_bytes > t->cap) {
+		void *nb = nullptr;
+
+		/* launches still reading the old allocation end first */
+		if (hipStreamSynchronize(c->stream) != hipSuccess ||
+		    hipMalloc(&nb, hdr.blob_bytes) != hipSuccess)
+			return -ENOMEM;
+		hipFree(t->dblob);
+		t->dblob = nb;
+		t->cap = hdr.blob_bytes;
+	}
+	t->blob.swap(blob);
+	t->hdr = hdr;
+	t->cycle = odpg_rules_has_cycle(t->blob, t->hdr);
+	t->qsig = table_qsig(t);
+	if (hipMemcpyAsync(t->dblob, t->blob.data(), t->hdr.blob_bytes, hipMemcpyHostToDevice,
+			   c->stream) != hipSuccess ||
+	    hipEventRecord(t->uploaded, c->stream) != hipSuccess)
+		return -EIO;
+	return 0;
+}
+
 void odpg_table_destroy(odpg_table_t *t)
 {
 	if (!t)
 		return;
 	hipSetDevice(t->device);
+	if (t->uploaded) {
+		hipEventSynchronize(t->uploaded);
+		hipEventDestroy(t->uploaded);
+	}
 	hipFree(t->dblob);
 	delete t;
 }
@@ -289,6 +340,7 @@ static void counters_free(odpg_counters_t *k)
 {
 	hipFree(k->drows);
 	hipFree(k->dqcol);
+	hipFree(k->ddev);
 	hipFree(k->dsum);
 	if (k->hsum)
 		hipHostFree(k->hsum);
@@ -344,16 +396,26 @@ int odpg_counters_create(odpg_ctx_t *c, const odpg_table_t *t, odpg_counters_t *
 
 	if (hipMalloc(&k->drows, rb) != hipSuccess ||
 	    hipMalloc(&k->dqcol, (size_t)(k->ncos + 1u) * 4u) != hipSuccess ||
+	    hipMalloc(&k->ddev, sizeof(odpg_cnt_dev)) != hipSuccess ||
 	    hipMalloc(&k->dsum, (size_t)k->words * 8u) != hipSuccess ||
 	    hipHostMalloc(&k->hsum, (size_t)k->words * 8u, hipHostMallocDefault) != hipSuccess ||
 	    hipEventCreateWithFlags(&k->done, hipEventDisableTiming) != hipSuccess) {
 		counters_free(k);
 		return -ENOMEM;
 	}
+	odpg_cnt_dev hd;
+
+	hd.rows = k->drows;
+	hd.qcol = k->dqcol;
+	hd.words = k->words;
+	hd.ncos = k->ncos;
+	hd.ncols = k->ncols;
+	hd.ident = k->ncols == k->ncos;
 	{
 		std::lock_guard<std::mutex> g(c->lock);
 
-		if (hipMemsetAsync(k->drows, 0, rb, c->stream) != hipSuccess ||
+		if (hipMemcpyAsync(k->ddev, &hd, sizeof(hd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+		    hipMemsetAsync(k->drows, 0, rb, c->stream) != hipSuccess ||
 		    hipMemsetAsync(k->dsum, 0, (size_t)k->words * 8u, c->stream) != hipSuccess ||
 		    hipMemcpyAsync(k->dqcol, k->qcol.data(), (size_t)(k->ncos + 1u) * 4u,
 				   hipMemcpyHostToDevice, c->stream) != hipSuccess ||
@@ -368,6 +430,11 @@ int odpg_counters_create(odpg_ctx_t *c, const odpg_table_t *t, odpg_counters_t *
 	}
 	*out = k;
 	return 0;
+}
+
+int odpg_counters_match(const odpg_counters_t *k, const odpg_table_t *t)
+{
+	return k && t && k->qsig == t->qsig && k->ncos == t->hdr.num_cos;
 }
 
 void odpg_counters_destroy(odpg_counters_t *k)
@@ -524,6 +591,7 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 
 		a.cnt.row = k->drows;
 		a.cnt.qcol = k->dqcol;
+		a.cnt.dev = k->ddev;
 		a.cnt.words = k->words;
 		a.cnt.rows = k->rows;
 		a.cnt.ncos = k->ncos;

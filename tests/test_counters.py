@@ -131,3 +131,58 @@ def test_counters_errors(gpu_ctx, fresh_cls):
     assert L.lib.odpg_classify(gpu_ctx.h, t1.h, C.byref(b), C.byref(r)) == 0
     gpu_ctx.sync()
     assert cnt.fold()["pktio"][0] == 256
+
+
+@pytest.mark.gpu
+def test_recv_batch_rule_changes(gpu_ctx, fresh_cls):
+    """odpg_pktio_recv_batch across rule changes: the binding is recompiled
+    in place (odpg_table_update) and its counters carry on; counts made
+    before a CoS was destroyed never reach the CoS later created in its slot
+    (the reference's cos_create zeroes its counters)."""
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    r = gen.build_c2_rules(fresh_cls, p, stats=True)
+    assert fresh_cls.pktio_start(p) == 0
+    n = 50000
+    fr = gen.c2_frames(n, seed=9)
+    fb = gpu_ctx.buffer(fr.nbytes)
+    fb.upload(fr)
+    ob = gpu_ctx.buffer(4 * n)
+    leaf = r["leaves"][5]
+
+    def recv():
+        o = oracle.classify(fresh_cls.pktio_rules(p), fr, n, stride=64, opt=ALL_CHKSUM)
+        rc = L.lib.odpg_pktio_recv_batch(p, gpu_ctx.h, fb.ptr, None, 64, n, 1, ob.ptr, None)
+        assert rc == 0
+        gpu_ctx.sync()
+        assert np.array_equal(ob.download(np.uint32, n), o["out"])
+        return o
+
+    o1 = recv()
+    # a PMR change: the CoS layout is kept
+    extra = fresh_cls.pmr_create([fresh_cls.Term(fresh_cls.PMR_UDP_SPORT, b"\x00\x07",
+                                                 b"\x00\xff")], r["l1"][0], leaf)
+    assert extra
+    o2 = recv()
+    want_leaf = int(o1["stats"][4 + fresh_cls.to_index(leaf)] + o2["stats"][4 + fresh_cls.to_index(leaf)])
+    rc, cs = fresh_cls.cos_stats(leaf)
+    assert rc == 0 and cs.packets == want_leaf
+    rc, qs = fresh_cls.queue_stats(leaf, fresh_cls.cos_queue(leaf))
+    q_want = sum(int(((o["out"] & 0xFFFF) == fresh_cls.to_index(leaf)).sum()) for o in (o1, o2))
+    assert rc == 0 and qs.packets == q_want
+    st = fresh_cls.pktio_stats(p)
+    assert st.in_packets == 2 * n
+    # destroy a leaf without reading its counters, create another CoS in its
+    # slot and route the same rules to it
+    slot = fresh_cls.to_index(leaf)
+    assert fresh_cls.pmr_destroy(extra) == 0
+    o3 = recv()                                       # counts for the old leaf
+    assert fresh_cls.cos_destroy(leaf) == 0
+    new = fresh_cls.cos_create("new_leaf", queue=fresh_cls.queue(77), stats_enable=True)
+    assert fresh_cls.to_index(new) == slot
+    o4 = recv()
+    rc, cs = fresh_cls.cos_stats(new)
+    assert rc == 0 and cs.packets == int(o4["stats"][4 + slot])
+    rc, qs = fresh_cls.queue_stats(new, fresh_cls.cos_queue(new))
+    assert rc == 0 and qs.packets == int(((o4["out"] & 0xFFFF) == slot).sum())
+    assert fresh_cls.pktio_stats(p).in_packets == 4 * n
+    del o3

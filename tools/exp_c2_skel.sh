@@ -2,5 +2,5 @@
 # (experiment builds under odp_amd/lib/exp_*)
 set -u
 export TMPDIR=/tmp
-VARIANTS="base exp_s8 exp_s64 exp_nodlv" STEPS=300 bash tools/ab.sh || exit 3
-TAG=r2 VARIANTS="base exp_s8 exp_s64 exp_nodlv" STEPS=300 bash tools/ab.sh || exit 3
+VARIANTS="base exp_nf exp_bnone exp_both" STEPS=300 bash tools/ab.sh || exit 3
+TAG=r2 VARIANTS="base exp_nf exp_bnone exp_both" STEPS=300 bash tools/ab.sh || exit 3
