@@ -13,8 +13,14 @@ sharded device counters odp_pktio_stats reads; it is reported as
 Launch:  python bench.py [--gpus N --steps K --warmup W --config c2]
          torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 Packets are independent: each rank classifies its own shard (weak scaling,
-no data-path collective). The only collective is the end-of-run RCCL
-all-reduce of the CoS / pktio counters (odp_cls_cos_stats semantics).
+no data-path collective). Rank 0 compiles the rule table once and broadcasts
+the image (odpg_rules_compile / odpg_table_import); the only other collective
+is the end-of-run all-reduce of the CoS / pktio counters (odp_cls_cos_stats
+semantics). --backend picks RCCL ("nccl", default) or gloo; ranks beyond the
+visible GPUs share them (LOCAL_RANK modulo the device count), so a 2-rank
+gloo run on one GPU exercises the whole multi-rank path. --source gpu0 adds
+a second workload: each step's batch originates on rank 0's GPU, is
+scattered over the ranks and the verdicts gathered back.
 
 Rank 0 prints one JSON line (contract in the task description) with a
 `roofline` object (kernel time from HIP events on the classify stream) and a
@@ -61,6 +67,10 @@ def parse_args():
                          "stores only")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-buffer path (pinned H2D + kernel + D2H)")
+    ap.add_argument("--backend", default=os.environ.get("ODPG_DIST_BACKEND", "nccl"),
+                    choices=["nccl", "gloo"], help="torch.distributed backend for N > 1")
+    ap.add_argument("--source", default="sharded", choices=["sharded", "gpu0"],
+                    help="gpu0: also time scatter-from-rank-0 + classify + gather-to-root")
     return ap.parse_args()
 
 
@@ -74,8 +84,10 @@ def main():
         import torch
         import torch.distributed as tdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        ndev = torch.cuda.device_count()
+        local = local % ndev if ndev else local     # ranks may share a GPU
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", rank=rank, world_size=world)
+        tdist.init_process_group(args.backend, rank=rank, world_size=world)
         dist = tdist
 
     import ctypes as C
@@ -120,6 +132,10 @@ def main():
                     "-> 55 leaf CoS), pktin ipv4+udp+tcp checksum verify")
     assert cls.pktio_start(pktio) == 0
     rules = cls.pktio_rules(pktio)
+    # the table is compiled once, on rank 0, and its image broadcast
+    dev = f"cuda:{local}" if dist is not None and args.backend == "nccl" else None
+    image = gpu.compile_rules(rules) if rank == 0 else None
+    image = shard.broadcast_bytes(image, dist, dev)
 
     n = args.batch
     # each rank owns a distinct shard of the synthetic capture
@@ -136,7 +152,7 @@ def main():
         bytes_per_pkt = stride + 4           # frame + verdict
     ctx = gpu.Context(local)
     ctx.set_kernel_mode(args.kernel_mode)
-    tbl = ctx.table(rules)
+    tbl = ctx.table(image=image)
     nbuf = args.buffers or max(2, -(-300 * (1 << 20) // frames.nbytes))
     fbufs, obufs, dbufs = [], [], []
     for _ in range(nbuf):
@@ -194,7 +210,6 @@ def main():
         L.check(lib.odpg_event_elapsed_ms(ctx.h, 0, 1, C.byref(ev_ms)), "event")
         return t1 - t0, ev_ms.value / max(args.steps, 1)
 
-    dev = f"cuda:{local}" if dist is not None else None
     wall, kernel_ms = timed(results)
     # max wall clock over ranks
     wall = shard.max_over_ranks(wall, dist, dev)
@@ -265,12 +280,84 @@ def main():
             out["diag"] = args.diag
         if args.e2e:
             out["e2e_host_path"] = e2e(ctx, tbl, frames, desc, n, stride, opt)
+    if args.source == "gpu0" and dist is not None and stride:
+        sg = bench_scatter_gather(args, ctx, tbl, frames, n, stride, opt, world, rank, local,
+                                  dist)
+        if out is not None:
+            out["scatter_gather"] = sg
+    if out is not None:
         print(json.dumps(out), flush=True)
     cnt.close()
     del tbl
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def bench_scatter_gather(args, ctx, tbl, frames, n, stride, opt, world, rank, local, dist):
+    """SURVEY §8(e) optional path: the whole batch (world x n frames) sits in
+    rank 0's HBM; per step it is scattered over the ranks (RCCL over xGMI, or
+    gloo through host memory), each rank classifies its shard, and the verdict
+    shards are gathered on rank 0. Timed like the headline loop (barriers,
+    max over ranks); value = world * n packets per step / time."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    from odp_amd import _lib as L
+    from odp_amd import shard
+    on_gpu = args.backend == "nccl"
+    cdev = torch.device(f"cuda:{local}") if on_gpu else torch.device("cpu")
+    per = torch.from_numpy(np.ascontiguousarray(frames).reshape(n, stride))
+    whole = per.repeat(world, 1).to(cdev) if rank == 0 else None
+    mine = torch.empty((n, stride), dtype=torch.uint8, device=cdev)
+    verd = torch.empty(n, dtype=torch.int32, device=cdev)
+    fb = ob = None
+    if not on_gpu:                  # gloo moves host tensors: stage them
+        fb, ob = ctx.buffer(n * stride), ctx.buffer(4 * n)
+    src = mine.data_ptr() if on_gpu else fb.ptr
+    dst = verd.data_ptr() if on_gpu else ob.ptr
+    b = L.odpg_batch_t(src, None, stride, n, opt, L.LAYER_ALL, 1)
+    r = L.odpg_result_t(dst, None, None, None, None)
+
+    def step():
+        shard.scatter_shards(whole, mine, dist)
+        if on_gpu:                  # the shard in HBM, classified in place
+            torch.cuda.current_stream().synchronize()
+        else:
+            fb.upload(mine.numpy())
+        L.check(L.lib.odpg_classify(ctx.h, tbl.h, C.byref(b), C.byref(r)), "odpg_classify")
+        ctx.sync()
+        if not on_gpu:
+            verd.copy_(torch.from_numpy(ob.download(np.int32, n)))
+        return shard.gather_to_root(verd, dist)
+
+    for _ in range(max(1, args.warmup // 4)):
+        step()
+    ctx.sync()
+    dist.barrier()
+    steps = max(1, args.steps // 4)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        got = step()
+    if on_gpu:
+        torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    dist.barrier()
+    wall = shard.max_over_ranks(t1 - t0, dist, cdev if on_gpu else None)
+    if rank == 0:
+        # every shard is the same capture: the gathered verdicts repeat
+        g = got.cpu().numpy().reshape(world, n)
+        assert all(np.array_equal(g[0], g[k]) for k in range(world)), "gathered shards differ"
+    for x in (fb, ob):
+        if x is not None:
+            x.free()
+    return {"value": round(world * n * steps / wall / 1e6, 1),
+            "ms_per_step": round(wall * 1e3 / steps, 4), "steps": steps,
+            "backend": args.backend,
+            "what": "batch on rank 0's GPU: scatter (64 B/pkt) + classify + gather 4 B "
+                    "verdicts to rank 0, per step"}
 
 
 def pmc_traffic(config):
@@ -339,7 +426,7 @@ def bench_tx(args, world, rank, local, dist):
     kernel_ms = ev_ms.value / max(args.steps, 1)
     out = obufs[(args.steps - 1) % nbuf].download(np.uint32, n)
     assert np.all(out & L.TX_OUT_IPV4) and np.all(out & L.TX_OUT_UDP)
-    wall = shard.max_over_ranks(wall, dist, f"cuda:{local}" if dist is not None else None)
+    wall = shard.max_over_ranks(wall, dist, f"cuda:{local}" if dist is not None and args.backend == "nccl" else None)
     value = n * world * args.steps / wall / 1e6
     bytes_per_pkt = 64 + 4 + 4           # frame read + two checksum fields + out word
     achieved = bytes_per_pkt * n / (kernel_ms * 1e-3) / 1e9
@@ -431,7 +518,7 @@ def bench_l3fwd(args, world, rank, local, dist):
     kernel_ms = ev_ms.value / max(args.steps, 1)
     out = obufs[(args.steps - 1) % nbuf].download(np.int32, n)
     assert (out >= 0).all(), "every C5 packet is IPv4 and forwarded"
-    wall = shard.max_over_ranks(wall, dist, f"cuda:{local}" if dist is not None else None)
+    wall = shard.max_over_ranks(wall, dist, f"cuda:{local}" if dist is not None and args.backend == "nccl" else None)
     value = n * world * args.steps / wall / 1e6
     bytes_per_pkt = 64 + 32 + 4          # frame read + header rewrite + port
     achieved = bytes_per_pkt * n / (kernel_ms * 1e-3) / 1e9

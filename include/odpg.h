@@ -251,6 +251,12 @@ int  odpg_ctx_sync(odpg_ctx_t *ctx);
  * is indeterminate", odp_classification.c:1348-1349); here each snapshot is
  * immutable and rebuilt per generation. */
 int  odpg_table_create(odpg_ctx_t *ctx, const odpg_rules_t *rules, odpg_table_t **tbl);
+/* Compiled-table image, host only (no device): the bytes a multi-GPU job
+ * compiles once and broadcasts; each rank imports them on its
+ * own device. With blob NULL or *size too small: -ENOSPC and *size = the
+ * bytes needed. */
+int  odpg_rules_compile(const odpg_rules_t *rules, void *blob, size_t *size);
+int  odpg_table_import(odpg_ctx_t *ctx, const void *blob, size_t size, odpg_table_t **tbl);
 /* Recompile `tbl` in place from new rules (a new generation): the upload is
  * ordered on the context stream after the launches already enqueued with the
  * old contents, so it needs no wait and no reallocation unless the table

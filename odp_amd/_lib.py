@@ -257,6 +257,8 @@ SIGNATURES = {
     "odpg_ctx_sync": (_i32, [_vp]),
     "odpg_table_create": (_i32, [_vp, C.POINTER(odpg_rules_t), C.POINTER(_vp)]),
     "odpg_table_update": (_i32, [_vp, _vp, C.POINTER(odpg_rules_t)]),
+    "odpg_rules_compile": (_i32, [C.POINTER(odpg_rules_t), _vp, C.POINTER(_sz)]),
+    "odpg_table_import": (_i32, [_vp, _vp, _sz, C.POINTER(_vp)]),
     "odpg_table_destroy": (None, [_vp]),
     "odpg_table_num_cos": (_u32, [_vp]),
     "odpg_table_has_cycle": (_i32, [_vp]),

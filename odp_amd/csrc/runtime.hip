@@ -231,17 +231,45 @@ int odpg_ctx_sync(odpg_ctx_t *c)
 	return 0;
 }
 
-int odpg_table_create(odpg_ctx_t *c, const odpg_rules_t *rules, odpg_table_t **out)
-{
-	if (!c || !rules || !out)
-		return -EINVAL;
-	odpg_table_t *t = new odpg_table_t();
-	int rc = odpg_compile_rules(rules, t->blob, &t->hdr);
+/* compiled-table image: this header, dtable_hdr_t, then the blob */
+struct table_image_hdr {
+	uint32_t magic;        /* IMAGE_MAGIC */
+	uint32_t abi;          /* ODPG_ABI_VERSION */
+	uint32_t hdr_bytes;    /* sizeof(dtable_hdr_t) */
+	uint32_t blob_bytes;
+};
+#define IMAGE_MAGIC 0x5450444fu   /* "ODPT" in memory order */
 
-	if (rc) {
-		delete t;
+int odpg_rules_compile(const odpg_rules_t *rules, void *image, size_t *size)
+{
+	if (!rules || !size)
+		return -EINVAL;
+	std::vector<uint8_t> blob;
+	dtable_hdr_t hdr;
+	int rc = odpg_compile_rules(rules, blob, &hdr);
+
+	if (rc)
 		return rc;
+	const size_t need = sizeof(table_image_hdr) + sizeof(dtable_hdr_t) + hdr.blob_bytes;
+
+	if (!image || *size < need) {
+		*size = need;
+		return -ENOSPC;
 	}
+	table_image_hdr ih = {IMAGE_MAGIC, ODPG_ABI_VERSION, (uint32_t)sizeof(dtable_hdr_t),
+			      hdr.blob_bytes};
+	uint8_t *o = (uint8_t *)image;
+
+	memcpy(o, &ih, sizeof(ih));
+	memcpy(o + sizeof(ih), &hdr, sizeof(hdr));
+	memcpy(o + sizeof(ih) + sizeof(hdr), blob.data(), hdr.blob_bytes);
+	*size = need;
+	return 0;
+}
+
+/* a compiled table (host blob + header) onto the context's device */
+static int table_upload(odpg_ctx_t *c, odpg_table_t *t, odpg_table_t **out)
+{
 	t->cycle = odpg_rules_has_cycle(t->blob, t->hdr);
 	t->device = c->device;
 	t->qsig = table_qsig(t);
@@ -261,6 +289,43 @@ int odpg_table_create(odpg_ctx_t *c, const odpg_rules_t *rules, odpg_table_t **o
 	}
 	*out = t;
 	return 0;
+}
+
+int odpg_table_import(odpg_ctx_t *c, const void *image, size_t size, odpg_table_t **out)
+{
+	if (!c || !image || !out || size < sizeof(table_image_hdr))
+		return -EINVAL;
+	table_image_hdr ih;
+
+	memcpy(&ih, image, sizeof(ih));
+	if (ih.magic != IMAGE_MAGIC || ih.abi != ODPG_ABI_VERSION ||
+	    ih.hdr_bytes != sizeof(dtable_hdr_t) ||
+	    size != sizeof(ih) + sizeof(dtable_hdr_t) + (size_t)ih.blob_bytes)
+		return -EINVAL;
+	odpg_table_t *t = new odpg_table_t();
+
+	memcpy(&t->hdr, (const uint8_t *)image + sizeof(ih), sizeof(dtable_hdr_t));
+	if (t->hdr.blob_bytes != ih.blob_bytes) {
+		delete t;
+		return -EINVAL;
+	}
+	t->blob.assign((const uint8_t *)image + sizeof(ih) + sizeof(dtable_hdr_t),
+		       (const uint8_t *)image + size);
+	return table_upload(c, t, out);
+}
+
+int odpg_table_create(odpg_ctx_t *c, const odpg_rules_t *rules, odpg_table_t **out)
+{
+	if (!c || !rules || !out)
+		return -EINVAL;
+	odpg_table_t *t = new odpg_table_t();
+	int rc = odpg_compile_rules(rules, t->blob, &t->hdr);
+
+	if (rc) {
+		delete t;
+		return rc;
+	}
+	return table_upload(c, t, out);
 }
 
 int odpg_table_update(odpg_ctx_t *c, odpg_table_t *t, const odpg_rules_t *rules)

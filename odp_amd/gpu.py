@@ -49,10 +49,27 @@ class DeviceBuffer:
             pass
 
 
+def compile_rules(rules):
+    """Compiled-table image of `rules` (host only, odpg_rules_compile): the
+    bytes a multi-GPU job compiles once and broadcasts."""
+    n = C.c_size_t(0)
+    rc = lib.odpg_rules_compile(C.byref(rules), None, C.byref(n))
+    if rc not in (0, -28):                 # -ENOSPC: size query
+        L.check(rc, "odpg_rules_compile")
+    buf = (C.c_uint8 * n.value)()
+    L.check(lib.odpg_rules_compile(C.byref(rules), buf, C.byref(n)), "odpg_rules_compile")
+    return bytes(buf)
+
+
 class Table:
-    def __init__(self, ctx, rules):
+    def __init__(self, ctx, rules=None, image=None):
         t = C.c_void_p()
-        L.check(lib.odpg_table_create(ctx.h, C.byref(rules), C.byref(t)), "odpg_table_create")
+        if image is not None:
+            b = (C.c_uint8 * len(image)).from_buffer_copy(image)
+            L.check(lib.odpg_table_import(ctx.h, b, len(image), C.byref(t)), "odpg_table_import")
+        else:
+            L.check(lib.odpg_table_create(ctx.h, C.byref(rules), C.byref(t)),
+                    "odpg_table_create")
         self.h = t.value
         self.num_cos = lib.odpg_table_num_cos(self.h)
         self.has_cycle = bool(lib.odpg_table_has_cycle(self.h))
@@ -131,8 +148,8 @@ class Context:
     def buffer(self, nbytes):
         return DeviceBuffer(self, nbytes)
 
-    def table(self, rules):
-        return Table(self, rules)
+    def table(self, rules=None, image=None):
+        return Table(self, rules, image)
 
     def counters(self, table):
         return Counters(self, table)

@@ -68,3 +68,49 @@ def gather_verdicts(out, dist, n_total, world, device=None):
     parts = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(parts, t)
     return np.concatenate([p.cpu().numpy()[:c].astype(np.uint32) for p, c in zip(parts, counts)])
+
+
+def broadcast_bytes(data, dist, device=None, src=0):
+    """Broadcast a byte string from ``src`` (the compiled table image,
+    odpg_rules_compile: once per table generation); other
+    ranks pass None and receive it."""
+    if dist is None:
+        return data
+    import torch
+    n = torch.tensor([len(data) if data is not None else 0], dtype=torch.int64)
+    if device is not None:
+        n = n.to(device)
+    dist.broadcast(n, src)
+    size = int(n.item())
+    if data is not None and dist.get_rank() == src:
+        buf = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    else:
+        buf = torch.zeros(size, dtype=torch.uint8)
+    if device is not None:
+        buf = buf.to(device)
+    dist.broadcast(buf, src)
+    return bytes(buf.cpu().numpy().tobytes())
+
+
+def scatter_shards(whole, shard, dist, src=0):
+    """One batch that originates on rank ``src``'s GPU, split by packet range
+    over the ranks (SURVEY §8(e) "scatter over xGMI"): ``whole`` is a
+    [world * per_rank, stride] uint8 tensor on ``src`` (None elsewhere),
+    ``shard`` this rank's [per_rank, stride] receive tensor. Equal shards."""
+    world = dist.get_world_size()
+    parts = list(whole.chunk(world)) if dist.get_rank() == src else None
+    dist.scatter(shard, parts, src=src)
+    return shard
+
+
+def gather_to_root(part, dist, dst=0):
+    """Every rank's verdict shard (equal sizes) concatenated on ``dst``
+    (grouped send/recv to the root); None on other ranks."""
+    import torch
+    world = dist.get_world_size()
+    if dist.get_rank() == dst:
+        parts = [torch.empty_like(part) for _ in range(world)]
+        dist.gather(part, parts, dst=dst)
+        return torch.cat(parts)
+    dist.gather(part, None, dst=dst)
+    return None

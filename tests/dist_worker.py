@@ -35,31 +35,52 @@ def main():
     gen.build_c2_rules(cls, pktio, stats=True)
     assert cls.pktio_start(pktio) == 0
     rules = cls.pktio_rules(pktio)
+    # the table image: compiled on rank 0 only and broadcast (bench.py's
+    # path); every rank checks it against its own compile of the same rules
+    from odp_amd import gpu
+    image = shard.broadcast_bytes(gpu.compile_rules(rules) if rank == 0 else None, dist)
+    image_bad = shard.reduce_counters([int(image != gpu.compile_rules(rules))], dist)[0]
     frames = gen.c2_frames(a.npkt).reshape(a.npkt, 64)
     start, count = shard.shard_range(a.npkt, rank, world)
     mine = np.ascontiguousarray(frames[start:start + count])
+    ctx = tbl = None
     if a.engine == "gpu":
-        from odp_amd import gpu
         ndev = max(1, L.lib.odpg_device_count())     # ranks may share one GPU
         ctx = gpu.Context(int(os.environ.get("LOCAL_RANK", "0")) % ndev)
-        tbl = ctx.table(rules)
-        res = ctx.classify(tbl, mine, count, stride=64, opt=opt)
-        out, stats = res["out"], res["stats"]
-        del tbl
-        ctx.close()
-    else:
-        import oracle
-        res = oracle.classify(rules, mine, count, stride=64, opt=opt)
-        out, stats = res["out"], res["stats"]
+        tbl = ctx.table(image=image)
+
+    def run(fr, n):
+        if a.engine == "gpu":
+            res = ctx.classify(tbl, fr, n, stride=64, opt=opt)
+        else:
+            import oracle
+            res = oracle.classify(rules, fr, n, stride=64, opt=opt)
+        return res["out"], res["stats"]
+
+    out, stats = run(mine, count)
     total = shard.reduce_counters(stats, dist)
     allout = shard.gather_verdicts(out, dist, a.npkt, world)
     slowest = shard.max_over_ranks(float(rank), dist)
+    # scatter-from-root / gather-to-root (equal shards of a batch on rank 0)
+    import torch
+    per = a.npkt // world
+    whole = torch.from_numpy(np.ascontiguousarray(frames[:per * world])) if rank == 0 else None
+    recv = torch.empty((per, 64), dtype=torch.uint8)
+    shard.scatter_shards(whole, recv, dist)
+    sout, _ = run(recv.numpy(), per)
+    gathered = shard.gather_to_root(torch.from_numpy(sout.astype(np.int32)), dist)
+    if tbl is not None:
+        del tbl
+        ctx.close()
     if rank == 0:
         with open(a.out, "w") as f:
             json.dump({"world": world, "stats": [int(x) for x in total],
                        "out_sha": int(np.bitwise_xor.reduce(allout.astype(np.uint64) *
                                                             np.arange(1, a.npkt + 1, dtype=np.uint64))),
-                       "n_out": int(len(allout)), "max_rank": slowest}, f)
+                       "n_out": int(len(allout)), "max_rank": slowest,
+                       "image_bad_ranks": int(image_bad), "image_bytes": len(image),
+                       "scatter_gather_equal": bool(np.array_equal(
+                           gathered.numpy().astype(np.uint32), allout[:per * world]))}, f)
         np.save(a.out + ".npy", allout)
     dist.destroy_process_group()
 

@@ -73,6 +73,9 @@ def test_two_rank_gloo_matches_whole_batch(tmp_path):
     np.testing.assert_array_equal(allout, ref["out"])
     assert got["stats"] == [int(x) for x in ref["stats"]]
     assert got["stats"][0] == n          # every packet delivered to a CoS queue
+    # rank 0's compiled image reached rank 1 byte-exact; scatter/gather path
+    assert got["image_bad_ranks"] == 0 and got["image_bytes"] > 0
+    assert got["scatter_gather_equal"]
 
 
 @pytest.mark.gpu
@@ -84,3 +87,24 @@ def test_two_rank_gpu_shards_match_whole_batch(tmp_path):
     ref = _whole(n)
     np.testing.assert_array_equal(allout, ref["out"])
     assert got["stats"] == [int(x) for x in ref["stats"]]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_gpu(tmp_path):
+    """bench.py itself with world size 2 over gloo, both ranks on one GPU:
+    the table image broadcast, per-rank shards, max-over-ranks timing, the
+    counter all-reduce and the scatter-from-rank-0 / gather-to-root loop."""
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "2", "--steps", "20",
+           "--warmup", "4", "--batch", str(1 << 16), "--no-cpu", "--backend", "gloo",
+           "--source", "gpu0"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["scaling"] == "weak"
+    assert d["with_pktio_counters"]["value"] > 0
+    assert d["scatter_gather"]["value"] > 0 and d["scatter_gather"]["backend"] == "gloo"
