@@ -12,13 +12,14 @@
  * drive the classifier the way pktio/loop.c does; it is not the full
  * odp_pktio API.
  *
- * Struct layouts follow the spec's field order; nested types the classifier
- * does not interpret (queue parameters, RED/BP, packet vectors) are
- * simplified — see INTEGRATION.md "ABI notes".
+ * Every struct the API passes has the reference's x86-64 layout (field
+ * order, types, sizes), checked against the reference header text by
+ * tests/test_abi_layout.py.
  */
 #ifndef ODP_CLS_H_
 #define ODP_CLS_H_
 
+#include <stdbool.h>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -28,22 +29,127 @@
 extern "C" {
 #endif
 
-typedef int odp_bool_t;
+/* ---- base and handle types ----------------------------------------------
+ * Layouts are those of the reference's x86-64 linux-generic ABI (a caller
+ * compiled against the reference headers passes the same bytes):
+ * odp_bool_t is C bool (abi-default/std_types.h), handles are pointers
+ * (ODP_HANDLE_T, include-abi), scheduler ids are int (abi-default/
+ * schedule_types.h). tests/test_abi_layout.py checks every struct below
+ * field by field against a layout computed from the reference header text. */
+typedef bool odp_bool_t;
+typedef uint32_t odp_percent_t;
 
-typedef struct _odp_cos_hdl   *odp_cos_t;
-typedef struct _odp_pmr_hdl   *odp_pmr_t;
-typedef struct _odp_queue_hdl *odp_queue_t;
-typedef struct _odp_pool_hdl  *odp_pool_t;
-typedef struct _odp_pktio_hdl *odp_pktio_t;
+typedef struct _odp_cos_hdl    *odp_cos_t;
+typedef struct _odp_pmr_hdl    *odp_pmr_t;
+typedef struct _odp_queue_hdl  *odp_queue_t;
+typedef struct _odp_pool_hdl   *odp_pool_t;
+typedef struct _odp_pktio_hdl  *odp_pktio_t;
+typedef struct _odp_packet_hdl *odp_packet_t;
 
-#define ODP_COS_INVALID   ((odp_cos_t)0)
-#define ODP_PMR_INVALID   ((odp_pmr_t)0)
-#define ODP_QUEUE_INVALID ((odp_queue_t)0)
-#define ODP_POOL_INVALID  ((odp_pool_t)0)
-#define ODP_PKTIO_INVALID ((odp_pktio_t)0)
+#define ODP_COS_INVALID    ((odp_cos_t)0)
+#define ODP_PMR_INVALID    ((odp_pmr_t)0)
+#define ODP_QUEUE_INVALID  ((odp_queue_t)0)
+#define ODP_POOL_INVALID   ((odp_pool_t)0)
+#define ODP_PKTIO_INVALID  ((odp_pktio_t)0)
+#define ODP_PACKET_INVALID ((odp_packet_t)0)
 
-#define ODP_COS_NAME_LEN  32
+#define ODP_COS_NAME_LEN     32
+#define ODP_PKTIN_MAX_QUEUES 64
 
+typedef enum odp_support_t {
+	ODP_SUPPORT_NO = 0,
+	ODP_SUPPORT_YES,
+	ODP_SUPPORT_PREFERRED
+} odp_support_t;
+
+/* ---- threshold.h ---------------------------------------------------------- */
+typedef enum odp_threshold_type_t {
+	ODP_THRESHOLD_PERCENT,
+	ODP_THRESHOLD_PACKET,
+	ODP_THRESHOLD_BYTE
+} odp_threshold_type_t;
+
+typedef union odp_threshold_types_t {
+	struct {
+		uint8_t percent : 1;
+		uint8_t packet  : 1;
+		uint8_t bytes   : 1;
+	};
+	uint8_t all_bits;
+} odp_threshold_types_t;
+
+typedef struct odp_threshold_t {
+	odp_threshold_type_t type;
+	union {
+		struct {
+			odp_percent_t max;
+			odp_percent_t min;
+		} percent;
+		struct {
+			uint64_t max;
+			uint64_t min;
+		} packet;
+		struct {
+			uint64_t max;
+			uint64_t min;
+		} byte;
+	};
+} odp_threshold_t;
+
+/* ---- queue / schedule parameters (queue_types.h, schedule_types.h) -------- */
+typedef int odp_schedule_prio_t;
+typedef int odp_schedule_sync_t;
+typedef int odp_schedule_group_t;
+
+#define ODP_SCHED_SYNC_PARALLEL 0
+#define ODP_SCHED_SYNC_ATOMIC   1
+#define ODP_SCHED_SYNC_ORDERED  2
+#define ODP_SCHED_GROUP_ALL     0
+#define ODP_SCHED_GROUP_WORKER  1
+#define ODP_SCHED_GROUP_CONTROL 2
+
+typedef enum odp_queue_type_t {
+	ODP_QUEUE_TYPE_PLAIN = 0,
+	ODP_QUEUE_TYPE_SCHED
+} odp_queue_type_t;
+
+typedef enum odp_queue_op_mode_t {
+	ODP_QUEUE_OP_MT = 0,
+	ODP_QUEUE_OP_MT_UNSAFE,
+	ODP_QUEUE_OP_DISABLED
+} odp_queue_op_mode_t;
+
+typedef enum odp_queue_order_t {
+	ODP_QUEUE_ORDER_KEEP = 0,
+	ODP_QUEUE_ORDER_IGNORE
+} odp_queue_order_t;
+
+typedef enum odp_nonblocking_t {
+	ODP_BLOCKING = 0,
+	ODP_NONBLOCKING_LF,
+	ODP_NONBLOCKING_WF
+} odp_nonblocking_t;
+
+typedef struct odp_schedule_param_t {
+	odp_schedule_prio_t  prio;
+	odp_schedule_sync_t  sync;
+	odp_schedule_group_t group;
+	uint32_t lock_count;
+} odp_schedule_param_t;
+
+typedef struct odp_queue_param_t {
+	odp_queue_type_t type;
+	odp_queue_op_mode_t enq_mode;
+	odp_queue_op_mode_t deq_mode;
+	odp_schedule_param_t sched;
+	odp_queue_order_t order;
+	odp_nonblocking_t nonblocking;
+	void *context;
+	uint32_t context_len;
+	uint32_t size;
+} odp_queue_param_t;
+
+/* ---- classification types (classification.h) ----------------------------- */
 typedef enum {
 	ODP_PMR_LEN = 0,
 	ODP_PMR_ETHTYPE_0,
@@ -116,31 +222,22 @@ typedef union odp_pktin_hash_proto_t {
 	uint32_t all_bits;
 } odp_pktin_hash_proto_t;
 
-/* simplified: the classifier only stores these */
-typedef struct odp_queue_param_t {
-	int type;
-	int sched_prio;
-	int sched_sync;
-	int sched_group;
-	uint32_t size;
-	uint32_t reserved[7];
-} odp_queue_param_t;
-
 typedef struct odp_red_param_t {
 	odp_bool_t enable;
-	uint32_t reserved[5];
+	odp_threshold_t threshold;
 } odp_red_param_t;
 
 typedef struct odp_bp_param_t {
 	odp_bool_t enable;
-	uint32_t reserved[5];
+	odp_threshold_t threshold;
+	uint8_t pfc_level;
 } odp_bp_param_t;
 
 typedef struct odp_pktin_vector_config_t {
 	odp_bool_t enable;
 	odp_pool_t pool;
-	uint32_t max_size;
 	uint64_t max_tmo_ns;
+	uint32_t max_size;
 } odp_pktin_vector_config_t;
 
 typedef struct odp_cls_cos_param {
@@ -194,6 +291,32 @@ typedef union odp_cls_pmr_terms_t {
 	uint64_t all_bits;
 } odp_cls_pmr_terms_t;
 
+/* counters a CoS / a CoS queue supports (one layout for both) */
+typedef struct odp_cls_stats_capability_t {
+	struct {
+		union {
+			struct {
+				uint64_t octets   : 1;
+				uint64_t packets  : 1;
+				uint64_t discards : 1;
+				uint64_t errors   : 1;
+			} counter;
+			uint64_t all_counters;
+		};
+	} cos;
+	struct {
+		union {
+			struct {
+				uint64_t octets   : 1;
+				uint64_t packets  : 1;
+				uint64_t discards : 1;
+				uint64_t errors   : 1;
+			} counter;
+			uint64_t all_counters;
+		};
+	} queue;
+} odp_cls_stats_capability_t;
+
 typedef struct odp_cls_capability_t {
 	odp_cls_pmr_terms_t supported_terms;
 	uint32_t max_pmr;
@@ -204,15 +327,12 @@ typedef struct odp_cls_capability_t {
 	uint32_t max_hash_queues;
 	odp_pktin_hash_proto_t hash_protocols;
 	odp_bool_t pmr_range_supported;
-	int random_early_detection;
-	uint64_t threshold_red;
-	int back_pressure;
-	uint64_t threshold_bp;
+	odp_support_t random_early_detection;
+	odp_threshold_types_t threshold_red;
+	odp_support_t back_pressure;
+	odp_threshold_types_t threshold_bp;
 	uint64_t max_mark;
-	struct {
-		struct { uint64_t all_counters; } cos;
-		struct { uint64_t all_counters; } queue;
-	} stats;
+	odp_cls_stats_capability_t stats;
 } odp_cls_capability_t;
 
 typedef struct odp_cls_cos_stats_t {
@@ -256,10 +376,22 @@ odp_pool_t odp_cls_cos_pool(odp_cos_t cos);
 int  odp_cls_cos_stats(odp_cos_t cos, odp_cls_cos_stats_t *stats);
 int  odp_cls_queue_stats(odp_cos_t cos, odp_queue_t queue, odp_cls_queue_stats_t *stats);
 void odp_cls_print_all(void);
+/* The queue of `cos` a packet is enqueued to (classification.h:769;
+ * odp_classification.c:384-414). This library's odp_packet_t is an
+ * odpg_packet_t: a frame and its parse result (the odpg_meta_t a classify
+ * launch writes), since packets live in device batches, not in a packet
+ * pool. ODP_QUEUE_INVALID on a bad CoS or packet. */
+typedef struct odpg_packet_s {
+	const uint8_t *data;
+	uint32_t len;
+	uint32_t reserved;
+	odpg_meta_t meta;
+} odpg_packet_t;
+odp_queue_t odp_cls_hash_result(odp_cos_t cos, odp_packet_t packet);
 uint64_t odp_cos_to_u64(odp_cos_t hdl);
 uint64_t odp_pmr_to_u64(odp_pmr_t hdl);
 
-/* ---- loop pktio subset (packet_io.h) ----------------------------------- */
+/* ---- loop pktio subset (packet_io.h, packet_io_types.h) ------------------ */
 typedef union odp_pktin_config_opt_t {
 	struct {
 		uint64_t ts_all        : 1;
@@ -277,6 +409,25 @@ typedef union odp_pktin_config_opt_t {
 	uint64_t all_bits;
 } odp_pktin_config_opt_t;
 
+typedef union odp_pktout_config_opt_t {
+	struct {
+		uint64_t ts_ena          : 1;
+		uint64_t ipv4_chksum_ena : 1;
+		uint64_t udp_chksum_ena  : 1;
+		uint64_t tcp_chksum_ena  : 1;
+		uint64_t sctp_chksum_ena : 1;
+		uint64_t ipv4_chksum     : 1;
+		uint64_t udp_chksum      : 1;
+		uint64_t tcp_chksum      : 1;
+		uint64_t sctp_chksum     : 1;
+		uint64_t no_packet_refs  : 1;
+		uint64_t aging_ena       : 1;
+		uint64_t deprecated_tx_compl_ena : 1;   /* ODP_DEPRECATE(tx_compl_ena) */
+		uint64_t proto_stats_ena : 1;
+	} bit;
+	uint64_t all_bits;
+} odp_pktout_config_opt_t;
+
 typedef enum odp_proto_layer_t {
 	ODP_PROTO_LAYER_NONE = 0,
 	ODP_PROTO_LAYER_L2,
@@ -285,20 +436,82 @@ typedef enum odp_proto_layer_t {
 	ODP_PROTO_LAYER_ALL
 } odp_proto_layer_t;
 
+typedef struct odp_pktio_parser_config_t {
+	odp_proto_layer_t layer;
+} odp_pktio_parser_config_t;
+
+typedef struct odp_reass_config_t {
+	odp_bool_t en_ipv4;
+	odp_bool_t en_ipv6;
+	uint64_t max_wait_time;
+	uint16_t max_num_frags;
+} odp_reass_config_t;
+
+typedef enum odp_pktio_link_pause_t {
+	ODP_PKTIO_LINK_PAUSE_UNKNOWN = -1,
+	ODP_PKTIO_LINK_PAUSE_OFF = 0,
+	ODP_PKTIO_LINK_PAUSE_ON = 1,
+	ODP_PKTIO_LINK_PFC_ON = 2
+} odp_pktio_link_pause_t;
+
 typedef struct odp_pktio_config_t {
 	odp_pktin_config_opt_t pktin;
-	uint64_t pktout_all_bits;
+	odp_pktout_config_opt_t pktout;
+	odp_pktio_parser_config_t parser;
+	odp_bool_t enable_loop;
+	odp_bool_t inbound_ipsec;
+	odp_bool_t outbound_ipsec;
+	odp_bool_t enable_lso;
+	odp_reass_config_t reassembly;
 	struct {
-		odp_proto_layer_t layer;
-	} parser;
+		odp_pktio_link_pause_t pause_rx;
+		odp_pktio_link_pause_t pause_tx;
+	} flow_control;
+	struct {
+		uint32_t mode_event : 1;
+		uint32_t mode_poll  : 1;
+		uint32_t max_compl_id;
+	} tx_compl;
 } odp_pktio_config_t;
 
+typedef enum odp_pktin_mode_t {
+	ODP_PKTIN_MODE_DIRECT = 0,
+	ODP_PKTIN_MODE_SCHED,
+	ODP_PKTIN_MODE_QUEUE,
+	ODP_PKTIN_MODE_DISABLED
+} odp_pktin_mode_t;
+
+typedef enum odp_pktout_mode_t {
+	ODP_PKTOUT_MODE_DIRECT = 0,
+	ODP_PKTOUT_MODE_QUEUE,
+	ODP_PKTOUT_MODE_TM,
+	ODP_PKTOUT_MODE_DISABLED
+} odp_pktout_mode_t;
+
+typedef struct odp_pktio_param_t {
+	odp_pktin_mode_t in_mode;
+	odp_pktout_mode_t out_mode;
+} odp_pktio_param_t;
+
+typedef enum odp_pktio_op_mode_t {
+	ODP_PKTIO_OP_MT = 0,
+	ODP_PKTIO_OP_MT_UNSAFE
+} odp_pktio_op_mode_t;
+
+typedef struct odp_pktin_queue_param_ovr_t {
+	odp_schedule_group_t group;
+} odp_pktin_queue_param_ovr_t;
+
 typedef struct odp_pktin_queue_param_t {
-	int op_mode;
+	odp_pktio_op_mode_t op_mode;
 	odp_bool_t classifier_enable;
 	odp_bool_t hash_enable;
 	odp_pktin_hash_proto_t hash_proto;
 	uint32_t num_queues;
+	uint32_t queue_size[ODP_PKTIN_MAX_QUEUES];
+	odp_queue_param_t queue_param;
+	odp_pktin_queue_param_ovr_t *queue_param_ovr;
+	odp_pktin_vector_config_t vector;
 } odp_pktin_queue_param_t;
 
 typedef struct odp_pktio_stats_t {
@@ -318,7 +531,9 @@ typedef struct odp_pktio_stats_t {
 	uint64_t out_errors;
 } odp_pktio_stats_t;
 
-odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const void *param);
+void odp_queue_param_init(odp_queue_param_t *param);
+void odp_pktio_param_init(odp_pktio_param_t *param);
+odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const odp_pktio_param_t *param);
 int  odp_pktio_close(odp_pktio_t pktio);
 void odp_pktio_config_init(odp_pktio_config_t *config);
 int  odp_pktio_config(odp_pktio_t pktio, const odp_pktio_config_t *config);

@@ -181,9 +181,15 @@ class odp_pmr_create_opt_t(C.Structure):
                 ("mark", C.c_uint64)]
 
 
+class odp_schedule_param_t(C.Structure):
+    _fields_ = [("prio", C.c_int), ("sync", C.c_int), ("group", C.c_int),
+                ("lock_count", C.c_uint32)]
+
+
 class odp_queue_param_t(C.Structure):
-    _fields_ = [("type", C.c_int), ("sched_prio", C.c_int), ("sched_sync", C.c_int),
-                ("sched_group", C.c_int), ("size", C.c_uint32), ("reserved", C.c_uint32 * 7)]
+    _fields_ = [("type", C.c_int), ("enq_mode", C.c_int), ("deq_mode", C.c_int),
+                ("sched", odp_schedule_param_t), ("order", C.c_int), ("nonblocking", C.c_int),
+                ("context", C.c_void_p), ("context_len", C.c_uint32), ("size", C.c_uint32)]
 
 
 class _qp_hash(C.Structure):
@@ -194,20 +200,37 @@ class _queue_union(C.Union):
     _fields_ = [("queue", C.c_void_p), ("h", _qp_hash)]
 
 
+class _u64pair(C.Structure):
+    _fields_ = [("max", C.c_uint64), ("min", C.c_uint64)]
+
+
+class _thr_union(C.Union):
+    _fields_ = [("percent", C.c_uint32 * 2), ("packet", _u64pair), ("byte", _u64pair)]
+
+
+class odp_threshold_t(C.Structure):
+    _anonymous_ = ("u",)
+    _fields_ = [("type", C.c_int), ("u", _thr_union)]
+
+
 class odp_red_param_t(C.Structure):
-    _fields_ = [("enable", C.c_int), ("reserved", C.c_uint32 * 5)]
+    _fields_ = [("enable", C.c_bool), ("threshold", odp_threshold_t)]
+
+
+class odp_bp_param_t(C.Structure):
+    _fields_ = [("enable", C.c_bool), ("threshold", odp_threshold_t), ("pfc_level", C.c_uint8)]
 
 
 class odp_pktin_vector_config_t(C.Structure):
-    _fields_ = [("enable", C.c_int), ("pool", C.c_void_p), ("max_size", C.c_uint32),
-                ("max_tmo_ns", C.c_uint64)]
+    _fields_ = [("enable", C.c_bool), ("pool", C.c_void_p), ("max_tmo_ns", C.c_uint64),
+                ("max_size", C.c_uint32)]
 
 
 class odp_cls_cos_param_t(C.Structure):
     _anonymous_ = ("u",)
-    _fields_ = [("action", C.c_int), ("stats_enable", C.c_int), ("num_queue", C.c_uint32),
+    _fields_ = [("action", C.c_int), ("stats_enable", C.c_bool), ("num_queue", C.c_uint32),
                 ("u", _queue_union), ("pool", C.c_void_p), ("red", odp_red_param_t),
-                ("bp", odp_red_param_t), ("vector", odp_pktin_vector_config_t)]
+                ("bp", odp_bp_param_t), ("vector", odp_pktin_vector_config_t)]
 
 
 class odp_cls_capability_t(C.Structure):
@@ -215,9 +238,9 @@ class odp_cls_capability_t(C.Structure):
                 ("max_pmr_per_cos", C.c_uint32), ("max_terms_per_pmr", C.c_uint32),
                 ("max_cos", C.c_uint32), ("max_cos_stats", C.c_uint32),
                 ("max_hash_queues", C.c_uint32), ("hash_protocols", C.c_uint32),
-                ("pmr_range_supported", C.c_int), ("random_early_detection", C.c_int),
-                ("threshold_red", C.c_uint64), ("back_pressure", C.c_int),
-                ("threshold_bp", C.c_uint64), ("max_mark", C.c_uint64),
+                ("pmr_range_supported", C.c_bool), ("random_early_detection", C.c_int),
+                ("threshold_red", C.c_uint8), ("back_pressure", C.c_int),
+                ("threshold_bp", C.c_uint8), ("max_mark", C.c_uint64),
                 ("stats_cos", C.c_uint64), ("stats_queue", C.c_uint64)]
 
 
@@ -226,13 +249,32 @@ class odp_cls_cos_stats_t(C.Structure):
                 ("errors", C.c_uint64)]
 
 
+class odp_reass_config_t(C.Structure):
+    _fields_ = [("en_ipv4", C.c_bool), ("en_ipv6", C.c_bool), ("max_wait_time", C.c_uint64),
+                ("max_num_frags", C.c_uint16)]
+
+
 class odp_pktio_config_t(C.Structure):
-    _fields_ = [("pktin", C.c_uint64), ("pktout", C.c_uint64), ("layer", C.c_int)]
+    _fields_ = [("pktin", C.c_uint64), ("pktout", C.c_uint64), ("layer", C.c_int),
+                ("enable_loop", C.c_bool), ("inbound_ipsec", C.c_bool),
+                ("outbound_ipsec", C.c_bool), ("enable_lso", C.c_bool),
+                ("reassembly", odp_reass_config_t),
+                ("pause_rx", C.c_int), ("pause_tx", C.c_int),
+                ("tx_compl_modes", C.c_uint32), ("tx_compl_max_id", C.c_uint32)]
 
 
 class odp_pktin_queue_param_t(C.Structure):
-    _fields_ = [("op_mode", C.c_int), ("classifier_enable", C.c_int), ("hash_enable", C.c_int),
-                ("hash_proto", C.c_uint32), ("num_queues", C.c_uint32)]
+    _fields_ = [("op_mode", C.c_int), ("classifier_enable", C.c_bool),
+                ("hash_enable", C.c_bool), ("hash_proto", C.c_uint32),
+                ("num_queues", C.c_uint32), ("queue_size", C.c_uint32 * 64),
+                ("queue_param", odp_queue_param_t), ("queue_param_ovr", C.c_void_p),
+                ("vector", odp_pktin_vector_config_t)]
+
+
+class odpg_packet_t(C.Structure):
+    """include/odp_cls.h: a frame and its parse result (odp_cls_hash_result)"""
+    _fields_ = [("data", C.c_void_p), ("len", C.c_uint32), ("reserved", C.c_uint32),
+                ("meta", odpg_meta_t)]
 
 
 class odp_pktio_stats_t(C.Structure):
@@ -302,6 +344,9 @@ SIGNATURES = {
     "odp_cls_cos_stats": (_i32, [_vp, C.POINTER(odp_cls_cos_stats_t)]),
     "odp_cls_queue_stats": (_i32, [_vp, _vp, C.POINTER(odp_cls_cos_stats_t)]),
     "odp_cls_print_all": (None, []),
+    "odp_cls_hash_result": (_vp, [_vp, C.POINTER(odpg_packet_t)]),
+    "odp_queue_param_init": (None, [C.POINTER(odp_queue_param_t)]),
+    "odp_pktio_param_init": (None, [_vp]),
     "odp_cos_to_u64": (_u64, [_vp]),
     "odp_pmr_to_u64": (_u64, [_vp]),
     "odp_pktio_open": (_vp, [C.c_char_p, _vp, _vp]),

@@ -396,7 +396,8 @@ void odp_cls_cos_param_init(odp_cls_cos_param_t *param)
 	param->queue = ODP_QUEUE_INVALID;
 	param->pool = ODP_POOL_INVALID;
 	param->num_queue = 1;
-	param->vector.enable = 0;
+	param->vector.enable = false;
+	odp_queue_param_init(&param->queue_param);   /* as the reference (:137-146) */
 }
 
 void odp_cls_pmr_param_init(odp_pmr_param_t *param)
@@ -905,6 +906,97 @@ int odp_cls_queue_stats(odp_cos_t cos_id, odp_queue_t queue, odp_cls_queue_stats
 	return 0;
 }
 
+/* thash_softrss (protocols/thash.h:81-99) with the default RSS key
+ * (odp_classification.c:50-58), as the classify kernels compute it */
+static uint32_t thash_words(const uint32_t *tuple, uint32_t n)
+{
+	static const uint32_t key[11] = {
+		0x6d5a56dau, 0x255b0ec2u, 0x4167253du, 0x43a38fb0u, 0xd0ca2bcbu,
+		0xae7b30b4u, 0x77cb2da3u, 0x8030f20cu, 0x6a42b73bu, 0xbeac01fau, 0u
+	};
+	uint32_t ret = 0;
+
+	for (uint32_t j = 0; j < n; j++)
+		for (uint32_t i = 0; i < 32; i++)
+			if (tuple[j] & (1u << (31 - i)))
+				ret ^= (key[j] << i) | (i ? (key[j + 1] >> (32 - i)) : 0u);
+	return ret;
+}
+
+static int rd32_le(const odpg_packet_t *pk, uint32_t off, uint32_t *v)
+{
+	if ((uint64_t)off + 4u > pk->len)
+		return -1;
+	memcpy(v, pk->data + off, 4);
+	return 0;
+}
+
+/* packet_rss_hash (odp_classification.c:1751-1817) on a parse result; hp is
+ * the CoS's hash protocol bits (hash_proto_bits): 1 IPv4, 2 IPv6, 4 UDP,
+ * 8 TCP */
+static int packet_rss_hash(const odpg_packet_t *pk, uint32_t hp, uint32_t *hash)
+{
+	const uint64_t inf = pk->meta.input_flags;
+	const uint32_t l3 = pk->meta.l3_offset, l4 = pk->meta.l4_offset;
+	const int tcp = (inf >> 25) & 1, udp = (inf >> 24) & 1;
+	const int ports = (tcp && (hp & 8u)) || (!tcp && udp && (hp & 4u));
+	uint32_t tuple[9] = {0}, n = 0, x;
+
+	if ((inf >> 15) & 1) {                         /* IPv4 */
+		if (hp & 1u) {
+			if (rd32_le(pk, l3 + 12u, &tuple[0]) || rd32_le(pk, l3 + 16u, &tuple[1]))
+				return -1;
+			n += 2;
+		}
+		if (ports) {
+			if (rd32_le(pk, l4, &tuple[2]))
+				return -1;
+			n += 1;
+		}
+	} else if ((inf >> 16) & 1) {                  /* IPv6 */
+		if (hp & 2u) {
+			for (uint32_t k = 0; k < 4; k++) {
+				if (rd32_le(pk, l3 + 8u + 4u * k, &x))
+					return -1;
+				tuple[k] = __builtin_bswap32(x);
+				if (rd32_le(pk, l3 + 24u + 4u * k, &x))
+					return -1;
+				tuple[4 + k] = __builtin_bswap32(x);
+			}
+			n += 8;
+		}
+		if (ports) {
+			if (rd32_le(pk, l4, &tuple[8]))
+				return -1;
+			n += 1;
+		}
+	}
+	*hash = n ? thash_words(tuple, n) : 0u;
+	return 0;
+}
+
+/* odp_cls_hash_result (odp_classification.c:384-414): get_dest_queue's
+ * queue, hash & (CLS_COS_QUEUE_MAX - 1) modulo the CoS's queue count */
+odp_queue_t odp_cls_hash_result(odp_cos_t cos_id, odp_packet_t packet)
+{
+	const odpg_packet_t *pk = (const odpg_packet_t *)packet;
+	odp_queue_t q = ODP_QUEUE_INVALID;
+	uint32_t h;
+
+	LOCK();
+	cos_e *c = get_cos(cos_id);
+
+	if (!c) {
+		ERR("Invalid odp_cos_t handle\n");
+	} else if (c->num_queue == 1) {
+		q = c->queue;
+	} else if (pk && pk->data && !packet_rss_hash(pk, c->hash_proto, &h)) {
+		q = c->hq[(h & (COS_QUEUE_MAX - 1u)) % c->num_queue];
+	}
+	UNLOCK();
+	return q;
+}
+
 /* odp_cls_print_all (odp_classification.c:1879-1981), reduced */
 void odp_cls_print_all(void)
 {
@@ -942,7 +1034,7 @@ uint64_t odp_pmr_to_u64(odp_pmr_t hdl)
 }
 
 /* ---- loop pktio subset -------------------------------------------------- */
-odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const void *param)
+odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const odp_pktio_param_t *param)
 {
 	odp_pktio_t ret = ODP_PKTIO_INVALID;
 
@@ -994,10 +1086,36 @@ int odp_pktio_close(odp_pktio_t hdl)
 	return 0;
 }
 
+/* odp_queue_param_init (queue_basic.c:653-667): plain, MT, blocking;
+ * scheduled queues get the parallel sync in the all-threads group */
+void odp_queue_param_init(odp_queue_param_t *param)
+{
+	memset(param, 0, sizeof(*param));
+	param->type = ODP_QUEUE_TYPE_PLAIN;
+	param->enq_mode = ODP_QUEUE_OP_MT;
+	param->deq_mode = ODP_QUEUE_OP_MT;
+	param->sched.sync = ODP_SCHED_SYNC_PARALLEL;
+	param->sched.group = ODP_SCHED_GROUP_ALL;
+	param->nonblocking = ODP_BLOCKING;
+	param->order = ODP_QUEUE_ORDER_KEEP;
+}
+
+/* odp_pktio_param_init (odp_packet_io.c:1304-1309) */
+void odp_pktio_param_init(odp_pktio_param_t *param)
+{
+	memset(param, 0, sizeof(*param));
+	param->in_mode = ODP_PKTIN_MODE_DIRECT;
+	param->out_mode = ODP_PKTOUT_MODE_DIRECT;
+}
+
+/* odp_pktio_config_init (odp_packet_io.c:1327-1335) */
 void odp_pktio_config_init(odp_pktio_config_t *config)
 {
 	memset(config, 0, sizeof(*config));
 	config->parser.layer = ODP_PROTO_LAYER_ALL;
+	config->reassembly.max_num_frags = 2;
+	config->flow_control.pause_rx = ODP_PKTIO_LINK_PAUSE_OFF;
+	config->flow_control.pause_tx = ODP_PKTIO_LINK_PAUSE_OFF;
 }
 
 /* odp_pktio_config (odp_packet_io.c:602-682) with the loop capability
@@ -1033,10 +1151,13 @@ int odp_pktio_config(odp_pktio_t hdl, const odp_pktio_config_t *config)
 	return rc;
 }
 
+/* odp_pktin_queue_param_init (odp_packet_io.c:1311-1318) */
 void odp_pktin_queue_param_init(odp_pktin_queue_param_t *param)
 {
 	memset(param, 0, sizeof(*param));
+	param->op_mode = ODP_PKTIO_OP_MT;
 	param->num_queues = 1;
+	odp_queue_param_init(&param->queue_param);
 }
 
 int odp_pktin_queue_config(odp_pktio_t hdl, const odp_pktin_queue_param_t *param)
