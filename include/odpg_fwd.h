@@ -17,13 +17,18 @@
  * device-resident batch: one lane per packet, frames rewritten in place.
  *
  * Flow cache: the reference's hash mode keeps a flow cache
- * (odp_l3fwd_db.c:37-63 Jenkins hash, :300-335 warm-up) in front of the
- * route scan. For routes whose subnet has no host bits set and whose depth
- * is 1..31 the cache only ever holds first-match results, so the verdict is
- * the first match itself; that is what the GPU computes (no cache). Routes
- * outside that domain (depth 32, host bits set) make the reference's results
- * depend on the cache warm-up order and capacity: odpg_fwd_create() rejects
- * them in hash mode with -ENOTSUP.
+ * (odp_l3fwd_db.c:37-63 Jenkins hash, :178-335) in front of the route scan.
+ * init_fwd_hash_cache() warms it deterministically: newest route first, the
+ * addresses addr + i for i < 2^(32 - depth) (wrapping at 2^32), stopping at
+ * the first address already cached or when the FWD_MAX_FLOW_COUNT (2^22)
+ * flows are used up. A lookup then returns a warmed address's cached route,
+ * else the first list match of the masked compare (as x86-64 computes it:
+ * a /32 route's mask is 0, so it only matches as 0.0.0.0/32; a route with
+ * host bits set never matches), which it caches without changing any later
+ * answer. So the decision is a function of the destination alone:
+ * odpg_fwd_create() folds the warmed ranges and the scan into one interval
+ * table that the kernel searches. Every route set of 1..32 routes, depth
+ * 1..32, is accepted in both modes.
  */
 #ifndef ODPG_FWD_H_
 #define ODPG_FWD_H_

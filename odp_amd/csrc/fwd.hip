@@ -39,7 +39,9 @@
 #define FN_END   0x80000000u
 #define FN_VALID 0x40000000u
 #define FN_VAL   0x00ffffffu
-#define FWD_MAX_IV (2 * ODPG_FWD_MAX_ROUTES + 1)
+/* hash-mode interval table: 0, two points per route's scan range, up to
+ * four per route's warmed ranges (two when a range wraps past 2^32) */
+#define FWD_MAX_IV (6 * ODPG_FWD_MAX_ROUTES + 1)
 
 struct odpg_fwd_s {
 	odpg_ctx_t *ctx;
@@ -396,17 +398,15 @@ extern "C" int odpg_fwd_create(odpg_ctx_t *ctx, const odpg_route_t *routes, uint
 		if (d < 1 || d > 32 || routes[k].oif_id < 0 ||
 		    (uint32_t)routes[k].oif_id >= ODPG_FWD_MAX_PORTS)
 			return -EINVAL;
-		/* hash mode: see odpg_fwd.h (cache-dependent results) */
-		if (param->mode == ODPG_FWD_HASH &&
-		    (d == 32 || (routes[k].addr & ((1u << (32u - d)) - 1u))))
-			return -ENOTSUP;
 	}
 	std::vector<uint4> rt, rm, pm(ODPG_FWD_MAX_PORTS);
 
 	for (int k = (int)num_routes - 1; k >= 0; k--) {      /* newest first */
 		const uint32_t d = routes[k].depth;
 
-		rt.push_back(make_uint4(routes[k].addr, ((1u << d) - 1u) << (32u - d),
+		/* find_fwd_db_entry's mask as x86-64 computes it: depth 32
+		 * shifts "1u << 32" by 0, giving mask 0 (odp_l3fwd_db.c:496-497) */
+		rt.push_back(make_uint4(routes[k].addr, ((1u << (d & 31u)) - 1u) << ((32u - d) & 31u),
 					(uint32_t)routes[k].oif_id, 0u));
 		uint4 m = mac_words(routes[k].dst_mac, routes[k].src_mac);
 
@@ -418,30 +418,90 @@ extern "C" int odpg_fwd_create(odpg_ctx_t *ctx, const odpg_route_t *routes, uint
 	std::vector<uint32_t> l1(FibTrie::kL1, FN_END), pool(16, FN_END);
 
 	if (param->mode == ODPG_FWD_HASH) {
-		/* fwd_intervals: the address space cut at every route's first and
-		 * one-past-last address; on each piece the newest route holding its
-		 * start (and so every address of it) is find_fwd_db_entry's answer
-		 * (odp_l3fwd_db.c:474-508). l1 = {count, {start, route | -1}...} */
-		std::vector<uint32_t> pts{0u};
+		/* find_fwd_db_entry (odp_l3fwd_db.c:474-508) is a function of the
+		 * destination alone once init_fwd_hash_cache (:304-335) has warmed
+		 * the flow cache: a warmed address returns its cached route, any
+		 * other the first list match (which is then cached, without
+		 * changing later answers). The warm-up walks the list newest
+		 * first, caching addr + i for i < 2^(32 - depth) (u32 wrap), and
+		 * stops at the first address already cached or when the
+		 * FWD_MAX_FLOW_COUNT flows are used up; so the warmed set is a few
+		 * ranges. Both are folded into one interval table:
+		 * l1 = {count, {start, route | -1}...} over [0, 2^32). */
+		struct Iv {
+			uint64_t lo, hi;    /* [lo, hi) */
+			uint32_t route;
+		};
+		std::vector<Iv> warm;
+		const uint64_t cap = 1ull << 22, space = 1ull << 32;
+		uint64_t used = 0;
+
+		for (size_t k = 0; k < rt.size(); k++) {
+			const uint32_t d = routes[num_routes - 1 - k].depth;
+			const uint64_t n = 1ull << (32u - d), a = rt[k].x;
+			/* the key sequence a, a + 1, ... as at most two segments */
+			const uint64_t seg[2][3] = {{a, std::min(a + n, space), 0},
+						    {0, a + n > space ? a + n - space : 0, space - a}};
+			uint64_t dup = n;
+
+			for (const Iv &w : warm)
+				for (const auto &g : seg) {
+					const uint64_t lo = std::max(g[0], w.lo), hi = std::min(g[1], w.hi);
+
+					if (lo < hi)
+						dup = std::min(dup, g[2] + (lo - g[0]));
+				}
+			const uint64_t take = std::min(dup, cap - used);
+
+			for (const auto &g : seg) {
+				const uint64_t lo = g[0], hi = std::min(g[1], g[0] + (take > g[2] ? take - g[2] : 0));
+
+				if (lo < hi)
+					warm.push_back({lo, hi, (uint32_t)k});
+			}
+			used += take;
+			if (take < n)
+				break;
+		}
+		/* first list match of the route scan: the newest route whose
+		 * masked compare holds (a route with host bits set never does) */
+		auto scan = [&](uint32_t ip) -> uint32_t {
+			for (size_t k = 0; k < rt.size(); k++)
+				if ((ip & rt[k].y) == rt[k].x)
+					return (uint32_t)k;
+			return 0xffffffffu;
+		};
+		std::vector<uint64_t> pts{0u};
 
 		for (const uint4 &r : rt) {
-			pts.push_back(r.x);
-			const uint32_t end = r.x | ~r.y;
-
-			if (end != 0xffffffffu)
-				pts.push_back(end + 1u);
+			pts.push_back(r.x & r.y);
+			pts.push_back((uint64_t)(r.x & r.y) + (uint64_t)(~r.y) + 1u);
+		}
+		for (const Iv &w : warm) {
+			pts.push_back(w.lo);
+			pts.push_back(w.hi);
 		}
 		std::sort(pts.begin(), pts.end());
 		pts.erase(std::unique(pts.begin(), pts.end()), pts.end());
+		while (!pts.empty() && pts.back() >= space)
+			pts.pop_back();
+		if (pts.size() > FWD_MAX_IV)
+			return -ENOSPC;
 		l1.assign(1u + 2u * pts.size(), 0u);
 		l1[0] = (uint32_t)pts.size();
 		for (size_t i = 0; i < pts.size(); i++) {
 			uint32_t a = 0xffffffffu;
+			bool hit = false;
 
-			for (size_t k = 0; k < rt.size() && a == 0xffffffffu; k++)
-				if ((pts[i] & rt[k].y) == rt[k].x)
-					a = (uint32_t)k;
-			l1[1 + 2 * i] = pts[i];
+			for (const Iv &w : warm)
+				if (pts[i] >= w.lo && pts[i] < w.hi) {
+					a = w.route;
+					hit = true;
+					break;
+				}
+			if (!hit)
+				a = scan((uint32_t)pts[i]);
+			l1[1 + 2 * i] = (uint32_t)pts[i];
 			l1[2 + 2 * i] = a;
 		}
 	}

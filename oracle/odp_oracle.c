@@ -1315,17 +1315,108 @@ static int fib_lookup(const fib_t *f, uint32_t ip, int32_t *port)
 }
 
 /* ---- find_fwd_db_entry (odp_l3fwd_db.c:474-508): first match in the list,
- * which create_fwd_db_entry() prepends to (:427-428), i.e. newest first */
+ * which create_fwd_db_entry() prepends to (:427-428), i.e. newest first. The
+ * mask is computed as the reference computes it on x86-64: for depth 32,
+ * "1u << 32" shifts by 32 mod 32, so the mask is 0 and only address 0.0.0.0
+ * matches; a route with host bits set never matches here. */
 static int route_first_match(const odpg_route_t *r, uint32_t n, uint32_t ip)
 {
 	for (int k = (int)n - 1; k >= 0; k--) {
 		uint32_t d = r[k].depth;
-		uint32_t mask = ((1u << d) - 1u) << (32u - d);   /* d in 1..31 */
+		uint32_t mask = ((1u << (d & 31u)) - 1u) << ((32u - d) & 31u);
 
 		if (r[k].addr == (ip & mask))
 			return k;
 	}
 	return -1;
+}
+
+/* ---- the hash-mode flow cache (odp_l3fwd_db.c:178-335, 474-508) --------
+ * FWD_MAX_FLOW_COUNT flows; keys carry the destination address only. The
+ * bucket layout (Jenkins hash, :37-63) decides where a flow sits, never
+ * whether it is found, so an exact-match table stands in for the buckets;
+ * what is restated literally is the content: init_fwd_hash_cache()'s
+ * warm-up walks the route list (newest first), inserting addr + i for
+ * i < 2^(32 - depth) (u32 wrap), and stops at the first address already
+ * cached or when the flow store is full; find_fwd_db_entry() returns a
+ * cached flow's route, else the first list match, which it then caches. */
+#define FWD_MAX_FLOW_COUNT (1u << 22)
+#define FC_SLOTS (1u << 23)                 /* open addressing, load <= 1/2 */
+
+typedef struct {
+	uint32_t *key;       /* dst + 1 (0 = empty) */
+	int32_t *route;
+	uint32_t used;
+} fcache_t;
+
+static uint32_t fc_slot(uint32_t dst)
+{
+	uint32_t h = dst * 0x9e3779b1u;
+
+	return (h ^ (h >> 15)) & (FC_SLOTS - 1u);
+}
+
+static int fc_find(const fcache_t *c, uint32_t dst, int32_t *route)
+{
+	for (uint32_t s = fc_slot(dst);; s = (s + 1u) & (FC_SLOTS - 1u)) {
+		if (c->key[s] == 0u)
+			return 0;
+		if (c->key[s] == dst + 1u) {
+			*route = c->route[s];
+			return 1;
+		}
+	}
+}
+
+/* insert_fwd_cache + get_new_flow: 0 when the flow store is exhausted */
+static int fc_insert(fcache_t *c, uint32_t dst, int32_t route)
+{
+	uint32_t s;
+
+	if (c->used >= FWD_MAX_FLOW_COUNT)
+		return 0;
+	for (s = fc_slot(dst); c->key[s] != 0u; s = (s + 1u) & (FC_SLOTS - 1u))
+		;
+	c->key[s] = dst + 1u;
+	c->route[s] = route;
+	c->used++;
+	return 1;
+}
+
+static int fc_warm(fcache_t *c, const odpg_route_t *r, uint32_t n)
+{
+	int32_t dummy;
+
+	c->key = calloc(FC_SLOTS, sizeof(uint32_t));
+	c->route = calloc(FC_SLOTS, sizeof(int32_t));
+	c->used = 0;
+	if (!c->key || !c->route)
+		return -1;
+	for (int k = (int)n - 1; k >= 0; k--) {
+		uint64_t nb = 1ull << (32u - r[k].depth);
+
+		for (uint64_t i = 0; i < nb; i++) {
+			uint32_t dst = r[k].addr + (uint32_t)i;
+
+			if (fc_find(c, dst, &dummy))
+				return 0;              /* "if (flow) return;" */
+			if (!fc_insert(c, dst, k))
+				return 0;              /* flow store exhausted: goto out */
+		}
+	}
+	return 0;
+}
+
+static int fwd_hash_lookup(fcache_t *c, const odpg_route_t *r, uint32_t n, uint32_t dst)
+{
+	int32_t k;
+
+	if (fc_find(c, dst, &k))
+		return k;
+	k = route_first_match(r, n, dst);
+	if (k >= 0)
+		fc_insert(c, dst, k);
+	return k;
 }
 
 static uint32_t rd_be32(const uint8_t *p)
@@ -1342,6 +1433,7 @@ int oracle_l3fwd(const odpg_route_t *routes, uint32_t nroutes, const odpg_fwd_pa
 		 int32_t *out_port)
 {
 	fib_t *fib = NULL;
+	fcache_t fc = { NULL, NULL, 0 };
 
 	pthread_once(&crc_once, crc_init);
 	if (nroutes > ODPG_FWD_MAX_ROUTES)
@@ -1360,11 +1452,13 @@ int oracle_l3fwd(const odpg_route_t *routes, uint32_t nroutes, const odpg_fwd_pa
 			return -1;
 		}
 	} else {
-		for (uint32_t k = 0; k < nroutes; k++) {
-			uint32_t d = routes[k].depth;
-
-			if (d < 1 || d > 31 || (routes[k].addr & ((1u << (32u - d)) - 1u)))
+		for (uint32_t k = 0; k < nroutes; k++)
+			if (routes[k].depth < 1 || routes[k].depth > 32)
 				return -1;
+		if (fc_warm(&fc, routes, nroutes)) {
+			free(fc.key);
+			free(fc.route);
+			return -1;
 		}
 	}
 	for (uint32_t i = 0; i < num; i++) {
@@ -1400,7 +1494,7 @@ int oracle_l3fwd(const odpg_route_t *routes, uint32_t nroutes, const odpg_fwd_pa
 			memcpy(fr, prm->dest_mac[dif], 6);
 			memcpy(fr + 6, prm->port_mac[dif], 6);
 		} else {
-			int k = route_first_match(routes, nroutes, dst);
+			int k = fwd_hash_lookup(&fc, routes, nroutes, dst);
 
 			if (k >= 0) {
 				memcpy(fr + 6, routes[k].src_mac, 6);
@@ -1414,6 +1508,8 @@ int oracle_l3fwd(const odpg_route_t *routes, uint32_t nroutes, const odpg_fwd_pa
 		out_port[i] = dif;
 	}
 	free(fib);
+	free(fc.key);
+	free(fc.route);
 	return 0;
 }
 

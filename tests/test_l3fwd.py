@@ -82,11 +82,50 @@ def test_hash_no_route_swaps_mac():
     assert (f2[0:6] == fr[6:12]).all() and (f2[6:12] == fr[6:12]).all()
 
 
-def test_hash_rejects_cache_dependent_routes():
-    with pytest.raises(ValueError):
-        run_oracle([R("10.0.0.1", 24, 1)], frames_to([ip("10.0.0.1")]))   # host bits set
-    with pytest.raises(ValueError):
-        run_oracle([R("10.0.0.1", 32, 1)], frames_to([ip("10.0.0.1")]))   # /32
+# ---- the hash-mode flow cache (odp_l3fwd_db.c:178-335, 474-508) ------------
+# Expected ports below are read off the reference code: init_fwd_hash_cache
+# caches addr + i for i < 2^(32 - depth), newest route first, and returns at
+# the first address already cached or when the 2^22 flows are used up;
+# find_fwd_db_entry answers from the cache, else from the masked first match
+# (depth 32: "1u << 32" is a shift by 0 on x86-64, mask 0).
+def test_hash_host_bits_route_is_served_by_the_warmed_cache():
+    out, _ = run_oracle([R("10.0.0.5", 24, 1)],
+                        frames_to([ip("10.0.0.5"), ip("10.0.1.4"), ip("10.0.0.4"),
+                                   ip("10.0.1.5")]), sif=3)
+    assert list(out) == [1, 1, 3, 3]      # 256 warmed hosts from .5; the scan never matches
+
+
+def test_hash_depth32_routes():
+    out, _ = run_oracle([R("10.0.0.7", 32, 2)], frames_to([ip("10.0.0.7"), ip("10.0.0.8")]),
+                        sif=0)
+    assert list(out) == [2, 0]
+    # 0.0.0.0/32 (newest): mask 0 matches every address the cache does not
+    # hold; the older /24's hosts were warmed after it and stay on the /24
+    out, _ = run_oracle([R("10.0.0.0", 24, 1), R(0, 32, 3)],
+                        frames_to([ip("10.0.0.9"), ip("192.0.2.1"), 0, ip("10.0.1.1")]), sif=0)
+    assert list(out) == [1, 3, 3, 3]
+
+
+def test_hash_warmup_stops_at_first_cached_address():
+    """The newest route (host bits set) warms 9.255.255.0 .. 10.0.0.255; the
+    older /24's first host is then already cached, so the warm-up returns:
+    10.0.0.9 stays on the newer route although the scan would pick the /24."""
+    routes = [R("10.0.0.0", 24, 1), R("9.255.255.0", 23, 2)]
+    out, _ = run_oracle(routes, frames_to([ip("10.0.0.9"), ip("10.0.1.200"), ip("10.0.2.1"),
+                                           ip("9.255.255.0"), ip("9.255.254.255")]), sif=0)
+    assert list(out) == [2, 0, 0, 2, 0]
+
+
+def test_hash_warmup_wraps_and_is_capped():
+    # 255.255.255.0 with depth 16 warms 65536 hosts, wrapping into 0.0.x.x
+    out, _ = run_oracle([R("255.255.255.0", 16, 1)],
+                        frames_to([ip("255.255.255.9"), ip("0.0.1.1"), ip("0.0.254.255"),
+                                   ip("0.0.255.0")]), sif=2)
+    assert list(out) == [1, 1, 1, 2]
+    # a /8 with host bits: only the first 2^22 hosts fit in the flow store
+    out, _ = run_oracle([R("10.0.0.1", 8, 1)],
+                        frames_to([ip("10.0.0.1"), ip("10.64.0.0"), ip("10.64.0.1")]), sif=2)
+    assert list(out) == [1, 1, 2]
 
 
 # ---- fib_tbl_insert / fib_tbl_lookup quirks (odp_l3fwd_lpm.c) ---------------
@@ -208,3 +247,62 @@ def test_gpu_c5_full_size(gpu_ctx, mode):
     o_out, o_fr = run_oracle(routes, fr, mode=mode)
     np.testing.assert_array_equal(g_out, o_out)
     np.testing.assert_array_equal(g_fr[:fr.nbytes], o_fr)
+
+
+def _random_routes(rng, nr):
+    out = []
+    for k in range(nr):
+        d = int(rng.choice([8, 12, 16, 20, 23, 24, 28, 30, 31, 32, int(rng.integers(1, 33))]))
+        a = int(rng.integers(0, 1 << 32))
+        if rng.random() < 0.5:                      # half aligned, half with host bits
+            a &= ((1 << d) - 1) << (32 - d)
+        if rng.random() < 0.2:                      # overlap an earlier route
+            a = (out[int(rng.integers(0, len(out)))][0] + int(rng.integers(0, 300))) % (1 << 32) \
+                if out else a
+        out.append(R(a, d, k % 4, k))
+    return out
+
+
+def _probe_dsts(rng, routes, n):
+    d = []
+    for a, dep, *_ in routes:
+        n_h = 1 << (32 - dep)
+        for off in (0, 1, n_h - 1, n_h, n_h + 1, -1, n_h // 2, 1 << 22, (1 << 22) - 1):
+            d.append((a + off) % (1 << 32))
+        m = ((1 << dep) - 1) << (32 - dep)
+        d += [a & m, ((a & m) + n_h - 1) % (1 << 32)]
+    d += [0, 0xFFFFFFFF] + list(rng.integers(0, 1 << 32, n))
+    return d
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_gpu_hash_flow_cache_parity(gpu_ctx, seed):
+    """Random route sets of every depth, half with host bits, overlapping and
+    wrapping: the GPU's interval table vs the oracle's literal flow cache."""
+    rng = np.random.default_rng(seed)
+    routes = _random_routes(rng, int(rng.integers(1, 33)))
+    dsts = _probe_dsts(rng, routes, 4000)
+    fr = frames_to(dsts)
+    fw = gpu.Forwarder(gpu_ctx, routes, mode=L.FWD_HASH)
+    g_out, g_fr = fw.run(fr, 64, len(dsts), src_port=3)
+    o_out, o_fr = run_oracle(routes, fr, sif=3)
+    np.testing.assert_array_equal(g_out, o_out)
+    np.testing.assert_array_equal(g_fr[:fr.nbytes], o_fr)
+
+
+@pytest.mark.gpu
+def test_gpu_hash_flow_cache_cases(gpu_ctx):
+    cases = [([R("10.0.0.5", 24, 1)], ["10.0.0.5", "10.0.1.4", "10.0.0.4", "10.0.1.5"]),
+             ([R("10.0.0.0", 24, 1), R(0, 32, 3)], ["10.0.0.9", "192.0.2.1", "0.0.0.0"]),
+             ([R("10.0.0.0", 24, 1), R("9.255.255.0", 23, 2)],
+              ["10.0.0.9", "10.0.1.200", "10.0.2.1", "9.255.255.0", "9.255.254.255"]),
+             ([R("255.255.255.0", 16, 1)], ["255.255.255.9", "0.0.1.1", "0.0.254.255",
+                                            "0.0.255.0"]),
+             ([R("10.0.0.1", 8, 1)], ["10.0.0.1", "10.64.0.0", "10.64.0.1"])]
+    for routes, qs in cases:
+        fr = frames_to([ip(q) for q in qs])
+        g_out, _ = gpu.Forwarder(gpu_ctx, routes, mode=L.FWD_HASH).run(fr, 64, len(qs),
+                                                                       src_port=2)
+        o_out, _ = run_oracle(routes, fr, sif=2)
+        np.testing.assert_array_equal(g_out, o_out)
