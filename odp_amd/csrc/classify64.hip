@@ -75,6 +75,7 @@ struct L64Args {
 	uint32_t def_cos;      /* CoS of error-free packets before the walk */
 	uint32_t def_act;
 	uint32_t def_rules;    /* the default CoS is valid and has rules: walk */
+	uint32_t depth;        /* longest rule chain (1..4: unrolled walk), 0 = loop */
 	odpg_out_t *out;
 	uint64_t *stats;       /* pktio counters (odpg.h), or NULL */
 	uint64_t *sred;        /* stats_commit scratch */
@@ -380,7 +381,28 @@ __global__ __launch_bounds__(LB, L64_WAVES * 256 / LB) void odpg_cls64_kernel(co
 			 * (pinfo4 carries the next CoS's mask) */
 			uint32_t mlo = err ? 0u : A.def_mlo, mhi = err ? 0u : A.def_mhi;
 
-			if (live && !pdrop) {
+			if (A.depth - 1u < 4u) {
+				/* acyclic table, longest chain A.depth rules: exactly that
+				 * many levels, branch-free (a level without a hit keeps
+				 * the state: its mask becomes 0) */
+#pragma unroll
+				for (uint32_t l = 0; l < 4u; ++l) {
+					if (l >= A.depth)
+						break;
+					const uint32_t xl = lo & mlo, xh = hi & mhi;
+					const bool hit = !pdrop & ((xl | xh) != 0u);
+					const uint32_t k = xl ? (uint32_t)__builtin_ctz(xl)
+							      : xh ? 32u + (uint32_t)__builtin_ctz(xh) : 0u;
+					const uint4 pi = pinfo4[k];
+
+					cos = hit ? (pi.x & 0xffffu) : cos;
+					mark = hit ? (pi.x >> 16) : mark;
+					act = hit ? pi.y : act;
+					mlo = hit ? pi.z : 0u;
+					mhi = hit ? pi.w : 0u;
+					any_match |= hit;
+				}
+			} else if (live && !pdrop) {
 				uint32_t steps = 0u;
 
 				for (;;) {
@@ -800,6 +822,7 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	A.def_cos = a->l64_def_cos;
 	A.def_act = a->l64_def_act;
 	A.def_rules = a->l64_def_rules;
+	A.depth = a->l64_depth;
 	A.cgroups = a->cgroups;
 	A.cents = (const uint2 *)a->cents;
 	A.num_cent = a->num_cent;

@@ -368,6 +368,7 @@ typedef struct odpg_launch_args {
 	 * copy of the table */
 	uint32_t l64_err_cos, l64_err_act, l64_def_cos, l64_def_act, l64_def_ci, l64_def_rules;
 	uint32_t l64_def_mlo, l64_def_mhi;   /* the default CoS's rule mask (pinfo4 form) */
+	uint32_t l64_depth;    /* longest rule chain from the default CoS, 0 = cyclic */
 	int mode;          /* 0 auto, 1 walk, 2 evaluate-all, 3 hash walk */
 	odpg_out_t *out;
 	uint16_t *mark;

@@ -65,6 +65,7 @@ struct odpg_table_s {
 	void *dblob;
 	int device;
 	int cycle;
+	uint32_t depth;    /* longest rule chain from the default CoS (0: a cycle) */
 	uint64_t qsig;     /* counter layout: CoS count, queues and stats flags */
 	size_t cap;        /* bytes allocated at dblob */
 	hipEvent_t uploaded;   /* the last upload of `blob` has been consumed */
@@ -86,6 +87,59 @@ struct odpg_counters_s {
 	std::vector<uint8_t> nq;
 	std::mutex lock;               /* one fold at a time */
 };
+
+/* The longest chain of rules cls_select_cos can follow from the default CoS
+ * (odp_classification.c:1599-1631: at CoS c every rule of c may lead to its
+ * destination, whose rules are tried next), or 0 when a cycle is reachable.
+ * The lean kernel walks exactly that many levels, without a loop. */
+static uint32_t table_walk_depth(const odpg_table_t *t)
+{
+	const dtable_hdr_t &h = t->hdr;
+	const dcos_t *hc = (const dcos_t *)(t->blob.data() + h.cos_off);
+	const uint32_t *pinfo = (const uint32_t *)(t->blob.data() + h.pinfo_off);
+	const int32_t dc = h.default_cos;
+
+	if (dc < 0 || (uint32_t)dc >= h.num_cos || !hc[dc].valid)
+		return 1;
+	std::vector<uint8_t> state(h.num_cos, 0);     /* 0 new, 1 on path, 2 done */
+	std::vector<uint32_t> len(h.num_cos, 0);
+	bool cyclic = false;
+	/* iterative DFS: longest number of rules from c */
+	std::vector<std::pair<uint32_t, uint32_t>> st{{(uint32_t)dc, 0u}};
+
+	state[dc] = 1;
+	while (!st.empty() && !cyclic) {
+		auto &[c, i] = st.back();
+
+		if (i < hc[c].nrule) {
+			const uint32_t k = hc[c].rule_start + i++;
+			const uint32_t d = k < h.num_pmr ? (pinfo[k] & 0xffffu) : 0xffffu;
+
+			if (d >= h.num_cos)
+				continue;
+			if (state[d] == 1) {
+				cyclic = true;
+			} else if (state[d] == 0) {
+				state[d] = 1;
+				st.push_back({d, 0u});
+			}
+		} else {
+			uint32_t best = 0;
+
+			for (uint32_t r = 0; r < hc[c].nrule; r++) {
+				const uint32_t k = hc[c].rule_start + r;
+				const uint32_t d = k < h.num_pmr ? (pinfo[k] & 0xffffu) : 0xffffu;
+
+				if (d < h.num_cos)
+					best = std::max(best, 1u + len[d]);
+			}
+			len[c] = best;
+			state[c] = 2;
+			st.pop_back();
+		}
+	}
+	return cyclic ? 0u : std::max(len[dc], 1u);
+}
 
 /* layout signature of a table's counters: a counters object serves every
  * table with the same CoS count, queue counts and stats flags */
@@ -271,6 +325,7 @@ int odpg_rules_compile(const odpg_rules_t *rules, void *image, size_t *size)
 static int table_upload(odpg_ctx_t *c, odpg_table_t *t, odpg_table_t **out)
 {
 	t->cycle = odpg_rules_has_cycle(t->blob, t->hdr);
+	t->depth = table_walk_depth(t);
 	t->device = c->device;
 	t->qsig = table_qsig(t);
 	t->uploaded = nullptr;
@@ -362,6 +417,7 @@ int odpg_table_update(odpg_ctx_t *c, odpg_table_t *t, const odpg_rules_t *rules)
 	t->blob.swap(blob);
 	t->hdr = hdr;
 	t->cycle = odpg_rules_has_cycle(t->blob, t->hdr);
+	t->depth = table_walk_depth(t);
 	t->qsig = table_qsig(t);
 	if (hipMemcpyAsync(t->dblob, t->blob.data(), t->hdr.blob_bytes, hipMemcpyHostToDevice,
 			   c->stream) != hipSuccess ||
@@ -643,6 +699,7 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 				    (hc[dc].nrule >= 64u ? ~0ull : ((1ull << hc[dc].nrule) - 1ull))
 				    << hc[dc].rule_start : 0ull;
 
+		a.l64_depth = t->depth;
 		a.l64_def_mlo = (uint32_t)dm;
 		a.l64_def_mhi = (uint32_t)(dm >> 32);
 	}
