@@ -696,6 +696,120 @@ __device__ __forceinline__ uint32_t coop_tail_sums(uint64_t m, const uint8_t *g,
 }
 
 
+/* inclusive prefix sum over the 64 lanes (DPP row scans, then the row
+ * carries by row_bcast:15 / row_bcast:31); every lane must be active */
+__device__ __forceinline__ uint32_t wave_scan_u32(uint32_t x)
+{
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+	return x;
+}
+
+/* Tail sums of the lanes in `m` as one balanced segmented reduction: the
+ * 16-byte chunks of every pending tail [a, b) (chunk-aligned at a & ~15 of
+ * the lane's frame g) are numbered across the wave in lane order (prefix sum
+ * of the per-frame chunk counts) and spread over the 64 lanes, 64 chunks per
+ * pass: a pass loads 1 KiB of tails with every lane busy, whatever the mix
+ * of frame lengths. Each lane masks its chunk to [a, b), sums its 16-bit
+ * halves (v_dot2) and folds; one wave prefix sum per pass then gives every
+ * frame's share of the pass as a difference of two lanes. Lane j receives
+ * its own tail sum (the same value coop_tail_sums returns: the one's-
+ * complement residue and zero-ness of the exact sum are kept). */
+#ifndef SEG_BATCH
+#define SEG_BATCH 4
+#endif
+__device__ __forceinline__ uint32_t seg_tail_sums(uint64_t m, const uint8_t *g, const L4Pend &pd)
+{
+#ifdef ODPG_EXP_NOTAIL      /* experiment builds only: cost without the tail reads */
+	return 0u;
+#endif
+	const uint32_t lane = __lane_id();
+	const uint64_t gv = (uint64_t)(uintptr_t)g;
+	const bool mine = ((m >> lane) & 1ull) && pd.b > pd.a;
+	const uint32_t c0 = pd.a & ~15u;
+	const uint32_t n = mine ? ((pd.b - 1u - c0) >> 4) + 1u : 0u;   /* chunks */
+	const uint32_t incl = wave_scan_u32(n);
+	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+	uint32_t acc = 0u;
+
+	/* SEG_BATCH passes at a time: their loads are all issued before the
+	 * first is summed, so a wave keeps several KiB of tails in flight */
+	for (uint32_t b0 = 0; b0 < total; b0 += 64u * SEG_BATCH) {   /* uniform */
+		uint4 q[SEG_BATCH];
+		uint32_t lead[SEG_BATCH], rem[SEG_BATCH];
+		uint64_t pass_frames[SEG_BATCH];
+
+#pragma unroll
+		for (int k = 0; k < SEG_BATCH; ++k) {
+			const uint32_t base = b0 + 64u * (uint32_t)k;
+			const uint32_t slot = base + lane;
+			const uint64_t in_pass = base < total ?
+				__ballot(n && incl > base && incl - n < base + 64u) : 0ull;
+			uint32_t own = 64u, first = 0u, glo = 0u, ghi = 0u, oa = 0u, ob = 0u, on = 0u;
+
+			pass_frames[k] = in_pass;
+			/* the frame owning this lane's chunk, and its fields */
+			for (uint64_t f = in_pass; f; f &= f - 1ull) {
+				const int j = __builtin_ctzll(f);
+				const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)incl, j);
+				const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)n, j);
+				const bool hit = slot >= ij - nj && slot < ij;
+
+				own = hit ? (uint32_t)j : own;
+				first = hit ? ij - nj : first;
+				on = hit ? nj : on;
+				glo = hit ? (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gv, j) : glo;
+				ghi = hit ? (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(gv >> 32), j) : ghi;
+				oa = hit ? (uint32_t)__builtin_amdgcn_readlane((int)pd.a, j) : oa;
+				ob = hit ? (uint32_t)__builtin_amdgcn_readlane((int)pd.b, j) : ob;
+			}
+			const uint32_t idx = slot - first;
+
+			q[k] = make_uint4(0u, 0u, 0u, 0u);
+			lead[k] = idx == 0u ? (oa & 15u) : 0u;
+			rem[k] = own < 64u ? (idx + 1u == on ? ((ob - 1u) & 15u) + 1u : 16u) : 0u;
+			if (own < 64u) {
+				const uint8_t *gp = (const uint8_t *)(uintptr_t)(((uint64_t)ghi << 32) | glo);
+
+				q[k] = *(const uint4 *)(gp + (oa & ~15u) + 16u * idx);
+			}
+		}
+#pragma unroll
+		for (int k = 0; k < SEG_BATCH; ++k) {
+			if (!pass_frames[k])
+				continue;
+			const uint32_t base = b0 + 64u * (uint32_t)k;
+			const int le = (int)lead[k], re = (int)rem[k];
+			uint32_t acc4 = 0u;
+
+			acc4 = tail_dot2(q[k].x & byte_mask(re) & ~byte_mask(le), acc4);
+			acc4 = tail_dot2(q[k].y & byte_mask(re - 4) & ~byte_mask(le - 4), acc4);
+			acc4 = tail_dot2(q[k].z & byte_mask(re - 8) & ~byte_mask(le - 8), acc4);
+			acc4 = tail_dot2(q[k].w & byte_mask(re - 12) & ~byte_mask(le - 12), acc4);
+			/* frames own contiguous lanes: a frame's share of the pass is
+			 * the prefix sum at its last lane minus the one before its first */
+			const uint32_t ps = wave_scan_u32(oc_fold(acc4));
+
+			for (uint64_t f = pass_frames[k]; f; f &= f - 1ull) {
+				const int j = __builtin_ctzll(f);
+				const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)incl, j);
+				const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)n, j);
+				const uint32_t lo = ij - nj > base ? ij - nj - base : 0u;
+				const uint32_t hi = (ij < base + 64u ? ij : base + 64u) - base - 1u;
+				const uint32_t sh = (uint32_t)__builtin_amdgcn_readlane((int)ps, (int)hi) -
+						    (lo ? (uint32_t)__builtin_amdgcn_readlane((int)ps, (int)lo - 1) : 0u);
+
+				acc += lane == (uint32_t)j ? sh : 0u;
+			}
+		}
+	}
+	return mine ? oc_fold(acc) : 0u;
+}
+
 /* ---- register fast path: plain 64-byte Eth/IPv4/UDP|TCP frames ----------
  * Frames whose generic parse takes the straight path (no SNAP / VLAN, IPv4
  * IHL 5, UDP length >= 8 or TCP header >= 20 B) are parsed from the 16
