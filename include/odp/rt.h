@@ -1,0 +1,285 @@
+/* SPDX-License-Identifier: BSD-3-Clause
+ *
+ * odp/rt.h — the ODP runtime subset around the GPU classifier (odp_api.h).
+ *
+ * Receive model: a pktio opened as "pcap:in=<file>[:loops=<n>]" (the pcap
+ * pktio, platform/linux-generic/pktio/pcap.c) or "loop" in
+ * ODP_PKTIN_MODE_SCHED mode with the classifier enabled is polled by the
+ * scheduler. Each poll takes a burst of frames, classifies it on the GPU
+ * (odpg_pktio_recv_batch's path: parse, checksums, PMR -> CoS, the pktio /
+ * CoS / queue counters) and enqueues the packets on their CoS's queue
+ * (_odp_cls_enq, odp_classification_internal.h:139-225); odp_schedule*()
+ * then returns them from the scheduled queues. Packets carry the parse
+ * result the kernel wrote (odpg_meta_t), which the odp_packet_has_* /
+ * l2 / l3 accessors read.
+ *
+ * Spec references: init.h, shared_memory.h, pool.h / pool_types.h,
+ * queue.h / queue_types.h, schedule.h, packet.h / packet_flags.h,
+ * packet_io.h, time.h, cpumask.h, thread.h, atomic.h, byteorder.h.
+ */
+#ifndef ODP_RT_H_
+#define ODP_RT_H_
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- hints, alignment, byte order ------------------------------------ */
+#define odp_likely(x)   __builtin_expect(!!(x), 1)
+#define odp_unlikely(x) __builtin_expect(!!(x), 0)
+#define ODP_CACHE_LINE_SIZE 64
+
+typedef uint16_t odp_u16be_t;
+typedef uint32_t odp_u32be_t;
+typedef uint64_t odp_u64be_t;
+typedef uint16_t odp_u16sum_t;
+
+static inline uint16_t odp_cpu_to_be_16(uint16_t x) { return __builtin_bswap16(x); }
+static inline uint32_t odp_cpu_to_be_32(uint32_t x) { return __builtin_bswap32(x); }
+static inline uint64_t odp_cpu_to_be_64(uint64_t x) { return __builtin_bswap64(x); }
+static inline uint16_t odp_be_to_cpu_16(uint16_t x) { return __builtin_bswap16(x); }
+static inline uint32_t odp_be_to_cpu_32(uint32_t x) { return __builtin_bswap32(x); }
+static inline uint64_t odp_be_to_cpu_64(uint64_t x) { return __builtin_bswap64(x); }
+
+/* ---- atomics (atomic.h), relaxed unless named otherwise --------------- */
+typedef struct { uint64_t v; } odp_atomic_u64_t;
+typedef struct { uint32_t v; } odp_atomic_u32_t;
+
+static inline void odp_atomic_init_u64(odp_atomic_u64_t *a, uint64_t v)
+{ __atomic_store_n(&a->v, v, __ATOMIC_RELAXED); }
+static inline uint64_t odp_atomic_load_u64(odp_atomic_u64_t *a)
+{ return __atomic_load_n(&a->v, __ATOMIC_RELAXED); }
+static inline void odp_atomic_store_u64(odp_atomic_u64_t *a, uint64_t v)
+{ __atomic_store_n(&a->v, v, __ATOMIC_RELAXED); }
+static inline void odp_atomic_add_u64(odp_atomic_u64_t *a, uint64_t v)
+{ __atomic_fetch_add(&a->v, v, __ATOMIC_RELAXED); }
+static inline void odp_atomic_inc_u64(odp_atomic_u64_t *a)
+{ __atomic_fetch_add(&a->v, 1, __ATOMIC_RELAXED); }
+static inline uint64_t odp_atomic_fetch_inc_u64(odp_atomic_u64_t *a)
+{ return __atomic_fetch_add(&a->v, 1, __ATOMIC_RELAXED); }
+static inline void odp_atomic_init_u32(odp_atomic_u32_t *a, uint32_t v)
+{ __atomic_store_n(&a->v, v, __ATOMIC_RELAXED); }
+static inline uint32_t odp_atomic_load_u32(odp_atomic_u32_t *a)
+{ return __atomic_load_n(&a->v, __ATOMIC_RELAXED); }
+static inline void odp_atomic_inc_u32(odp_atomic_u32_t *a)
+{ __atomic_fetch_add(&a->v, 1, __ATOMIC_RELAXED); }
+
+/* ---- init (init.h) ------------------------------------------------------ */
+typedef uint64_t odp_instance_t;
+
+typedef enum odp_mem_model_t {
+	ODP_MEM_MODEL_THREAD = 0,
+	ODP_MEM_MODEL_PROCESS
+} odp_mem_model_t;
+
+typedef enum odp_thread_type_t {
+	ODP_THREAD_WORKER = 0,
+	ODP_THREAD_CONTROL
+} odp_thread_type_t;
+
+#define ODP_THREAD_COUNT_MAX 256
+
+typedef struct odp_init_t {
+	int num_worker;
+	int num_control;
+	const void *worker_cpus;
+	const void *control_cpus;
+	int (*log_fn)(int level, const char *fmt, ...);
+	void (*abort_fn)(void);
+	odp_mem_model_t mem_model;
+	uint64_t reserved[8];
+} odp_init_t;
+
+void odp_init_param_init(odp_init_t *param);
+int  odp_init_global(odp_instance_t *instance, const odp_init_t *param, const void *platform);
+int  odp_init_local(odp_instance_t instance, odp_thread_type_t thr_type);
+int  odp_term_local(void);
+int  odp_term_global(odp_instance_t instance);
+void odp_sys_info_print(void);
+int  odp_thread_id(void);
+int  odp_cpu_count(void);
+
+/* ---- CPU masks (cpumask.h) --------------------------------------------- */
+#define ODP_CPUMASK_SIZE     1024
+#define ODP_CPUMASK_STR_SIZE ((ODP_CPUMASK_SIZE + 3) / 4 + 3)
+
+typedef struct odp_cpumask_t {
+	uint64_t bits[ODP_CPUMASK_SIZE / 64];
+} odp_cpumask_t;
+
+void    odp_cpumask_zero(odp_cpumask_t *mask);
+void    odp_cpumask_set(odp_cpumask_t *mask, int cpu);
+int     odp_cpumask_isset(const odp_cpumask_t *mask, int cpu);
+int     odp_cpumask_count(const odp_cpumask_t *mask);
+int     odp_cpumask_first(const odp_cpumask_t *mask);
+int     odp_cpumask_next(const odp_cpumask_t *mask, int cpu);
+int32_t odp_cpumask_to_str(const odp_cpumask_t *mask, char *str, int32_t size);
+int     odp_cpumask_default_worker(odp_cpumask_t *mask, int num);
+int     odp_cpumask_default_control(odp_cpumask_t *mask, int num);
+
+/* ---- time (time.h) ------------------------------------------------------ */
+#define ODP_TIME_USEC_IN_NS 1000ULL
+#define ODP_TIME_MSEC_IN_NS 1000000ULL
+#define ODP_TIME_SEC_IN_NS  1000000000ULL
+
+typedef struct odp_time_t {
+	uint64_t nsec;
+} odp_time_t;
+
+odp_time_t odp_time_local(void);
+odp_time_t odp_time_global(void);
+uint64_t   odp_time_diff_ns(odp_time_t t2, odp_time_t t1);
+uint64_t   odp_time_to_ns(odp_time_t time);
+void       odp_time_wait_ns(uint64_t ns);
+
+/* ---- shared memory (shared_memory.h) ------------------------------------ */
+typedef struct _odp_shm_hdl *odp_shm_t;
+#define ODP_SHM_INVALID ((odp_shm_t)0)
+
+odp_shm_t odp_shm_reserve(const char *name, uint64_t size, uint64_t align, uint32_t flags);
+void     *odp_shm_addr(odp_shm_t shm);
+int       odp_shm_free(odp_shm_t shm);
+
+/* ---- packet pools (pool.h, pool_types.h) -------------------------------- */
+#define ODP_POOL_NAME_LEN 32
+
+typedef enum odp_pool_type_t {
+	ODP_POOL_BUFFER = 1,
+	ODP_POOL_PACKET,
+	ODP_POOL_TIMEOUT,
+	ODP_POOL_VECTOR
+} odp_pool_type_t;
+
+typedef struct odp_pool_param_t {
+	odp_pool_type_t type;
+	struct {
+		uint32_t num;
+		uint32_t size;
+		uint32_t align;
+	} buf;
+	struct {
+		uint32_t num;
+		uint32_t max_num;
+		uint32_t len;
+		uint32_t max_len;
+		uint32_t seg_len;
+		uint32_t uarea_size;
+		uint32_t headroom;
+	} pkt;
+	uint64_t reserved[8];
+} odp_pool_param_t;
+
+void       odp_pool_param_init(odp_pool_param_t *param);
+odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param);
+int        odp_pool_destroy(odp_pool_t pool);
+void       odp_pool_print(odp_pool_t pool);
+void       odp_pool_print_all(void);
+
+/* ---- events, queues, scheduler (queue.h, schedule.h) -------------------- */
+typedef struct _odp_event_hdl *odp_event_t;
+#define ODP_EVENT_INVALID ((odp_event_t)0)
+
+#define ODP_QUEUE_NAME_LEN 32
+
+typedef struct odp_queue_info_t {
+	const char *name;
+	odp_queue_param_t param;
+} odp_queue_info_t;
+
+odp_queue_t odp_queue_create(const char *name, const odp_queue_param_t *param);
+int         odp_queue_destroy(odp_queue_t queue);
+int         odp_queue_info(odp_queue_t queue, odp_queue_info_t *info);
+int         odp_queue_enq(odp_queue_t queue, odp_event_t ev);
+odp_event_t odp_queue_deq(odp_queue_t queue);
+
+#define ODP_SCHED_WAIT    UINT64_MAX
+#define ODP_SCHED_NO_WAIT 0
+
+typedef struct odp_schedule_config_t {
+	uint32_t num_queues;
+	uint32_t queue_size;
+	uint64_t reserved[4];
+} odp_schedule_config_t;
+
+void     odp_schedule_config_init(odp_schedule_config_t *config);
+int      odp_schedule_config(const odp_schedule_config_t *config);
+uint64_t odp_schedule_wait_time(uint64_t ns);
+odp_event_t odp_schedule(odp_queue_t *from, uint64_t wait);
+int      odp_schedule_multi(odp_queue_t *from, uint64_t wait, odp_event_t events[], int num);
+int      odp_schedule_default_prio(void);
+
+/* ---- packets (packet.h, packet_flags.h) --------------------------------- */
+odp_event_t  odp_packet_to_event(odp_packet_t pkt);
+odp_packet_t odp_packet_from_event(odp_event_t ev);
+void     odp_packet_from_event_multi(odp_packet_t pkt[], const odp_event_t ev[], int num);
+odp_packet_t odp_packet_alloc(odp_pool_t pool, uint32_t len);
+void     odp_packet_free(odp_packet_t pkt);
+void     odp_packet_free_multi(const odp_packet_t pkt[], int num);
+uint32_t odp_packet_len(odp_packet_t pkt);
+void    *odp_packet_data(odp_packet_t pkt);
+odp_pool_t odp_packet_pool(odp_packet_t pkt);
+int      odp_packet_has_error(odp_packet_t pkt);
+int      odp_packet_has_eth(odp_packet_t pkt);
+int      odp_packet_has_ipv4(odp_packet_t pkt);
+int      odp_packet_has_ipv6(odp_packet_t pkt);
+int      odp_packet_has_udp(odp_packet_t pkt);
+int      odp_packet_has_tcp(odp_packet_t pkt);
+void    *odp_packet_l2_ptr(odp_packet_t pkt, uint32_t *len);
+void    *odp_packet_l3_ptr(odp_packet_t pkt, uint32_t *len);
+void    *odp_packet_l4_ptr(odp_packet_t pkt, uint32_t *len);
+uint32_t odp_packet_l2_offset(odp_packet_t pkt);
+uint32_t odp_packet_l3_offset(odp_packet_t pkt);
+uint32_t odp_packet_l4_offset(odp_packet_t pkt);
+odp_cos_t odp_packet_cos(odp_packet_t pkt);
+int      odp_packet_has_flow_hash(odp_packet_t pkt);
+void     odp_packet_print_data(odp_packet_t pkt, uint32_t offset, uint32_t len);
+
+/* ---- pktio beyond the classifier setters (packet_io.h) ------------------ */
+typedef struct odp_pktout_queue_t {
+	odp_pktio_t pktio;
+	int index;
+} odp_pktout_queue_t;
+
+typedef struct odp_pktout_queue_param_t {
+	odp_pktio_op_mode_t op_mode;
+	odp_bool_t hash_enable;
+	odp_pktin_hash_proto_t hash_proto;
+	uint32_t num_queues;
+	uint32_t queue_size[ODP_PKTIN_MAX_QUEUES];
+} odp_pktout_queue_param_t;
+
+typedef union odp_pktio_set_op_t {
+	struct {
+		uint32_t promisc_mode : 1;
+		uint32_t mac_addr     : 1;
+		uint32_t maxlen       : 1;
+	} op;
+	uint32_t all_bits;
+} odp_pktio_set_op_t;
+
+typedef struct odp_pktio_capability_t {
+	uint32_t max_input_queues;
+	uint32_t max_output_queues;
+	odp_pktio_config_t config;
+	odp_pktio_set_op_t set_op;
+	odp_bool_t loop_supported;
+	uint64_t reserved[8];
+} odp_pktio_capability_t;
+
+int  odp_pktio_capability(odp_pktio_t pktio, odp_pktio_capability_t *capa);
+void odp_pktout_queue_param_init(odp_pktout_queue_param_t *param);
+int  odp_pktout_queue_config(odp_pktio_t pktio, const odp_pktout_queue_param_t *param);
+int  odp_pktout_queue(odp_pktio_t pktio, odp_pktout_queue_t queues[], int num);
+int  odp_pktout_send(odp_pktout_queue_t queue, const odp_packet_t packets[], int num);
+int  odp_pktio_promisc_mode(odp_pktio_t pktio);
+int  odp_pktio_promisc_mode_set(odp_pktio_t pktio, odp_bool_t enable);
+int  odp_pktio_mac_addr(odp_pktio_t pktio, void *mac_addr, int size);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

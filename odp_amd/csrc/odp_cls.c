@@ -26,6 +26,7 @@
 #include <string.h>
 
 #include "../../include/odp_cls.h"
+#include "odp_rt_internal.h"
 
 #define REF_MAX_COS          64      /* CLS_COS_MAX_ENTRY   */
 #define REF_MAX_PMR          256     /* CLS_PMR_MAX_ENTRY   */
@@ -1038,9 +1039,8 @@ odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const odp_pktio_pa
 {
 	odp_pktio_t ret = ODP_PKTIO_INVALID;
 
-	(void)param;
-	if (!name || strncmp(name, "loop", 4) != 0) {
-		ERR("only loop pktio is supported: %s\n", name ? name : "(null)");
+	if (!name || (strncmp(name, "loop", 4) != 0 && strncmp(name, "pcap:", 5) != 0)) {
+		ERR("only loop and pcap pktio are supported: %s\n", name ? name : "(null)");
 		return ODP_PKTIO_INVALID;
 	}
 	LOCK();
@@ -1061,11 +1061,16 @@ odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const odp_pktio_pa
 		break;
 	}
 	UNLOCK();
+	if (ret != ODP_PKTIO_INVALID && odpg_rt_pktio_open(ret, name, param)) {
+		odp_pktio_close(ret);
+		return ODP_PKTIO_INVALID;
+	}
 	return ret;
 }
 
 int odp_pktio_close(odp_pktio_t hdl)
 {
+	odpg_rt_pktio_close(hdl);
 	LOCK();
 	pktio_e *p = get_pktio(hdl);
 
@@ -1499,9 +1504,9 @@ static bind_t *bind_get_locked(pktio_e *p, odpg_ctx_t *ctx, int *rc)
 	return b;
 }
 
-int odpg_pktio_recv_batch(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
-			  const odpg_desc_t *desc, uint32_t stride, uint32_t num,
-			  int device_ptrs, odpg_out_t *out, uint16_t *mark)
+static int recv_impl(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
+		     const odpg_desc_t *desc, uint32_t stride, uint32_t num,
+		     int device_ptrs, odpg_out_t *out, uint16_t *mark, odpg_meta_t *meta)
 {
 	int rc = 0;
 	odpg_batch_t b;
@@ -1538,6 +1543,7 @@ int odpg_pktio_recv_batch(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frame
 	memset(&res, 0, sizeof(res));
 	res.out = out;
 	res.mark = mark;
+	res.meta = meta;
 	res.counters = bd->cnt;
 	rc = device_ptrs ? odpg_classify(ctx, bd->tbl, &b, &res)
 			 : odpg_classify_host(ctx, bd->tbl, &b, &res, 0);
@@ -1554,4 +1560,28 @@ int odpg_pktio_recv_batch(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frame
 	}
 	UNLOCK();
 	return rc;
+}
+
+int odpg_pktio_recv_batch(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
+			  const odpg_desc_t *desc, uint32_t stride, uint32_t num,
+			  int device_ptrs, odpg_out_t *out, uint16_t *mark)
+{
+	return recv_impl(hdl, ctx, frames, desc, stride, num, device_ptrs, out, mark, NULL);
+}
+
+int odpg_cls_pktio_recv_meta(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
+			     const odpg_desc_t *desc, uint32_t num, odpg_out_t *out,
+			     odpg_meta_t *meta)
+{
+	return recv_impl(hdl, ctx, frames, desc, 0, num, 0, out, NULL, meta);
+}
+
+int odpg_cls_pktio_classifies(odp_pktio_t hdl)
+{
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+	const int r = p && p->started && p->cls_enabled;
+
+	UNLOCK();
+	return r;
 }

@@ -1,0 +1,25 @@
+# The reference's own applications, compiled UNMODIFIED from where they lie
+# under /root/reference against this repository's ODP headers (include/) and
+# linked to the product library (odp_amd/lib/libodpg.so): the drop-in check
+# of SURVEY §8(f) rank 4. Outputs only into oracle/_ref/ (git-ignored; it
+# travels to the GPU box like the built libraries). Nothing here is copied
+# from the reference; without /root/reference this makefile does nothing.
+# Usage: make -C oracle -f ref_apps.mk
+REF     ?= /root/reference
+CC      ?= gcc
+OUT     := _ref
+LIB     := $(abspath ../odp_amd/lib)
+APPS    := $(if $(wildcard $(REF)/example/classifier/odp_classifier.c),$(OUT)/odp_classifier)
+
+all: $(APPS)
+
+$(OUT)/odp_classifier: $(REF)/example/classifier/odp_classifier.c $(LIB)/libodpg.so \
+		../include/odp_api.h ../include/odp/rt.h ../include/odp/helper/odph_api.h ../include/odp_cls.h
+	@mkdir -p $(OUT)
+	$(CC) -std=gnu11 -O2 -Wall -I../include -o $@ $< -L$(LIB) -lodpg \
+	    -Wl,-rpath,'$$ORIGIN/../../odp_amd/lib' -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib
+
+clean:
+	rm -rf $(OUT)/odp_classifier
+
+.PHONY: all clean
