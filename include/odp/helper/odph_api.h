@@ -9,6 +9,7 @@
 
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "../../odp_api.h"
 
@@ -19,6 +20,15 @@ extern "C" {
 #define ODPH_ERR(fmt, ...) \
 	fprintf(stderr, "%s:%d:%s(): " fmt, __FILE__, __LINE__, __func__, ##__VA_ARGS__)
 #define ODPH_DBG(fmt, ...) do { } while (0)
+#define ODPH_ABORT(fmt, ...) do { \
+	fprintf(stderr, "%s:%d:%s(): " fmt, __FILE__, __LINE__, __func__, ##__VA_ARGS__); \
+	abort(); \
+} while (0)
+#define ODPH_ASSERT(cond) do { \
+	if (!(cond)) \
+		ODPH_ABORT("%s\n", #cond); \
+} while (0)
+#define ODPH_ARRAY_SIZE(x) (sizeof(x) / sizeof((x)[0]))
 
 /* ---- protocol headers (eth.h, ip.h, udp.h, tcp.h) ----------------------- */
 #define ODPH_ETHADDR_LEN   6

@@ -15,7 +15,8 @@
  *
  * Spec references: init.h, shared_memory.h, pool.h / pool_types.h,
  * queue.h / queue_types.h, schedule.h, packet.h / packet_flags.h,
- * packet_io.h, time.h, cpumask.h, thread.h, atomic.h, byteorder.h.
+ * packet_io.h, packet_io_stats.h, time.h, cpu.h, cpumask.h, thread.h,
+ * atomic.h, byteorder.h, hints.h, debug.h.
  */
 #ifndef ODP_RT_H_
 #define ODP_RT_H_
@@ -30,6 +31,9 @@ extern "C" {
 /* ---- hints, alignment, byte order ------------------------------------ */
 #define odp_likely(x)   __builtin_expect(!!(x), 1)
 #define odp_unlikely(x) __builtin_expect(!!(x), 0)
+#define ODP_UNUSED      __attribute__((__unused__))
+#define ODP_PRINTF_FORMAT(x, y) __attribute__((format(printf, (x), (y))))
+#define ODP_STATIC_ASSERT(cond, msg) _Static_assert(cond, msg)
 #define ODP_CACHE_LINE_SIZE 64
 
 typedef uint16_t odp_u16be_t;
@@ -64,8 +68,14 @@ static inline void odp_atomic_init_u32(odp_atomic_u32_t *a, uint32_t v)
 { __atomic_store_n(&a->v, v, __ATOMIC_RELAXED); }
 static inline uint32_t odp_atomic_load_u32(odp_atomic_u32_t *a)
 { return __atomic_load_n(&a->v, __ATOMIC_RELAXED); }
+static inline void odp_atomic_store_u32(odp_atomic_u32_t *a, uint32_t v)
+{ __atomic_store_n(&a->v, v, __ATOMIC_RELAXED); }
 static inline void odp_atomic_inc_u32(odp_atomic_u32_t *a)
 { __atomic_fetch_add(&a->v, 1, __ATOMIC_RELAXED); }
+static inline void odp_atomic_add_u32(odp_atomic_u32_t *a, uint32_t v)
+{ __atomic_fetch_add(&a->v, v, __ATOMIC_RELAXED); }
+static inline uint32_t odp_atomic_fetch_inc_u32(odp_atomic_u32_t *a)
+{ return __atomic_fetch_add(&a->v, 1, __ATOMIC_RELAXED); }
 
 /* ---- init (init.h) ------------------------------------------------------ */
 typedef uint64_t odp_instance_t;
@@ -102,6 +112,12 @@ void odp_sys_info_print(void);
 int  odp_thread_id(void);
 int  odp_cpu_count(void);
 
+/* ---- CPU cycle counter (cpu.h) ------------------------------------------ */
+uint64_t odp_cpu_cycles(void);
+uint64_t odp_cpu_cycles_diff(uint64_t c2, uint64_t c1);
+uint64_t odp_cpu_cycles_max(void);
+uint64_t odp_cpu_cycles_resolution(void);
+
 /* ---- CPU masks (cpumask.h) --------------------------------------------- */
 #define ODP_CPUMASK_SIZE     1024
 #define ODP_CPUMASK_STR_SIZE ((ODP_CPUMASK_SIZE + 3) / 4 + 3)
@@ -124,16 +140,35 @@ int     odp_cpumask_default_control(odp_cpumask_t *mask, int num);
 #define ODP_TIME_USEC_IN_NS 1000ULL
 #define ODP_TIME_MSEC_IN_NS 1000000ULL
 #define ODP_TIME_SEC_IN_NS  1000000000ULL
+#define ODP_TIME_MIN_IN_NS  60000000000ULL
+#define ODP_TIME_HOUR_IN_NS 3600000000000ULL
 
 typedef struct odp_time_t {
 	uint64_t nsec;
 } odp_time_t;
 
+#define ODP_TIME_NULL ((odp_time_t){ 0 })
+
+/* one monotonic nanosecond clock serves local and global time; the
+ * _strict variants order the read against earlier loads and stores */
 odp_time_t odp_time_local(void);
 odp_time_t odp_time_global(void);
+odp_time_t odp_time_local_strict(void);
+odp_time_t odp_time_global_strict(void);
+uint64_t   odp_time_local_ns(void);
+uint64_t   odp_time_global_ns(void);
+uint64_t   odp_time_local_strict_ns(void);
+odp_time_t odp_time_local_from_ns(uint64_t ns);
+odp_time_t odp_time_global_from_ns(uint64_t ns);
+odp_time_t odp_time_diff(odp_time_t t2, odp_time_t t1);
 uint64_t   odp_time_diff_ns(odp_time_t t2, odp_time_t t1);
+odp_time_t odp_time_sum(odp_time_t t1, odp_time_t t2);
+odp_time_t odp_time_add_ns(odp_time_t time, uint64_t ns);
+int        odp_time_cmp(odp_time_t t2, odp_time_t t1);
 uint64_t   odp_time_to_ns(odp_time_t time);
+uint64_t   odp_time_local_res(void);
 void       odp_time_wait_ns(uint64_t ns);
+void       odp_time_wait_until(odp_time_t time);
 
 /* ---- shared memory (shared_memory.h) ------------------------------------ */
 typedef struct _odp_shm_hdl *odp_shm_t;
@@ -172,6 +207,76 @@ typedef struct odp_pool_param_t {
 	uint64_t reserved[8];
 } odp_pool_param_t;
 
+/* odp_pool_capability_t (pool_types.h), field for field */
+typedef union odp_pool_stats_opt_t {
+	struct {
+		uint64_t available          : 1;
+		uint64_t alloc_ops          : 1;
+		uint64_t alloc_fails        : 1;
+		uint64_t free_ops           : 1;
+		uint64_t total_ops          : 1;
+		uint64_t cache_available    : 1;
+		uint64_t cache_alloc_ops    : 1;
+		uint64_t cache_free_ops     : 1;
+		uint64_t thread_cache_available : 1;
+	} bit;
+	uint64_t all;
+} odp_pool_stats_opt_t;
+
+typedef struct odp_pool_capability_t {
+	uint32_t max_pools;
+	struct {
+		uint32_t max_pools;
+		uint32_t max_align;
+		uint32_t max_size;
+		uint32_t max_num;
+		uint32_t max_uarea_size;
+		odp_bool_t uarea_persistence;
+		uint32_t min_cache_size;
+		uint32_t max_cache_size;
+		odp_pool_stats_opt_t stats;
+	} buf;
+	struct {
+		uint32_t max_pools;
+		uint32_t max_len;
+		uint32_t max_num;
+		uint32_t max_align;
+		uint32_t min_headroom;
+		uint32_t max_headroom;
+		uint32_t min_tailroom;
+		uint32_t max_segs_per_pkt;
+		uint32_t min_seg_len;
+		uint32_t max_seg_len;
+		uint32_t max_uarea_size;
+		odp_bool_t uarea_persistence;
+		uint8_t max_num_subparam;
+		uint32_t min_cache_size;
+		uint32_t max_cache_size;
+		odp_pool_stats_opt_t stats;
+	} pkt;
+	struct {
+		uint32_t max_pools;
+		uint32_t max_num;
+		uint32_t max_uarea_size;
+		odp_bool_t uarea_persistence;
+		uint32_t min_cache_size;
+		uint32_t max_cache_size;
+		odp_pool_stats_opt_t stats;
+	} tmo;
+	struct {
+		uint32_t max_pools;
+		uint32_t max_num;
+		uint32_t max_size;
+		uint32_t max_uarea_size;
+		odp_bool_t uarea_persistence;
+		uint32_t min_cache_size;
+		uint32_t max_cache_size;
+		odp_pool_stats_opt_t stats;
+	} vector;
+} odp_pool_capability_t;
+
+/* packet pools only; buffer / timeout / vector pools report max_pools 0 */
+int        odp_pool_capability(odp_pool_capability_t *capa);
 void       odp_pool_param_init(odp_pool_param_t *param);
 odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param);
 int        odp_pool_destroy(odp_pool_t pool);
@@ -194,6 +299,10 @@ int         odp_queue_destroy(odp_queue_t queue);
 int         odp_queue_info(odp_queue_t queue, odp_queue_info_t *info);
 int         odp_queue_enq(odp_queue_t queue, odp_event_t ev);
 odp_event_t odp_queue_deq(odp_queue_t queue);
+int         odp_queue_enq_multi(odp_queue_t queue, const odp_event_t ev[], int num);
+int         odp_queue_deq_multi(odp_queue_t queue, odp_event_t ev[], int num);
+void        odp_event_free(odp_event_t event);
+void        odp_event_free_multi(const odp_event_t event[], int num);
 
 #define ODP_SCHED_WAIT    UINT64_MAX
 #define ODP_SCHED_NO_WAIT 0
@@ -204,6 +313,20 @@ typedef struct odp_schedule_config_t {
 	uint64_t reserved[4];
 } odp_schedule_config_t;
 
+/* odp_schedule_capability_t (schedule_types.h), field for field */
+typedef struct odp_schedule_capability_t {
+	uint32_t max_ordered_locks;
+	uint32_t max_groups;
+	uint32_t max_prios;
+	uint32_t max_queues;
+	uint32_t max_queue_size;
+	uint32_t max_flow_id;
+	odp_support_t lockfree_queues;
+	odp_support_t waitfree_queues;
+	odp_support_t order_wait;
+} odp_schedule_capability_t;
+
+int      odp_schedule_capability(odp_schedule_capability_t *capa);
 void     odp_schedule_config_init(odp_schedule_config_t *config);
 int      odp_schedule_config(const odp_schedule_config_t *config);
 uint64_t odp_schedule_wait_time(uint64_t ns);
@@ -238,17 +361,40 @@ int      odp_packet_has_flow_hash(odp_packet_t pkt);
 void     odp_packet_print_data(odp_packet_t pkt, uint32_t offset, uint32_t len);
 
 /* ---- pktio beyond the classifier setters (packet_io.h) ------------------ */
+typedef struct odp_pktin_queue_t {
+	odp_pktio_t pktio;
+	int index;
+} odp_pktin_queue_t;
+
 typedef struct odp_pktout_queue_t {
 	odp_pktio_t pktio;
 	int index;
 } odp_pktout_queue_t;
 
+/* packet_io_stats.h */
+typedef struct odp_pktin_queue_stats_t {
+	uint64_t octets;
+	uint64_t packets;
+	uint64_t discards;
+	uint64_t errors;
+} odp_pktin_queue_stats_t;
+
+typedef struct odp_pktout_queue_stats_t {
+	uint64_t octets;
+	uint64_t packets;
+	uint64_t discards;
+	uint64_t errors;
+} odp_pktout_queue_stats_t;
+
+#ifndef ODP_PKTOUT_MAX_QUEUES
+#define ODP_PKTOUT_MAX_QUEUES 64
+#endif
+
+/* packet_io_types.h:325-339 */
 typedef struct odp_pktout_queue_param_t {
 	odp_pktio_op_mode_t op_mode;
-	odp_bool_t hash_enable;
-	odp_pktin_hash_proto_t hash_proto;
 	uint32_t num_queues;
-	uint32_t queue_size[ODP_PKTIN_MAX_QUEUES];
+	uint32_t queue_size[ODP_PKTOUT_MAX_QUEUES];
 } odp_pktout_queue_param_t;
 
 typedef union odp_pktio_set_op_t {
@@ -270,6 +416,24 @@ typedef struct odp_pktio_capability_t {
 } odp_pktio_capability_t;
 
 int  odp_pktio_capability(odp_pktio_t pktio, odp_pktio_capability_t *capa);
+odp_pktio_t odp_pktio_lookup(const char *name);
+
+/* input: the loop device (frames sent on it come back, pktio/loop.c) and
+ * the pcap device are received through the GPU classifier, in bursts:
+ * ODP_PKTIN_MODE_DIRECT by odp_pktin_recv(), ODP_PKTIN_MODE_QUEUE by a
+ * dequeue from the pktin event queue, ODP_PKTIN_MODE_SCHED by the
+ * scheduler. Packets the classifier places go to their CoS queue; with the
+ * classifier disabled they are returned / enqueued on the pktin queue. */
+int  odp_pktin_queue(odp_pktio_t pktio, odp_pktin_queue_t queues[], int num);
+int  odp_pktin_event_queue(odp_pktio_t pktio, odp_queue_t queues[], int num);
+int  odp_pktin_recv(odp_pktin_queue_t queue, odp_packet_t packets[], int num);
+int  odp_pktin_queue_stats(odp_pktin_queue_t queue, odp_pktin_queue_stats_t *stats);
+int  odp_pktin_event_queue_stats(odp_pktio_t pktio, odp_queue_t queue,
+				 odp_pktin_queue_stats_t *stats);
+int  odp_pktout_event_queue(odp_pktio_t pktio, odp_queue_t queues[], int num);
+int  odp_pktout_queue_stats(odp_pktout_queue_t queue, odp_pktout_queue_stats_t *stats);
+int  odp_pktout_event_queue_stats(odp_pktio_t pktio, odp_queue_t queue,
+				  odp_pktout_queue_stats_t *stats);
 void odp_pktout_queue_param_init(odp_pktout_queue_param_t *param);
 int  odp_pktout_queue_config(odp_pktio_t pktio, const odp_pktout_queue_param_t *param);
 int  odp_pktout_queue(odp_pktio_t pktio, odp_pktout_queue_t queues[], int num);

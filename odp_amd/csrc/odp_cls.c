@@ -1044,6 +1044,12 @@ odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const odp_pktio_pa
 		return ODP_PKTIO_INVALID;
 	}
 	LOCK();
+	for (int i = 0; i < MAX_PKTIO; i++)
+		if (g.pktio[i].valid && !strncmp(g.pktio[i].name, name, sizeof(g.pktio[i].name))) {
+			UNLOCK();
+			ERR("pktio device %s already opened\n", name);   /* odp_packet_io.c:406-410 */
+			return ODP_PKTIO_INVALID;
+		}
 	for (int i = 0; i < MAX_PKTIO; i++) {
 		pktio_e *p = &g.pktio[i];
 
@@ -1061,10 +1067,27 @@ odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const odp_pktio_pa
 		break;
 	}
 	UNLOCK();
-	if (ret != ODP_PKTIO_INVALID && odpg_rt_pktio_open(ret, name, param)) {
+	if (ret != ODP_PKTIO_INVALID && odpg_rt_pktio_open(ret, name, pool, param)) {
 		odp_pktio_close(ret);
 		return ODP_PKTIO_INVALID;
 	}
+	return ret;
+}
+
+/* odp_pktio_lookup (odp_packet_io.c:798-829): an open pktio by name */
+odp_pktio_t odp_pktio_lookup(const char *name)
+{
+	odp_pktio_t ret = ODP_PKTIO_INVALID;
+
+	if (!name)
+		return ret;
+	LOCK();
+	for (int i = 0; i < MAX_PKTIO; i++)
+		if (g.pktio[i].valid && !strncmp(g.pktio[i].name, name, sizeof(g.pktio[i].name))) {
+			ret = (odp_pktio_t)(uintptr_t)(i + 1);
+			break;
+		}
+	UNLOCK();
 	return ret;
 }
 
@@ -1165,20 +1188,34 @@ void odp_pktin_queue_param_init(odp_pktin_queue_param_t *param)
 	odp_queue_param_init(&param->queue_param);
 }
 
+/* odp_pktin_queue_config (odp_packet_io.c): with the classifier enabled one
+ * input queue; otherwise num_queues (at least 1, at most the capability).
+ * The runtime creates the pktin event queue of SCHED / QUEUE mode. */
 int odp_pktin_queue_config(odp_pktio_t hdl, const odp_pktin_queue_param_t *param)
 {
+	odp_pktin_queue_param_t def;
 	int rc = 0;
 
+	if (!param) {
+		odp_pktin_queue_param_init(&def);
+		param = &def;
+	}
+	if (!param->classifier_enable && param->num_queues == 0) {
+		ERR("invalid num_queues for operation mode\n");
+		return -1;
+	}
 	LOCK();
 	pktio_e *p = get_pktio(hdl);
 
 	if (!p || p->started) {
 		rc = -1;
 	} else {
-		p->cls_enabled = param ? !!param->classifier_enable : 0;
+		p->cls_enabled = !!param->classifier_enable;
 		bump();
 	}
 	UNLOCK();
+	if (rc == 0)
+		rc = odpg_rt_pktin_config(hdl, param->classifier_enable ? 1u : param->num_queues);
 	return rc;
 }
 
@@ -1574,6 +1611,32 @@ int odpg_cls_pktio_recv_meta(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *fr
 			     odpg_meta_t *meta)
 {
 	return recv_impl(hdl, ctx, frames, desc, 0, num, 0, out, NULL, meta);
+}
+
+void odpg_cls_pktio_count(odp_pktio_t hdl, int64_t in_packets, int64_t in_octets,
+			  uint64_t in_discards, uint64_t out_packets, uint64_t out_octets)
+{
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+
+	if (p) {
+		p->stats.in_packets += (uint64_t)in_packets;
+		p->stats.in_octets += (uint64_t)in_octets;
+		p->stats.in_discards += in_discards;
+		p->stats.out_packets += out_packets;
+		p->stats.out_octets += out_octets;
+	}
+	UNLOCK();
+}
+
+int odpg_cls_pktio_started(odp_pktio_t hdl)
+{
+	LOCK();
+	pktio_e *p = get_pktio(hdl);
+	const int r = p && p->started;
+
+	UNLOCK();
+	return r;
 }
 
 int odpg_cls_pktio_classifies(odp_pktio_t hdl)

@@ -7,17 +7,23 @@
  * pcap / loop pktio input, packet accessors, time, CPU masks, helper
  * threads.
  *
- * Receive path: the scheduler polls every started pktio opened in
- * ODP_PKTIN_MODE_SCHED. A poll takes a burst of frames from the pktio's
+ * Receive path: one burst of a pktio's input — the next frames of its
  * capture (pktio/pcap.c's pcapif_recv_pkt role: "pcap:in=<file>", with
- * ":loops=<n>"), classifies the burst on the GPU through the classifier's
- * own receive entry point (odpg_pktio_recv_batch's path: parse, checksum
- * verdicts, PMR -> CoS, the pktio / CoS / queue counters), and enqueues
- * every packet on its CoS's queue, as loopback_recv() ->
- * _odp_cls_enq() does (pktio/loop.c:304-374, odp_classification_internal.h:
- * 139-225). The parse result each packet carries is the odpg_meta_t the
- * kernel wrote. Packets that get no CoS, a drop CoS or a parse drop are
- * freed there, as the reference's receive loop frees them.
+ * ":loops=<n>"), or the packets sent on a loop device (pktio/loop.c: what
+ * odp_pktout_send() put on the device comes back) — is classified on the
+ * GPU through the classifier's own receive entry point
+ * (odpg_pktio_recv_batch's path: parse, checksum verdicts, PMR -> CoS, the
+ * pktio / CoS / queue counters). Every packet with a CoS goes to its CoS
+ * queue, as loopback_recv() -> _odp_cls_enq() does (pktio/loop.c:304-374,
+ * odp_classification_internal.h:139-225), in the CoS's pool (the pktio's
+ * when the CoS names none, odp_classification.c:1734-1736); with the
+ * classifier disabled the packet is the receive call's (DIRECT mode,
+ * odp_pktin_recv) or goes to the pktin event queue (QUEUE / SCHED mode).
+ * Bursts are taken by odp_pktin_recv(), by a dequeue from an empty QUEUE-mode
+ * pktin queue, and by the scheduler for SCHED-mode pktios. The parse result
+ * each packet carries is the odpg_meta_t the kernel wrote. Packets that get
+ * no CoS, a drop CoS or a parse drop are freed there, as the reference's
+ * receive loop frees them.
  *
  * This is a functional runtime, not a fast path: the device-resident batch
  * API (odpg.h) is the throughput path.
@@ -70,18 +76,33 @@ typedef struct rt_queue {
 	rt_pkt_t *head, *tail;
 	struct rt_queue *next_sched;
 	int dead;
+	odp_pktio_t pktin;         /* a QUEUE-mode pktin queue: dequeue polls it */
+	odp_pktio_t pktout;        /* a pktout event queue: enqueue transmits */
 } rt_queue_t;
 #define QUEUE_MAGIC 0x51554555u
 
 typedef struct rt_pktio {
 	int valid;
-	int sched_in;              /* ODP_PKTIN_MODE_SCHED */
+	int in_mode;               /* odp_pktin_mode_t */
+	int out_mode;              /* odp_pktout_mode_t */
+	int loopdev;               /* "loop...": transmitted packets come back */
+	odp_pool_t pool;           /* the pktio's packet pool */
 	odpg_capture_t cap;
 	int have_cap;
 	uint32_t pos;              /* next frame of the capture */
 	uint32_t loops, loop;      /* passes over the capture, done */
 	int promisc;
+	uint32_t mtu;
+	uint32_t num_in, num_out;  /* configured input / output queues */
+	rt_queue_t *inq;           /* pktin event queue (QUEUE / SCHED mode) */
+	rt_queue_t *outq;          /* pktout event queue (QUEUE mode) */
+	pthread_mutex_t ring_lock; /* the loop device's packets in flight */
+	rt_pkt_t *ring_head, *ring_tail;
+	uint8_t *stage;            /* loop packets gathered for one launch */
+	size_t stage_cap;
 } rt_pktio_t;
+
+#define LOOP_MTU 65535u            /* LOOP_MTU_MAX (pktio/loop.c:45) */
 
 static struct {
 	pthread_mutex_t lock;      /* object tables */
@@ -309,11 +330,112 @@ uint64_t odp_time_to_ns(odp_time_t time)
 	return time.nsec;
 }
 
+odp_time_t odp_time_local_strict(void)
+{
+	__atomic_thread_fence(__ATOMIC_SEQ_CST);
+	return odp_time_local();
+}
+
+odp_time_t odp_time_global_strict(void)
+{
+	return odp_time_local_strict();
+}
+
+uint64_t odp_time_local_ns(void)
+{
+	return odp_time_local().nsec;
+}
+
+uint64_t odp_time_global_ns(void)
+{
+	return odp_time_local().nsec;
+}
+
+uint64_t odp_time_local_strict_ns(void)
+{
+	return odp_time_local_strict().nsec;
+}
+
+odp_time_t odp_time_local_from_ns(uint64_t ns)
+{
+	odp_time_t t = { ns };
+
+	return t;
+}
+
+odp_time_t odp_time_global_from_ns(uint64_t ns)
+{
+	return odp_time_local_from_ns(ns);
+}
+
+odp_time_t odp_time_diff(odp_time_t t2, odp_time_t t1)
+{
+	odp_time_t t = { t2.nsec - t1.nsec };
+
+	return t;
+}
+
+odp_time_t odp_time_sum(odp_time_t t1, odp_time_t t2)
+{
+	odp_time_t t = { t1.nsec + t2.nsec };
+
+	return t;
+}
+
+odp_time_t odp_time_add_ns(odp_time_t time, uint64_t ns)
+{
+	time.nsec += ns;
+	return time;
+}
+
+int odp_time_cmp(odp_time_t t2, odp_time_t t1)
+{
+	return t2.nsec < t1.nsec ? -1 : t2.nsec > t1.nsec;
+}
+
+uint64_t odp_time_local_res(void)
+{
+	return ODP_TIME_SEC_IN_NS;
+}
+
 void odp_time_wait_ns(uint64_t ns)
 {
 	struct timespec ts = { (time_t)(ns / ODP_TIME_SEC_IN_NS), (long)(ns % ODP_TIME_SEC_IN_NS) };
 
 	nanosleep(&ts, NULL);
+}
+
+void odp_time_wait_until(odp_time_t time)
+{
+	const odp_time_t now = odp_time_local();
+
+	if (time.nsec > now.nsec)
+		odp_time_wait_ns(time.nsec - now.nsec);
+}
+
+/* ---- CPU cycle counter (the TSC on x86-64, else the nanosecond clock) ----- */
+uint64_t odp_cpu_cycles(void)
+{
+#if defined(__x86_64__)
+	return __builtin_ia32_rdtsc();
+#else
+	return odp_time_local().nsec;
+#endif
+}
+
+uint64_t odp_cpu_cycles_diff(uint64_t c2, uint64_t c1)
+{
+	return c2 - c1;
+}
+
+uint64_t odp_cpu_cycles_max(void)
+{
+	return UINT64_MAX;
+}
+
+uint64_t odp_cpu_cycles_resolution(void)
+{
+	return 1;
 }
 
 /* ---- shared memory -------------------------------------------------------- */
@@ -350,6 +472,24 @@ static rt_pool_t *get_pool(odp_pool_t hdl)
 	const uintptr_t n = (uintptr_t)hdl;
 
 	return n && n <= RT_MAX_POOL && rt.pool[n - 1].valid ? &rt.pool[n - 1] : NULL;
+}
+
+/* packet pools of malloc'd packets, one segment each */
+int odp_pool_capability(odp_pool_capability_t *capa)
+{
+	if (!capa)
+		return -1;
+	memset(capa, 0, sizeof(*capa));
+	capa->max_pools = RT_MAX_POOL;
+	capa->pkt.max_pools = RT_MAX_POOL;
+	capa->pkt.max_len = LOOP_MTU;
+	capa->pkt.max_num = 0;                 /* no limit but memory */
+	capa->pkt.max_align = 64;
+	capa->pkt.max_segs_per_pkt = 1;
+	capa->pkt.min_seg_len = 1;
+	capa->pkt.max_seg_len = LOOP_MTU;
+	capa->pkt.max_num_subparam = 0;
+	return 0;
 }
 
 void odp_pool_param_init(odp_pool_param_t *param)
@@ -566,6 +706,9 @@ void odp_packet_print_data(odp_packet_t pkt, uint32_t offset, uint32_t len)
 }
 
 /* ---- queues ---------------------------------------------------------------- */
+static int pktout_send_impl(odp_pktio_t pktio, const odp_packet_t packets[], int num);
+static void pktin_queue_fill(odp_pktio_t pktio);
+
 static rt_queue_t *get_queue(odp_queue_t q)
 {
 	rt_queue_t *x = (rt_queue_t *)q;
@@ -633,6 +776,11 @@ int odp_queue_enq(odp_queue_t queue, odp_event_t ev)
 
 	if (!q || !k)
 		return -1;
+	if (q->pktout) {                    /* pktout event queue: transmit */
+		const odp_packet_t pkt = (odp_packet_t)k;
+
+		return pktout_send_impl(q->pktout, &pkt, 1) == 1 ? 0 : -1;
+	}
 	k->next = NULL;
 	pthread_mutex_lock(&q->lock);
 	if (q->tail)
@@ -651,6 +799,8 @@ odp_event_t odp_queue_deq(odp_queue_t queue)
 
 	if (!q)
 		return ODP_EVENT_INVALID;
+	if (q->pktin && !__atomic_load_n(&q->head, __ATOMIC_RELAXED))
+		pktin_queue_fill(q->pktin);     /* QUEUE mode: receive a burst */
 	pthread_mutex_lock(&q->lock);
 	k = q->head;
 	if (k) {
@@ -660,6 +810,40 @@ odp_event_t odp_queue_deq(odp_queue_t queue)
 	}
 	pthread_mutex_unlock(&q->lock);
 	return (odp_event_t)k;
+}
+
+int odp_queue_enq_multi(odp_queue_t queue, const odp_event_t ev[], int num)
+{
+	int n = 0;
+
+	while (n < num && odp_queue_enq(queue, ev[n]) == 0)
+		n++;
+	return n ? n : (num > 0 ? -1 : 0);
+}
+
+static int deq_multi(rt_queue_t *q, odp_event_t ev[], int num);
+
+int odp_queue_deq_multi(odp_queue_t queue, odp_event_t ev[], int num)
+{
+	rt_queue_t *q = get_queue(queue);
+
+	if (!q)
+		return -1;
+	if (q->pktin && !__atomic_load_n(&q->head, __ATOMIC_RELAXED))
+		pktin_queue_fill(q->pktin);
+	return deq_multi(q, ev, num);
+}
+
+/* every event here is a packet */
+void odp_event_free(odp_event_t event)
+{
+	odp_packet_free((odp_packet_t)event);
+}
+
+void odp_event_free_multi(const odp_event_t event[], int num)
+{
+	for (int i = 0; i < num; i++)
+		odp_packet_free((odp_packet_t)event[i]);
 }
 
 /* up to num events of one queue */
@@ -688,19 +872,54 @@ static rt_pktio_t *get_rt_pktio(odp_pktio_t hdl)
 	return n && n <= RT_MAX_PKTIO && rt.pktio[n - 1].valid ? &rt.pktio[n - 1] : NULL;
 }
 
-/* "pcap:in=<file>[:loops=<n>]" (pktio/pcap.c's device string) */
-int odpg_rt_pktio_open(odp_pktio_t hdl, const char *name, const odp_pktio_param_t *param)
+/* a queue the pktio owns: unlinked from use, its packets freed; the memory
+ * stays (schedulers may still walk it) */
+static void pktio_queue_kill(rt_queue_t *q)
+{
+	if (!q)
+		return;
+	pthread_mutex_lock(&q->lock);
+	rt_pkt_t *k = q->head;
+
+	q->head = q->tail = NULL;
+	q->dead = 1;
+	q->pktin = q->pktout = ODP_PKTIO_INVALID;
+	pthread_mutex_unlock(&q->lock);
+	while (k) {
+		rt_pkt_t *nx = k->next;
+
+		odp_packet_free((odp_packet_t)k);
+		k = nx;
+	}
+}
+
+/* "loop[...]" (pktio/loop.c) or "pcap:in=<file>[:loops=<n>]" (pktio/pcap.c's
+ * device string) */
+int odpg_rt_pktio_open(odp_pktio_t hdl, const char *name, odp_pool_t pool,
+		       const odp_pktio_param_t *param)
 {
 	const uintptr_t n = (uintptr_t)hdl;
 	rt_pktio_t *p;
+	odp_pktio_param_t def;
 
 	if (!n || n > RT_MAX_PKTIO)
 		return -1;
+	if (!param) {
+		odp_pktio_param_init(&def);
+		param = &def;
+	}
+	if (rt.pktio[n - 1].valid)          /* left over by odpg_cls_reset() */
+		odpg_rt_pktio_close(hdl);
 	p = &rt.pktio[n - 1];
 	memset(p, 0, sizeof(*p));
 	p->valid = 1;
 	p->loops = 1;
-	p->sched_in = param && param->in_mode == ODP_PKTIN_MODE_SCHED;
+	p->in_mode = param->in_mode;
+	p->out_mode = param->out_mode;
+	p->pool = pool;
+	p->mtu = LOOP_MTU;
+	p->loopdev = !strncmp(name, "loop", 4);
+	pthread_mutex_init(&p->ring_lock, NULL);
 	if (!strncmp(name, "pcap:", 5)) {
 		char buf[1024], *save = NULL, *tok;
 
@@ -734,11 +953,54 @@ void odpg_rt_pktio_close(odp_pktio_t hdl)
 	rt_pktio_t *p = get_rt_pktio(hdl);
 
 	if (p) {
+		rt_pkt_t *k = p->ring_head;
+
 		if (p->have_cap)
 			odpg_pcap_free(&p->cap);
+		pktio_queue_kill(p->inq);
+		pktio_queue_kill(p->outq);
+		while (k) {
+			rt_pkt_t *nx = k->next;
+
+			odp_packet_free((odp_packet_t)k);
+			k = nx;
+		}
+		free(p->stage);
+		pthread_mutex_destroy(&p->ring_lock);
 		memset(p, 0, sizeof(*p));
 	}
 	pthread_mutex_unlock(&rt.poll_lock);
+}
+
+/* the input queues odp_pktin_queue_config() asked for; QUEUE / SCHED mode
+ * get their event queue ("odp-pktin-<i>-<q>", odp_packet_io.c) */
+int odpg_rt_pktin_config(odp_pktio_t hdl, uint32_t num_queues)
+{
+	rt_pktio_t *p = get_rt_pktio(hdl);
+	odp_queue_param_t qp;
+	char name[ODP_QUEUE_NAME_LEN];
+
+	if (!p)
+		return -1;
+	if (p->in_mode == ODP_PKTIN_MODE_DISABLED)
+		return 0;
+	if (num_queues > 1) {
+		ERR("pktio %" PRIu64 ": too many input queues\n", (uint64_t)(uintptr_t)hdl);
+		return -1;
+	}
+	p->num_in = num_queues;
+	if (p->in_mode != ODP_PKTIN_MODE_QUEUE && p->in_mode != ODP_PKTIN_MODE_SCHED)
+		return 0;
+	pktio_queue_kill(p->inq);
+	odp_queue_param_init(&qp);
+	qp.type = p->in_mode == ODP_PKTIN_MODE_SCHED ? ODP_QUEUE_TYPE_SCHED : ODP_QUEUE_TYPE_PLAIN;
+	snprintf(name, sizeof(name), "odp-pktin-%u-0", (unsigned)(uintptr_t)hdl);
+	p->inq = (rt_queue_t *)odp_queue_create(name, &qp);
+	if (!p->inq)
+		return -1;
+	if (p->in_mode == ODP_PKTIN_MODE_QUEUE)
+		p->inq->pktin = hdl;
+	return 0;
 }
 
 /* the CoS queue a verdict names (get_dest_queue's pick for hash CoS) */
@@ -757,8 +1019,156 @@ static odp_queue_t dest_queue(uint32_t w, odp_cos_t *cos)
 	return n == 1 ? qs[0] : qs[ODPG_OUT_HASHQ(w) % n];
 }
 
-/* one burst of every polled pktio: classify on the GPU, enqueue by CoS.
- * Returns the packets enqueued (0: nothing left to read). */
+#define ALIGN64(x) (((x) + 63u) & ~(size_t)63u)
+
+/* One burst of the pktio's input through the GPU classifier (loopback_recv,
+ * pktio/loop.c:304-374; pcapif_recv_pkt + the same classify step). Packets
+ * with a CoS are enqueued on its queue; with the classifier disabled
+ * (ODPG_COS_NOCLS) they are returned in pkts[]. *nret = packets returned.
+ * Returns the frames taken from the input (0: none waiting), or -1.
+ * Caller holds rt.poll_lock (the launch buffers are shared). */
+static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num, int *nret)
+{
+	rt_pkt_t *src[RT_BURST];
+	const uint8_t *frames;
+	uint32_t n = 0, first = 0;
+
+	*nret = 0;
+	if (num > RT_BURST)
+		num = RT_BURST;
+	if (num <= 0 || !rt.init || !odpg_cls_pktio_started(hdl))
+		return 0;
+	if (p->loopdev) {
+		size_t need = 0, off = 0;
+
+		pthread_mutex_lock(&p->ring_lock);
+		while (n < (uint32_t)num && p->ring_head) {
+			src[n] = p->ring_head;
+			p->ring_head = p->ring_head->next;
+			need += ALIGN64(src[n]->len);
+			n++;
+		}
+		if (!p->ring_head)
+			p->ring_tail = NULL;
+		pthread_mutex_unlock(&p->ring_lock);
+		if (!n)
+			return 0;
+		if (need > p->stage_cap) {
+			uint8_t *b = NULL;
+
+			if (posix_memalign((void **)&b, 64, need)) {
+				for (uint32_t k = 0; k < n; k++)
+					odp_packet_free((odp_packet_t)src[k]);
+				return -1;
+			}
+			free(p->stage);
+			p->stage = b;
+			p->stage_cap = need;
+		}
+		for (uint32_t k = 0; k < n; k++) {
+			memcpy(p->stage + off, src[k]->data, src[k]->len);
+			rt.desc[k].offset = (uint32_t)off;
+			rt.desc[k].len = src[k]->len;
+			off += ALIGN64(src[k]->len);
+		}
+		frames = p->stage;
+	} else if (p->have_cap) {
+		if (p->pos >= p->cap.num) {
+			if (p->loops != 0 && p->loop + 1 >= p->loops)
+				return 0;
+			p->loop++;
+			p->pos = 0;
+		}
+		first = p->pos;
+		n = p->cap.num - first < (uint32_t)num ? p->cap.num - first : (uint32_t)num;
+		if (!n)
+			return 0;
+		memcpy(rt.desc, p->cap.desc + first, n * sizeof(odpg_desc_t));
+		frames = p->cap.frames;
+	} else {
+		return 0;
+	}
+	if (odpg_cls_pktio_recv_meta(hdl, rt.ctx, frames, rt.desc, n, rt.out, rt.meta)) {
+		ERR("classify failed\n");
+		if (p->loopdev)
+			for (uint32_t k = 0; k < n; k++)
+				odp_packet_free((odp_packet_t)src[k]);
+		return -1;
+	}
+	if (!p->loopdev)
+		p->pos += n;
+	for (uint32_t k = 0; k < n; k++) {
+		const uint32_t w = rt.out[k];
+		const uint32_t len = rt.desc[k].len;
+		rt_pkt_t *have = p->loopdev ? src[k] : NULL;
+		odp_cos_t cos = ODP_COS_INVALID;
+		odp_queue_t q = ODP_QUEUE_INVALID;
+		odp_pool_t pool = p->pool;
+		odp_packet_t pkt;
+
+		if (ODPG_OUT_COS(w) != ODPG_COS_NOCLS) {
+			q = dest_queue(w, &cos);
+			if (q == ODP_QUEUE_INVALID || !get_queue(q)) {
+				if (have)                 /* no CoS / drop / parse drop */
+					odp_packet_free((odp_packet_t)have);
+				continue;
+			}
+			if (odp_cls_cos_pool(cos) != ODP_POOL_INVALID)
+				pool = odp_cls_cos_pool(cos);
+		}
+		if (have && have->pool == pool) {
+			pkt = (odp_packet_t)have;
+		} else {
+			/* into the CoS's pool (_odp_pktio_packet_to_pool) */
+			pkt = odp_packet_alloc(pool, len);
+			if (pkt != ODP_PACKET_INVALID)
+				memcpy(PK(pkt)->data, frames + rt.desc[k].offset, len);
+			if (have)
+				odp_packet_free((odp_packet_t)have);
+			if (pkt == ODP_PACKET_INVALID) {
+				const int counted = !(w & ODPG_OUT_ERROR);
+
+				odpg_cls_pktio_count(hdl, counted ? -1 : 0,
+						     counted ? -(int64_t)len : 0, 1, 0, 0);
+				continue;
+			}
+		}
+		PK(pkt)->meta = rt.meta[k];
+		PK(pkt)->cos = cos;
+		if (q == ODP_QUEUE_INVALID) {
+			pkts[(*nret)++] = pkt;
+		} else if (odp_queue_enq(q, (odp_event_t)pkt)) {
+			odp_packet_free(pkt);
+		}
+	}
+	return (int)n;
+}
+
+/* a burst of a QUEUE / SCHED mode pktio onto its pktin event queue */
+static int rx_to_inq(rt_pktio_t *p, odp_pktio_t hdl)
+{
+	odp_packet_t pkts[RT_BURST];
+	int nret;
+	const int took = rx_burst(p, hdl, pkts, RT_BURST, &nret);
+
+	for (int k = 0; k < nret; k++)
+		if (!p->inq || odp_queue_enq((odp_queue_t)p->inq, (odp_event_t)pkts[k]))
+			odp_packet_free(pkts[k]);
+	return took;
+}
+
+static void pktin_queue_fill(odp_pktio_t hdl)
+{
+	pthread_mutex_lock(&rt.poll_lock);
+	rt_pktio_t *p = get_rt_pktio(hdl);
+
+	if (p && p->in_mode == ODP_PKTIN_MODE_QUEUE)
+		rx_to_inq(p, hdl);
+	pthread_mutex_unlock(&rt.poll_lock);
+}
+
+/* one burst of every SCHED-mode pktio (the scheduler's pktin poll).
+ * Returns the frames taken (0: nothing waiting). */
 static int poll_input(void)
 {
 	int got = 0;
@@ -767,55 +1177,140 @@ static int poll_input(void)
 		return 0;
 	for (int i = 0; i < RT_MAX_PKTIO && rt.init; i++) {
 		rt_pktio_t *p = &rt.pktio[i];
-		const odp_pktio_t hdl = (odp_pktio_t)(uintptr_t)(i + 1);
 
-		if (!p->valid || !p->sched_in || !p->have_cap || !odpg_cls_pktio_classifies(hdl))
+		if (!p->valid || p->in_mode != ODP_PKTIN_MODE_SCHED)
 			continue;
-		if (p->pos >= p->cap.num) {
-			if (p->loop + 1 >= p->loops && p->loops != 0)
-				continue;
-			p->loop++;
-			p->pos = 0;
-		}
-		const uint32_t first = p->pos;
-		const uint32_t num = p->cap.num - first < RT_BURST ? p->cap.num - first : RT_BURST;
+		const int took = rx_to_inq(p, (odp_pktio_t)(uintptr_t)(i + 1));
 
-		memcpy(rt.desc, p->cap.desc + first, num * sizeof(odpg_desc_t));
-		if (odpg_cls_pktio_recv_meta(hdl, rt.ctx, p->cap.frames, rt.desc, num, rt.out,
-					     rt.meta)) {
-			ERR("classify failed\n");
-			continue;
-		}
-		p->pos += num;
-		for (uint32_t k = 0; k < num; k++) {
-			odp_cos_t cos = ODP_COS_INVALID;
-			const odp_queue_t q = dest_queue(rt.out[k], &cos);
-			odp_pool_t pool = cos != ODP_COS_INVALID ? odp_cls_cos_pool(cos)
-								 : ODP_POOL_INVALID;
-			const odpg_desc_t *d = &p->cap.desc[first + k];
-			odp_packet_t pkt;
-
-			if (q == ODP_QUEUE_INVALID || !get_queue(q))
-				continue;         /* no CoS / drop / parse drop: freed */
-			if (pool == ODP_POOL_INVALID)
-				continue;
-			pkt = odp_packet_alloc(pool, d->len);
-			if (pkt == ODP_PACKET_INVALID)
-				continue;         /* pool empty: dropped, as the reference */
-			memcpy(PK(pkt)->data, p->cap.frames + d->offset, d->len);
-			PK(pkt)->meta = rt.meta[k];
-			PK(pkt)->cos = cos;
-			if (odp_queue_enq(q, (odp_event_t)pkt))
-				odp_packet_free(pkt);
-			else
-				got++;
-		}
+		if (took > 0)
+			got += took;
 	}
 	pthread_mutex_unlock(&rt.poll_lock);
 	return got;
 }
 
+/* odp_pktin_queue (odp_packet_io.c:2404-2441) */
+int odp_pktin_queue(odp_pktio_t pktio, odp_pktin_queue_t queues[], int num)
+{
+	rt_pktio_t *p = get_rt_pktio(pktio);
+
+	if (!p || num < 0)
+		return -1;
+	if (p->in_mode == ODP_PKTIN_MODE_DISABLED)
+		return 0;
+	if (p->in_mode != ODP_PKTIN_MODE_DIRECT)
+		return -1;
+	for (int i = 0; queues && i < num && i < (int)p->num_in; i++) {
+		queues[i].pktio = pktio;
+		queues[i].index = i;
+	}
+	return (int)p->num_in;
+}
+
+/* odp_pktin_event_queue (odp_packet_io.c:2364-2402) */
+int odp_pktin_event_queue(odp_pktio_t pktio, odp_queue_t queues[], int num)
+{
+	rt_pktio_t *p = get_rt_pktio(pktio);
+
+	if (!p || num < 0)
+		return -1;
+	if (p->in_mode == ODP_PKTIN_MODE_DISABLED)
+		return 0;
+	if (p->in_mode != ODP_PKTIN_MODE_QUEUE && p->in_mode != ODP_PKTIN_MODE_SCHED)
+		return -1;
+	if (queues && num > 0 && p->inq)
+		queues[0] = (odp_queue_t)p->inq;
+	return p->inq ? 1 : 0;
+}
+
+/* DIRECT-mode receive: one burst through the GPU classifier */
+int odp_pktin_recv(odp_pktin_queue_t queue, odp_packet_t packets[], int num)
+{
+	int nret = 0;
+
+	pthread_mutex_lock(&rt.poll_lock);
+	rt_pktio_t *p = get_rt_pktio(queue.pktio);
+
+	if (!p || p->in_mode != ODP_PKTIN_MODE_DIRECT || queue.index < 0 ||
+	    (uint32_t)queue.index >= p->num_in) {
+		pthread_mutex_unlock(&rt.poll_lock);
+		return -1;
+	}
+	const int rc = rx_burst(p, queue.pktio, packets, num, &nret);
+
+	pthread_mutex_unlock(&rt.poll_lock);
+	return rc < 0 ? -1 : nret;
+}
+
+/* per-queue counters: one input / output queue per pktio here, so queue 0
+ * carries the interface's counters (loopback_pktin_stats /
+ * loopback_pktout_stats, pktio/loop.c:762-786) */
+static int in_queue_stats(odp_pktio_t pktio, uint32_t index, odp_pktin_queue_stats_t *st)
+{
+	odp_pktio_stats_t s;
+
+	if (!st || index != 0 || odp_pktio_stats(pktio, &s))
+		return -1;
+	memset(st, 0, sizeof(*st));
+	st->octets = s.in_octets;
+	st->packets = s.in_packets;
+	st->discards = s.in_discards;
+	st->errors = s.in_errors;
+	return 0;
+}
+
+static int out_queue_stats(odp_pktio_t pktio, uint32_t index, odp_pktout_queue_stats_t *st)
+{
+	odp_pktio_stats_t s;
+
+	if (!st || index != 0 || odp_pktio_stats(pktio, &s))
+		return -1;
+	memset(st, 0, sizeof(*st));
+	st->octets = s.out_octets;
+	st->packets = s.out_packets;
+	return 0;
+}
+
+/* odp_pktin_queue_stats (odp_packet_io.c:1696-1730): DIRECT mode only */
+int odp_pktin_queue_stats(odp_pktin_queue_t queue, odp_pktin_queue_stats_t *stats)
+{
+	rt_pktio_t *p = get_rt_pktio(queue.pktio);
+
+	if (!p || p->in_mode != ODP_PKTIN_MODE_DIRECT || queue.index < 0 ||
+	    (uint32_t)queue.index >= p->num_in)
+		return -1;
+	return in_queue_stats(queue.pktio, (uint32_t)queue.index, stats);
+}
+
+/* odp_pktin_event_queue_stats (odp_packet_io.c:1732-1769): QUEUE / SCHED */
+int odp_pktin_event_queue_stats(odp_pktio_t pktio, odp_queue_t queue,
+				odp_pktin_queue_stats_t *stats)
+{
+	rt_pktio_t *p = get_rt_pktio(pktio);
+
+	if (!p || (p->in_mode != ODP_PKTIN_MODE_SCHED && p->in_mode != ODP_PKTIN_MODE_QUEUE) ||
+	    !p->inq || queue != (odp_queue_t)p->inq)
+		return -1;
+	return in_queue_stats(pktio, 0, stats);
+}
+
 /* ---- scheduler -------------------------------------------------------------- */
+/* one scheduling priority and group; queues are limited by memory only */
+int odp_schedule_capability(odp_schedule_capability_t *capa)
+{
+	if (!capa)
+		return -1;
+	memset(capa, 0, sizeof(*capa));
+	capa->max_prios = 1;
+	capa->max_groups = 1;
+	capa->max_queues = 1u << 20;
+	capa->max_queue_size = 0;          /* no limit */
+	capa->lockfree_queues = ODP_SUPPORT_NO;
+	capa->waitfree_queues = ODP_SUPPORT_NO;
+	capa->order_wait = ODP_SUPPORT_NO;
+	return 0;
+}
+
 void odp_schedule_config_init(odp_schedule_config_t *config)
 {
 	memset(config, 0, sizeof(*config));
@@ -900,7 +1395,7 @@ int odp_pktio_capability(odp_pktio_t pktio, odp_pktio_capability_t *capa)
 		return -1;
 	memset(capa, 0, sizeof(*capa));
 	capa->max_input_queues = 1;
-	capa->max_output_queues = ODP_PKTIN_MAX_QUEUES;
+	capa->max_output_queues = 1;
 	odp_pktio_config_init(&capa->config);
 	capa->config.pktin.bit.ipv4_chksum = 1;
 	capa->config.pktin.bit.udp_chksum = 1;
@@ -917,31 +1412,150 @@ void odp_pktout_queue_param_init(odp_pktout_queue_param_t *param)
 	param->num_queues = 1;
 }
 
+/* odp_pktout_queue_config (odp_packet_io.c): QUEUE mode gets its event
+ * queue, whose enqueue transmits */
 int odp_pktout_queue_config(odp_pktio_t pktio, const odp_pktout_queue_param_t *param)
 {
-	if (!get_rt_pktio(pktio) || !param || param->num_queues > ODP_PKTIN_MAX_QUEUES)
+	rt_pktio_t *p = get_rt_pktio(pktio);
+	odp_pktout_queue_param_t def;
+	odp_queue_param_t qp;
+	char name[ODP_QUEUE_NAME_LEN];
+
+	if (!param) {
+		odp_pktout_queue_param_init(&def);
+		param = &def;
+	}
+	if (!p || odpg_cls_pktio_started(pktio))
 		return -1;
+	if (p->out_mode == ODP_PKTOUT_MODE_DISABLED)
+		return 0;
+	if (param->num_queues == 0 || param->num_queues > 1) {
+		ERR("pktio %" PRIu64 ": invalid number of output queues\n",
+		    (uint64_t)(uintptr_t)pktio);
+		return -1;
+	}
+	p->num_out = param->num_queues;
+	if (p->out_mode != ODP_PKTOUT_MODE_QUEUE)
+		return 0;
+	pktio_queue_kill(p->outq);
+	odp_queue_param_init(&qp);
+	snprintf(name, sizeof(name), "odp-pktout-%u-0", (unsigned)(uintptr_t)pktio);
+	p->outq = (rt_queue_t *)odp_queue_create(name, &qp);
+	if (!p->outq)
+		return -1;
+	p->outq->pktout = pktio;
 	return 0;
 }
 
+/* odp_pktout_queue (odp_packet_io.c:2474-2503): DIRECT mode */
 int odp_pktout_queue(odp_pktio_t pktio, odp_pktout_queue_t queues[], int num)
 {
-	if (!get_rt_pktio(pktio))
+	rt_pktio_t *p = get_rt_pktio(pktio);
+
+	if (!p)
 		return -1;
-	for (int i = 0; i < num; i++) {
+	if (p->out_mode == ODP_PKTOUT_MODE_DISABLED)
+		return 0;
+	if (p->out_mode != ODP_PKTOUT_MODE_DIRECT)
+		return -1;
+	for (int i = 0; queues && i < num && i < (int)p->num_out; i++) {
 		queues[i].pktio = pktio;
 		queues[i].index = i;
 	}
-	return num;
+	return (int)p->num_out;
 }
 
-/* transmit: the pcap / loop pktio here has no wire; packets are consumed */
+/* odp_pktout_event_queue (odp_packet_io.c:2443-2472): QUEUE mode */
+int odp_pktout_event_queue(odp_pktio_t pktio, odp_queue_t queues[], int num)
+{
+	rt_pktio_t *p = get_rt_pktio(pktio);
+
+	if (!p)
+		return -1;
+	if (p->out_mode == ODP_PKTOUT_MODE_DISABLED)
+		return 0;
+	if (p->out_mode != ODP_PKTOUT_MODE_QUEUE)
+		return -1;
+	if (queues && num > 0 && p->outq)
+		queues[0] = (odp_queue_t)p->outq;
+	return p->outq ? 1 : 0;
+}
+
+/* transmit (loopback_send, pktio/loop.c:525-580): on a loop device the
+ * packets go back to its input, up to the first one over the MTU (-1 if
+ * that is the first); the pcap device here has no output file, so its
+ * packets are consumed. Counted as out_packets / out_octets. */
+static int pktout_send_impl(odp_pktio_t pktio, const odp_packet_t packets[], int num)
+{
+	rt_pktio_t *p = get_rt_pktio(pktio);
+	uint64_t octets = 0;
+	int n = 0;
+
+	if (!p || num < 0)
+		return -1;
+	if (!odpg_cls_pktio_started(pktio))
+		return 0;
+	for (; n < num; n++) {
+		rt_pkt_t *k = PK(packets[n]);
+
+		if (k->len > p->mtu) {
+			if (n == 0)
+				return -1;
+			break;
+		}
+		octets += k->len;
+	}
+	if (p->loopdev) {
+		pthread_mutex_lock(&p->ring_lock);
+		for (int i = 0; i < n; i++) {
+			rt_pkt_t *k = PK(packets[i]);
+
+			k->next = NULL;
+			if (p->ring_tail)
+				p->ring_tail->next = k;
+			else
+				p->ring_head = k;
+			p->ring_tail = k;
+		}
+		pthread_mutex_unlock(&p->ring_lock);
+	} else {
+		odp_packet_free_multi(packets, n);
+	}
+	odpg_cls_pktio_count(pktio, 0, 0, 0, (uint64_t)n, octets);
+	return n;
+}
+
 int odp_pktout_send(odp_pktout_queue_t queue, const odp_packet_t packets[], int num)
 {
-	if (!get_rt_pktio(queue.pktio))
+	rt_pktio_t *p = get_rt_pktio(queue.pktio);
+
+	if (!p || p->out_mode != ODP_PKTOUT_MODE_DIRECT || queue.index < 0 ||
+	    (uint32_t)queue.index >= p->num_out)
 		return -1;
-	odp_packet_free_multi(packets, num);
-	return num;
+	return pktout_send_impl(queue.pktio, packets, num);
+}
+
+/* odp_pktout_queue_stats (odp_packet_io.c:1771-1805): DIRECT mode */
+int odp_pktout_queue_stats(odp_pktout_queue_t queue, odp_pktout_queue_stats_t *stats)
+{
+	rt_pktio_t *p = get_rt_pktio(queue.pktio);
+
+	if (!p || p->out_mode != ODP_PKTOUT_MODE_DIRECT || queue.index < 0 ||
+	    (uint32_t)queue.index >= p->num_out)
+		return -1;
+	return out_queue_stats(queue.pktio, (uint32_t)queue.index, stats);
+}
+
+/* odp_pktout_event_queue_stats (odp_packet_io.c:1807-1843): QUEUE mode */
+int odp_pktout_event_queue_stats(odp_pktio_t pktio, odp_queue_t queue,
+				 odp_pktout_queue_stats_t *stats)
+{
+	rt_pktio_t *p = get_rt_pktio(pktio);
+
+	if (!p || p->out_mode != ODP_PKTOUT_MODE_QUEUE || !p->outq ||
+	    queue != (odp_queue_t)p->outq)
+		return -1;
+	return out_queue_stats(pktio, 0, stats);
 }
 
 int odp_pktio_promisc_mode(odp_pktio_t pktio)

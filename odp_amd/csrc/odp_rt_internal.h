@@ -9,15 +9,25 @@
 #include "../../include/odp_cls.h"
 
 /* odp_rt.c: a pktio was opened / is closing (its receive state) */
-int  odpg_rt_pktio_open(odp_pktio_t pktio, const char *name, const odp_pktio_param_t *param);
+int  odpg_rt_pktio_open(odp_pktio_t pktio, const char *name, odp_pool_t pool,
+			const odp_pktio_param_t *param);
 void odpg_rt_pktio_close(odp_pktio_t pktio);
+/* odp_rt.c: odp_pktin_queue_config's input queues (the event queue of
+ * SCHED / QUEUE mode); 0 or -1 (too many queues) */
+int  odpg_rt_pktin_config(odp_pktio_t pktio, uint32_t num_queues);
 
 /* odp_cls.c: odpg_pktio_recv_batch's host path, also writing the parse
  * result of every packet (meta may be NULL) */
 int odpg_cls_pktio_recv_meta(odp_pktio_t pktio, odpg_ctx_t *ctx, const uint8_t *frames,
 			     const odpg_desc_t *desc, uint32_t num, odpg_out_t *out,
 			     odpg_meta_t *meta);
-/* the pktio is started with the classifier enabled */
+/* the pktio is started (with the classifier enabled) */
+int odpg_cls_pktio_started(odp_pktio_t pktio);
 int odpg_cls_pktio_classifies(odp_pktio_t pktio);
+/* host-side counter changes the kernel does not see: a packet it counted
+ * that the runtime then discarded (CoS pool copy failed, loop.c's
+ * _odp_pktio_packet_to_pool branch), and transmits */
+void odpg_cls_pktio_count(odp_pktio_t pktio, int64_t in_packets, int64_t in_octets,
+			  uint64_t in_discards, uint64_t out_packets, uint64_t out_octets);
 
 #endif

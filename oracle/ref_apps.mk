@@ -9,17 +9,27 @@ REF     ?= /root/reference
 CC      ?= gcc
 OUT     := _ref
 LIB     := $(abspath ../odp_amd/lib)
-APPS    := $(if $(wildcard $(REF)/example/classifier/odp_classifier.c),$(OUT)/odp_classifier)
+HDRS    := ../include/odp_api.h ../include/odp/rt.h ../include/odp/helper/odph_api.h \
+	   ../include/odp_cls.h
+LINK    := -L$(LIB) -lodpg -Wl,-rpath,'$$ORIGIN/../../odp_amd/lib' -L/opt/rocm/lib \
+	   -Wl,-rpath,/opt/rocm/lib
+APPS    := $(if $(wildcard $(REF)/example/classifier/odp_classifier.c),$(OUT)/odp_classifier) \
+	   $(if $(wildcard $(REF)/test/performance/odp_bench_pktio_sp.c),$(OUT)/odp_bench_pktio_sp)
+# test/performance/odp_bench_pktio_sp.c with its two test/common sources
+BENCH_SP := $(REF)/test/performance/odp_bench_pktio_sp.c $(REF)/test/common/bench_common.c \
+	    $(REF)/test/common/export_results.c
 
 all: $(APPS)
 
-$(OUT)/odp_classifier: $(REF)/example/classifier/odp_classifier.c $(LIB)/libodpg.so \
-		../include/odp_api.h ../include/odp/rt.h ../include/odp/helper/odph_api.h ../include/odp_cls.h
+$(OUT)/odp_classifier: $(REF)/example/classifier/odp_classifier.c $(LIB)/libodpg.so $(HDRS)
 	@mkdir -p $(OUT)
-	$(CC) -std=gnu11 -O2 -Wall -I../include -o $@ $< -L$(LIB) -lodpg \
-	    -Wl,-rpath,'$$ORIGIN/../../odp_amd/lib' -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib
+	$(CC) -std=gnu11 -O2 -Wall -I../include -o $@ $< $(LINK)
+
+$(OUT)/odp_bench_pktio_sp: $(BENCH_SP) $(LIB)/libodpg.so $(HDRS)
+	@mkdir -p $(OUT)
+	$(CC) -std=gnu11 -O2 -Wall -I../include -I$(REF)/test/common -o $@ $(BENCH_SP) $(LINK)
 
 clean:
-	rm -rf $(OUT)/odp_classifier
+	rm -rf $(OUT)/odp_classifier $(OUT)/odp_bench_pktio_sp
 
 .PHONY: all clean

@@ -4,7 +4,11 @@ example/classifier source, compiled unmodified against these headers and
 linked to libodpg.so (oracle/ref_apps.mk), classifies
 example/classifier/udp64.pcap with the reference run script's rule and
 passes its own CI packet-count check (odp_classifier_run.sh:17-19,
-pktio_env: 100 packets to queue1, 100 to DefaultCos)."""
+pktio_env: 100 packets to queue1, 100 to DefaultCos); the reference's
+test/performance/odp_bench_pktio_sp.c (with test/common/bench_common.c and
+export_results.c) builds the same way and runs all its cases; and the loop
+device (tests/c/odp_rt_loop.c) sends packets back through the GPU
+classifier in DIRECT, SCHED and QUEUE input modes."""
 import ctypes as C
 import os
 import re
@@ -20,6 +24,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 REF_APP = os.path.join(ROOT, "oracle", "_ref", "odp_classifier")
 REF_SRC = "/root/reference/example/classifier/odp_classifier.c"
+REF_BENCH = os.path.join(ROOT, "oracle", "_ref", "odp_bench_pktio_sp")
+LOOP_TEST = os.path.join(HERE, "c", "odp_rt_loop")
 PROTO = re.compile(r"^[A-Za-z_][\w \*]*?\b((?:odph|odp)_\w+)\s*\(", re.M)
 
 
@@ -47,9 +53,64 @@ def test_runtime_symbols_exported():
 def test_reference_classifier_builds_unmodified():
     subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "-f", "ref_apps.mk"],
                    check=True, capture_output=True)
-    assert os.access(REF_APP, os.X_OK)
-    out = subprocess.run(["ldd", REF_APP], capture_output=True, text=True).stdout
-    assert "libodpg.so" in out
+    for app in (REF_APP, REF_BENCH):
+        assert os.access(app, os.X_OK), app
+        out = subprocess.run(["ldd", app], capture_output=True, text=True).stdout
+        assert "libodpg.so" in out, app
+
+
+def test_loop_test_program_builds():
+    subprocess.run(["make", "-C", os.path.join(HERE, "c")], check=True, capture_output=True)
+    assert os.access(LOOP_TEST, os.X_OK)
+
+
+def test_pktio_lookup_modes_and_capabilities():
+    """No GPU needed: name rules and the mode checks of the queue accessors
+    (odp_packet_io.c:406-410, 798-829, 2364-2503)."""
+    from odp_amd import cls
+    lib = C.CDLL(L.LIB_PATH)
+    cls.reset()
+
+    class PktioParam(C.Structure):
+        _fields_ = [("in_mode", C.c_int), ("out_mode", C.c_int), ("rest", C.c_uint8 * 64)]
+    lib.odp_pktio_open.restype = C.c_void_p
+    lib.odp_pktio_lookup.restype = C.c_void_p
+    pp = PktioParam()
+    lib.odp_pktio_param_init(C.byref(pp))
+    assert (pp.in_mode, pp.out_mode) == (0, 0)            # DIRECT / DIRECT
+    a = lib.odp_pktio_open(b"loop", None, C.byref(pp))
+    assert a
+    assert not lib.odp_pktio_open(b"loop", None, C.byref(pp))     # already opened
+    assert lib.odp_pktio_lookup(b"loop") == a and not lib.odp_pktio_lookup(b"loop3")
+    pp.in_mode, pp.out_mode = 2, 1                        # SCHED / QUEUE
+    b = lib.odp_pktio_open(b"loop3", None, C.byref(pp))
+    assert b and lib.odp_pktio_lookup(b"loop3") == b
+    for h in (a, b):
+        assert lib.odp_pktin_queue_config(C.c_void_p(h), None) == 0
+        assert lib.odp_pktout_queue_config(C.c_void_p(h), None) == 0
+    qs = (C.c_void_p * 4)()
+    pq = (C.c_uint64 * 8)()
+    assert lib.odp_pktin_queue(C.c_void_p(a), pq, 4) == 1
+    assert lib.odp_pktin_event_queue(C.c_void_p(a), qs, 4) == -1
+    assert lib.odp_pktout_queue(C.c_void_p(a), pq, 4) == 1
+    assert lib.odp_pktout_event_queue(C.c_void_p(a), qs, 4) == -1
+    assert lib.odp_pktin_queue(C.c_void_p(b), pq, 4) == -1
+    assert lib.odp_pktin_event_queue(C.c_void_p(b), qs, 4) == 1 and qs[0]
+    assert lib.odp_pktout_queue(C.c_void_p(b), pq, 4) == -1
+    assert lib.odp_pktout_event_queue(C.c_void_p(b), qs, 4) == 1 and qs[0]
+    # one input / output queue per pktio: more is refused
+    pq2 = (C.c_uint8 * 512)()
+    lib.odp_pktout_queue_param_init(pq2)
+    struct.pack_into("<I", pq2, 4, 2)                     # num_queues (after op_mode)
+    assert lib.odp_pktout_queue_config(C.c_void_p(a), pq2) == -1
+    assert lib.odp_pktio_close(C.c_void_p(a)) == 0 and lib.odp_pktio_close(C.c_void_p(b)) == 0
+    assert not lib.odp_pktio_lookup(b"loop")
+    # capabilities the reference bench sizes itself by
+    pc = (C.c_uint32 * 64)()
+    assert lib.odp_pool_capability(pc) == 0 and pc[0] > 0
+    sc = (C.c_uint32 * 9)()
+    assert lib.odp_schedule_capability(sc) == 0 and sc[3] > 1000    # max_queues
+    cls.reset()
 
 
 def test_host_side_runtime_pieces():
@@ -87,6 +148,26 @@ def test_host_side_runtime_pieces():
     lib.odp_packet_free(C.c_void_p(b))
     assert lib.odp_queue_destroy(C.c_void_p(q)) == 0
     assert lib.odp_pool_destroy(C.c_void_p(pool)) == 0
+
+
+@pytest.mark.gpu
+def test_loop_device_through_gpu_classifier():
+    assert os.access(LOOP_TEST, os.X_OK), "make -C tests/c (built by __graft_entry__.build)"
+    r = subprocess.run(["timeout", "-k", "10", "100", LOOP_TEST], capture_output=True, text=True)
+    assert r.returncode == 0 and "PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-2000:])
+    assert "A direct: received 300" in r.stdout and "C queue: 300 packets" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_BENCH), reason="reference bench not built here")
+def test_reference_bench_pktio_sp_runs_every_case():
+    r = subprocess.run(["timeout", "-k", "10", "100", REF_BENCH, "-r", "20"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-2000:])
+    cases = re.findall(r"^\[(\d\d)\] (\w+)(.*)$", r.stdout, re.M)
+    assert [int(c[0]) for c in cases] == list(range(1, 11)), r.stdout[-3000:]
+    assert not [c for c in cases if "n/a" in c[2]], r.stdout[-3000:]   # cls_pmr_create ran
+    assert "odp_cls_pmr_create()" in r.stdout and "odp_pktin_queue_stats()" in r.stdout
 
 
 def write_pcap(path, frames):
