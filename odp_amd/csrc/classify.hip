@@ -607,10 +607,12 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 		const uint64_t pm = __ballot(ret == PARSE_PEND);
 
 		if (pm) {
-#ifdef ODPG_COOP_TAIL   /* experiment builds only: the per-frame wave passes */
+#if defined(ODPG_COOP_TAIL)   /* experiment builds only: the per-frame wave passes */
 			const uint32_t tail = coop_tail_sums(pm, g, pd);
-#else
+#elif defined(ODPG_SEG_V1)    /* experiment builds only: per-frame pass loops */
 			const uint32_t tail = seg_tail_sums(pm, g, pd);
+#else
+			const uint32_t tail = seg_tail_sums2(pm, g, pd);
 #endif
 
 			if (ret == PARSE_PEND)

@@ -810,6 +810,102 @@ __device__ __forceinline__ uint32_t seg_tail_sums(uint64_t m, const uint8_t *g, 
 	return mine ? oc_fold(acc) : 0u;
 }
 
+/* lane `src`'s value of v (ds_bpermute; every lane active) */
+__device__ __forceinline__ uint32_t lane_pull(uint32_t v, uint32_t src)
+{
+	return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+
+/* seg_tail_sums with the per-pass bookkeeping done lane-parallel (round 2,
+ * second form): the owner of a lane's chunk is found by a binary search of
+ * the inclusive chunk counts over the lanes that can own a chunk of this
+ * pass (ds_bpermute per step: log2 of that lane range, 2-4 steps for IMIX),
+ * the owner's chunk base address and bounds are pulled in four more
+ * bpermutes, and each frame pulls its share of the pass from two lanes of
+ * the pass's prefix sum. No per-frame loops: the pass costs the same
+ * whatever number of frames it touches. Same result as seg_tail_sums. */
+__device__ __forceinline__ uint32_t seg_tail_sums2(uint64_t m, const uint8_t *g, const L4Pend &pd)
+{
+#ifdef ODPG_EXP_NOTAIL
+	return 0u;
+#endif
+	const uint32_t lane = __lane_id();
+	const bool mine = ((m >> lane) & 1ull) && pd.b > pd.a;
+	const uint32_t c0 = pd.a & ~15u;
+	const uint32_t n = mine ? ((pd.b - 1u - c0) >> 4) + 1u : 0u;   /* chunks */
+	const uint32_t incl = wave_scan_u32(n);
+	const uint32_t first = incl - n;                                /* first slot */
+	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+	/* the address of slot s of this lane's frame is cb + 16 s */
+	const uint64_t cb = (uint64_t)(uintptr_t)g + c0 - 16ull * first;
+	const uint32_t cb_lo = (uint32_t)cb, cb_hi = (uint32_t)(cb >> 32);
+	const uint32_t pk = (incl & 0xffffffu) | ((pd.a & 15u) << 24) | (((pd.b - 1u) & 15u) << 28);
+	uint32_t acc = 0u;
+
+	for (uint32_t b0 = 0; b0 < total; b0 += 64u * SEG_BATCH) {   /* uniform */
+		uint4 q[SEG_BATCH];
+		uint32_t lead[SEG_BATCH], rem[SEG_BATCH];
+
+#pragma unroll
+		for (int k = 0; k < SEG_BATCH; ++k) {
+			const uint32_t base = b0 + 64u * (uint32_t)k;
+			const uint32_t slot = base + lane;
+			const bool valid = slot < total;
+			/* owners of this pass's chunks lie in lanes [lo, hi] (uniform) */
+			const uint64_t past = __ballot(incl > base);
+			const uint64_t beyond = __ballot(incl > base + 63u);
+			const uint32_t lo = past ? (uint32_t)__builtin_ctzll(past) : 63u;
+			const uint32_t hi = beyond ? (uint32_t)__builtin_ctzll(beyond) : 63u;
+			const uint32_t span = hi > lo ? hi - lo : 0u;
+			int p = -1;        /* lanes lo .. lo + p hold incl <= slot */
+
+			for (uint32_t step = span ? 1u << (31 - __builtin_clz(span)) : 0u; step;
+			     step >>= 1) {                                  /* uniform */
+				const uint32_t cand = (uint32_t)(p + (int)step);
+				const uint32_t src = lo + cand < 64u ? lo + cand : 63u;
+				const uint32_t v = lane_pull(incl, src);
+
+				if (cand <= span && v <= slot)
+					p = (int)cand;
+			}
+			const uint32_t own = lo + (uint32_t)(p + 1);
+			const uint32_t olo = lane_pull(cb_lo, own), ohi = lane_pull(cb_hi, own);
+			const uint32_t opk = lane_pull(pk, own), ofirst = lane_pull(first, own);
+
+			q[k] = make_uint4(0u, 0u, 0u, 0u);
+			lead[k] = slot == ofirst ? (opk >> 24) & 15u : 0u;
+			rem[k] = !valid ? 0u : slot + 1u == (opk & 0xffffffu) ? (opk >> 28) + 1u : 16u;
+			if (valid)
+				q[k] = *(const uint4 *)(uintptr_t)((((uint64_t)ohi << 32) | olo) +
+								   16ull * slot);
+		}
+#pragma unroll
+		for (int k = 0; k < SEG_BATCH; ++k) {
+			const uint32_t base = b0 + 64u * (uint32_t)k;
+
+			if (base >= total)                                  /* uniform */
+				break;
+			const int le = (int)lead[k], re = (int)rem[k];
+			uint32_t acc4 = 0u;
+
+			acc4 = tail_dot2(q[k].x & byte_mask(re) & ~byte_mask(le), acc4);
+			acc4 = tail_dot2(q[k].y & byte_mask(re - 4) & ~byte_mask(le - 4), acc4);
+			acc4 = tail_dot2(q[k].z & byte_mask(re - 8) & ~byte_mask(le - 8), acc4);
+			acc4 = tail_dot2(q[k].w & byte_mask(re - 12) & ~byte_mask(le - 12), acc4);
+			const uint32_t ps = wave_scan_u32(oc_fold(acc4));
+			/* this lane's frame: its chunks of the pass are lanes [fl, ll] */
+			const bool in = n && incl > base && first < base + 64u;
+			const uint32_t fl = in && first > base ? first - base : 0u;
+			const uint32_t ll = in ? (incl - 1u < base + 63u ? incl - 1u - base : 63u) : 0u;
+			const uint32_t hv = lane_pull(ps, ll);
+			const uint32_t lv = lane_pull(ps, fl ? fl - 1u : 0u);
+
+			acc += in ? hv - (fl ? lv : 0u) : 0u;
+		}
+	}
+	return mine ? oc_fold(acc) : 0u;
+}
+
 /* ---- register fast path: plain 64-byte Eth/IPv4/UDP|TCP frames ----------
  * Frames whose generic parse takes the straight path (no SNAP / VLAN, IPv4
  * IHL 5, UDP length >= 8 or TCP header >= 20 B) are parsed from the 16
