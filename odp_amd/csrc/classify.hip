@@ -611,8 +611,10 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 			const uint32_t tail = coop_tail_sums(pm, g, pd);
 #elif defined(ODPG_SEG_V1)    /* experiment builds only: per-frame pass loops */
 			const uint32_t tail = seg_tail_sums(pm, g, pd);
-#else
+#elif defined(ODPG_SEG_V2)    /* experiment builds only: 16-byte units */
 			const uint32_t tail = seg_tail_sums2(pm, g, pd);
+#else
+			const uint32_t tail = seg_tail_sums3(pm, g, pd);
 #endif
 
 			if (ret == PARSE_PEND)

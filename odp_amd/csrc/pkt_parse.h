@@ -906,6 +906,121 @@ __device__ __forceinline__ uint32_t seg_tail_sums2(uint64_t m, const uint8_t *g,
 	return mine ? oc_fold(acc) : 0u;
 }
 
+/* bytes [0, n) of a little-endian word, n clamped to [0, 4] */
+__device__ __forceinline__ uint32_t keep_below(int n)
+{
+	const int c = n < 0 ? 0 : n > 4 ? 4 : n;
+
+	return c >= 4 ? ~0u : ~(~0u << (8 * c));
+}
+
+/* seg_tail_sums2 over 64-byte units (third form, the default): a lane
+ * loads and sums 64 contiguous bytes of one tail per pass (4 x 16 B), so the
+ * per-pass bookkeeping — owner search, owner fields, the pass prefix sum
+ * and the per-frame shares — is paid once per 64 bytes instead of once per
+ * 16, and the next pass's owners are found while this pass's loads are in
+ * flight. A unit's bytes outside [a, b) are masked per word. Same result as
+ * seg_tail_sums. */
+__device__ __forceinline__ uint32_t seg_tail_sums3(uint64_t m, const uint8_t *g, const L4Pend &pd)
+{
+#ifdef ODPG_EXP_NOTAIL
+	return 0u;
+#endif
+	const uint32_t lane = __lane_id();
+	const bool mine = ((m >> lane) & 1ull) && pd.b > pd.a;
+	const uint32_t c0 = pd.a & ~15u;
+	const uint32_t n = mine ? ((pd.b - 1u - c0) >> 6) + 1u : 0u;   /* 64-byte units */
+	const uint32_t incl = wave_scan_u32(n);
+	const uint32_t first = incl - n;                                /* first unit slot */
+	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+	/* unit slot s of this lane's frame starts at cb + 64 s */
+	const uint64_t cb = (uint64_t)(uintptr_t)g + c0 - 64ull * first;
+	const uint32_t cb_lo = (uint32_t)cb, cb_hi = (uint32_t)(cb >> 32);
+	/* inclusive end slot | bytes to drop at the start | bytes of the last unit - 1 */
+	const uint32_t pk = (incl & 0xfffffu) | ((pd.a & 15u) << 20) | (((pd.b - 1u - c0) & 63u) << 24);
+	uint32_t acc = 0u;
+
+	/* the owner of slot base + lane: a binary search of incl over the lanes
+	 * that can own a unit of the pass, then its fields */
+	auto owner = [&](uint32_t base, uint32_t &olo, uint32_t &ohi, uint32_t &opk,
+			 uint32_t &ofirst) {
+		const uint32_t slot = base + lane;
+		const uint64_t past = __ballot(incl > base);
+		const uint64_t beyond = __ballot(incl > base + 63u);
+		const uint32_t lo = past ? (uint32_t)__builtin_ctzll(past) : 63u;
+		const uint32_t hi = beyond ? (uint32_t)__builtin_ctzll(beyond) : 63u;
+		const uint32_t span = hi > lo ? hi - lo : 0u;
+		int p = -1;
+
+		for (uint32_t step = span ? 1u << (31 - __builtin_clz(span)) : 0u; step;
+		     step >>= 1) {                                     /* uniform */
+			const uint32_t cand = (uint32_t)(p + (int)step);
+			const uint32_t src = lo + cand < 64u ? lo + cand : 63u;
+			const uint32_t v = lane_pull(incl, src);
+
+			if (cand <= span && v <= slot)
+				p = (int)cand;
+		}
+		const uint32_t own = lo + (uint32_t)(p + 1);
+
+		olo = lane_pull(cb_lo, own);
+		ohi = lane_pull(cb_hi, own);
+		opk = lane_pull(pk, own);
+		ofirst = lane_pull(first, own);
+	};
+	uint32_t olo, ohi, opk, ofirst;
+
+	if (total)                                                     /* uniform */
+		owner(0u, olo, ohi, opk, ofirst);
+	for (uint32_t base = 0; base < total; base += 64u) {            /* uniform */
+		const uint32_t slot = base + lane;
+		const bool valid = slot < total;
+		const int le = slot == ofirst ? (int)((opk >> 20) & 15u) : 0;
+		const int re = !valid ? 0 : slot + 1u == (opk & 0xfffffu) ? (int)(opk >> 24) + 1 : 64;
+		uint4 q[4];
+
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			q[k] = make_uint4(0u, 0u, 0u, 0u);
+		if (valid) {
+			const uint4 *src = (const uint4 *)(uintptr_t)((((uint64_t)ohi << 32) | olo) +
+								     64ull * slot);
+#pragma unroll
+			for (int k = 0; k < 4; ++k)
+				q[k] = src[k];
+		}
+		/* the next pass's owners while the loads are in flight */
+		if (base + 64u < total)                                 /* uniform */
+			owner(base + 64u, olo, ohi, opk, ofirst);
+		uint32_t acc4 = 0u;
+
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			const uint32_t w[4] = { q[k].x, q[k].y, q[k].z, q[k].w };
+
+#pragma unroll
+			for (int j = 0; j < 4; ++j) {
+				const int o = 16 * k + 4 * j;
+				uint32_t msk = keep_below(re - o);
+
+				if (k == 0)
+					msk &= ~keep_below(le - o);
+				acc4 = tail_dot2(w[j] & msk, acc4);
+			}
+		}
+		const uint32_t ps = wave_scan_u32(oc_fold(acc4));
+		/* this lane's frame: its units of the pass are lanes [fl, ll] */
+		const bool in = n && incl > base && first < base + 64u;
+		const uint32_t fl = in && first > base ? first - base : 0u;
+		const uint32_t ll = in ? (incl - 1u < base + 63u ? incl - 1u - base : 63u) : 0u;
+		const uint32_t hv = lane_pull(ps, ll);
+		const uint32_t lv = lane_pull(ps, fl ? fl - 1u : 0u);
+
+		acc += in ? hv - (fl ? lv : 0u) : 0u;
+	}
+	return mine ? oc_fold(acc) : 0u;
+}
+
 /* ---- register fast path: plain 64-byte Eth/IPv4/UDP|TCP frames ----------
  * Frames whose generic parse takes the straight path (no SNAP / VLAN, IPv4
  * IHL 5, UDP length >= 8 or TCP header >= 20 B) are parsed from the 16
