@@ -332,6 +332,9 @@ template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST, bool LEAN>
 #ifndef GEN_WAVES
 #define GEN_WAVES 6
 #endif
+#ifndef ODPG_TAIL_DEFER
+#define ODPG_TAIL_DEFER 1
+#endif
 __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) void odpg_classify_kernel(
 	const uint8_t *__restrict__ frames, const odpg_desc_t *__restrict__ desc,
 	uint32_t stride, uint32_t num, uint64_t opt, uint32_t layer, uint32_t classify,
@@ -601,9 +604,17 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 		else
 			ret = parse_common(p, v, layer, opt);
 	}
-	if constexpr (GF) {
-		/* long UDP / TCP frames: tails summed by the whole wave (all 64
-		 * lanes active here, as the cooperative loads and DPP need) */
+	/* long UDP / TCP frames: tails summed by the whole wave (all 64 lanes
+	 * active, as the cooperative loads and DPP need). Odd waves sum them
+	 * after the CoS walk instead of before it: the walk does not depend on
+	 * the L4 checksum (a frame it fails is re-pointed to the error CoS
+	 * afterwards, as cls_select_cos would have done), and with half the
+	 * waves in each order the memory-bound tail passes of some waves run
+	 * while others issue their walks. Launches that count per-CoS packets
+	 * keep the original order (the walk counts the CoSes it visits). */
+	const bool defer = GF && ODPG_TAIL_DEFER && !do_cos_stats &&
+			   (((blockIdx.x * (BLOCK / 64u)) + (tid >> 6)) & 1u);
+	auto run_tails = [&]() {
 		const uint64_t pm = __ballot(ret == PARSE_PEND);
 
 		if (pm) {
@@ -613,13 +624,20 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 			const uint32_t tail = seg_tail_sums(pm, g, pd);
 #elif defined(ODPG_SEG_V2)    /* experiment builds only: 16-byte units */
 			const uint32_t tail = seg_tail_sums2(pm, g, pd);
-#else
+#elif defined(ODPG_SEG_V3)    /* experiment builds only: masked shared units */
 			const uint32_t tail = seg_tail_sums3(pm, g, pd);
+#else
+			const uint32_t tail = seg_tail_sums4(pm, g, pd);
 #endif
 
 			if (ret == PARSE_PEND)
 				ret = finish_l4(p, pd, tail, opt);
 		}
+	};
+
+	if constexpr (GF) {
+		if (!defer)
+			run_tails();
 	}
 
 	/* ---- 3. CoS walk ------------------------------------------------- */
@@ -627,7 +645,7 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 	int cret = 0;
 	bool any_match = false;
 	uint32_t mark = 0u;
-	const bool want_cls = live && layer && classify && ret >= 0;
+	bool want_cls = live && layer && classify && ret >= 0;
 	bool active = false;
 	uint32_t steps = 0;
 
@@ -1076,6 +1094,20 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 				} else {
 					active = false;
 				}
+			}
+		}
+	}
+
+	if constexpr (GF) {
+		if (defer) {
+			run_tails();
+			if (ret < 0) {
+				want_cls = false;           /* pktin drop option */
+			} else if (want_cls && (p.fl & FL_ERROR_MASK)) {
+				/* cls_select_cos's error branch (no PMR walk) */
+				cos = error_cos < 0 ? ODPG_COS_NONE : (uint32_t)error_cos;
+				any_match = false;
+				mark = 0u;
 			}
 		}
 	}

@@ -1021,6 +1021,144 @@ __device__ __forceinline__ uint32_t seg_tail_sums3(uint64_t m, const uint8_t *g,
 	return mine ? oc_fold(acc) : 0u;
 }
 
+/* 16-byte load through a global (address space 1) pointer: an address
+ * rebuilt from integers would otherwise become a flat load, which also counts
+ * on lgkmcnt, so every LDS / bpermute wait after it would wait for the load */
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+
+__device__ __forceinline__ uint4 ld_g16(uint64_t addr)
+{
+	const u32x4 v = *(g_u32x4 *)(uintptr_t)addr;
+
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+/* sum of bytes [lead, re) of the 64-byte unit at addr (16-byte aligned), as
+ * 16-bit halves (v_dot2), 0 <= lead < re <= 64. Only the 16-byte chunks
+ * holding bytes below re are read, so nothing past the aligned 16 bytes
+ * holding the frame's last byte is touched. */
+__device__ __forceinline__ uint32_t unit_sum_masked(uint64_t addr, int lead, int re)
+{
+	uint32_t acc = 0u;
+
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		uint4 q = make_uint4(0u, 0u, 0u, 0u);
+
+		if (16 * k < re)
+			q = ld_g16(addr + 16u * k);
+		const uint32_t w[4] = { q.x, q.y, q.z, q.w };
+
+#pragma unroll
+		for (int j = 0; j < 4; ++j) {
+			const int o = 16 * k + 4 * j;
+
+			acc = tail_dot2(w[j] & keep_below(re - o) & ~keep_below(lead - o), acc);
+		}
+	}
+	return acc;
+}
+
+/* Tail sums, fourth form (the default): each tail [a, b) is cut into 64-byte
+ * units from c0 = a & ~15. The units that need byte masks — the frame's last
+ * one, and its first one when a is not 16-aligned — are summed by the lane
+ * itself, once per frame; every other unit is a whole 64 bytes inside the
+ * tail, and those are spread over the wave as in seg_tail_sums3 but need no
+ * masks, no per-unit bounds and only the owner's base address (two
+ * bpermutes). All loads go through global pointers. Same result as
+ * seg_tail_sums. */
+__device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g, const L4Pend &pd)
+{
+#ifdef ODPG_EXP_NOTAIL
+	return 0u;
+#endif
+	const uint32_t lane = __lane_id();
+	const bool mine = ((m >> lane) & 1ull) && pd.b > pd.a;
+	const uint32_t c0 = pd.a & ~15u;
+	const uint32_t lead = pd.a & 15u;
+	const uint32_t nu = mine ? ((pd.b - 1u - c0) >> 6) + 1u : 0u;   /* 64-byte units */
+	const bool own_first = mine && lead != 0u && nu >= 2u;
+	const uint32_t f0 = own_first ? 1u : 0u;                        /* first shared unit */
+	const uint32_t ni = mine ? nu - 1u - f0 : 0u;                   /* shared units */
+	const uint64_t gb = (uint64_t)(uintptr_t)g + c0;
+	uint32_t own = 0u;
+
+	/* the lane's own units: last (masked to b, and to a when it is the
+	 * first), then the first when it carries a lead */
+	if (mine) {
+		const uint32_t lu = nu - 1u;
+
+		own = unit_sum_masked(gb + 64ull * lu, lu ? 0 : (int)lead,
+				      (int)(pd.b - c0 - 64u * lu));
+		if (own_first)
+			own = oc_add(own, unit_sum_masked(gb, (int)lead, 64));
+	}
+
+	const uint32_t incl = wave_scan_u32(ni);
+	const uint32_t first = incl - ni;                               /* first shared slot */
+	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+	/* shared slot s of this lane's frame starts at cb + 64 s */
+	const uint64_t cb = gb + 64ull * f0 - 64ull * first;
+	const uint32_t cb_lo = (uint32_t)cb, cb_hi = (uint32_t)(cb >> 32);
+	uint32_t acc = 0u;
+
+	/* base address of the owner of slot min(base + lane, total - 1): binary
+	 * search of incl over the lanes that can own a slot of the pass */
+	auto owner = [&](uint32_t base) -> uint64_t {
+		const uint32_t slot = min(base + lane, total - 1u);
+		const uint64_t past = __ballot(incl > base);
+		const uint64_t beyond = __ballot(incl > base + 63u);
+		const uint32_t lo = past ? (uint32_t)__builtin_ctzll(past) : 63u;
+		const uint32_t hi = beyond ? (uint32_t)__builtin_ctzll(beyond) : 63u;
+		const uint32_t span = hi > lo ? hi - lo : 0u;
+		int p = -1;
+
+		for (uint32_t step = span ? 1u << (31 - __builtin_clz(span)) : 0u; step;
+		     step >>= 1) {                                         /* uniform */
+			const uint32_t cand = (uint32_t)(p + (int)step);
+			const uint32_t src = lo + cand < 64u ? lo + cand : 63u;
+			const uint32_t v = lane_pull(incl, src);
+
+			if (cand <= span && v <= slot)
+				p = (int)cand;
+		}
+		const uint32_t o = lo + (uint32_t)(p + 1);
+
+		return (((uint64_t)lane_pull(cb_hi, o) << 32) | lane_pull(cb_lo, o)) + 64ull * slot;
+	};
+	uint64_t addr = total ? owner(0u) : 0ull;
+
+	for (uint32_t base = 0; base < total; base += 64u) {            /* uniform */
+		uint4 q[4];
+
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			q[k] = ld_g16(addr + 16u * k);
+		/* the next pass's owners while the loads are in flight */
+		if (base + 64u < total)                                 /* uniform */
+			addr = owner(base + 64u);
+		uint32_t s = 0u;
+
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			s = tail_dot2(q[k].x, s);
+			s = tail_dot2(q[k].y, s);
+			s = tail_dot2(q[k].z, s);
+			s = tail_dot2(q[k].w, s);
+		}
+		const uint32_t ps = wave_scan_u32(base + lane < total ? oc_fold(s) : 0u);
+		/* this lane's frame: its slots of the pass are lanes [fl, ll] */
+		const bool in = ni && incl > base && first < base + 64u;
+		const uint32_t fl = in && first > base ? first - base : 0u;
+		const uint32_t ll = in ? (incl - 1u < base + 63u ? incl - 1u - base : 63u) : 0u;
+		const uint32_t hv = lane_pull(ps, ll);
+		const uint32_t lv = lane_pull(ps, fl ? fl - 1u : 0u);
+
+		acc += in ? hv - (fl ? lv : 0u) : 0u;
+	}
+	return mine ? oc_fold(oc_add(oc_fold(acc), oc_fold(own))) : 0u;
+}
+
 /* ---- register fast path: plain 64-byte Eth/IPv4/UDP|TCP frames ----------
  * Frames whose generic parse takes the straight path (no SNAP / VLAN, IPv4
  * IHL 5, UDP length >= 8 or TCP header >= 20 B) are parsed from the 16

@@ -27,6 +27,13 @@ def both(ctx, rules, buf, num, stride=0, desc=None, opt=0, layer=L.LAYER_ALL, cl
         ctx.set_kernel_mode(mode)
         res[mode] = ctx.classify(tbl, buf, num, stride=stride, desc=desc, opt=opt,
                                  layer=layer, classify=classify)
+    # verdicts, marks and metadata without counters: in such launches the
+    # general kernel's odd waves sum their checksum tails after the CoS walk
+    for mode in (3, 0):
+        ctx.set_kernel_mode(mode)
+        vo = ctx.classify(tbl, buf, num, stride=stride, desc=desc, opt=opt, layer=layer,
+                          classify=classify, want_stats=False)
+        assert_same(res[1], vo, f"no-counter launch, mode {mode}")
     ctx.set_kernel_mode(0)
     assert_same(res[1], res[2], "walk vs evaluate-all")
     assert_same(res[1], res[3], "walk vs hash walk")
@@ -349,6 +356,25 @@ def test_c3_imix_dag(gpu_ctx, fresh_cls, n):
     buf, desc = gen.c3_frames(n)
     g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), buf, n, desc=desc, opt=ALL_CHKSUM)
     assert_same(g, o, "c3")
+
+
+@pytest.mark.parametrize("drop", [L.PKTIN_DROP_UDP_ERR | L.PKTIN_DROP_TCP_ERR,
+                                  L.PKTIN_DROP_IPV4_ERR | L.PKTIN_DROP_UDP_ERR])
+def test_c3_drop_options(gpu_ctx, fresh_cls, drop):
+    """C3 traffic with pktin drop options: frames whose L4 checksum (summed
+    over the long tails) fails are dropped before classification, also when
+    the wave sums its tails after the CoS walk."""
+    opt = ALL_CHKSUM | drop
+    # the loop pktio's capability has no drop options (pktio/loop.c:650-670):
+    # they reach the kernel through the batch's pktin word only
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    gen.build_c3_rules(fresh_cls, p, stats=False)
+    assert fresh_cls.pktio_start(p) == 0
+    n = 40000
+    buf, desc = gen.c3_frames(n, seed=123)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), buf, n, desc=desc, opt=opt)
+    assert_same(g, o, f"c3 drop {drop:#x}")
+    assert np.any((o["out"] & 0xFFFF) == L.ODPG_COS_PDROP)
 
 
 def test_c3_host_path(gpu_ctx, fresh_cls):
