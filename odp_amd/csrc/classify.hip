@@ -723,23 +723,48 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 			uint32_t best = 0xffffffffu;
 			uint32_t xs = 0u, xn = 0u;
 
-			if (active && xkeys) {
-				const uint2 xe = xcos_l[cos];
+			if (xkeys) {
+				/* every key group, wave-uniform control flow: a group's
+				 * table is probed at exactly its longest displacement
+				 * (maxp, cls_compile) with no early exit, and the result
+				 * kept when the CoS has a rule in the group (gm). A key
+				 * that is in the table sits within maxp slots of its
+				 * home, so the result is the probe loop's. */
+				const uint2 xe = active ? xcos_l[cos] : make_uint2(0u, 0u);
 				const uint32_t gm = xe.y & gok;
+				const uint32_t ck = cos * 0x85EBCA6Bu;
 
 				xs = xe.x & 0xffffu;
 				xn = xe.x >> 16;
 #pragma unroll
 				for (uint32_t gi = 0; gi < XK; ++gi) {
-					if (gi < num_hgroups && ((gm >> gi) & 1u)) {
-						const uint4 g0 = *(const uint4 *)(hgroups + gi);
-						const uint2 g1 = *(const uint2 *)((const uint32_t *)(hgroups + gi) + 4);
-						const uint32_t lg = __builtin_amdgcn_readfirstlane(g0.w);
-						const uint32_t goff = __builtin_amdgcn_readfirstlane(g1.x);
-						const uint32_t h = walk_hash(kvx[gi], cos, lg);
+					if (gi >= num_hgroups)
+						break;
+					const uint4 g0 = *(const uint4 *)(hgroups + gi);
+					const uint4 g1 = *((const uint4 *)(hgroups + gi) + 1);
+					const uint32_t lg = __builtin_amdgcn_readfirstlane(g0.w);
+					const uint32_t goff = __builtin_amdgcn_readfirstlane(g1.x);
+					const uint32_t maxp = __builtin_amdgcn_readfirstlane(g1.z);
+					const uint32_t szm = (1u << lg) - 1u;
+					const uint32_t kv = kvx[gi];
+					const uint32_t h = ((kv ^ ck) * 0x9E3779B1u) >> (32u - lg);
+
+					if (hent_in_lds && maxp - 1u < XWALK_MAXP) {
+						uint32_t r = 0xffffffffu;
+
+#pragma unroll
+						for (uint32_t pr = 0; pr < XWALK_MAXP; ++pr) {
+							if (pr >= maxp)
+								break;
+							const uint2 e = hents_l[goff + ((h + pr) & szm)];
+
+							r = (e.x == kv && (e.y & 0xffffu) == cos) ? e.y >> 16 : r;
+						}
+						best = ((gm >> gi) & 1u) && r < best ? r : best;
+					} else if (active && ((gm >> gi) & 1u)) {
 						const uint32_t r = hent_in_lds
-							? probe(hents_l, goff, h, (1u << lg) - 1u, kvx[gi], cos)
-							: probe((const uint2 *)hents_g, goff, h, (1u << lg) - 1u, kvx[gi], cos);
+							? probe(hents_l, goff, h, szm, kv, cos)
+							: probe((const uint2 *)hents_g, goff, h, szm, kv, cos);
 
 						best = r < best ? r : best;
 					}

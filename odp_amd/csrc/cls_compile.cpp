@@ -633,13 +633,38 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			g.off = (uint32_t)wents.size();
 			g.count = (uint32_t)first.size();
 			wents.resize(wents.size() + (1u << lg), dwent_t{0u, HENT_EMPTY});
-			for (auto &f : first) {
-				uint32_t hsh = walk_hash(f.first.second, f.first.first, lg);
+			/* Robin Hood insertion (an entry displaced less than the one
+			 * being placed gives up its slot): the same probe-until-empty
+			 * lookup finds every key, and the longest displacement, which
+			 * the hybrid walk probes branch-free, stays short */
+			const uint32_t szm = (1u << lg) - 1u;
 
-				while (wents[g.off + hsh].cos_pmr != HENT_EMPTY)
-					hsh = (hsh + 1) & ((1u << lg) - 1);
-				wents[g.off + hsh].value = f.first.second;
-				wents[g.off + hsh].cos_pmr = f.first.first | (f.second << 16);
+			for (auto &f : first) {
+				dwent_t cur = {f.first.second, f.first.first | (f.second << 16)};
+				uint32_t hsh = walk_hash(cur.value, cur.cos_pmr & 0xffffu, lg);
+				uint32_t d = 0;
+
+				while (wents[g.off + hsh].cos_pmr != HENT_EMPTY) {
+					dwent_t &o = wents[g.off + hsh];
+					const uint32_t od = (hsh - walk_hash(o.value, o.cos_pmr & 0xffffu, lg)) & szm;
+
+					if (od < d) {
+						std::swap(cur, o);
+						d = od;
+					}
+					hsh = (hsh + 1) & szm;
+					d++;
+				}
+				wents[g.off + hsh] = cur;
+			}
+			for (uint32_t e = 0; e <= szm; e++) {
+				const dwent_t &o = wents[g.off + e];
+
+				if (o.cos_pmr != HENT_EMPTY) {
+					const uint32_t np = ((e - walk_hash(o.value, o.cos_pmr & 0xffffu, lg)) & szm) + 1;
+
+					g.maxp = np > g.maxp ? np : g.maxp;
+				}
 			}
 			wgroups.push_back(g);
 		}

@@ -157,7 +157,9 @@ typedef struct dhgroup_s {
 	uint32_t log2sz;
 	uint32_t off;       /* first dhent_t of this group */
 	uint32_t count;     /* real entries */
-	uint32_t pad[2];
+	uint32_t maxp;      /* CoS-keyed walk groups: longest probe sequence of
+			     * any entry (1 = every entry in its home slot) */
+	uint32_t pad;
 } dhgroup_t;            /* 32 bytes */
 
 typedef struct dhent_s {
@@ -179,6 +181,9 @@ typedef struct dwent_s {
 #define XWALK_MAX_GROUPS 32  /* hybrid walk: per-CoS group mask is one word */
 #ifndef XWALK_KEYS
 #define XWALK_KEYS 12        /* hybrid walk: group keys held in registers */
+#endif
+#ifndef XWALK_MAXP
+#define XWALK_MAXP 4         /* hybrid walk: groups probed branch-free up to this */
 #endif
 
 /* Mask groups (TBL_SIMPLE tables of <= 64 PMRs, the u64 hit-map kernel):

@@ -1067,6 +1067,9 @@ __device__ __forceinline__ uint32_t unit_sum_masked(uint64_t addr, int lead, int
  * masks, no per-unit bounds and only the owner's base address (two
  * bpermutes). All loads go through global pointers. Same result as
  * seg_tail_sums. */
+#ifndef SEG4_PIPE
+#define SEG4_PIPE 1
+#endif
 __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g, const L4Pend &pd)
 {
 #ifdef ODPG_EXP_NOTAIL
@@ -1126,17 +1129,9 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 
 		return (((uint64_t)lane_pull(cb_hi, o) << 32) | lane_pull(cb_lo, o)) + 64ull * slot;
 	};
-	uint64_t addr = total ? owner(0u) : 0ull;
-
-	for (uint32_t base = 0; base < total; base += 64u) {            /* uniform */
-		uint4 q[4];
-
-#pragma unroll
-		for (int k = 0; k < 4; ++k)
-			q[k] = ld_g16(addr + 16u * k);
-		/* the next pass's owners while the loads are in flight */
-		if (base + 64u < total)                                 /* uniform */
-			addr = owner(base + 64u);
+	/* a pass's sum: each lane's unit, then every frame's share of the pass
+	 * from the pass prefix sum (its slots of the pass are lanes [fl, ll]) */
+	auto consume = [&](const uint4 (&q)[4], uint32_t base) {
 		uint32_t s = 0u;
 
 #pragma unroll
@@ -1147,7 +1142,6 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 			s = tail_dot2(q[k].w, s);
 		}
 		const uint32_t ps = wave_scan_u32(base + lane < total ? oc_fold(s) : 0u);
-		/* this lane's frame: its slots of the pass are lanes [fl, ll] */
 		const bool in = ni && incl > base && first < base + 64u;
 		const uint32_t fl = in && first > base ? first - base : 0u;
 		const uint32_t ll = in ? (incl - 1u < base + 63u ? incl - 1u - base : 63u) : 0u;
@@ -1155,7 +1149,54 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 		const uint32_t lv = lane_pull(ps, fl ? fl - 1u : 0u);
 
 		acc += in ? hv - (fl ? lv : 0u) : 0u;
+	};
+	auto load = [&](uint4 (&q)[4], uint64_t a) {
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			q[k] = ld_g16(a + 16u * k);
+	};
+	uint64_t addr = total ? owner(0u) : 0ull;
+	uint4 qa[4], qb[4];
+
+#if SEG4_PIPE
+	/* two passes in flight (8 KiB per wave): pass p + 2's loads are issued
+	 * as soon as pass p is summed, and each pass's owners are found while
+	 * the loads before it are in flight */
+	if (total) {                                                   /* uniform */
+		load(qa, addr);
+		if (64u < total) {
+			addr = owner(64u);
+			load(qb, addr);
+			if (128u < total)
+				addr = owner(128u);
+		}
 	}
+	for (uint32_t base = 0; base < total; base += 128u) {           /* uniform */
+		consume(qa, base);
+		if (base + 128u < total) {
+			load(qa, addr);
+			if (base + 192u < total)
+				addr = owner(base + 192u);
+		}
+		if (base + 64u < total) {
+			consume(qb, base + 64u);
+			if (base + 192u < total) {
+				load(qb, addr);
+				if (base + 256u < total)
+					addr = owner(base + 256u);
+			}
+		}
+	}
+#else
+	for (uint32_t base = 0; base < total; base += 64u) {            /* uniform */
+		load(qa, addr);
+		/* the next pass's owners while the loads are in flight */
+		if (base + 64u < total)                                 /* uniform */
+			addr = owner(base + 64u);
+		consume(qa, base);
+	}
+	(void)qb;
+#endif
 	return mine ? oc_fold(oc_add(oc_fold(acc), oc_fold(own))) : 0u;
 }
 
