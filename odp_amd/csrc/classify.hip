@@ -740,6 +740,10 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 				for (uint32_t gi = 0; gi < XK; ++gi) {
 					if (gi >= num_hgroups)
 						break;
+					/* deep levels: few lanes still walking, most
+					 * groups hold no rule of their CoSes */
+					if (!__ballot((gm >> gi) & 1u))
+						continue;
 					const uint4 g0 = *(const uint4 *)(hgroups + gi);
 					const uint4 g1 = *((const uint4 *)(hgroups + gi) + 1);
 					const uint32_t lg = __builtin_amdgcn_readfirstlane(g0.w);
@@ -808,7 +812,11 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 				 * one PMR at a time across the wave (uniform index:
 				 * scalar term loads, as MODE 0) */
 				uint32_t xk = 0u;
+#ifdef ODPG_EXP_NOXLIST        /* experiment builds only: cost without complex rules */
+				bool xp = false;
+#else
 				bool xp = active && xn != 0u && xlist_l[xs].x < best;
+#endif
 
 				while (__ballot(xp)) {
 					if (xp) {
