@@ -295,9 +295,17 @@ __global__ __launch_bounds__(LB, L64_WAVES * 256 / LB) void odpg_cls64_kernel(co
 				mg[g] = load_mg(A.mgroups + g);
 		}
 	}
+	/* CM 2: the counter layout is read now, not behind the tile loop's
+	 * last wait; the workgroup's last wave to finish flushes the histogram */
+	__shared__ uint32_t waves_done;
+	odpg_cnt_dev C = {};
+
 	if constexpr (CM == 2) {
+		C = *A.cnt;
 		for (uint32_t k = threadIdx.x; k < A.num_cos + BIN_EXTRA; k += LB)
 			dlv[k] = 0u;
+		if (threadIdx.x == 0u)
+			waves_done = 0u;
 	}
 	__syncthreads();
 
@@ -747,30 +755,42 @@ __global__ __launch_bounds__(LB, L64_WAVES * 256 / LB) void odpg_cls64_kernel(co
 		if (A.num_cos != 12345u)
 			return;
 #endif
-		__syncthreads();
-		const odpg_cnt_dev C = *A.cnt;
+		/* no barrier: each wave counts itself done after its histogram
+		 * adds (LDS operations of a wave complete in order; the fence
+		 * makes that explicit) and the last of the workgroup's waves
+		 * flushes while the others have already exited */
+		__threadfence_block();
+		uint32_t prev = 0u;
+
+		if (lane == 0u)
+			prev = atomicAdd(&waves_done, 1u);
+		if ((uint32_t)__builtin_amdgcn_readfirstlane((int)prev) != LB / 64u - 1u)
+			return;
+		__threadfence_block();
 		unsigned long long *r = (unsigned long long *)(C.rows + (size_t)blockIdx.x * C.words);
 		const uint32_t nc = A.num_cos < C.ncos ? A.num_cos : C.ncos;
 		/* without hash queues each CoS owns one column; else its first */
 		auto col = [&](uint32_t c) { return 4u + C.ncos + (C.ident ? c : C.qcol[c]); };
+		uint32_t tot = 0u;
 
-		for (uint32_t k0 = 0; k0 < nc; k0 += LB) {
-			const uint32_t k = k0 + threadIdx.x;
+		for (uint32_t k0 = 0; k0 < nc; k0 += 64u) {
+			const uint32_t k = k0 + lane;
 			const uint32_t x = k < nc ? dlv[BIN_EXTRA + k] : 0u;
 
 			if (x)
 				atomicAdd(r + col(k), (unsigned long long)x);
-			const uint32_t t = wave_sum_u32(x);     /* in_packets, in_octets */
-
-			if (lane == 0u && t) {
-				atomicAdd(r + 0, (unsigned long long)t);
-				atomicAdd(r + 1, (unsigned long long)t * 64ull);
-			}
+			tot += x;
 		}
-		if (threadIdx.x == 0u) {
+		const uint32_t t = wave_sum_u32(tot);            /* in_packets, in_octets */
+
+		if (lane == 0u) {
 			const uint32_t ne = dlv[BIN_ERR], np = dlv[BIN_PDROP];
 			uint32_t nd = dlv[BIN_NOCOS];
 
+			if (t) {
+				atomicAdd(r + 0, (unsigned long long)t);
+				atomicAdd(r + 1, (unsigned long long)t * 64ull);
+			}
 			if (ne && A.err_cos < nc && A.err_act != 1u)
 				atomicAdd(r + col(A.err_cos), (unsigned long long)ne);
 			else if (A.err_cos >= nc)
