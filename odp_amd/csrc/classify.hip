@@ -394,7 +394,10 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 	const bool do_stats = pk_partial != nullptr || cnt.row != nullptr;
 	const bool do_cos_stats = cos_partial != nullptr || (cnt.row && cnt.cos);
 	uint32_t *row = smem + tid * RW;
-	uint64_t lane_pkt = 0, lane_oct = 0, lane_err = 0, lane_disc = 0;
+	/* loopback_recv counts: packets / errors / discards as wave-uniform
+	 * ballot counts (scalar registers), octets per lane */
+	uint32_t w_pkt = 0u, w_err = 0u, w_disc = 0u;
+	uint64_t lane_oct = 0;
 
 	/* persistent workgroups: tiles of BLOCK packets */
 	const uint32_t ntiles = (num + BLOCK - 1) / BLOCK;
@@ -1205,9 +1208,17 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 		 * counters, odp_classification_internal.h:64-78) */
 		if (cnt.row && cret == 0 && want_cls && cos < num_cos)
 			atomicAdd(&dlv[cnt.qcol[cos] + ((w >> 24) & 31u)], 1u);
-		pend_i = i;
-		pend_w = w;
-		pend_mk = mk;
+		if constexpr (FAST) {
+			pend_i = i;
+			pend_w = w;
+			pend_mk = mk;
+		} else {
+			/* no frame prefetch to keep ahead of: store now, and no
+			 * deferred-store registers live across the next tile */
+			out[i] = w;
+			if (mark_out)
+				mark_out[i] = (uint16_t)mk;
+		}
 		if (meta_out) {
 			odpg_meta_t m;
 
@@ -1226,12 +1237,12 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 	if (do_stats) {
 		const bool is_pkt = live && ret >= 0 && cret == 0 && !(p.fl & FL_ERROR_MASK);
 
-		lane_err += (live && layer && ret != 0) ? 1u : 0u;
-		lane_disc += (live && (cret == -1 || cret == -2)) ? 1u : 0u;
-		lane_pkt += is_pkt ? 1u : 0u;
+		w_err += (uint32_t)__popcll(__ballot(live && layer && ret != 0));
+		w_disc += (uint32_t)__popcll(__ballot(live && (cret == -1 || cret == -2)));
+		w_pkt += (uint32_t)__popcll(__ballot(is_pkt));
 		lane_oct += is_pkt ? (uint64_t)len : 0u;
 	}
-	pend = live;
+	pend = FAST && live;
 	if (COOP)
 		__syncthreads();          /* LDS rows are reused by the next tile */
 	}   /* tile loop */
@@ -1243,8 +1254,8 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 
 	/* ---- 6. per-workgroup counter partials ---------------------------- */
 	if (do_stats) {
-		uint64_t a = wave_sum_u64(lane_pkt), o = wave_sum_u64(lane_oct);
-		uint64_t e = wave_sum_u64(lane_err), d = wave_sum_u64(lane_disc);
+		uint64_t a = w_pkt, o = wave_sum_u64(lane_oct);
+		uint64_t e = w_err, d = w_disc;
 
 		if (sred && !cnt.row) {
 			/* pktio counters only: committed in-kernel (stats_commit.h) */
