@@ -335,6 +335,9 @@ template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST, bool LEAN>
 #ifndef ODPG_TAIL_DEFER
 #define ODPG_TAIL_DEFER 1
 #endif
+#ifndef ODPG_SWEEP
+#define ODPG_SWEEP 0
+#endif
 __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) void odpg_classify_kernel(
 	const uint8_t *__restrict__ frames, const odpg_desc_t *__restrict__ desc,
 	uint32_t stride, uint32_t num, uint64_t opt, uint32_t layer, uint32_t classify,
@@ -355,6 +358,12 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 	uint32_t num_xwords, const odpg_cnt_args cnt)
 {
 	constexpr uint32_t RW = W / 4 + 1;       /* odd dword row stride */
+	/* descriptor batches with the 64-byte window: one coalesced sweep of
+	 * every frame byte per tile (sweep_frames). Experiment build
+	 * (-DODPG_SWEEP=1): HBM reads at the algorithmic bytes (C3 1.04x vs
+	 * 1.27x) but 139 vs 126 us, as the walk no longer overlaps other
+	 * waves' tail passes */
+	constexpr bool SWEEP = GF && DESC && W == 64 && !FAST && !COOP && ODPG_SWEEP;
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 	/* u64 hit-map kernel: mask-group entries (16 B aligned, after the rows)
 	 * and the one-read-per-level resolve table */
@@ -496,6 +505,7 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 
 	uint32_t f[16];
 	bool wave_fast = false;
+	uint32_t sweep_sum = 0u;
 
 	if constexpr (FAST) {
 		/* 64-byte frames straight into 16 registers, 4 x 16 B per lane;
@@ -548,6 +558,11 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 			dst[2] = x.z;
 			dst[3] = x.w;
 		}
+	} else if (SWEEP) {
+		/* every byte of the wave's frames in one coalesced sweep: the
+		 * windows land in the LDS rows, the sums of bytes [64, len) in
+		 * sweep_sum (pkt_parse.h) */
+		sweep_sum = sweep_frames(g, len, smem + (tid & ~63u) * RW, RW);
 	} else {
 #pragma unroll
 		for (uint32_t part = 0; part < W / 16; ++part) {
@@ -615,12 +630,20 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 	 * waves in each order the memory-bound tail passes of some waves run
 	 * while others issue their walks. Launches that count per-CoS packets
 	 * keep the original order (the walk counts the CoSes it visits). */
-	const bool defer = GF && ODPG_TAIL_DEFER && !do_cos_stats &&
+	const bool defer = GF && !SWEEP && ODPG_TAIL_DEFER && !do_cos_stats &&
 			   (((blockIdx.x * (BLOCK / 64u)) + (tid >> 6)) & 1u);
 	auto run_tails = [&]() {
 		const uint64_t pm = __ballot(ret == PARSE_PEND);
 
-		if (pm) {
+		if (SWEEP && pm) {
+			/* the sweep summed [64, len); tails that start later (L4
+			 * header past the window) are summed again, rare */
+			const uint64_t late = __ballot(ret == PARSE_PEND && pd.a != (uint32_t)W);
+			const uint32_t t2 = late ? seg_tail_sums4(late, g, pd) : 0u;
+
+			if (ret == PARSE_PEND)
+				ret = finish_l4(p, pd, pd.a == (uint32_t)W ? sweep_sum : t2, opt);
+		} else if (pm) {
 #if defined(ODPG_COOP_TAIL)   /* experiment builds only: the per-frame wave passes */
 			const uint32_t tail = coop_tail_sums(pm, g, pd);
 #elif defined(ODPG_SEG_V1)    /* experiment builds only: per-frame pass loops */

@@ -1067,6 +1067,116 @@ __device__ __forceinline__ uint32_t unit_sum_masked(uint64_t addr, int lead, int
  * masks, no per-unit bounds and only the owner's base address (two
  * bpermutes). All loads go through global pointers. Same result as
  * seg_tail_sums. */
+/* One coalesced sweep over every byte of a wave's 64 frames (descriptor
+ * batches, 64-byte window): frame f's 64-byte units [0, len) are numbered
+ * across the wave frame after frame (a DPP prefix sum of the per-frame unit
+ * counts) and spread over the lanes, 64 units per pass, so a frame's window,
+ * its tail and the neighbouring frames' bytes are requested by neighbouring
+ * lanes of the same or the next load instruction: each 128-byte line is
+ * fetched once. A lane holding a frame's unit 0 writes it (zero past the
+ * frame) into that frame's LDS row, the window the parse reads; every other
+ * unit is masked to the frame and summed (v_dot2). Returns the lane's own
+ * frame's sum of bytes [64, len) as a one's-complement partial (residue and
+ * zero-ness kept). `rows` is the wave's first row, `rw` the row stride in
+ * dwords. All lanes must be active. */
+__device__ __forceinline__ uint32_t sweep_frames(const uint8_t *g, uint32_t len, uint32_t *rows,
+						 uint32_t rw)
+{
+	const uint32_t lane = __lane_id();
+	const uint32_t nu = len ? ((len - 1u) >> 6) + 1u : 0u;
+	const uint32_t incl = wave_scan_u32(nu);
+	const uint32_t first = incl - nu;
+	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+	/* unit slot s of this lane's frame starts at cb + 64 s */
+	const uint64_t cb = (uint64_t)(uintptr_t)g - 64ull * first;
+	const uint32_t cb_lo = (uint32_t)cb, cb_hi = (uint32_t)(cb >> 32);
+	uint32_t acc = 0u;
+
+	if (len == 0u) {                                  /* empty frame: zero window */
+#pragma unroll
+		for (int w = 0; w < 16; ++w)
+			rows[lane * rw + w] = 0u;
+	}
+	for (uint32_t base = 0; base < total; base += 64u) {            /* uniform */
+		const uint32_t slot = min(base + lane, total - 1u);
+		const bool valid = base + lane < total;
+		const uint64_t past = __ballot(incl > base);
+		const uint64_t beyond = __ballot(incl > base + 63u);
+		const uint32_t lo = past ? (uint32_t)__builtin_ctzll(past) : 63u;
+		const uint32_t hi = beyond ? (uint32_t)__builtin_ctzll(beyond) : 63u;
+		const uint32_t span = hi > lo ? hi - lo : 0u;
+		int p = -1;
+
+		for (uint32_t st = span ? 1u << (31 - __builtin_clz(span)) : 0u; st;
+		     st >>= 1) {                                       /* uniform */
+			const uint32_t cand = (uint32_t)(p + (int)st);
+			const uint32_t src = lo + cand < 64u ? lo + cand : 63u;
+			const uint32_t v = lane_pull(incl, src);
+
+			if (cand <= span && v <= slot)
+				p = (int)cand;
+		}
+		const uint32_t o = lo + (uint32_t)(p + 1);
+		const uint64_t a = (((uint64_t)lane_pull(cb_hi, o) << 32) | lane_pull(cb_lo, o)) +
+				   64ull * slot;
+		/* pulled with every lane active: a bpermute under a partial exec
+		 * mask reads inactive source lanes as 0 */
+		const uint32_t ofirst = lane_pull(first, o), olen = lane_pull(len, o);
+		const uint32_t u = slot - ofirst;
+		const int rem = valid ? (int)(olen - 64u * u) : 0;     /* >= 1 */
+		/* whole words below rem kept by a compare each; the one partial
+		 * word (rem not a multiple of 4) is read again as a dword (a cache
+		 * hit: its 16 bytes were just loaded) and masked */
+		const uint32_t nw = rem > 0 ? (uint32_t)rem >> 2 : 0u;
+		const uint32_t pb = (uint32_t)rem & 3u;
+		uint32_t pv = 0u;
+		uint32_t w[16];
+
+		if (rem > 0 && pb && nw < 16u)
+			pv = *(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)(a + 4u * nw) &
+			     ((1u << (8u * pb)) - 1u);
+#pragma unroll
+		for (int j = 0; j < 4; ++j) {
+			uint4 q = make_uint4(0u, 0u, 0u, 0u);
+
+			if (16 * j < rem)
+				q = ld_g16(a + 16u * j);
+			w[4 * j + 0] = 4 * j + 0 < (int)nw ? q.x : 0u;
+			w[4 * j + 1] = 4 * j + 1 < (int)nw ? q.y : 0u;
+			w[4 * j + 2] = 4 * j + 2 < (int)nw ? q.z : 0u;
+			w[4 * j + 3] = 4 * j + 3 < (int)nw ? q.w : 0u;
+		}
+		uint32_t sum = 0u;
+
+		if (valid && u == 0u) {
+			uint32_t *r = rows + o * rw;
+
+#pragma unroll
+			for (int k = 0; k < 16; ++k)
+				r[k] = w[k];
+			if (pb && nw < 16u)
+				r[nw] = pv;
+		} else {
+#pragma unroll
+			for (int k = 0; k < 16; ++k)
+				sum = tail_dot2(w[k], sum);
+			sum = tail_dot2(pv, sum);
+		}
+		/* this lane's frame: its units of the pass are lanes [fl, ll] */
+		const uint32_t ps = wave_scan_u32(oc_fold(sum));
+		const bool in = nu && incl > base && first < base + 64u;
+		const uint32_t fl = in && first > base ? first - base : 0u;
+		const uint32_t ll = in ? (incl - 1u < base + 63u ? incl - 1u - base : 63u) : 0u;
+		const uint32_t hv = lane_pull(ps, ll);
+		const uint32_t lv = lane_pull(ps, fl ? fl - 1u : 0u);
+
+		acc += in ? hv - (fl ? lv : 0u) : 0u;
+	}
+	/* the rows written by other lanes are read next by their own lanes */
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+	return oc_fold(acc);
+}
+
 #ifndef SEG4_PIPE
 #define SEG4_PIPE 1
 #endif
