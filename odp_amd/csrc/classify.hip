@@ -335,6 +335,10 @@ template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST, bool LEAN>
 #ifndef ODPG_TAIL_DEFER
 #define ODPG_TAIL_DEFER 1
 #endif
+#ifndef ODPG_DEFER_MOD          /* waves w with w % MOD < K sum tails after the walk */
+#define ODPG_DEFER_MOD 3
+#define ODPG_DEFER_K 1
+#endif
 #ifndef ODPG_SWEEP
 #define ODPG_SWEEP 0
 #endif
@@ -631,7 +635,8 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 	 * while others issue their walks. Launches that count per-CoS packets
 	 * keep the original order (the walk counts the CoSes it visits). */
 	const bool defer = GF && !SWEEP && ODPG_TAIL_DEFER && !do_cos_stats &&
-			   (((blockIdx.x * (BLOCK / 64u)) + (tid >> 6)) & 1u);
+			   (((blockIdx.x * (BLOCK / 64u)) + (tid >> 6)) % ODPG_DEFER_MOD) <
+				   ODPG_DEFER_K;
 	auto run_tails = [&]() {
 		const uint64_t pm = __ballot(ret == PARSE_PEND);
 
