@@ -553,7 +553,11 @@ def bench_l3fwd(args, world, rank, local, dist):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(args.config), "kernel_ms": round(kernel_ms, 5),
-                         "bytes_per_pkt": bytes_per_pkt, "pkts_per_launch": n},
+                         "bytes_per_pkt": bytes_per_pkt, "pkts_per_launch": n,
+                         "bytes_note": ("SURVEY.md 8(d) prices C5 at 196 B/pkt (frame + a "
+                                        "hash-table probe); the interval table replaces "
+                                        "the probe with an LDS search, so 64 B read + "
+                                        "32 B header rewrite + 4 B port = 100 B")},
             "cpu_baseline": cpu,
         }
         print(json.dumps(res), flush=True)
