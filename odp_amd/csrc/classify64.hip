@@ -39,8 +39,14 @@
 #include "cls_match.h"
 #include "stats_commit.h"
 
+/* waves per SIMD the launch bounds ask for: verdict-only and pktio-block
+ * launches at 8 (64 VGPRs, no spills), sharded-counter launches at 6 (their
+ * histogram flush spills more scalar registers at 8: 15.9 vs 15.3 us) */
 #ifndef L64_WAVES
-#define L64_WAVES 6
+#define L64_WAVES 8
+#endif
+#ifndef L64_WAVES_CNT
+#define L64_WAVES_CNT 6
 #endif
 #ifndef L64_BUF          /* frames / verdicts through range-checked buffer ops */
 #define L64_BUF 0
@@ -233,7 +239,8 @@ __device__ __forceinline__ MGd load_mg(const dmgroup_t *g, bool single = true)
  * group is a cuckoo group over a frame word (TBL_MG_CUCKOO): no per-group
  * kind tests in the tile loop. */
 template <int NG, bool HW, int CM, bool CK>
-__global__ __launch_bounds__(LB, L64_WAVES * 256 / LB) void odpg_cls64_kernel(const L64Args A)
+__global__ __launch_bounds__(LB, (CM == 2 ? L64_WAVES_CNT : L64_WAVES) * 256 / LB) void
+odpg_cls64_kernel(const L64Args A)
 {
 	static_assert(!HW || NG > 0, "walk groups are hoisted");
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
