@@ -48,6 +48,9 @@
 #ifndef L64_WAVES_CNT
 #define L64_WAVES_CNT 6
 #endif
+#ifndef L64_WAVES_HW     /* CoS-keyed cuckoo (walk-group) tables, e.g. C4 */
+#define L64_WAVES_HW 6
+#endif
 #ifndef L64_BUF          /* frames / verdicts through range-checked buffer ops */
 #define L64_BUF 0
 #endif
@@ -239,7 +242,7 @@ __device__ __forceinline__ MGd load_mg(const dmgroup_t *g, bool single = true)
  * group is a cuckoo group over a frame word (TBL_MG_CUCKOO): no per-group
  * kind tests in the tile loop. */
 template <int NG, bool HW, int CM, bool CK>
-__global__ __launch_bounds__(LB, (CM == 2 ? L64_WAVES_CNT : L64_WAVES) * 256 / LB) void
+__global__ __launch_bounds__(LB, (CM == 2 ? L64_WAVES_CNT : HW ? L64_WAVES_HW : L64_WAVES) * 256 / LB) void
 odpg_cls64_kernel(const L64Args A)
 {
 	static_assert(!HW || NG > 0, "walk groups are hoisted");
