@@ -12,6 +12,10 @@ sharded device counters odp_pktio_stats reads; it is reported as
 
 Launch:  python bench.py [--gpus N --steps K --warmup W --config c2]
          torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+`python bench.py --gpus N` with N > 1 and no launcher environment starts the
+N rank processes itself (a torch.distributed.run child process, before any
+GPU call) and exits with its status; under a launcher WORLD_SIZE must equal
+--gpus. n_gpus in the line is the process group's size.
 Packets are independent: each rank classifies its own shard (weak scaling,
 no data-path collective). Rank 0 compiles the rule table once and broadcasts
 the image (odpg_rules_compile / odpg_table_import); the only other collective
@@ -70,25 +74,61 @@ def parse_args():
     ap.add_argument("--backend", default=os.environ.get("ODPG_DIST_BACKEND", "nccl"),
                     choices=["nccl", "gloo"], help="torch.distributed backend for N > 1")
     ap.add_argument("--source", default="sharded", choices=["sharded", "gpu0"],
-                    help="gpu0: also time scatter-from-rank-0 + classify + gather-to-root")
+                    help="gpu0: also time scatter-from-rank-0 + classify + gather-to-root "
+                         "(initialises the process group even for one rank)")
+    ap.add_argument("--spawn-check", action="store_true",
+                    help="ranks print their rank / world size and exit before any GPU "
+                         "call (tests the launcher path on CPU)")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(args):
+    """--gpus N > 1 without a launcher: one rank process per GPU through a
+    torch.distributed.run child (never an exec of this process), rendezvous
+    on 127.0.0.1; returns the child's exit status."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
     args = parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
+    if args.spawn_check:
+        print(json.dumps({"rank": rank, "world": world}), flush=True)
+        return
     dist = None
-    if world > 1:
+    if world > 1 or args.source == "gpu0":
         import torch
         import torch.distributed as tdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            os.environ["MASTER_PORT"] = str(_free_port())
         ndev = torch.cuda.device_count()
         local = local % ndev if ndev else local     # ranks may share a GPU
         torch.cuda.set_device(local)
         tdist.init_process_group(args.backend, rank=rank, world_size=world)
         dist = tdist
+        world = tdist.get_world_size()
 
     import ctypes as C
 
@@ -280,6 +320,12 @@ def main():
             out["diag"] = args.diag
         if args.e2e:
             out["e2e_host_path"] = e2e(ctx, tbl, frames, desc, n, stride, opt)
+        if dist is not None:
+            out["distributed"] = {
+                "backend": args.backend, "world": world,
+                "collectives": ["broadcast (table image)", "all_reduce max (wall clock)",
+                                "all_reduce sum (counters)"]
+                + (["scatter (frames)", "gather (verdicts)"] if args.source == "gpu0" else [])}
     if args.source == "gpu0" and dist is not None and stride:
         sg = bench_scatter_gather(args, ctx, tbl, frames, n, stride, opt, world, rank, local,
                                   dist)

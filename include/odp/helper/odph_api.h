@@ -35,9 +35,24 @@ extern "C" {
 #define ODPH_ETHHDR_LEN    14
 #define ODPH_ETHTYPE_IPV4  0x0800
 #define ODPH_ETHTYPE_IPV6  0x86dd
+#define ODPH_ETHTYPE_ARP   0x0806
+#define ODPH_ETHTYPE_VLAN  0x8100
+#define ODPH_ETHTYPE_VLAN_OUTER 0x88A8
+#define ODPH_IPV4          4
 #define ODPH_IPV4HDR_LEN   20
+#define ODPH_IPV4HDR_IHL_MIN 5
+#define ODPH_IPV4ADDR_LEN  4
+#define ODPH_IPV4HDR_VER(ver_ihl) (((ver_ihl) & 0xf0) >> 4)
+#define ODPH_IPV4HDR_IHL(ver_ihl) ((ver_ihl) & 0x0f)
+#define ODPH_IPV4HDR_CSUM_OFFSET 10
+#define ODPH_IPV6          6
+#define ODPH_IPV6HDR_LEN   40
+#define ODPH_UDPHDR_LEN    8
+#define ODPH_TCPHDR_LEN    20
 #define ODPH_IPPROTO_UDP   0x11
 #define ODPH_IPPROTO_TCP   0x06
+#define ODPH_IPPROTO_ICMPV4 0x01
+#define ODPH_IPPROTO_SCTP  0x84
 
 typedef struct __attribute__((packed)) odph_ethaddr_t {
 	uint8_t addr[ODPH_ETHADDR_LEN];
@@ -71,6 +86,12 @@ typedef struct odph_udphdr_t {
 
 int odph_eth_addr_parse(odph_ethaddr_t *mac, const char *str);
 int odph_ipv4_addr_parse(uint32_t *ip_addr, const char *str);
+
+/* IPv4 header checksum at the packet's L3 offset (helper ip.h:98-193):
+ * _update writes it (0, or < 0 when there is no IPv4 header there), _valid
+ * returns 1 when the stored one is right, else 0 */
+int odph_ipv4_csum_update(odp_packet_t pkt);
+int odph_ipv4_csum_valid(odp_packet_t pkt);
 
 /* odph_strcpy (helper/include/odp/helper/string.h): strncpy that always
  * terminates; returns dst */

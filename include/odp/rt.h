@@ -35,6 +35,10 @@ extern "C" {
 #define ODP_PRINTF_FORMAT(x, y) __attribute__((format(printf, (x), (y))))
 #define ODP_STATIC_ASSERT(cond, msg) _Static_assert(cond, msg)
 #define ODP_CACHE_LINE_SIZE 64
+#define ODP_ALIGNED(x)    __attribute__((__aligned__(x)))
+#define ODP_ALIGNED_CACHE ODP_ALIGNED(ODP_CACHE_LINE_SIZE)
+#define ODP_PACKED        __attribute__((__packed__))
+#define ODP_PAGE_SIZE     4096
 
 typedef uint16_t odp_u16be_t;
 typedef uint32_t odp_u32be_t;
@@ -76,6 +80,41 @@ static inline void odp_atomic_add_u32(odp_atomic_u32_t *a, uint32_t v)
 { __atomic_fetch_add(&a->v, v, __ATOMIC_RELAXED); }
 static inline uint32_t odp_atomic_fetch_inc_u32(odp_atomic_u32_t *a)
 { return __atomic_fetch_add(&a->v, 1, __ATOMIC_RELAXED); }
+static inline uint32_t odp_atomic_fetch_add_u32(odp_atomic_u32_t *a, uint32_t v)
+{ return __atomic_fetch_add(&a->v, v, __ATOMIC_RELAXED); }
+static inline uint32_t odp_atomic_fetch_sub_u32(odp_atomic_u32_t *a, uint32_t v)
+{ return __atomic_fetch_sub(&a->v, v, __ATOMIC_RELAXED); }
+static inline void odp_atomic_sub_u32(odp_atomic_u32_t *a, uint32_t v)
+{ __atomic_fetch_sub(&a->v, v, __ATOMIC_RELAXED); }
+static inline void odp_atomic_dec_u32(odp_atomic_u32_t *a)
+{ __atomic_fetch_sub(&a->v, 1, __ATOMIC_RELAXED); }
+static inline uint32_t odp_atomic_fetch_dec_u32(odp_atomic_u32_t *a)
+{ return __atomic_fetch_sub(&a->v, 1, __ATOMIC_RELAXED); }
+static inline int odp_atomic_cas_u32(odp_atomic_u32_t *a, uint32_t *old, uint32_t nv)
+{ return __atomic_compare_exchange_n(&a->v, old, nv, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED); }
+static inline uint32_t odp_atomic_load_acq_u32(odp_atomic_u32_t *a)
+{ return __atomic_load_n(&a->v, __ATOMIC_ACQUIRE); }
+static inline void odp_atomic_store_rel_u32(odp_atomic_u32_t *a, uint32_t v)
+{ __atomic_store_n(&a->v, v, __ATOMIC_RELEASE); }
+static inline uint64_t odp_atomic_fetch_add_u64(odp_atomic_u64_t *a, uint64_t v)
+{ return __atomic_fetch_add(&a->v, v, __ATOMIC_RELAXED); }
+static inline uint64_t odp_atomic_fetch_sub_u64(odp_atomic_u64_t *a, uint64_t v)
+{ return __atomic_fetch_sub(&a->v, v, __ATOMIC_RELAXED); }
+static inline void odp_atomic_sub_u64(odp_atomic_u64_t *a, uint64_t v)
+{ __atomic_fetch_sub(&a->v, v, __ATOMIC_RELAXED); }
+static inline void odp_atomic_dec_u64(odp_atomic_u64_t *a)
+{ __atomic_fetch_sub(&a->v, 1, __ATOMIC_RELAXED); }
+static inline int odp_atomic_cas_u64(odp_atomic_u64_t *a, uint64_t *old, uint64_t nv)
+{ return __atomic_compare_exchange_n(&a->v, old, nv, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED); }
+
+/* ---- barrier (barrier.h): count threads meet, reusable ------------------- */
+typedef struct odp_barrier_t {
+	uint32_t count;
+	odp_atomic_u32_t bar;      /* arrivals, 0 .. 2 * count - 1 (two phases) */
+} odp_barrier_t;
+
+void odp_barrier_init(odp_barrier_t *barr, int count);
+void odp_barrier_wait(odp_barrier_t *barr);
 
 /* ---- init (init.h) ------------------------------------------------------ */
 typedef uint64_t odp_instance_t;
@@ -109,7 +148,14 @@ int  odp_init_local(odp_instance_t instance, odp_thread_type_t thr_type);
 int  odp_term_local(void);
 int  odp_term_global(odp_instance_t instance);
 void odp_sys_info_print(void);
+/* thread ids (thread.h): the lowest free id in [0, ODP_THREAD_COUNT_MAX) is
+ * taken by odp_init_local() and given back by odp_term_local(), as the
+ * reference's thread table does (odp_thread.c:alloc_id / free_id) */
 int  odp_thread_id(void);
+int  odp_thread_count(void);
+int  odp_thread_count_max(void);
+odp_thread_type_t odp_thread_type(void);
+int  odp_cpu_id(void);
 int  odp_cpu_count(void);
 
 /* ---- CPU cycle counter (cpu.h) ------------------------------------------ */
@@ -174,9 +220,13 @@ void       odp_time_wait_until(odp_time_t time);
 typedef struct _odp_shm_hdl *odp_shm_t;
 #define ODP_SHM_INVALID ((odp_shm_t)0)
 
+/* named blocks: odp_shm_lookup() finds a block by the name it was reserved
+ * under (the newest, if names repeat) */
 odp_shm_t odp_shm_reserve(const char *name, uint64_t size, uint64_t align, uint32_t flags);
+odp_shm_t odp_shm_lookup(const char *name);
 void     *odp_shm_addr(odp_shm_t shm);
 int       odp_shm_free(odp_shm_t shm);
+uint64_t  odp_shm_to_u64(odp_shm_t shm);
 
 /* ---- packet pools (pool.h, pool_types.h) -------------------------------- */
 #define ODP_POOL_NAME_LEN 32
@@ -280,6 +330,8 @@ int        odp_pool_capability(odp_pool_capability_t *capa);
 void       odp_pool_param_init(odp_pool_param_t *param);
 odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param);
 int        odp_pool_destroy(odp_pool_t pool);
+odp_pool_t odp_pool_lookup(const char *name);
+uint64_t   odp_pool_to_u64(odp_pool_t pool);
 void       odp_pool_print(odp_pool_t pool);
 void       odp_pool_print_all(void);
 
@@ -287,6 +339,25 @@ void       odp_pool_print_all(void);
 typedef struct _odp_event_hdl *odp_event_t;
 #define ODP_EVENT_INVALID ((odp_event_t)0)
 
+/* odp_event_type_t (include-abi/odp/api/abi/event_types.h): every event of
+ * this runtime is a packet */
+typedef enum odp_event_type_t {
+	ODP_EVENT_BUFFER = 1,
+	ODP_EVENT_PACKET = 2,
+	ODP_EVENT_TIMEOUT = 3,
+	ODP_EVENT_IPSEC_STATUS = 5,
+	ODP_EVENT_PACKET_VECTOR = 6,
+	ODP_EVENT_PACKET_TX_COMPL = 7,
+	ODP_EVENT_DMA_COMPL = 8,
+	ODP_EVENT_ML_COMPL = 9
+} odp_event_type_t;
+
+odp_event_type_t odp_event_type(odp_event_t event);
+
+/* Queue handles come from a registry (odp_queue_create): a tag in the top
+ * bits that no user-space pointer has, and the queue's slot. Any other value
+ * (e.g. an integer an application hands the classifier as a queue) is not a
+ * queue here: operations on it fail. */
 #define ODP_QUEUE_NAME_LEN 32
 
 typedef struct odp_queue_info_t {
@@ -297,6 +368,8 @@ typedef struct odp_queue_info_t {
 odp_queue_t odp_queue_create(const char *name, const odp_queue_param_t *param);
 int         odp_queue_destroy(odp_queue_t queue);
 int         odp_queue_info(odp_queue_t queue, odp_queue_info_t *info);
+odp_queue_type_t odp_queue_type(odp_queue_t queue);
+uint64_t    odp_queue_to_u64(odp_queue_t queue);
 int         odp_queue_enq(odp_queue_t queue, odp_event_t ev);
 odp_event_t odp_queue_deq(odp_queue_t queue);
 int         odp_queue_enq_multi(odp_queue_t queue, const odp_event_t ev[], int num);
@@ -344,21 +417,184 @@ void     odp_packet_free_multi(const odp_packet_t pkt[], int num);
 uint32_t odp_packet_len(odp_packet_t pkt);
 void    *odp_packet_data(odp_packet_t pkt);
 odp_pool_t odp_packet_pool(odp_packet_t pkt);
-int      odp_packet_has_error(odp_packet_t pkt);
-int      odp_packet_has_eth(odp_packet_t pkt);
-int      odp_packet_has_ipv4(odp_packet_t pkt);
-int      odp_packet_has_ipv6(odp_packet_t pkt);
-int      odp_packet_has_udp(odp_packet_t pkt);
-int      odp_packet_has_tcp(odp_packet_t pkt);
+/* the pktio a packet was received on (ODP_PKTIO_INVALID if none) */
+odp_pktio_t odp_packet_input(odp_packet_t pkt);
+int      odp_packet_input_index(odp_packet_t pkt);
 void    *odp_packet_l2_ptr(odp_packet_t pkt, uint32_t *len);
 void    *odp_packet_l3_ptr(odp_packet_t pkt, uint32_t *len);
 void    *odp_packet_l4_ptr(odp_packet_t pkt, uint32_t *len);
 uint32_t odp_packet_l2_offset(odp_packet_t pkt);
 uint32_t odp_packet_l3_offset(odp_packet_t pkt);
 uint32_t odp_packet_l4_offset(odp_packet_t pkt);
+/* 0, or -1 for an offset past the packet (packet.h) */
+int      odp_packet_l2_offset_set(odp_packet_t pkt, uint32_t offset);
+int      odp_packet_l3_offset_set(odp_packet_t pkt, uint32_t offset);
+int      odp_packet_l4_offset_set(odp_packet_t pkt, uint32_t offset);
+/* 0, or -1 when [offset, offset + len) leaves the packet */
+int      odp_packet_copy_to_mem(odp_packet_t pkt, uint32_t offset, uint32_t len, void *dst);
+int      odp_packet_copy_from_mem(odp_packet_t pkt, uint32_t offset, uint32_t len,
+				  const void *src);
 odp_cos_t odp_packet_cos(odp_packet_t pkt);
-int      odp_packet_has_flow_hash(odp_packet_t pkt);
 void     odp_packet_print_data(odp_packet_t pkt, uint32_t offset, uint32_t len);
+
+/* The receive verdict a packet carries: the parse result the GPU kernel
+ * wrote for it (odpg_meta_t = packet_parser_t) and its classifier mark. The
+ * accessors decode it exactly as the reference's inline accessors decode
+ * packet_parser_t (include/odp/api/plat/packet_inlines.h:334-417,617,
+ * packet_flag_inlines.h:62-288). */
+typedef enum odp_packet_chksum_status_t {
+	ODP_PACKET_CHKSUM_UNKNOWN = 0,
+	ODP_PACKET_CHKSUM_BAD,
+	ODP_PACKET_CHKSUM_OK
+} odp_packet_chksum_status_t;
+
+odp_packet_chksum_status_t odp_packet_l3_chksum_status(odp_packet_t pkt);
+odp_packet_chksum_status_t odp_packet_l4_chksum_status(odp_packet_t pkt);
+uint64_t odp_packet_cls_mark(odp_packet_t pkt);
+
+int odp_packet_has_error(odp_packet_t pkt);
+int odp_packet_has_l2_error(odp_packet_t pkt);
+int odp_packet_has_l3_error(odp_packet_t pkt);
+int odp_packet_has_l4_error(odp_packet_t pkt);
+int odp_packet_has_l2(odp_packet_t pkt);
+int odp_packet_has_l3(odp_packet_t pkt);
+int odp_packet_has_l4(odp_packet_t pkt);
+int odp_packet_has_eth(odp_packet_t pkt);
+int odp_packet_has_eth_bcast(odp_packet_t pkt);
+int odp_packet_has_eth_mcast(odp_packet_t pkt);
+int odp_packet_has_jumbo(odp_packet_t pkt);
+int odp_packet_has_vlan(odp_packet_t pkt);
+int odp_packet_has_vlan_qinq(odp_packet_t pkt);
+int odp_packet_has_arp(odp_packet_t pkt);
+int odp_packet_has_ipv4(odp_packet_t pkt);
+int odp_packet_has_ipv6(odp_packet_t pkt);
+int odp_packet_has_ip_bcast(odp_packet_t pkt);
+int odp_packet_has_ip_mcast(odp_packet_t pkt);
+int odp_packet_has_ipfrag(odp_packet_t pkt);
+int odp_packet_has_ipopt(odp_packet_t pkt);
+int odp_packet_has_ipsec(odp_packet_t pkt);
+int odp_packet_has_udp(odp_packet_t pkt);
+int odp_packet_has_tcp(odp_packet_t pkt);
+int odp_packet_has_sctp(odp_packet_t pkt);
+int odp_packet_has_icmp(odp_packet_t pkt);
+int odp_packet_has_flow_hash(odp_packet_t pkt);
+int odp_packet_has_ts(odp_packet_t pkt);
+
+/* protocol types (packet_types.h:60-175) */
+typedef uint8_t  odp_proto_l2_type_t;
+typedef uint16_t odp_proto_l3_type_t;
+typedef uint8_t  odp_proto_l4_type_t;
+#define ODP_PROTO_L2_TYPE_NONE    0
+#define ODP_PROTO_L2_TYPE_ETH     1
+#define ODP_PROTO_L3_TYPE_NONE    0xFFFF
+#define ODP_PROTO_L3_TYPE_ARP     0x0806
+#define ODP_PROTO_L3_TYPE_IPV4    0x0800
+#define ODP_PROTO_L3_TYPE_IPV6    0x86DD
+#define ODP_PROTO_L4_TYPE_NONE    255
+#define ODP_PROTO_L4_TYPE_ICMPV4  1
+#define ODP_PROTO_L4_TYPE_TCP     6
+#define ODP_PROTO_L4_TYPE_UDP     17
+#define ODP_PROTO_L4_TYPE_ESP     50
+#define ODP_PROTO_L4_TYPE_AH      51
+#define ODP_PROTO_L4_TYPE_ICMPV6  58
+#define ODP_PROTO_L4_TYPE_NO_NEXT 59
+#define ODP_PROTO_L4_TYPE_SCTP    132
+
+odp_proto_l2_type_t odp_packet_l2_type(odp_packet_t pkt);
+odp_proto_l3_type_t odp_packet_l3_type(odp_packet_t pkt);
+odp_proto_l4_type_t odp_packet_l4_type(odp_packet_t pkt);
+
+/* Parsing packets the application holds (packet.h, odp_packet_parse):
+ * the batch goes through the same GPU parser as a receive, starting at
+ * `offset` with the given protocol. odp_packet_parse_multi() parses up to
+ * the first packet that fails and returns its index (num when none does),
+ * as odp_packet.c:2064-2075; packets after it keep their metadata. */
+typedef enum odp_proto_t {
+	ODP_PROTO_NONE = 0,
+	ODP_PROTO_ETH,
+	ODP_PROTO_IPV4,
+	ODP_PROTO_IPV6
+} odp_proto_t;
+
+typedef union odp_proto_chksums_t {
+	struct {
+		uint32_t ipv4 : 1;
+		uint32_t udp  : 1;
+		uint32_t tcp  : 1;
+		uint32_t sctp : 1;
+	} chksum;
+	uint32_t all_chksum;
+} odp_proto_chksums_t;
+
+typedef struct odp_packet_parse_param_t {
+	odp_proto_t proto;
+	odp_proto_layer_t last_layer;
+	odp_proto_chksums_t chksums;
+} odp_packet_parse_param_t;
+
+typedef union odp_packet_parse_result_flag_t {
+	uint64_t all;
+	struct {
+		uint64_t has_error     : 1;
+		uint64_t has_l2_error  : 1;
+		uint64_t has_l3_error  : 1;
+		uint64_t has_l4_error  : 1;
+		uint64_t has_l2        : 1;
+		uint64_t has_l3        : 1;
+		uint64_t has_l4        : 1;
+		uint64_t has_eth       : 1;
+		uint64_t has_eth_bcast : 1;
+		uint64_t has_eth_mcast : 1;
+		uint64_t has_jumbo     : 1;
+		uint64_t has_vlan      : 1;
+		uint64_t has_vlan_qinq : 1;
+		uint64_t has_arp       : 1;
+		uint64_t has_ipv4      : 1;
+		uint64_t has_ipv6      : 1;
+		uint64_t has_ip_bcast  : 1;
+		uint64_t has_ip_mcast  : 1;
+		uint64_t has_ipfrag    : 1;
+		uint64_t has_ipopt     : 1;
+		uint64_t has_ipsec     : 1;
+		uint64_t has_udp       : 1;
+		uint64_t has_tcp       : 1;
+		uint64_t has_sctp      : 1;
+		uint64_t has_icmp      : 1;
+	};
+} odp_packet_parse_result_flag_t;
+
+typedef struct odp_packet_parse_result_t {
+	odp_packet_parse_result_flag_t flag;
+	uint32_t packet_len;
+	uint32_t l2_offset;
+	uint32_t l3_offset;
+	uint32_t l4_offset;
+	odp_packet_chksum_status_t l3_chksum_status;
+	odp_packet_chksum_status_t l4_chksum_status;
+	odp_proto_l2_type_t l2_type;
+	odp_proto_l3_type_t l3_type;
+	odp_proto_l4_type_t l4_type;
+} odp_packet_parse_result_t;
+
+int  odp_packet_parse(odp_packet_t pkt, uint32_t offset, const odp_packet_parse_param_t *param);
+int  odp_packet_parse_multi(const odp_packet_t pkt[], const uint32_t offset[], int num,
+			    const odp_packet_parse_param_t *param);
+void odp_packet_parse_result(odp_packet_t pkt, odp_packet_parse_result_t *result);
+void odp_packet_parse_result_multi(const odp_packet_t pkt[], odp_packet_parse_result_t *result[],
+				   int num);
+
+/* A runtime packet as the batch API sees a frame (odp_cls.h odpg_packet_t):
+ * its bytes and the parse result it carries (odpg_meta_t, the
+ * packet_parser_t layout plus cls_mark). 0, or -1 if `pkt` is not a packet
+ * of this runtime. */
+int odpg_packet_view(odp_packet_t pkt, odpg_packet_t *view);
+
+/* checksum (chksum.h:26-40): the 16-bit ones' complement sum (not inverted)
+ * of the data's 16-bit words in memory byte order, an odd tail byte padded
+ * with zero (odp_chksum.c: chksum_finalize(chksum_partial(p, len, 0))) */
+uint16_t odp_chksum_ones_comp16(const void *data, uint32_t len);
+
+#define ODP_PACKET_OFFSET_INVALID 0xFFFFu
 
 /* ---- pktio beyond the classifier setters (packet_io.h) ------------------ */
 typedef struct odp_pktin_queue_t {

@@ -377,10 +377,14 @@ int  odp_cls_cos_stats(odp_cos_t cos, odp_cls_cos_stats_t *stats);
 int  odp_cls_queue_stats(odp_cos_t cos, odp_queue_t queue, odp_cls_queue_stats_t *stats);
 void odp_cls_print_all(void);
 /* The queue of `cos` a packet is enqueued to (classification.h:769;
- * odp_classification.c:384-414). This library's odp_packet_t is an
- * odpg_packet_t: a frame and its parse result (the odpg_meta_t a classify
- * launch writes), since packets live in device batches, not in a packet
- * pool. ODP_QUEUE_INVALID on a bad CoS or packet. */
+ * odp_classification.c:384-414): the CoS queue, or for a hash-queue CoS the
+ * queue get_dest_queue() picks from the packet's parse result.
+ * odp_cls_hash_result() takes the runtime's packets (odp/rt.h: what
+ * odp_schedule / odp_queue_deq / odp_pktin_recv hand out, or
+ * odp_packet_alloc + odp_packet_parse). odpg_cls_hash_result() is the same
+ * for a frame of a device batch described by an odpg_packet_t (frame bytes +
+ * the odpg_meta_t a classify launch wrote for it). ODP_QUEUE_INVALID on a
+ * bad CoS or packet. */
 typedef struct odpg_packet_s {
 	const uint8_t *data;
 	uint32_t len;
@@ -388,6 +392,7 @@ typedef struct odpg_packet_s {
 	odpg_meta_t meta;
 } odpg_packet_t;
 odp_queue_t odp_cls_hash_result(odp_cos_t cos, odp_packet_t packet);
+odp_queue_t odpg_cls_hash_result(odp_cos_t cos, const odpg_packet_t *packet);
 uint64_t odp_cos_to_u64(odp_cos_t hdl);
 uint64_t odp_pmr_to_u64(odp_pmr_t hdl);
 

@@ -272,7 +272,7 @@ class odp_pktin_queue_param_t(C.Structure):
 
 
 class odpg_packet_t(C.Structure):
-    """include/odp_cls.h: a frame and its parse result (odp_cls_hash_result)"""
+    """include/odp_cls.h: a frame and its parse result (odpg_cls_hash_result)"""
     _fields_ = [("data", C.c_void_p), ("len", C.c_uint32), ("reserved", C.c_uint32),
                 ("meta", odpg_meta_t)]
 
@@ -344,7 +344,8 @@ SIGNATURES = {
     "odp_cls_cos_stats": (_i32, [_vp, C.POINTER(odp_cls_cos_stats_t)]),
     "odp_cls_queue_stats": (_i32, [_vp, _vp, C.POINTER(odp_cls_cos_stats_t)]),
     "odp_cls_print_all": (None, []),
-    "odp_cls_hash_result": (_vp, [_vp, C.POINTER(odpg_packet_t)]),
+    "odp_cls_hash_result": (_vp, [_vp, _vp]),
+    "odpg_cls_hash_result": (_vp, [_vp, C.POINTER(odpg_packet_t)]),
     "odp_queue_param_init": (None, [C.POINTER(odp_queue_param_t)]),
     "odp_pktio_param_init": (None, [_vp]),
     "odp_cos_to_u64": (_u64, [_vp]),

@@ -16,7 +16,17 @@
  * binding's device-resident sharded counters (odpg.h); the statistics calls
  * fold them into the host totals when they are read, as the reference reads
  * its atomics at query time. The global lock covers the object model and the
- * binding lookup, never the GPU work of a receive.
+ * binding lookup, never a receive's launch. It is held, though, while a
+ * binding is recompiled for a new rule generation (odpg_table_update, which
+ * orders its upload on the context stream and may wait for that stream when
+ * the table grows) and while statistics are folded (odpg_counters_fold
+ * waits for the launches before it): a rule change or a statistics read
+ * can therefore wait for GPU work already queued.
+ *
+ * A CoS with num_queue > 1 owns its hash queues: they are created with the
+ * CoS's queue_param as "_odp_cos_hq_<cos>_<i>" by odp_queue_create (the
+ * runtime's queues, odp/rt.h) and destroyed with the CoS
+ * (odp_classification.c:283-307, 464-478).
  */
 #include <errno.h>
 #include <inttypes.h>
@@ -25,7 +35,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "../../include/odp_cls.h"
+#include "../../include/odp_api.h"
 #include "odp_rt_internal.h"
 
 #define REF_MAX_COS          64      /* CLS_COS_MAX_ENTRY   */
@@ -112,14 +122,13 @@ static struct {
 	pmr_e *pmr;
 	pktio_e pktio[MAX_PKTIO];
 	uint64_t generation;
-	uintptr_t next_queue_id;
 	uint64_t next_uid;
 	/* snapshot buffers */
 	odpg_cos_t *s_cos;
 	odpg_pmr_t *s_pmr;
 	uint32_t *s_rule_pmr, *s_rule_dst;
 } g = { 0, PTHREAD_MUTEX_INITIALIZER, REF_MAX_COS, REF_MAX_PMR, REF_MAX_PMR_PER_COS,
-	NULL, NULL, {{0}}, 1, 0x40000000u, 1, NULL, NULL, NULL, NULL };
+	NULL, NULL, {{0}}, 1, 1, NULL, NULL, NULL, NULL };
 
 static void free_tables(void)
 {
@@ -429,6 +438,24 @@ static uint32_t hash_proto_bits(odp_pktin_hash_proto_t hp)
 	return b;
 }
 
+/* the hash queues of CoS slot i (odp_classification.c:283-307): -1, with
+ * the ones made so far destroyed again, if one cannot be created */
+static int hash_queues_create(cos_e *c, uint32_t i, uint32_t num)
+{
+	for (uint32_t j = 0; j < num; j++) {
+		char hq_name[ODP_QUEUE_NAME_LEN];
+
+		snprintf(hq_name, sizeof(hq_name), "_odp_cos_hq_%u_%u", i, j);
+		c->hq[j] = odp_queue_create(hq_name, &c->queue_param);
+		if (c->hq[j] == ODP_QUEUE_INVALID) {
+			while (j > 0)                  /* _cls_queue_unwind */
+				odp_queue_destroy(c->hq[--j]);
+			return -1;
+		}
+	}
+	return 0;
+}
+
 /* odp_cls_cos_create (odp_classification.c:231-347) */
 odp_cos_t odp_cls_cos_create(const char *name, const odp_cls_cos_param_t *param_in)
 {
@@ -481,8 +508,8 @@ odp_cos_t odp_cls_cos_create(const char *name, const odp_cls_cos_param_t *param_
 			c->queue_group = 1;
 			c->queue = ODP_QUEUE_INVALID;
 			c->hash_proto = hash_proto_bits(param.hash_proto);
-			for (uint32_t j = 0; j < param.num_queue; j++)
-				c->hq[j] = (odp_queue_t)(g.next_queue_id++);
+			if (hash_queues_create(c, i, param.num_queue))
+				break;
 		} else {
 			c->queue_group = 0;
 			c->queue = param.queue;
@@ -536,6 +563,9 @@ int odp_cos_destroy(odp_cos_t cos_id)
 		ERR("Invalid odp_cos_t handle\n");
 		rc = -1;
 	} else {
+		if (c->queue_group)           /* _cls_queue_unwind */
+			for (uint32_t j = 0; j < c->num_queue; j++)
+				odp_queue_destroy(c->hq[j]);
 		c->valid = 0;
 		bump();
 	}
@@ -978,9 +1008,8 @@ static int packet_rss_hash(const odpg_packet_t *pk, uint32_t hp, uint32_t *hash)
 
 /* odp_cls_hash_result (odp_classification.c:384-414): get_dest_queue's
  * queue, hash & (CLS_COS_QUEUE_MAX - 1) modulo the CoS's queue count */
-odp_queue_t odp_cls_hash_result(odp_cos_t cos_id, odp_packet_t packet)
+odp_queue_t odpg_cls_hash_result(odp_cos_t cos_id, const odpg_packet_t *pk)
 {
-	const odpg_packet_t *pk = (const odpg_packet_t *)packet;
 	odp_queue_t q = ODP_QUEUE_INVALID;
 	uint32_t h;
 
@@ -996,6 +1025,33 @@ odp_queue_t odp_cls_hash_result(odp_cos_t cos_id, odp_packet_t packet)
 	}
 	UNLOCK();
 	return q;
+}
+
+/* the same on the runtime's packets (the frame and the parse result a
+ * receive or odp_packet_parse left on it) */
+odp_queue_t odp_cls_hash_result(odp_cos_t cos_id, odp_packet_t packet)
+{
+	odpg_packet_t view;
+
+	if (packet == ODP_PACKET_INVALID || odpg_packet_view(packet, &view)) {
+		ERR("Invalid odp_packet_t handle\n");
+		return ODP_QUEUE_INVALID;
+	}
+	return odpg_cls_hash_result(cos_id, &view);
+}
+
+void odpg_cls_queue_count(odp_cos_t cos_id, odp_queue_t queue, int64_t packets,
+			  uint64_t discards)
+{
+	LOCK();
+	cos_e *c = get_cos(cos_id);
+	const int qi = c ? cos_queue_idx(c, queue) : -1;
+
+	if (qi >= 0) {
+		c->q_packets[qi] += (uint64_t)packets;
+		c->q_discards[qi] += discards;
+	}
+	UNLOCK();
 }
 
 /* odp_cls_print_all (odp_classification.c:1879-1981), reduced */
@@ -1091,14 +1147,22 @@ odp_pktio_t odp_pktio_lookup(const char *name)
 	return ret;
 }
 
+/* odp_pktio_close (odp_packet_io.c:497-545): refused while started
+ * ("Missing odp_pktio_stop() before close", :507-510) or while a receive
+ * holds one of its tables; only then is the receive state (capture, loop
+ * ring, pktin / pktout queues) torn down and the slot freed */
 int odp_pktio_close(odp_pktio_t hdl)
 {
-	odpg_rt_pktio_close(hdl);
 	LOCK();
 	pktio_e *p = get_pktio(hdl);
 
 	if (!p) {
 		UNLOCK();
+		return -1;
+	}
+	if (p->started) {
+		UNLOCK();
+		ERR("Missing odp_pktio_stop() before close.\n");
 		return -1;
 	}
 	for (bind_t *b = p->binds; b; b = b->next)
@@ -1107,9 +1171,17 @@ int odp_pktio_close(odp_pktio_t hdl)
 			ERR("pktio close during a receive\n");
 			return -1;
 		}
-	binds_release_locked(p, NULL, 0);   /* CoS counts outlive the pktio */
-	memset(p, 0, sizeof(*p));
-	bump();
+	UNLOCK();
+	/* a stopped pktio takes no new receive (recv_impl, rx_burst), so
+	 * nothing re-binds while the lock is dropped for the runtime side */
+	odpg_rt_pktio_close(hdl);
+	LOCK();
+	p = get_pktio(hdl);
+	if (p) {
+		binds_release_locked(p, NULL, 0);   /* CoS counts outlive the pktio */
+		memset(p, 0, sizeof(*p));
+		bump();
+	}
 	UNLOCK();
 	return 0;
 }

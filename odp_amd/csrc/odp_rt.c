@@ -2,10 +2,11 @@
  *
  * The ODP runtime subset around the GPU classifier (include/odp_api.h,
  * include/odp/rt.h, include/odp/helper/odph_api.h): what an ODP application
- * such as the reference's example/classifier needs to receive classified
- * packets — init, shared memory, packet pools, queues and the scheduler,
- * pcap / loop pktio input, packet accessors, time, CPU masks, helper
- * threads.
+ * such as the reference's example/classifier or test/performance's
+ * odp_pktio_perf needs to receive classified packets — init, thread ids,
+ * named shared memory, barriers, packet pools, queues and the scheduler,
+ * pcap / loop pktio input, packet accessors and odp_packet_parse, time, CPU
+ * masks, helper threads.
  *
  * Receive path: one burst of a pktio's input — the next frames of its
  * capture (pktio/pcap.c's pcapif_recv_pkt role: "pcap:in=<file>", with
@@ -14,16 +15,21 @@
  * GPU through the classifier's own receive entry point
  * (odpg_pktio_recv_batch's path: parse, checksum verdicts, PMR -> CoS, the
  * pktio / CoS / queue counters). Every packet with a CoS goes to its CoS
- * queue, as loopback_recv() -> _odp_cls_enq() does (pktio/loop.c:304-374,
- * odp_classification_internal.h:139-225), in the CoS's pool (the pktio's
- * when the CoS names none, odp_classification.c:1734-1736); with the
- * classifier disabled the packet is the receive call's (DIRECT mode,
- * odp_pktin_recv) or goes to the pktin event queue (QUEUE / SCHED mode).
- * Bursts are taken by odp_pktin_recv(), by a dequeue from an empty QUEUE-mode
- * pktin queue, and by the scheduler for SCHED-mode pktios. The parse result
- * each packet carries is the odpg_meta_t the kernel wrote. Packets that get
- * no CoS, a drop CoS or a parse drop are freed there, as the reference's
- * receive loop frees them.
+ * queue (the hash queue get_dest_queue picks for a hash-queue CoS), in the
+ * CoS's pool (the pktio's when the CoS names none, odp_classification.c:
+ * 1734-1736), and consecutive packets for the same (CoS, queue) are
+ * enqueued with one odp_queue_enq_multi, as loopback_recv() ->
+ * _odp_cls_enq() batches them (pktio/loop.c:304-374,
+ * odp_classification_internal.h:139-225); a failed enqueue frees the rest
+ * of the run and counts it as the queue's discards. With the classifier
+ * disabled the packet is the receive call's (DIRECT mode, odp_pktin_recv)
+ * or goes to the pktin event queue (QUEUE / SCHED mode). Bursts are taken
+ * by odp_pktin_recv(), by a dequeue from an empty QUEUE-mode pktin queue,
+ * and by the scheduler for SCHED-mode pktios. The parse result each packet
+ * carries is the odpg_meta_t the kernel wrote (the packet_parser_t layout,
+ * cls_mark included), which the odp_packet_has_* / chksum status / cls_mark
+ * accessors decode. Packets that get no CoS, a drop CoS or a parse drop are
+ * freed there, as the reference's receive loop frees them.
  *
  * This is a functional runtime, not a fast path: the device-resident batch
  * API (odpg.h) is the throughput path.
@@ -50,12 +56,16 @@
 #define RT_BURST     1024
 
 /* ---- objects -------------------------------------------------------------- */
+#define PKT_MAGIC 0x504b5452u
+
 typedef struct rt_pkt {
-	odp_pool_t pool;
+	uint32_t magic;
 	uint32_t len;
 	uint32_t cap;
+	odp_pool_t pool;
 	odp_cos_t cos;
-	odpg_meta_t meta;
+	odp_pktio_t input;         /* the pktio it was received on */
+	odpg_meta_t meta;          /* parse result: packet_parser_t + cls_mark */
 	uint8_t *data;
 	struct rt_pkt *next;       /* queue link */
 } rt_pkt_t;
@@ -70,6 +80,7 @@ typedef struct rt_pool {
 
 typedef struct rt_queue {
 	uint32_t magic;
+	odp_queue_t hdl;           /* registry handle */
 	char name[ODP_QUEUE_NAME_LEN];
 	odp_queue_param_t param;
 	pthread_mutex_t lock;
@@ -90,7 +101,7 @@ typedef struct rt_pktio {
 	odpg_capture_t cap;
 	int have_cap;
 	uint32_t pos;              /* next frame of the capture */
-	uint32_t loops, loop;      /* passes over the capture, done */
+	uint32_t loops, loop_cnt;  /* pcap.c's loops / loop_cnt (starts at 1) */
 	int promisc;
 	uint32_t mtu;
 	uint32_t num_in, num_out;  /* configured input / output queues */
@@ -113,17 +124,23 @@ static struct {
 	rt_pktio_t pktio[RT_MAX_PKTIO];
 	rt_queue_t *sched;         /* scheduled queues */
 	uint32_t rr;
-	int next_thread;
 	/* poll buffers */
 	odpg_out_t out[RT_BURST];
 	odpg_meta_t meta[RT_BURST];
 	odpg_desc_t desc[RT_BURST];
 } rt = { PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, 0, NULL, {{0}}, {{0}},
-	 NULL, 0, 0, {0}, {{0}}, {{0}} };
-
-static __thread int thr_id = -1;
+	 NULL, 0, {0}, {{0}}, {{0}} };
 
 /* ---- init / threads ------------------------------------------------------- */
+/* thread ids: the lowest free id, given back at odp_term_local (odp_thread.c
+ * alloc_id / free_id), so ids stay below ODP_THREAD_COUNT_MAX however many
+ * threads come and go (odp_pktio_perf indexes its stats by them) */
+static pthread_mutex_t thr_lock = PTHREAD_MUTEX_INITIALIZER;
+static uint64_t thr_used[ODP_THREAD_COUNT_MAX / 64];
+static int thr_count;
+static __thread int thr_id = -1;
+static __thread odp_thread_type_t thr_type = ODP_THREAD_WORKER;
+
 void odp_init_param_init(odp_init_t *param)
 {
 	memset(param, 0, sizeof(*param));
@@ -152,9 +169,12 @@ int odp_init_global(odp_instance_t *instance, const odp_init_t *param, const voi
 	return 0;
 }
 
+static void parse_release(void);
+
 int odp_term_global(odp_instance_t instance)
 {
 	(void)instance;
+	parse_release();
 	pthread_mutex_lock(&rt.lock);
 	if (rt.init) {
 		odpg_ctx_destroy(rt.ctx);
@@ -165,23 +185,66 @@ int odp_term_global(odp_instance_t instance)
 	return 0;
 }
 
-int odp_init_local(odp_instance_t instance, odp_thread_type_t thr_type)
+int odp_init_local(odp_instance_t instance, odp_thread_type_t type)
 {
 	(void)instance;
-	(void)thr_type;
-	if (thr_id < 0)
-		thr_id = __atomic_fetch_add(&rt.next_thread, 1, __ATOMIC_RELAXED);
+	if (thr_id >= 0)
+		return 0;
+	pthread_mutex_lock(&thr_lock);
+	for (int i = 0; i < ODP_THREAD_COUNT_MAX; i++) {
+		if (thr_used[i / 64] & (1ull << (i % 64)))
+			continue;
+		thr_used[i / 64] |= 1ull << (i % 64);
+		thr_count++;
+		thr_id = i;
+		break;
+	}
+	pthread_mutex_unlock(&thr_lock);
+	if (thr_id < 0) {
+		ERR("all %d thread ids in use\n", ODP_THREAD_COUNT_MAX);
+		return -1;
+	}
+	thr_type = type;
 	return 0;
 }
 
 int odp_term_local(void)
 {
+	if (thr_id < 0)
+		return 0;
+	pthread_mutex_lock(&thr_lock);
+	thr_used[thr_id / 64] &= ~(1ull << (thr_id % 64));
+	thr_count--;
+	pthread_mutex_unlock(&thr_lock);
+	thr_id = -1;
 	return 0;
 }
 
 int odp_thread_id(void)
 {
 	return thr_id < 0 ? 0 : thr_id;
+}
+
+int odp_thread_count(void)
+{
+	return __atomic_load_n(&thr_count, __ATOMIC_RELAXED);
+}
+
+int odp_thread_count_max(void)
+{
+	return ODP_THREAD_COUNT_MAX;
+}
+
+odp_thread_type_t odp_thread_type(void)
+{
+	return thr_type;
+}
+
+int odp_cpu_id(void)
+{
+	const int c = sched_getcpu();
+
+	return c < 0 ? 0 : c;
 }
 
 int odp_cpu_count(void)
@@ -198,6 +261,42 @@ void odp_sys_info_print(void)
 	       odpg_abi_version());
 	printf("CPU count:       %i\n", odp_cpu_count());
 	printf("GPU devices:     %i\n\n", odpg_device_count());
+}
+
+/* ---- barrier: two-phase arrival count, spin then yield -------------------- */
+void odp_barrier_init(odp_barrier_t *barr, int count)
+{
+	barr->count = (uint32_t)count;
+	odp_atomic_init_u32(&barr->bar, 0);
+}
+
+/* arrivals count 0 .. 2 * count - 1: the first count arrivals meet in phase
+ * 0, the next count in phase 1, so a fast thread re-entering the barrier
+ * cannot overtake a slow one still leaving it */
+void odp_barrier_wait(odp_barrier_t *barr)
+{
+	const uint32_t count = barr->count;
+	const uint32_t n = __atomic_fetch_add(&barr->bar.v, 1, __ATOMIC_ACQ_REL);
+	const int phase = n >= count;
+	uint32_t spins = 0;
+
+	if (n + 1 == count)
+		return;                    /* the last of phase 0 releases it */
+	if (n + 1 == 2 * count) {
+		/* the last of phase 1 releases it by wrapping to 0 */
+		__atomic_store_n(&barr->bar.v, 0, __ATOMIC_RELEASE);
+		return;
+	}
+	for (;;) {
+		const uint32_t v = __atomic_load_n(&barr->bar.v, __ATOMIC_ACQUIRE);
+
+		/* phase 0 is released once every thread arrived (v >= count);
+		 * phase 1 once the count wrapped to zero */
+		if (phase == 0 ? v >= count : v < count)
+			return;
+		if (++spins > 1000)
+			sched_yield();
+	}
 }
 
 /* ---- CPU masks ------------------------------------------------------------ */
@@ -438,32 +537,88 @@ uint64_t odp_cpu_cycles_resolution(void)
 	return 1;
 }
 
-/* ---- shared memory -------------------------------------------------------- */
+/* ---- shared memory: named blocks ------------------------------------------ */
+#define SHM_MAGIC 0x53484d42u
+
+typedef struct rt_shm {
+	uint32_t magic;
+	char name[64];
+	void *addr;
+	struct rt_shm *next;
+} rt_shm_t;
+
+static pthread_mutex_t shm_lock = PTHREAD_MUTEX_INITIALIZER;
+static rt_shm_t *shm_list;     /* newest first */
+
 odp_shm_t odp_shm_reserve(const char *name, uint64_t size, uint64_t align, uint32_t flags)
 {
+	rt_shm_t *s = calloc(1, sizeof(*s));
 	void *p = NULL;
 
-	(void)name;
 	(void)flags;
+	if (!s)
+		return ODP_SHM_INVALID;
 	if (align < sizeof(void *))
 		align = sizeof(void *);
-	if (posix_memalign(&p, align, size ? size : 1))
+	if (posix_memalign(&p, align, size ? size : 1)) {
+		free(s);
 		return ODP_SHM_INVALID;
+	}
 	memset(p, 0, size);
-	return (odp_shm_t)p;
+	s->magic = SHM_MAGIC;
+	snprintf(s->name, sizeof(s->name), "%s", name ? name : "");
+	s->addr = p;
+	pthread_mutex_lock(&shm_lock);
+	s->next = shm_list;
+	shm_list = s;
+	pthread_mutex_unlock(&shm_lock);
+	return (odp_shm_t)s;
+}
+
+odp_shm_t odp_shm_lookup(const char *name)
+{
+	rt_shm_t *s;
+
+	if (!name)
+		return ODP_SHM_INVALID;
+	pthread_mutex_lock(&shm_lock);
+	for (s = shm_list; s; s = s->next)
+		if (!strcmp(s->name, name))
+			break;
+	pthread_mutex_unlock(&shm_lock);
+	return (odp_shm_t)s;
 }
 
 void *odp_shm_addr(odp_shm_t shm)
 {
-	return (void *)shm;
+	rt_shm_t *s = (rt_shm_t *)shm;
+
+	return s && s->magic == SHM_MAGIC ? s->addr : NULL;
 }
 
 int odp_shm_free(odp_shm_t shm)
 {
-	if (shm == ODP_SHM_INVALID)
+	rt_shm_t *s = (rt_shm_t *)shm, **pp;
+
+	if (!s)
 		return -1;
-	free(shm);
+	pthread_mutex_lock(&shm_lock);
+	for (pp = &shm_list; *pp && *pp != s; pp = &(*pp)->next)
+		;
+	if (*pp)
+		*pp = s->next;
+	pthread_mutex_unlock(&shm_lock);
+	if (s->magic != SHM_MAGIC)
+		return -1;
+	s->magic = 0;
+	free(s->addr);
+	free(s);
 	return 0;
+}
+
+uint64_t odp_shm_to_u64(odp_shm_t shm)
+{
+	return (uint64_t)(uintptr_t)shm;
 }
 
 /* ---- pools ---------------------------------------------------------------- */
@@ -539,6 +694,28 @@ int odp_pool_destroy(odp_pool_t hdl)
 	return rc;
 }
 
+/* odp_pool_lookup (odp_pool.c): a pool by the name it was created with */
+odp_pool_t odp_pool_lookup(const char *name)
+{
+	odp_pool_t ret = ODP_POOL_INVALID;
+
+	if (!name)
+		return ret;
+	pthread_mutex_lock(&rt.lock);
+	for (int i = 0; i < RT_MAX_POOL; i++)
+		if (rt.pool[i].valid && !strcmp(rt.pool[i].name, name)) {
+			ret = (odp_pool_t)(uintptr_t)(i + 1);
+			break;
+		}
+	pthread_mutex_unlock(&rt.lock);
+	return ret;
+}
+
+uint64_t odp_pool_to_u64(odp_pool_t pool)
+{
+	return (uint64_t)(uintptr_t)pool;
+}
+
 void odp_pool_print(odp_pool_t hdl)
 {
 	rt_pool_t *p = get_pool(hdl);
@@ -583,6 +760,7 @@ odp_packet_t odp_packet_alloc(odp_pool_t pool, uint32_t len)
 		pthread_mutex_unlock(&p->lock);
 		return ODP_PACKET_INVALID;
 	}
+	k->magic = PKT_MAGIC;
 	k->pool = pool;
 	k->len = len;
 	k->cap = len;
@@ -603,6 +781,7 @@ void odp_packet_free(odp_packet_t pkt)
 		p->in_use--;
 		pthread_mutex_unlock(&p->lock);
 	}
+	k->magic = 0;
 	free(k->data);
 	free(k);
 }
@@ -615,7 +794,24 @@ void odp_packet_free_multi(const odp_packet_t pkt[], int num)
 
 /* ---- packet accessors ------------------------------------------------------ */
 #define PK(p) ((rt_pkt_t *)(p))
+
+/* _odp_packet_input_flags_t bits (packet_inline_types.h:60-113) */
+enum {
+	IF_DST_QUEUE = 0, IF_CLS_MARK, IF_FLOW_HASH, IF_TIMESTAMP, IF_L2, IF_L3, IF_L4,
+	IF_ETH, IF_ETH_BCAST, IF_ETH_MCAST, IF_JUMBO, IF_VLAN, IF_VLAN_QINQ, IF_SNAP, IF_ARP,
+	IF_IPV4, IF_IPV6, IF_IP_BCAST, IF_IP_MCAST, IF_IPFRAG, IF_IPOPT, IF_IPSEC,
+	IF_IPSEC_AH, IF_IPSEC_ESP, IF_UDP, IF_TCP, IF_SCTP, IF_ICMP, IF_NO_NEXT_HDR,
+	IF_L3_CHKSUM_DONE = 32, IF_L4_CHKSUM_DONE
+};
+/* _odp_packet_flags_t error bits (packet_inline_types.h:150-164) */
+enum {
+	F_SNAP_LEN_ERR = 25, F_IP_ERR, F_L3_CHKSUM_ERR, F_TCP_ERR, F_UDP_ERR, F_SCTP_ERR,
+	F_L4_CHKSUM_ERR
+};
+#define F_ERROR_MASK 0xFE000000u
+
 #define IFLAG(p, bit) ((int)((PK(p)->meta.input_flags >> (bit)) & 1u))
+#define EFLAG(p, bit) ((int)((PK(p)->meta.flags >> (bit)) & 1u))
 
 odp_event_t odp_packet_to_event(odp_packet_t pkt)
 {
@@ -633,6 +829,12 @@ void odp_packet_from_event_multi(odp_packet_t pkt[], const odp_event_t ev[], int
 		pkt[i] = (odp_packet_t)ev[i];
 }
 
+odp_event_type_t odp_event_type(odp_event_t event)
+{
+	(void)event;
+	return ODP_EVENT_PACKET;
+}
+
 uint32_t odp_packet_len(odp_packet_t pkt)
 {
 	return PK(pkt)->len;
@@ -648,19 +850,128 @@ odp_pool_t odp_packet_pool(odp_packet_t pkt)
 	return PK(pkt)->pool;
 }
 
-/* packet_flags.h over packet_parser_t (input_flags bits as
- * packet_inline_types.h:60-113, error flags as odpg_meta_t.flags) */
-int odp_packet_has_error(odp_packet_t pkt)
+odp_pktio_t odp_packet_input(odp_packet_t pkt)
 {
-	return (PK(pkt)->meta.flags & 0xFE000000u) != 0u;   /* error_flags (FL_ERROR_MASK) */
+	return PK(pkt)->input;
 }
 
-int odp_packet_has_eth(odp_packet_t pkt)  { return IFLAG(pkt, 7); }
-int odp_packet_has_ipv4(odp_packet_t pkt) { return IFLAG(pkt, 15); }
-int odp_packet_has_ipv6(odp_packet_t pkt) { return IFLAG(pkt, 16); }
-int odp_packet_has_udp(odp_packet_t pkt)  { return IFLAG(pkt, 24); }
-int odp_packet_has_tcp(odp_packet_t pkt)  { return IFLAG(pkt, 25); }
-int odp_packet_has_flow_hash(odp_packet_t pkt) { return IFLAG(pkt, 2); }
+int odp_packet_input_index(odp_packet_t pkt)
+{
+	return PK(pkt)->input == ODP_PKTIO_INVALID ? -1 : 0;
+}
+
+int odpg_packet_view(odp_packet_t pkt, odpg_packet_t *view)
+{
+	const rt_pkt_t *k = PK(pkt);
+
+	if (!k || k->magic != PKT_MAGIC || !view)
+		return -1;
+	memset(view, 0, sizeof(*view));
+	view->data = k->data;
+	view->len = k->len;
+	view->meta = k->meta;
+	return 0;
+}
+
+/* packet_flag_inlines.h:62-288 over the kernel's packet_parser_t */
+int odp_packet_has_error(odp_packet_t pkt)
+{
+	return (PK(pkt)->meta.flags & F_ERROR_MASK) != 0u;   /* flags.all.error */
+}
+
+int odp_packet_has_l2_error(odp_packet_t pkt) { return EFLAG(pkt, F_SNAP_LEN_ERR); }
+int odp_packet_has_l3_error(odp_packet_t pkt) { return EFLAG(pkt, F_IP_ERR); }
+
+int odp_packet_has_l4_error(odp_packet_t pkt)
+{
+	return EFLAG(pkt, F_TCP_ERR) | EFLAG(pkt, F_UDP_ERR);
+}
+
+int odp_packet_has_l2(odp_packet_t pkt)         { return IFLAG(pkt, IF_L2); }
+int odp_packet_has_l3(odp_packet_t pkt)         { return IFLAG(pkt, IF_L3); }
+int odp_packet_has_l4(odp_packet_t pkt)         { return IFLAG(pkt, IF_L4); }
+int odp_packet_has_eth(odp_packet_t pkt)        { return IFLAG(pkt, IF_ETH); }
+int odp_packet_has_eth_bcast(odp_packet_t pkt)  { return IFLAG(pkt, IF_ETH_BCAST); }
+int odp_packet_has_eth_mcast(odp_packet_t pkt)  { return IFLAG(pkt, IF_ETH_MCAST); }
+int odp_packet_has_jumbo(odp_packet_t pkt)      { return IFLAG(pkt, IF_JUMBO); }
+int odp_packet_has_vlan(odp_packet_t pkt)       { return IFLAG(pkt, IF_VLAN); }
+int odp_packet_has_vlan_qinq(odp_packet_t pkt)  { return IFLAG(pkt, IF_VLAN_QINQ); }
+int odp_packet_has_arp(odp_packet_t pkt)        { return IFLAG(pkt, IF_ARP); }
+int odp_packet_has_ipv4(odp_packet_t pkt)       { return IFLAG(pkt, IF_IPV4); }
+int odp_packet_has_ipv6(odp_packet_t pkt)       { return IFLAG(pkt, IF_IPV6); }
+int odp_packet_has_ip_bcast(odp_packet_t pkt)   { return IFLAG(pkt, IF_IP_BCAST); }
+int odp_packet_has_ip_mcast(odp_packet_t pkt)   { return IFLAG(pkt, IF_IP_MCAST); }
+int odp_packet_has_ipfrag(odp_packet_t pkt)     { return IFLAG(pkt, IF_IPFRAG); }
+int odp_packet_has_ipopt(odp_packet_t pkt)      { return IFLAG(pkt, IF_IPOPT); }
+int odp_packet_has_ipsec(odp_packet_t pkt)      { return IFLAG(pkt, IF_IPSEC); }
+int odp_packet_has_udp(odp_packet_t pkt)        { return IFLAG(pkt, IF_UDP); }
+int odp_packet_has_tcp(odp_packet_t pkt)        { return IFLAG(pkt, IF_TCP); }
+int odp_packet_has_sctp(odp_packet_t pkt)       { return IFLAG(pkt, IF_SCTP); }
+int odp_packet_has_icmp(odp_packet_t pkt)       { return IFLAG(pkt, IF_ICMP); }
+int odp_packet_has_flow_hash(odp_packet_t pkt)  { return IFLAG(pkt, IF_FLOW_HASH); }
+int odp_packet_has_ts(odp_packet_t pkt)         { return IFLAG(pkt, IF_TIMESTAMP); }
+
+/* packet_inlines.h:385-417 */
+static odp_packet_chksum_status_t chksum_status(odp_packet_t pkt, int done_bit, int err_bit)
+{
+	if (!IFLAG(pkt, done_bit))
+		return ODP_PACKET_CHKSUM_UNKNOWN;
+	return EFLAG(pkt, err_bit) ? ODP_PACKET_CHKSUM_BAD : ODP_PACKET_CHKSUM_OK;
+}
+
+odp_packet_chksum_status_t odp_packet_l3_chksum_status(odp_packet_t pkt)
+{
+	return chksum_status(pkt, IF_L3_CHKSUM_DONE, F_L3_CHKSUM_ERR);
+}
+
+odp_packet_chksum_status_t odp_packet_l4_chksum_status(odp_packet_t pkt)
+{
+	return chksum_status(pkt, IF_L4_CHKSUM_DONE, F_L4_CHKSUM_ERR);
+}
+
+/* packet_inlines.h:617: the mark of the last PMR matched, if one was */
+uint64_t odp_packet_cls_mark(odp_packet_t pkt)
+{
+	return IFLAG(pkt, IF_CLS_MARK) ? PK(pkt)->meta.cls_mark : 0;
+}
+
+/* packet_inlines.h:334-383 */
+odp_proto_l2_type_t odp_packet_l2_type(odp_packet_t pkt)
+{
+	return IFLAG(pkt, IF_ETH) ? ODP_PROTO_L2_TYPE_ETH : ODP_PROTO_L2_TYPE_NONE;
+}
+
+odp_proto_l3_type_t odp_packet_l3_type(odp_packet_t pkt)
+{
+	if (IFLAG(pkt, IF_IPV4))
+		return ODP_PROTO_L3_TYPE_IPV4;
+	if (IFLAG(pkt, IF_IPV6))
+		return ODP_PROTO_L3_TYPE_IPV6;
+	if (IFLAG(pkt, IF_ARP))
+		return ODP_PROTO_L3_TYPE_ARP;
+	return ODP_PROTO_L3_TYPE_NONE;
+}
+
+odp_proto_l4_type_t odp_packet_l4_type(odp_packet_t pkt)
+{
+	if (IFLAG(pkt, IF_TCP))
+		return ODP_PROTO_L4_TYPE_TCP;
+	if (IFLAG(pkt, IF_UDP))
+		return ODP_PROTO_L4_TYPE_UDP;
+	if (IFLAG(pkt, IF_SCTP))
+		return ODP_PROTO_L4_TYPE_SCTP;
+	if (IFLAG(pkt, IF_IPSEC_AH))
+		return ODP_PROTO_L4_TYPE_AH;
+	if (IFLAG(pkt, IF_IPSEC_ESP))
+		return ODP_PROTO_L4_TYPE_ESP;
+	if (IFLAG(pkt, IF_ICMP) && IFLAG(pkt, IF_IPV4))
+		return ODP_PROTO_L4_TYPE_ICMPV4;
+	if (IFLAG(pkt, IF_ICMP) && IFLAG(pkt, IF_IPV6))
+		return ODP_PROTO_L4_TYPE_ICMPV6;
+	if (IFLAG(pkt, IF_NO_NEXT_HDR))
+		return ODP_PROTO_L4_TYPE_NO_NEXT;
+	return ODP_PROTO_L4_TYPE_NONE;
+}
 
 static void *layer_ptr(odp_packet_t pkt, uint32_t off, uint32_t *len)
 {
@@ -690,6 +1001,54 @@ uint32_t odp_packet_l2_offset(odp_packet_t pkt) { return PK(pkt)->meta.l2_offset
 uint32_t odp_packet_l3_offset(odp_packet_t pkt) { return PK(pkt)->meta.l3_offset; }
 uint32_t odp_packet_l4_offset(odp_packet_t pkt) { return PK(pkt)->meta.l4_offset; }
 
+/* odp_packet_lN_offset_set (odp_packet.c): offsets inside the packet; the
+ * L2 setter also marks the packet as having L2 (packet_hdr_has_l2_set) */
+static int offset_set(odp_packet_t pkt, uint16_t *field, uint32_t off)
+{
+	if (off >= PK(pkt)->len)
+		return -1;
+	*field = (uint16_t)off;
+	return 0;
+}
+
+int odp_packet_l2_offset_set(odp_packet_t pkt, uint32_t offset)
+{
+	if (offset_set(pkt, &PK(pkt)->meta.l2_offset, offset))
+		return -1;
+	PK(pkt)->meta.input_flags |= 1ull << IF_L2;
+	return 0;
+}
+
+int odp_packet_l3_offset_set(odp_packet_t pkt, uint32_t offset)
+{
+	return offset_set(pkt, &PK(pkt)->meta.l3_offset, offset);
+}
+
+int odp_packet_l4_offset_set(odp_packet_t pkt, uint32_t offset)
+{
+	return offset_set(pkt, &PK(pkt)->meta.l4_offset, offset);
+}
+
+int odp_packet_copy_to_mem(odp_packet_t pkt, uint32_t offset, uint32_t len, void *dst)
+{
+	const rt_pkt_t *k = PK(pkt);
+
+	if ((uint64_t)offset + len > k->len)
+		return -1;
+	memcpy(dst, k->data + offset, len);
+	return 0;
+}
+
+int odp_packet_copy_from_mem(odp_packet_t pkt, uint32_t offset, uint32_t len, const void *src)
+{
+	rt_pkt_t *k = PK(pkt);
+
+	if ((uint64_t)offset + len > k->len)
+		return -1;
+	memcpy(k->data + offset, src, len);
+	return 0;
+}
+
 odp_cos_t odp_packet_cos(odp_packet_t pkt)
 {
 	return PK(pkt)->cos;
@@ -705,42 +1064,367 @@ void odp_packet_print_data(odp_packet_t pkt, uint32_t offset, uint32_t len)
 	printf("\n");
 }
 
-/* ---- queues ---------------------------------------------------------------- */
+/* odp_chksum.c: chksum_finalize(chksum_partial(p, len, 0)) — 32-bit
+ * little-endian words into a 64-bit sum, a 16-bit and a byte tail, folded */
+uint16_t odp_chksum_ones_comp16(const void *data, uint32_t len)
+{
+	const uint8_t *b = data;
+	uint64_t sum = 0;
+	uint32_t w;
+	uint16_t h;
+
+	for (; len >= 4; b += 4, len -= 4) {
+		memcpy(&w, b, 4);
+		sum += w;
+	}
+	if (len >= 2) {
+		memcpy(&h, b, 2);
+		sum += h;
+		b += 2;
+		len -= 2;
+	}
+	if (len)
+		sum += *b;
+	sum = (sum >> 32) + (sum & 0xffffffffu);
+	sum = (sum >> 16) + (sum & 0xffffu);
+	return (uint16_t)((sum >> 16) + sum);
+}
+
+/* ---- odp_packet_parse on the GPU parser ------------------------------------
+ * odp_packet.c:1986-2075. The packets' bytes from `offset` are staged into
+ * one 64-byte aligned buffer and parsed by the classifier kernel with
+ * classification off, the batch's parse layer and the parameter's checksum
+ * options. A parse that starts at L3 (ODP_PROTO_IPV4 / IPV6) is staged
+ * behind a 14-byte Ethernet header carrying that ethertype; the L2 result
+ * of that header is then removed again (l2 / eth / jumbo flags, L2 offset),
+ * which is exactly the reference's state after _odp_packet_parse_common_l3_l4
+ * was called with that ethtype: every L3 / L4 check is relative to the
+ * parse offset and the frame's end, so the header in front changes none of
+ * them. Offsets are rebased to the packet. A packet fails (-1) when the
+ * parser returned non-zero, i.e. any error flag (or a drop) — as
+ * odp_packet_parse returns -1 on a non-zero _odp_packet_parse_common_l3_l4
+ * or _odp_packet_l4_chksum. Flags outside the error group are kept
+ * (packet_parse_reset(pkt_hdr, 0)). */
+static struct {
+	pthread_mutex_t lock;
+	odpg_table_t *tbl;         /* an empty rule table: parse only */
+	uint8_t *buf;
+	size_t cap;
+	odpg_desc_t *desc;
+	odpg_out_t *out;
+	odpg_meta_t *meta;
+	uint32_t n_cap;
+} prs = { PTHREAD_MUTEX_INITIALIZER, NULL, NULL, 0, NULL, NULL, NULL, 0 };
+
+static void parse_release(void)
+{
+	pthread_mutex_lock(&prs.lock);
+	if (prs.tbl)
+		odpg_table_destroy(prs.tbl);
+	prs.tbl = NULL;
+	free(prs.buf);
+	free(prs.desc);
+	free(prs.out);
+	free(prs.meta);
+	prs.buf = NULL;
+	prs.desc = NULL;
+	prs.out = NULL;
+	prs.meta = NULL;
+	prs.cap = 0;
+	prs.n_cap = 0;
+	pthread_mutex_unlock(&prs.lock);
+}
+
+#define ALIGN64(x) (((x) + 63u) & ~(size_t)63u)
+#define PARSE_FAKE_L2 14u
+
+static int parse_batch(const odp_packet_t pkt[], const uint32_t offset[], int num,
+		       const odp_packet_parse_param_t *param)
+{
+	const int l3start = param->proto != ODP_PROTO_ETH;
+	const uint32_t pre = l3start ? PARSE_FAKE_L2 : 0u;
+	uint16_t ethtype = 0xffffu;        /* unknown: not IPv4 / IPv6 / ARP / VLAN / SNAP */
+	uint64_t opt = 0;
+	size_t need = 0, off = 0;
+	int ok = 0;
+
+	if (num <= 0)
+		return 0;
+	if (param->proto == ODP_PROTO_NONE || param->last_layer == ODP_PROTO_LAYER_NONE)
+		return 0;                  /* the first packet fails */
+	if (param->proto == ODP_PROTO_IPV4)
+		ethtype = 0x0800;
+	else if (param->proto == ODP_PROTO_IPV6)
+		ethtype = 0x86dd;
+	if (param->chksums.chksum.ipv4)
+		opt |= ODPG_PKTIN_IPV4_CHKSUM;
+	if (param->chksums.chksum.udp)
+		opt |= ODPG_PKTIN_UDP_CHKSUM;
+	if (param->chksums.chksum.tcp)
+		opt |= ODPG_PKTIN_TCP_CHKSUM;
+	if (param->chksums.chksum.sctp)
+		opt |= ODPG_PKTIN_SCTP_CHKSUM;
+
+	/* stage up to the first packet whose offset is past its end (packet_map
+	 * fails: -1 before anything is parsed) */
+	int n = 0;
+
+	for (; n < num; n++) {
+		const rt_pkt_t *k = PK(pkt[n]);
+
+		if (offset[n] >= k->len)
+			break;
+		need += ALIGN64(pre + k->len - offset[n]);
+	}
+	if (n == 0)
+		return 0;
+	if (!rt.init && odp_init_global(NULL, NULL, NULL))
+		return -1;
+	pthread_mutex_lock(&prs.lock);
+	if (!prs.tbl) {
+		odpg_rules_t none;
+
+		memset(&none, 0, sizeof(none));
+		none.default_cos = -1;
+		none.error_cos = -1;
+		if (odpg_table_create(rt.ctx, &none, &prs.tbl)) {
+			pthread_mutex_unlock(&prs.lock);
+			return -1;
+		}
+	}
+	need += 128;
+	if (need > prs.cap) {
+		uint8_t *b = NULL;
+
+		if (posix_memalign((void **)&b, 64, need)) {
+			pthread_mutex_unlock(&prs.lock);
+			return -1;
+		}
+		free(prs.buf);
+		prs.buf = b;
+		prs.cap = need;
+	}
+	if ((uint32_t)n > prs.n_cap) {
+		free(prs.desc);
+		free(prs.out);
+		free(prs.meta);
+		prs.desc = malloc((size_t)n * sizeof(*prs.desc));
+		prs.out = malloc((size_t)n * sizeof(*prs.out));
+		prs.meta = malloc((size_t)n * sizeof(*prs.meta));
+		prs.n_cap = prs.desc && prs.out && prs.meta ? (uint32_t)n : 0;
+		if (!prs.n_cap) {
+			pthread_mutex_unlock(&prs.lock);
+			return -1;
+		}
+	}
+	for (int i = 0; i < n; i++) {
+		const rt_pkt_t *k = PK(pkt[i]);
+		uint8_t *d = prs.buf + off;
+		const uint32_t len = k->len - offset[i];
+
+		if (pre) {
+			memset(d, 0, 12);
+			d[0] = 0x02;               /* locally administered unicast */
+			d[12] = (uint8_t)(ethtype >> 8);
+			d[13] = (uint8_t)ethtype;
+		}
+		memcpy(d + pre, k->data + offset[i], len);
+		prs.desc[i].offset = (uint32_t)off;
+		prs.desc[i].len = pre + len;
+		off += ALIGN64(pre + len);
+	}
+	memset(prs.buf + off, 0, 128);
+
+	odpg_batch_t b;
+	odpg_result_t r;
+
+	memset(&b, 0, sizeof(b));
+	memset(&r, 0, sizeof(r));
+	b.frames = prs.buf;
+	b.desc = prs.desc;
+	b.num = (uint32_t)n;
+	b.pktin_opt = opt;
+	b.layer = (uint32_t)param->last_layer;
+	b.classify = 0;
+	r.out = prs.out;
+	r.meta = prs.meta;
+	if (odpg_classify_host(rt.ctx, prs.tbl, &b, &r, 0)) {
+		pthread_mutex_unlock(&prs.lock);
+		return -1;
+	}
+	for (int i = 0; i < n; i++) {
+		rt_pkt_t *k = PK(pkt[i]);
+		odpg_meta_t m = prs.meta[i];
+		const uint32_t base = offset[i];
+
+		if (l3start) {
+			m.input_flags &= ~((1ull << IF_L2) | (1ull << IF_ETH) | (1ull << IF_JUMBO) |
+					   (1ull << IF_ETH_BCAST) | (1ull << IF_ETH_MCAST));
+			m.l2_offset = 0xffff;
+		} else if (m.l2_offset != 0xffff) {
+			m.l2_offset = (uint16_t)(m.l2_offset + base);
+		}
+		if (m.l3_offset != 0xffff)
+			m.l3_offset = (uint16_t)(m.l3_offset - pre + base);
+		if (m.l4_offset != 0xffff)
+			m.l4_offset = (uint16_t)(m.l4_offset - pre + base);
+		m.flags = (k->meta.flags & ~F_ERROR_MASK) | (m.flags & F_ERROR_MASK);
+		m.cls_mark = 0;
+		m.reserved = 0;
+		k->meta = m;
+		if (prs.out[i] & ODPG_OUT_PARSE_ERR)
+			break;                     /* odp_packet_parse returned -1 */
+		ok++;
+	}
+	pthread_mutex_unlock(&prs.lock);
+	return ok;
+}
+
+int odp_packet_parse(odp_packet_t pkt, uint32_t offset, const odp_packet_parse_param_t *param)
+{
+	const int r = parse_batch(&pkt, &offset, 1, param);
+
+	return r == 1 ? 0 : -1;
+}
+
+int odp_packet_parse_multi(const odp_packet_t pkt[], const uint32_t offset[], int num,
+			   const odp_packet_parse_param_t *param)
+{
+	const int r = parse_batch(pkt, offset, num, param);
+
+	return r < 0 ? -1 : r;
+}
+
+/* odp_packet.c:2077-2126 */
+void odp_packet_parse_result(odp_packet_t pkt, odp_packet_parse_result_t *res)
+{
+	res->flag.all = 0;
+	res->flag.has_error = odp_packet_has_error(pkt);
+	res->flag.has_l2_error = odp_packet_has_l2_error(pkt);
+	res->flag.has_l3_error = odp_packet_has_l3_error(pkt);
+	res->flag.has_l4_error = odp_packet_has_l4_error(pkt);
+	res->flag.has_l2 = odp_packet_has_l2(pkt);
+	res->flag.has_l3 = odp_packet_has_l3(pkt);
+	res->flag.has_l4 = odp_packet_has_l4(pkt);
+	res->flag.has_eth = odp_packet_has_eth(pkt);
+	res->flag.has_eth_bcast = odp_packet_has_eth_bcast(pkt);
+	res->flag.has_eth_mcast = odp_packet_has_eth_mcast(pkt);
+	res->flag.has_jumbo = odp_packet_has_jumbo(pkt);
+	res->flag.has_vlan = odp_packet_has_vlan(pkt);
+	res->flag.has_vlan_qinq = odp_packet_has_vlan_qinq(pkt);
+	res->flag.has_arp = odp_packet_has_arp(pkt);
+	res->flag.has_ipv4 = odp_packet_has_ipv4(pkt);
+	res->flag.has_ipv6 = odp_packet_has_ipv6(pkt);
+	res->flag.has_ip_bcast = odp_packet_has_ip_bcast(pkt);
+	res->flag.has_ip_mcast = odp_packet_has_ip_mcast(pkt);
+	res->flag.has_ipfrag = odp_packet_has_ipfrag(pkt);
+	res->flag.has_ipopt = odp_packet_has_ipopt(pkt);
+	res->flag.has_ipsec = odp_packet_has_ipsec(pkt);
+	res->flag.has_udp = odp_packet_has_udp(pkt);
+	res->flag.has_tcp = odp_packet_has_tcp(pkt);
+	res->flag.has_sctp = odp_packet_has_sctp(pkt);
+	res->flag.has_icmp = odp_packet_has_icmp(pkt);
+	res->packet_len = odp_packet_len(pkt);
+	res->l2_offset = odp_packet_l2_offset(pkt);
+	res->l3_offset = odp_packet_l3_offset(pkt);
+	res->l4_offset = odp_packet_l4_offset(pkt);
+	res->l3_chksum_status = odp_packet_l3_chksum_status(pkt);
+	res->l4_chksum_status = odp_packet_l4_chksum_status(pkt);
+	res->l2_type = odp_packet_l2_type(pkt);
+	res->l3_type = odp_packet_l3_type(pkt);
+	res->l4_type = odp_packet_l4_type(pkt);
+}
+
+void odp_packet_parse_result_multi(const odp_packet_t pkt[], odp_packet_parse_result_t *result[],
+				   int num)
+{
+	for (int i = 0; i < num; i++)
+		odp_packet_parse_result(pkt[i], result[i]);
+}
+
+/* ---- queues: a registry of tagged handles ---------------------------------- */
 static int pktout_send_impl(odp_pktio_t pktio, const odp_packet_t packets[], int num);
 static void pktin_queue_fill(odp_pktio_t pktio);
 
+#define QH_TAG      0x0DD0000000000000ull  /* no user-space pointer has these bits */
+#define QH_TAG_MASK 0xFFFF000000000000ull
+#define QCHUNK      4096u
+#define QCHUNKS     256u                   /* up to 1 M queues */
+
+static struct {
+	pthread_mutex_t lock;
+	rt_queue_t **chunk[QCHUNKS];
+	uint32_t num;              /* slots handed out (published with release) */
+} qreg = { PTHREAD_MUTEX_INITIALIZER, {0}, 0 };
+
+static rt_queue_t *queue_slot(odp_queue_t q)
+{
+	const uint64_t v = (uint64_t)(uintptr_t)q;
+
+	if ((v & QH_TAG_MASK) != QH_TAG)
+		return NULL;
+	const uint64_t idx = (v & ~QH_TAG_MASK) - 1u;
+
+	if (idx >= __atomic_load_n(&qreg.num, __ATOMIC_ACQUIRE))
+		return NULL;
+	return qreg.chunk[idx / QCHUNK][idx % QCHUNK];
+}
+
 static rt_queue_t *get_queue(odp_queue_t q)
 {
-	rt_queue_t *x = (rt_queue_t *)q;
+	rt_queue_t *x = queue_slot(q);
 
-	/* the classifier's own hash-queue handles are small integers */
-	if (!x || (uintptr_t)x < 0x100000000ull || x->magic != QUEUE_MAGIC || x->dead)
+	if (!x || x->magic != QUEUE_MAGIC || x->dead)
 		return NULL;
 	return x;
 }
 
-odp_queue_t odp_queue_create(const char *name, const odp_queue_param_t *param)
+static rt_queue_t *queue_new(const char *name, const odp_queue_param_t *param)
 {
 	rt_queue_t *q = calloc(1, sizeof(*q));
 
 	if (!q)
-		return ODP_QUEUE_INVALID;
+		return NULL;
+	pthread_mutex_lock(&qreg.lock);
+	const uint32_t idx = qreg.num;
+
+	if (idx >= QCHUNK * QCHUNKS ||
+	    (!qreg.chunk[idx / QCHUNK] &&
+	     !(qreg.chunk[idx / QCHUNK] = calloc(QCHUNK, sizeof(rt_queue_t *))))) {
+		pthread_mutex_unlock(&qreg.lock);
+		free(q);
+		ERR("queue registry full\n");
+		return NULL;
+	}
 	q->magic = QUEUE_MAGIC;
+	q->hdl = (odp_queue_t)(uintptr_t)(QH_TAG | (uint64_t)(idx + 1u));
 	snprintf(q->name, sizeof(q->name), "%s", name ? name : "");
 	if (param)
 		q->param = *param;
 	else
 		odp_queue_param_init(&q->param);
 	pthread_mutex_init(&q->lock, NULL);
+	qreg.chunk[idx / QCHUNK][idx % QCHUNK] = q;
+	__atomic_store_n(&qreg.num, idx + 1u, __ATOMIC_RELEASE);
+	pthread_mutex_unlock(&qreg.lock);
 	if (q->param.type == ODP_QUEUE_TYPE_SCHED) {
 		pthread_mutex_lock(&rt.lock);
 		q->next_sched = rt.sched;
 		rt.sched = q;
 		pthread_mutex_unlock(&rt.lock);
 	}
-	return (odp_queue_t)q;
+	return q;
 }
 
+odp_queue_t odp_queue_create(const char *name, const odp_queue_param_t *param)
+{
+	rt_queue_t *q = queue_new(name, param);
+
+	return q ? q->hdl : ODP_QUEUE_INVALID;
+}
+
+/* a destroyed queue stays in the registry (schedulers may still hold it);
+ * its handle stops being a queue */
 int odp_queue_destroy(odp_queue_t queue)
 {
 	rt_queue_t *q = get_queue(queue);
@@ -753,7 +1437,7 @@ int odp_queue_destroy(odp_queue_t queue)
 		ERR("queue '%s' not empty\n", q->name);
 		return -1;
 	}
-	q->dead = 1;      /* stays linked: schedulers may still hold it */
+	q->dead = 1;
 	pthread_mutex_unlock(&q->lock);
 	return 0;
 }
@@ -769,59 +1453,64 @@ int odp_queue_info(odp_queue_t queue, odp_queue_info_t *info)
 	return 0;
 }
 
-int odp_queue_enq(odp_queue_t queue, odp_event_t ev)
+odp_queue_type_t odp_queue_type(odp_queue_t queue)
 {
 	rt_queue_t *q = get_queue(queue);
-	rt_pkt_t *k = (rt_pkt_t *)ev;
 
-	if (!q || !k)
-		return -1;
-	if (q->pktout) {                    /* pktout event queue: transmit */
-		const odp_packet_t pkt = (odp_packet_t)k;
+	return q ? q->param.type : ODP_QUEUE_TYPE_PLAIN;
+}
 
-		return pktout_send_impl(q->pktout, &pkt, 1) == 1 ? 0 : -1;
-	}
-	k->next = NULL;
+uint64_t odp_queue_to_u64(odp_queue_t queue)
+{
+	return (uint64_t)(uintptr_t)queue;
+}
+
+/* link a chain of packets at the queue's tail */
+static void queue_append(rt_queue_t *q, rt_pkt_t *first, rt_pkt_t *last)
+{
+	last->next = NULL;
 	pthread_mutex_lock(&q->lock);
 	if (q->tail)
-		q->tail->next = k;
+		q->tail->next = first;
 	else
-		q->head = k;
-	q->tail = k;
+		q->head = first;
+	q->tail = last;
 	pthread_mutex_unlock(&q->lock);
-	return 0;
 }
 
-odp_event_t odp_queue_deq(odp_queue_t queue)
+int odp_queue_enq(odp_queue_t queue, odp_event_t ev)
 {
-	rt_queue_t *q = get_queue(queue);
-	rt_pkt_t *k;
-
-	if (!q)
-		return ODP_EVENT_INVALID;
-	if (q->pktin && !__atomic_load_n(&q->head, __ATOMIC_RELAXED))
-		pktin_queue_fill(q->pktin);     /* QUEUE mode: receive a burst */
-	pthread_mutex_lock(&q->lock);
-	k = q->head;
-	if (k) {
-		q->head = k->next;
-		if (!q->head)
-			q->tail = NULL;
-	}
-	pthread_mutex_unlock(&q->lock);
-	return (odp_event_t)k;
+	return odp_queue_enq_multi(queue, &ev, 1) == 1 ? 0 : -1;
 }
 
+/* all num events in one append (queue_basic.c enq_multi), or -1 */
 int odp_queue_enq_multi(odp_queue_t queue, const odp_event_t ev[], int num)
 {
-	int n = 0;
+	rt_queue_t *q = get_queue(queue);
 
-	while (n < num && odp_queue_enq(queue, ev[n]) == 0)
-		n++;
-	return n ? n : (num > 0 ? -1 : 0);
+	if (!q || num < 0)
+		return -1;
+	if (num == 0)
+		return 0;
+	for (int i = 0; i < num; i++)
+		if (!ev[i])
+			return -1;
+	if (q->pktout)                  /* pktout event queue: transmit */
+		return pktout_send_impl(q->pktout, (const odp_packet_t *)ev, num);
+	for (int i = 0; i + 1 < num; i++)
+		((rt_pkt_t *)ev[i])->next = (rt_pkt_t *)ev[i + 1];
+	queue_append(q, (rt_pkt_t *)ev[0], (rt_pkt_t *)ev[num - 1]);
+	return num;
 }
 
 static int deq_multi(rt_queue_t *q, odp_event_t ev[], int num);
+
+odp_event_t odp_queue_deq(odp_queue_t queue)
+{
+	odp_event_t ev = ODP_EVENT_INVALID;
+
+	return odp_queue_deq_multi(queue, &ev, 1) == 1 ? ev : ODP_EVENT_INVALID;
+}
 
 int odp_queue_deq_multi(odp_queue_t queue, odp_event_t ev[], int num)
 {
@@ -830,7 +1519,7 @@ int odp_queue_deq_multi(odp_queue_t queue, odp_event_t ev[], int num)
 	if (!q)
 		return -1;
 	if (q->pktin && !__atomic_load_n(&q->head, __ATOMIC_RELAXED))
-		pktin_queue_fill(q->pktin);
+		pktin_queue_fill(q->pktin);     /* QUEUE mode: receive a burst */
 	return deq_multi(q, ev, num);
 }
 
@@ -894,7 +1583,7 @@ static void pktio_queue_kill(rt_queue_t *q)
 }
 
 /* "loop[...]" (pktio/loop.c) or "pcap:in=<file>[:loops=<n>]" (pktio/pcap.c's
- * device string) */
+ * device string, _pcapif_parse_devname) */
 int odpg_rt_pktio_open(odp_pktio_t hdl, const char *name, odp_pool_t pool,
 		       const odp_pktio_param_t *param)
 {
@@ -913,7 +1602,8 @@ int odpg_rt_pktio_open(odp_pktio_t hdl, const char *name, odp_pool_t pool,
 	p = &rt.pktio[n - 1];
 	memset(p, 0, sizeof(*p));
 	p->valid = 1;
-	p->loops = 1;
+	p->loops = 1;                       /* pcapif_init: loops = 1, loop_cnt = 1 */
+	p->loop_cnt = 1;
 	p->in_mode = param->in_mode;
 	p->out_mode = param->out_mode;
 	p->pool = pool;
@@ -995,7 +1685,7 @@ int odpg_rt_pktin_config(odp_pktio_t hdl, uint32_t num_queues)
 	odp_queue_param_init(&qp);
 	qp.type = p->in_mode == ODP_PKTIN_MODE_SCHED ? ODP_QUEUE_TYPE_SCHED : ODP_QUEUE_TYPE_PLAIN;
 	snprintf(name, sizeof(name), "odp-pktin-%u-0", (unsigned)(uintptr_t)hdl);
-	p->inq = (rt_queue_t *)odp_queue_create(name, &qp);
+	p->inq = queue_new(name, &qp);
 	if (!p->inq)
 		return -1;
 	if (p->in_mode == ODP_PKTIN_MODE_QUEUE)
@@ -1019,7 +1709,24 @@ static odp_queue_t dest_queue(uint32_t w, odp_cos_t *cos)
 	return n == 1 ? qs[0] : qs[ODPG_OUT_HASHQ(w) % n];
 }
 
-#define ALIGN64(x) (((x) + 63u) & ~(size_t)63u)
+/* _odp_cos_enq (odp_classification_internal.h:139-156): a run of packets
+ * for one (CoS, queue) in one odp_queue_enq_multi; what is not enqueued is
+ * freed and counted as the queue's discards (the kernel counted the run as
+ * delivered) */
+static void cos_enq(odp_cos_t cos, odp_queue_t q, odp_packet_t run[], int num)
+{
+	int ret;
+
+	if (num <= 0)
+		return;
+	ret = odp_queue_enq_multi(q, (const odp_event_t *)run, num);
+	if (ret < 0)
+		ret = 0;
+	if (ret != num) {
+		odp_packet_free_multi(&run[ret], num - ret);
+		odpg_cls_queue_count(cos, q, -(int64_t)(num - ret), (uint64_t)(num - ret));
+	}
+}
 
 /* One burst of the pktio's input through the GPU classifier (loopback_recv,
  * pktio/loop.c:304-374; pcapif_recv_pkt + the same classify step). Packets
@@ -1030,8 +1737,12 @@ static odp_queue_t dest_queue(uint32_t w, odp_cos_t *cos)
 static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num, int *nret)
 {
 	rt_pkt_t *src[RT_BURST];
+	odp_packet_t run[RT_BURST];
 	const uint8_t *frames;
 	uint32_t n = 0, first = 0;
+	int nrun = 0;
+	odp_cos_t run_cos = ODP_COS_INVALID;
+	odp_queue_t run_q = ODP_QUEUE_INVALID;
 
 	*nret = 0;
 	if (num > RT_BURST)
@@ -1074,9 +1785,10 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 		frames = p->stage;
 	} else if (p->have_cap) {
 		if (p->pos >= p->cap.num) {
-			if (p->loops != 0 && p->loop + 1 >= p->loops)
+			/* _pcapif_reopen: loops = 0 repeats forever, else the
+			 * capture is read again while ++loop_cnt < loops */
+			if (p->loops != 0 && ++p->loop_cnt >= p->loops)
 				return 0;
-			p->loop++;
 			p->pos = 0;
 		}
 		first = p->pos;
@@ -1108,7 +1820,7 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 
 		if (ODPG_OUT_COS(w) != ODPG_COS_NOCLS) {
 			q = dest_queue(w, &cos);
-			if (q == ODP_QUEUE_INVALID || !get_queue(q)) {
+			if (q == ODP_QUEUE_INVALID) {
 				if (have)                 /* no CoS / drop / parse drop */
 					odp_packet_free((odp_packet_t)have);
 				continue;
@@ -1126,21 +1838,34 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 			if (have)
 				odp_packet_free((odp_packet_t)have);
 			if (pkt == ODP_PACKET_INVALID) {
+				/* loop.c:320-326: in_discards, and never counted
+				 * as received nor handed to the CoS queue */
 				const int counted = !(w & ODPG_OUT_ERROR);
 
 				odpg_cls_pktio_count(hdl, counted ? -1 : 0,
 						     counted ? -(int64_t)len : 0, 1, 0, 0);
+				if (q != ODP_QUEUE_INVALID)
+					odpg_cls_queue_count(cos, q, -1, 0);
 				continue;
 			}
 		}
 		PK(pkt)->meta = rt.meta[k];
 		PK(pkt)->cos = cos;
+		PK(pkt)->input = hdl;
 		if (q == ODP_QUEUE_INVALID) {
 			pkts[(*nret)++] = pkt;
-		} else if (odp_queue_enq(q, (odp_event_t)pkt)) {
-			odp_packet_free(pkt);
+			continue;
 		}
+		/* _odp_cls_enq: runs of the same (CoS, queue) */
+		if (nrun && (q != run_q || cos != run_cos)) {
+			cos_enq(run_cos, run_q, run, nrun);
+			nrun = 0;
+		}
+		run_cos = cos;
+		run_q = q;
+		run[nrun++] = pkt;
 	}
+	cos_enq(run_cos, run_q, run, nrun);
 	return (int)n;
 }
 
@@ -1151,9 +1876,9 @@ static int rx_to_inq(rt_pktio_t *p, odp_pktio_t hdl)
 	int nret;
 	const int took = rx_burst(p, hdl, pkts, RT_BURST, &nret);
 
-	for (int k = 0; k < nret; k++)
-		if (!p->inq || odp_queue_enq((odp_queue_t)p->inq, (odp_event_t)pkts[k]))
-			odp_packet_free(pkts[k]);
+	if (nret > 0 && (!p->inq || odp_queue_enq_multi(p->inq->hdl, (const odp_event_t *)pkts,
+							 nret) != nret))
+		odp_packet_free_multi(pkts, nret);
 	return took;
 }
 
@@ -1219,7 +1944,7 @@ int odp_pktin_event_queue(odp_pktio_t pktio, odp_queue_t queues[], int num)
 	if (p->in_mode != ODP_PKTIN_MODE_QUEUE && p->in_mode != ODP_PKTIN_MODE_SCHED)
 		return -1;
 	if (queues && num > 0 && p->inq)
-		queues[0] = (odp_queue_t)p->inq;
+		queues[0] = p->inq->hdl;
 	return p->inq ? 1 : 0;
 }
 
@@ -1289,7 +2014,7 @@ int odp_pktin_event_queue_stats(odp_pktio_t pktio, odp_queue_t queue,
 	rt_pktio_t *p = get_rt_pktio(pktio);
 
 	if (!p || (p->in_mode != ODP_PKTIN_MODE_SCHED && p->in_mode != ODP_PKTIN_MODE_QUEUE) ||
-	    !p->inq || queue != (odp_queue_t)p->inq)
+	    !p->inq || queue != p->inq->hdl)
 		return -1;
 	return in_queue_stats(pktio, 0, stats);
 }
@@ -1303,7 +2028,7 @@ int odp_schedule_capability(odp_schedule_capability_t *capa)
 	memset(capa, 0, sizeof(*capa));
 	capa->max_prios = 1;
 	capa->max_groups = 1;
-	capa->max_queues = 1u << 20;
+	capa->max_queues = QCHUNK * QCHUNKS;
 	capa->max_queue_size = 0;          /* no limit */
 	capa->lockfree_queues = ODP_SUPPORT_NO;
 	capa->waitfree_queues = ODP_SUPPORT_NO;
@@ -1354,7 +2079,7 @@ static int sched_once(odp_queue_t *from, odp_event_t ev[], int num)
 
 		if (n) {
 			if (from)
-				*from = (odp_queue_t)q;
+				*from = q->hdl;
 			return n;
 		}
 	}
@@ -1440,7 +2165,7 @@ int odp_pktout_queue_config(odp_pktio_t pktio, const odp_pktout_queue_param_t *p
 	pktio_queue_kill(p->outq);
 	odp_queue_param_init(&qp);
 	snprintf(name, sizeof(name), "odp-pktout-%u-0", (unsigned)(uintptr_t)pktio);
-	p->outq = (rt_queue_t *)odp_queue_create(name, &qp);
+	p->outq = queue_new(name, &qp);
 	if (!p->outq)
 		return -1;
 	p->outq->pktout = pktio;
@@ -1477,7 +2202,7 @@ int odp_pktout_event_queue(odp_pktio_t pktio, odp_queue_t queues[], int num)
 	if (p->out_mode != ODP_PKTOUT_MODE_QUEUE)
 		return -1;
 	if (queues && num > 0 && p->outq)
-		queues[0] = (odp_queue_t)p->outq;
+		queues[0] = p->outq->hdl;
 	return p->outq ? 1 : 0;
 }
 
@@ -1553,7 +2278,7 @@ int odp_pktout_event_queue_stats(odp_pktio_t pktio, odp_queue_t queue,
 	rt_pktio_t *p = get_rt_pktio(pktio);
 
 	if (!p || p->out_mode != ODP_PKTOUT_MODE_QUEUE || !p->outq ||
-	    queue != (odp_queue_t)p->outq)
+	    queue != p->outq->hdl)
 		return -1;
 	return out_queue_stats(pktio, 0, stats);
 }
@@ -1683,14 +2408,14 @@ int odph_thread_join(odph_thread_t thread[], int num)
 	return n;
 }
 
-/* "aa:bb:cc:dd:ee:ff" (helper/eth.c odph_eth_addr_parse) */
+/* "aa:bb:cc:dd:ee:ff" (helper/eth.c odph_eth_addr_parse: sscanf, trailing
+ * characters ignored) */
 int odph_eth_addr_parse(odph_ethaddr_t *mac, const char *str)
 {
 	unsigned b[6];
-	char tail;
 
-	if (!str || sscanf(str, "%x:%x:%x:%x:%x:%x%c", &b[0], &b[1], &b[2], &b[3], &b[4], &b[5],
-			   &tail) != 6)
+	if (!str || sscanf(str, "%x:%x:%x:%x:%x:%x", &b[0], &b[1], &b[2], &b[3], &b[4],
+			   &b[5]) != 6)
 		return -1;
 	for (int i = 0; i < 6; i++) {
 		if (b[i] > 255)
@@ -1700,19 +2425,62 @@ int odph_eth_addr_parse(odph_ethaddr_t *mac, const char *str)
 	return 0;
 }
 
-/* "a.b.c.d" in host byte order (helper/ip.c odph_ipv4_addr_parse) */
+/* "a.b.c.d" in host byte order (helper/ip.c odph_ipv4_addr_parse: sscanf,
+ * trailing characters ignored) */
 int odph_ipv4_addr_parse(uint32_t *ip_addr, const char *str)
 {
 	unsigned b[4];
-	char tail;
 
-	if (!str || sscanf(str, "%u.%u.%u.%u%c", &b[0], &b[1], &b[2], &b[3], &tail) != 4)
+	if (!str || sscanf(str, "%u.%u.%u.%u", &b[0], &b[1], &b[2], &b[3]) != 4)
 		return -1;
 	for (int i = 0; i < 4; i++)
 		if (b[i] > 255)
 			return -1;
 	*ip_addr = (b[0] << 24) | (b[1] << 16) | (b[2] << 8) | b[3];
 	return 0;
+}
+
+/* odph_ipv4_csum (helper ip.h:98-131): the header's ihl * 4 bytes with the
+ * checksum field zeroed; < 0 when ihl < 5 or the header leaves the packet */
+static int ipv4_csum(odp_packet_t pkt, uint32_t l3, uint16_t *sum)
+{
+	uint8_t hdr[60];
+	uint32_t hl;
+
+	if (l3 == ODP_PACKET_OFFSET_INVALID ||
+	    odp_packet_copy_to_mem(pkt, l3, ODPH_IPV4HDR_LEN, hdr))
+		return -1;
+	hl = (uint32_t)ODPH_IPV4HDR_IHL(hdr[0]) * 4u;
+	if (hl < ODPH_IPV4HDR_LEN)
+		return -1;
+	if (hl > ODPH_IPV4HDR_LEN &&
+	    odp_packet_copy_to_mem(pkt, l3 + ODPH_IPV4HDR_LEN, hl - ODPH_IPV4HDR_LEN,
+				   hdr + ODPH_IPV4HDR_LEN))
+		return -1;
+	hdr[ODPH_IPV4HDR_CSUM_OFFSET] = hdr[ODPH_IPV4HDR_CSUM_OFFSET + 1] = 0;
+	*sum = (uint16_t)~odp_chksum_ones_comp16(hdr, hl);
+	return 0;
+}
+
+int odph_ipv4_csum_update(odp_packet_t pkt)
+{
+	const uint32_t l3 = odp_packet_l3_offset(pkt);
+	uint16_t sum;
+
+	if (ipv4_csum(pkt, l3, &sum))
+		return -1;
+	return odp_packet_copy_from_mem(pkt, l3 + ODPH_IPV4HDR_CSUM_OFFSET, 2, &sum);
+}
+
+int odph_ipv4_csum_valid(odp_packet_t pkt)
+{
+	const uint32_t l3 = odp_packet_l3_offset(pkt);
+	uint16_t sum, cur;
+
+	if (ipv4_csum(pkt, l3, &sum) ||
+	    odp_packet_copy_to_mem(pkt, l3 + ODPH_IPV4HDR_CSUM_OFFSET, 2, &cur))
+		return 0;
+	return sum == cur;
 }
 
 char *odph_strcpy(char *dst, const char *src, size_t sz)

@@ -2,6 +2,12 @@
  *
  * Private seam between the classifier object model (odp_cls.c) and the ODP
  * runtime subset (odp_rt.c), both inside libodpg.so.
+ *
+ * Lock order: odp_rt.c's poll lock (held across a receive burst) may be
+ * held while odp_cls.c's lock is taken, never the other way round; odp_cls.c
+ * calls back into odp_rt.c only for queue creation / destruction (the
+ * runtime's queue registry lock) and, with its lock released, to close a
+ * pktio's receive state.
  */
 #ifndef ODP_RT_INTERNAL_H_
 #define ODP_RT_INTERNAL_H_
@@ -29,5 +35,12 @@ int odpg_cls_pktio_classifies(odp_pktio_t pktio);
  * _odp_pktio_packet_to_pool branch), and transmits */
 void odpg_cls_pktio_count(odp_pktio_t pktio, int64_t in_packets, int64_t in_octets,
 			  uint64_t in_discards, uint64_t out_packets, uint64_t out_octets);
+/* per-queue counters of a CoS the kernel cannot know: packets it counted as
+ * delivered to `queue` that the runtime could not enqueue (_odp_cos_enq's
+ * failed odp_queue_enq_multi -> _odp_cos_queue_stats_add(cos, dst, ret,
+ * num - ret), odp_classification_internal.h:139-156) or did not hand to the
+ * queue at all (pool copy failure) */
+void odpg_cls_queue_count(odp_cos_t cos, odp_queue_t queue, int64_t packets,
+			  uint64_t discards);
 
 #endif

@@ -210,16 +210,17 @@ static uint16_t parse_eth(hdr_t *prs, const pv_t *v, uint32_t *offset, uint32_t 
 {
 	uint64_t inf = IFB(IF_L2) | IFB(IF_ETH);
 	uint16_t ethtype;
-	uint16_t mac0 = be16(v, 0);
+	const uint32_t s = *offset;        /* 0 on receive; odp_packet_parse's offset */
+	uint16_t mac0 = be16(v, s);
 
 	if (frame_len - *offset > ETH_LEN_MAX)
 		inf |= IFB(IF_JUMBO);
 	if ((mac0 & 0x0100) == 0x0100)
 		inf |= IFB(IF_ETH_MCAST);
-	if (mac0 == 0xffff && be16(v, 2) == 0xffff && be16(v, 4) == 0xffff)
+	if (mac0 == 0xffff && be16(v, s + 2) == 0xffff && be16(v, s + 4) == 0xffff)
 		inf |= IFB(IF_ETH_BCAST);
 
-	ethtype = be16(v, 12);
+	ethtype = be16(v, s + 12);
 	*offset += 14;
 
 	if (ethtype < ETH_LEN_MAX) {                       /* SNAP, :61-71 */
@@ -564,6 +565,59 @@ static int parse_common(hdr_t *h, const pv_t *v, uint32_t seg_len, int layer, ui
 	if (!r && layer >= LAYER_L4)
 		r = l4_chksum(h, v, opt, l4_part_sum);
 	return r;
+}
+
+/* ---- odp_packet_parse (odp_packet.c:1986-2052) -------------------------
+ * One single-segment packet parsed from `offset`, starting with protocol
+ * `proto` (odp_proto_t: 1 ETH, 2 IPV4, 3 IPV6, else none known) up to
+ * `layer`, with the odp_proto_chksums_t bits `chksums` (ipv4, udp, tcp,
+ * sctp) as the checksum options. *meta is updated in place as the packet
+ * header is: packet_parse_reset(pkt_hdr, 0) keeps the non-error flags.
+ * Returns 0, or -1 as odp_packet_parse does. */
+static int packet_parse(const pv_t *v, uint32_t offset, int proto, int layer, uint32_t chksums,
+			odpg_meta_t *meta)
+{
+	hdr_t h;
+	uint64_t opt = 0, l4_part_sum = 0;
+	uint16_t ethtype;
+	int ret;
+
+	if (proto == 0 || layer == LAYER_NONE)
+		return -1;
+	if (offset >= v->len)                      /* packet_map: no data there */
+		return -1;
+	memset(&h, 0, sizeof(h));
+	h.l2_offset = h.l3_offset = h.l4_offset = OFFSET_INVALID;
+	h.flags = meta->flags & ~F_ERROR_MASK;
+	if (chksums & 1u)
+		opt |= ODPG_PKTIN_IPV4_CHKSUM;
+	if (chksums & 2u)
+		opt |= ODPG_PKTIN_UDP_CHKSUM;
+	if (chksums & 4u)
+		opt |= ODPG_PKTIN_TCP_CHKSUM;
+	if (chksums & 8u)
+		opt |= ODPG_PKTIN_SCTP_CHKSUM;
+	if (proto == 1) {
+		h.l2_offset = (uint16_t)offset;
+		ethtype = parse_eth(&h, v, &offset, v->len);
+	} else if (proto == 2) {
+		ethtype = ETHTYPE_IPV4;
+	} else if (proto == 3) {
+		ethtype = ETHTYPE_IPV6;
+	} else {
+		ethtype = 0;
+	}
+	ret = parse_l3_l4(&h, v, offset, v->len, v->len, layer, ethtype, &l4_part_sum, opt);
+	if (!ret && layer >= LAYER_L4)
+		ret = l4_chksum(&h, v, opt, l4_part_sum);
+	meta->input_flags = h.input_flags;
+	meta->flags = h.flags;
+	meta->l2_offset = h.l2_offset;
+	meta->l3_offset = h.l3_offset;
+	meta->l4_offset = h.l4_offset;
+	meta->cls_mark = 0;
+	meta->reserved = 0;
+	return ret ? -1 : 0;
 }
 
 /* ---- verify_pmr and the per-term matchers (odp_classification.c:906-1490) */
@@ -1067,6 +1121,24 @@ int oracle_classify_mt(const odpg_rules_t *rules, const uint8_t *frames,
 /* Exposed for the checksum known-answer tests (test/validation/api/chksum):
  * odp_chksum_ones_comp16() == chksum_finalize(chksum_partial(p, len, 0))
  * (odp_chksum.c:11). */
+/* odp_packet_parse_multi (odp_packet.c:2064-2075) over a batch: returns
+ * the index of the first packet that fails (num if none); packets after it
+ * are not touched. ret[i] gets each parsed packet's return value. */
+int oracle_packet_parse_multi(const uint8_t *frames, const odpg_desc_t *desc, uint32_t num,
+			      const uint32_t *offset, int proto, int layer, uint32_t chksums,
+			      odpg_meta_t *meta, int32_t *ret)
+{
+	pthread_once(&crc_once, crc_init);
+	for (uint32_t i = 0; i < num; i++) {
+		pv_t v = { frames + desc[i].offset, desc[i].len };
+
+		ret[i] = packet_parse(&v, offset[i], proto, layer, chksums, &meta[i]);
+		if (ret[i])
+			return (int)i;
+	}
+	return (int)num;
+}
+
 uint16_t oracle_chksum_ones_comp16(const uint8_t *p, uint32_t len)
 {
 	return chksum_finalize(chksum_partial_mem(p, len, 0));

@@ -41,6 +41,8 @@ def _load():
     lib.oracle_l3fwd.argtypes = [vp, u32, vp, vp, u32, u32, i32, i32, vp]
     lib.oracle_tx_prepare.restype = i32
     lib.oracle_tx_prepare.argtypes = [vp, vp, u32, u32, vp, vp, vp]
+    lib.oracle_packet_parse_multi.restype = i32
+    lib.oracle_packet_parse_multi.argtypes = [vp, vp, u32, vp, i32, i32, u32, vp, vp]
     lib.oracle_fib_lookup.restype = i32
     lib.oracle_fib_lookup.argtypes = [vp, u32, vp, u32, vp, vp]
     return lib
@@ -90,6 +92,22 @@ def classify_mt(rules, frames, num, stride=0, desc=None, opt=0, layer=4, classif
                                layer, int(bool(classify)), out.ctypes.data, nthreads, reps,
                                cp.ctypes.data if cp is not None else None)
     return out, n
+
+
+def packet_parse_multi(frames, desc, offsets, proto, layer, chksums, meta):
+    """odp_packet_parse_multi restated (odp_packet.c:1986-2075): parses from
+    offsets[i] with odp_proto_t `proto` up to `layer`, checksum bits
+    (ipv4 1, udp 2, tcp 4, sctp 8). `meta` (META_DT, updated in place) holds
+    each packet's metadata before the call. Returns (first failing index or
+    num, per-packet return values)."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    desc = np.ascontiguousarray(desc, dtype=DESC_DT)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint32)
+    ret = np.zeros(len(desc), np.int32)
+    n = lib.oracle_packet_parse_multi(frames.ctypes.data, desc.ctypes.data, len(desc),
+                                      offs.ctypes.data, proto, layer, chksums,
+                                      meta.ctypes.data, ret.ctypes.data)
+    return n, ret
 
 
 def ones_comp16(data: bytes) -> int:

@@ -14,7 +14,8 @@ HDRS    := ../include/odp_api.h ../include/odp/rt.h ../include/odp/helper/odph_a
 LINK    := -L$(LIB) -lodpg -Wl,-rpath,'$$ORIGIN/../../odp_amd/lib' -L/opt/rocm/lib \
 	   -Wl,-rpath,/opt/rocm/lib
 APPS    := $(if $(wildcard $(REF)/example/classifier/odp_classifier.c),$(OUT)/odp_classifier) \
-	   $(if $(wildcard $(REF)/test/performance/odp_bench_pktio_sp.c),$(OUT)/odp_bench_pktio_sp)
+	   $(if $(wildcard $(REF)/test/performance/odp_bench_pktio_sp.c),$(OUT)/odp_bench_pktio_sp) \
+	   $(if $(wildcard $(REF)/test/performance/odp_pktio_perf.c),$(OUT)/odp_pktio_perf)
 # test/performance/odp_bench_pktio_sp.c with its two test/common sources
 BENCH_SP := $(REF)/test/performance/odp_bench_pktio_sp.c $(REF)/test/common/bench_common.c \
 	    $(REF)/test/common/export_results.c
@@ -29,7 +30,13 @@ $(OUT)/odp_bench_pktio_sp: $(BENCH_SP) $(LIB)/libodpg.so $(HDRS)
 	@mkdir -p $(OUT)
 	$(CC) -std=gnu11 -O2 -Wall -I../include -I$(REF)/test/common -o $@ $(BENCH_SP) $(LINK)
 
+# test/performance/odp_pktio_perf.c: the loop-pktio transmit -> receive
+# throughput search
+$(OUT)/odp_pktio_perf: $(REF)/test/performance/odp_pktio_perf.c $(LIB)/libodpg.so $(HDRS)
+	@mkdir -p $(OUT)
+	$(CC) -std=gnu11 -O2 -Wall -I../include -o $@ $< $(LINK)
+
 clean:
-	rm -rf $(OUT)/odp_classifier $(OUT)/odp_bench_pktio_sp
+	rm -rf $(OUT)/odp_classifier $(OUT)/odp_bench_pktio_sp $(OUT)/odp_pktio_perf
 
 .PHONY: all clean

@@ -12,13 +12,18 @@
  *      queue counters.
  *   C  QUEUE in / QUEUE out, classifier off: enqueue on the pktout event
  *      queue transmits, dequeue from the pktin event queue receives.
+ *   D  pcap input "pcap:in=<file>:loops=<n>": the capture is read
+ *      max(1, n - 1) times for n >= 1 (pcapif_init sets loop_cnt = 1 and
+ *      _pcapif_reopen stops when ++loop_cnt >= loops, pktio/pcap.c:215,266).
  * Plus the pktio lookup / duplicate-open rule and the mode checks of the
- * queue accessors (odp_packet_io.c:406-410, 798-829, 1696-1843, 2364-2503).
+ * queue accessors (odp_packet_io.c:406-410, 798-829, 1696-1843, 2364-2503),
+ * and close refused while started (odp_packet_io.c:507-510).
  * Prints one line per check; exit status 0 when all pass.
  */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <odp_api.h>
 #include <odp/helper/odph_api.h>
@@ -225,6 +230,8 @@ static void case_direct(odp_pool_t pool)
 	      os.packets == NPKT, "pktout queue stats");
 	CHECK(odp_pktio_stats_reset(pktio) == 0 && odp_pktin_queue_stats(inq, &is) == 0 &&
 	      is.packets == 0, "stats reset");
+	CHECK(odp_pktio_close(pktio) == -1, "close refused while started");
+	CHECK(odp_pktio_lookup("loop") == pktio, "still open after the refused close");
 	CHECK(odp_pktio_stop(pktio) == 0, "stop");
 	CHECK(odp_pktio_close(pktio) == 0, "close");
 	CHECK(odp_pktio_lookup("loop") == ODP_PKTIO_INVALID, "lookup after close");
@@ -348,6 +355,65 @@ static void case_queue(odp_pool_t pool)
 	printf("C queue: %d packets\n", got);
 }
 
+/* a capture of the first 20 frames */
+static int write_pcap(const char *path)
+{
+	FILE *f = fopen(path, "wb");
+	const uint32_t gh[6] = { 0xa1b2c3d4u, 0x00040002u, 0, 0, 65535, 1 };
+
+	if (!f)
+		return -1;
+	fwrite(gh, 4, 6, f);
+	for (int k = 0; k < 20; k++) {
+		const uint32_t rh[4] = { (uint32_t)k, 0, flen[k], flen[k] };
+
+		fwrite(rh, 4, 4, f);
+		fwrite(frame[k], 1, flen[k], f);
+	}
+	return fclose(f);
+}
+
+static void case_pcap_loops(odp_pool_t pool)
+{
+	char path[] = "/tmp/odp_rt_loop_XXXXXX";
+	const int fd = mkstemp(path);
+	const uint32_t loops[4] = { 1, 2, 3, 4 }, passes[4] = { 1, 1, 2, 3 };
+
+	CHECK(fd >= 0 && write_pcap(path) == 0, "write capture");
+	if (fd < 0)
+		return;
+	close(fd);
+	for (int t = 0; t < 4; t++) {
+		char dev[128];
+		odp_pktin_queue_t inq;
+		odp_packet_t pkts[64];
+		int got = 0;
+
+		snprintf(dev, sizeof(dev), "pcap:in=%s:loops=%u", path, loops[t]);
+		odp_pktio_t pktio = open_loop(dev, pool, ODP_PKTIN_MODE_DIRECT,
+					      ODP_PKTOUT_MODE_DIRECT, 0);
+
+		CHECK(pktio != ODP_PKTIO_INVALID, "open %s", dev);
+		if (pktio == ODP_PKTIO_INVALID)
+			continue;
+		CHECK(odp_pktin_queue(pktio, &inq, 1) == 1 && odp_pktio_start(pktio) == 0,
+		      "start pcap");
+		for (int tries = 0; tries < 100; tries++) {
+			const int n = odp_pktin_recv(inq, pkts, 64);
+
+			if (n <= 0)
+				break;
+			got += n;
+			odp_packet_free_multi(pkts, n);
+		}
+		CHECK(got == (int)(20 * passes[t]), "loops=%u: %d packets, want %u", loops[t], got,
+		      20 * passes[t]);
+		CHECK(odp_pktio_stop(pktio) == 0 && odp_pktio_close(pktio) == 0, "stop/close pcap");
+		printf("D pcap loops=%u: %d packets\n", loops[t], got);
+	}
+	unlink(path);
+}
+
 int main(void)
 {
 	odp_instance_t inst;
@@ -373,6 +439,7 @@ int main(void)
 	case_direct(pool);
 	case_sched_cls(pool);
 	case_queue(pool);
+	case_pcap_loops(pool);
 	CHECK(odp_pool_destroy(pool) == 0, "pool destroy");
 	odp_term_local();
 	odp_term_global(inst);

@@ -108,3 +108,45 @@ def test_bench_two_ranks_one_gpu(tmp_path):
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["scaling"] == "weak"
     assert d["with_pktio_counters"]["value"] > 0
     assert d["scatter_gather"]["value"] > 0 and d["scatter_gather"]["backend"] == "gloo"
+
+
+def test_bench_spawns_its_ranks_without_a_launcher():
+    """`python bench.py --gpus N` (no WORLD_SIZE) starts N ranks itself through
+    a torch.distributed.run child; each sees world N (checked before any GPU
+    call, so this runs on CPU)."""
+    cmd = [sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "3",
+           "--backend", "gloo", "--spawn-check"]
+    r = subprocess.run(cmd, env=dict(os.environ, OMP_NUM_THREADS="1"), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = sorted(json.loads(x)["rank"] for x in r.stdout.splitlines() if x.startswith("{"))
+    assert got == [0, 1, 2]
+    assert all(json.loads(x)["world"] == 3 for x in r.stdout.splitlines() if x.startswith("{"))
+
+
+def test_bench_refuses_a_world_size_mismatch():
+    cmd = [sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "2",
+           "--spawn-check"]
+    r = subprocess.run(cmd, env=dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "launcher started 1 ranks" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_rccl_path_on_one_gpu():
+    """bench.py with the RCCL ("nccl") process group at world size 1: the
+    table-image broadcast, the max / sum all-reduces and the scatter-from-
+    rank-0 / gather-to-root loop run as RCCL collectives on the MI355X (the
+    8-GPU run's code path, one rank)."""
+    cmd = [sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "1",
+           "--steps", "20", "--warmup", "4", "--batch", str(1 << 16), "--no-cpu",
+           "--backend", "nccl", "--source", "gpu0"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert d["distributed"]["backend"] == "nccl" and d["distributed"]["world"] == 1
+    assert d["scatter_gather"]["value"] > 0 and d["scatter_gather"]["backend"] == "nccl"

@@ -25,6 +25,7 @@ ROOT = os.path.dirname(HERE)
 REF_APP = os.path.join(ROOT, "oracle", "_ref", "odp_classifier")
 REF_SRC = "/root/reference/example/classifier/odp_classifier.c"
 REF_BENCH = os.path.join(ROOT, "oracle", "_ref", "odp_bench_pktio_sp")
+REF_PERF = os.path.join(ROOT, "oracle", "_ref", "odp_pktio_perf")
 LOOP_TEST = os.path.join(HERE, "c", "odp_rt_loop")
 PROTO = re.compile(r"^[A-Za-z_][\w \*]*?\b((?:odph|odp)_\w+)\s*\(", re.M)
 
@@ -53,7 +54,7 @@ def test_runtime_symbols_exported():
 def test_reference_classifier_builds_unmodified():
     subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "-f", "ref_apps.mk"],
                    check=True, capture_output=True)
-    for app in (REF_APP, REF_BENCH):
+    for app in (REF_APP, REF_BENCH, REF_PERF):
         assert os.access(app, os.X_OK), app
         out = subprocess.run(["ldd", app], capture_output=True, text=True).stdout
         assert "libodpg.so" in out, app
@@ -156,6 +157,7 @@ def test_loop_device_through_gpu_classifier():
     r = subprocess.run(["timeout", "-k", "10", "100", LOOP_TEST], capture_output=True, text=True)
     assert r.returncode == 0 and "PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-2000:])
     assert "A direct: received 300" in r.stdout and "C queue: 300 packets" in r.stdout
+    assert "D pcap loops=3: 40 packets" in r.stdout
 
 
 @pytest.mark.gpu
@@ -168,6 +170,21 @@ def test_reference_bench_pktio_sp_runs_every_case():
     assert [int(c[0]) for c in cases] == list(range(1, 11)), r.stdout[-3000:]
     assert not [c for c in cases if "n/a" in c[2]], r.stdout[-3000:]   # cls_pmr_create ran
     assert "odp_cls_pmr_create()" in r.stdout and "odp_pktin_queue_stats()" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_PERF), reason="reference pktio perf test not built here")
+def test_reference_pktio_perf_passes_at_fixed_rate():
+    """test/performance/odp_pktio_perf.c, unmodified: one TX and one RX
+    worker on the loop device, 100 ms at 1 Mpps, every packet transmitted
+    must come back through the GPU receive path (scheduler input)."""
+    r = subprocess.run(["timeout", "-k", "10", "100", REF_PERF, "-r", "1000000"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-2000:])
+    assert "Result: PASSED" in r.stdout, r.stdout[-3000:]
+    tx = int(re.search(r"TxPkts: (\d+)", r.stdout).group(1))
+    rx = int(re.search(r"RxPkts: (\d+)", r.stdout).group(1))
+    assert tx >= 99000 and rx >= tx, r.stdout[-2000:]
 
 
 def write_pcap(path, frames):
