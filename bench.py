@@ -294,7 +294,7 @@ def main():
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": None, "kernel_ms": round(kernel_ms, 5),
                     "bytes_per_pkt": round(bytes_per_pkt, 2), "pkts_per_launch": n}
-        roofline["traffic"] = pmc_traffic(args.config)
+        roofline["traffic"], roofline["traffic_source"] = pmc_traffic(args.config)
         cpu = None
         if not args.no_cpu and world == 1:
             cpu = cpu_baseline(rules, frames, desc, n, stride, opt, args)
@@ -409,12 +409,24 @@ def bench_scatter_gather(args, ctx, tbl, frames, n, stride, opt, world, rank, lo
 def pmc_traffic(config):
     """HBM bytes per launch of the timed kernel from the committed rocprofv3
     PMC summary (profiles/pmc_traffic_<config>.json, tools/pmc.sh +
-    tools/pmc_summary.py: FETCH_SIZE x 2 on gfx950 + WRITE_SIZE), or None."""
+    tools/pmc_summary.py: FETCH_SIZE x 2 on gfx950 + WRITE_SIZE), or None;
+    and where the figure comes from: the summary records a fingerprint of the
+    kernel sources it was collected on (tools/kernel_fingerprint.py), so a
+    figure from other kernels is reported as stale, not as this run's."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from kernel_fingerprint import fingerprint
     tf = os.path.join(ROOT, "profiles", f"pmc_traffic_{config}.json")
     try:
-        return json.load(open(tf)).get("bytes_per_launch")
+        rec = json.load(open(tf))
     except (OSError, ValueError):
-        return None
+        return None, "no PMC summary for this config"
+    src = (f"profiles/pmc_traffic_{config}.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of "
+           f"{rec.get('kernel')} in a separate run, not this one")
+    if rec.get("kernel_sources_sha256") == fingerprint():
+        src += "; collected on these kernel sources"
+    else:
+        src += "; STALE: collected on other kernel sources"
+    return rec.get("bytes_per_launch"), src
 
 
 def bench_tx(args, world, rank, local, dist):
@@ -505,7 +517,9 @@ def bench_tx(args, world, rank, local, dist):
                        "parallelism": f"dp{world} (packet shards, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(args.config), "kernel_ms": round(kernel_ms, 5),
+                         "traffic": pmc_traffic(args.config)[0],
+                         "traffic_source": pmc_traffic(args.config)[1],
+                         "kernel_ms": round(kernel_ms, 5),
                          "bytes_per_pkt": bytes_per_pkt, "pkts_per_launch": n},
             "cpu_baseline": cpu,
         }
@@ -598,7 +612,9 @@ def bench_l3fwd(args, world, rank, local, dist):
                        "parallelism": f"dp{world} (packet shards, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(args.config), "kernel_ms": round(kernel_ms, 5),
+                         "traffic": pmc_traffic(args.config)[0],
+                         "traffic_source": pmc_traffic(args.config)[1],
+                         "kernel_ms": round(kernel_ms, 5),
                          "bytes_per_pkt": bytes_per_pkt, "pkts_per_launch": n,
                          "bytes_note": ("SURVEY.md 8(d) prices C5 at 196 B/pkt (frame + a "
                                         "hash-table probe); the interval table replaces "
@@ -641,6 +657,25 @@ def cpu_baseline(rules, frames, desc, n, stride, opt, args):
         _, used = oracle.classify_mt(rules, frames, n, stride=stride, desc=desc, opt=opt,
                                      nthreads=threads, reps=reps, cpus=cpus)
         rates.append(n * reps / (time.perf_counter() - t) / 1e6)
+    # SURVEY.md §8(d) also asks for every core (nproc): the whole affinity
+    # mask, pinned, median of 3 shorter runs
+    allc = None
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = list(range(os.cpu_count() or 1))
+    if len(aff) > used:
+        reps_a = max(1, int(args.cpu_seconds / 6 * one * len(aff) * 1e6 / n * 0.5))
+        ar = []
+        for _ in range(3):
+            t = time.perf_counter()
+            _, ua = oracle.classify_mt(rules, frames, n, stride=stride, desc=desc, opt=opt,
+                                       nthreads=len(aff), reps=reps_a, cpus=aff)
+            ar.append(n * reps_a / (time.perf_counter() - t) / 1e6)
+        allc = {"value": round(statistics.median(ar), 2), "cores": ua,
+                "runs_mpps": [round(r, 2) for r in ar],
+                "sample": f"median of 3 runs, each {reps_a} passes x {n} pkts, {ua} threads "
+                          f"pinned one per CPU of the whole affinity mask (nproc)"}
     model = ""
     try:
         for ln in open("/proc/cpuinfo"):
@@ -652,6 +687,7 @@ def cpu_baseline(rules, frames, desc, n, stride, opt, args):
     return {"value": round(statistics.median(rates), 2), "unit": "Mpps", "cores": used,
             "kind": "port", "value_1thread": round(one, 2), "cpu_model": model,
             "runs_mpps": [round(r, 2) for r in rates], "core_share": share,
+            "all_cores": allc,
             "sample": f"median of {runs} runs, each {reps} passes x {n} pkts of the same "
                       f"{args.config.upper()} batch in host DRAM, {used} threads pinned one per "
                       f"core ({share})"}

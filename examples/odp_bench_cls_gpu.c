@@ -16,7 +16,9 @@
  *    call with an unchanged generation.
  * 3. recv_batch: device-resident batches of 64-byte Eth/IPv4/UDP frames whose
  *    source ports hit the PMRs round-robin, through odpg_pktio_recv_batch
- *    (classify + pktio / CoS counter updates), in Mpps.
+ *    (classify + pktio / CoS counter updates), in Mpps. The batches rotate
+ *    over copies in HBM that together exceed the 256 MiB Infinity Cache (at
+ *    least five), so every launch streams its frames from HBM.
  *
  * Usage: odp_bench_cls_gpu [-n num_pmr] [-r rounds] [-b batch] [-s steps]
  * -n is the reference's PMR count option (default 64 here, the headline rule
@@ -33,6 +35,8 @@
 
 #include <odp_cls.h>
 #include <odpg.h>
+
+#define NBUF_MAX 64
 
 typedef struct {
 	const char *name;
@@ -263,6 +267,8 @@ int main(int argc, char *argv[])
 	/* 2 + 3: device side */
 	odpg_ctx_t *ctx = NULL;
 	uint8_t *hframes = NULL, *dframes = NULL;
+	uint8_t *dbuf[NBUF_MAX] = { NULL };
+	uint32_t nbuf = 0;
 	odpg_out_t *dout = NULL;
 	odpg_out_t *hout = NULL;
 	int rc;
@@ -281,6 +287,16 @@ int main(int argc, char *argv[])
 	make_frames(hframes, batch, num_pmr);
 	if (odpg_memcpy_h2d(ctx, dframes, hframes, (size_t)batch * 64u))
 		goto out;
+	/* rotating HBM copies: >= 5 and > 320 MiB in all */
+	nbuf = (uint32_t)((320ull << 20) / ((uint64_t)batch * 64u) + 1u);
+	nbuf = nbuf < 5u ? 5u : nbuf > NBUF_MAX ? NBUF_MAX : nbuf;
+	dbuf[0] = dframes;
+	for (uint32_t k = 1; k < nbuf; k++)
+		if (odpg_dev_alloc(ctx, (size_t)batch * 64u, (void **)&dbuf[k]) ||
+		    odpg_memcpy_h2d(ctx, dbuf[k], hframes, (size_t)batch * 64u)) {
+			fprintf(stderr, "Error: allocation failed\n");
+			goto out;
+		}
 
 	tm_rec_t rc_rebuild = { "recv_batch, new rules", 0, 0, 0, 0 };
 	tm_rec_t rc_same = { "recv_batch, same rules", 0, 0, 0, 0 };
@@ -320,7 +336,8 @@ int main(int argc, char *argv[])
 	uint64_t t1 = now_ns();
 
 	for (uint32_t s = 0; s < steps; s++)
-		if (odpg_pktio_recv_batch(pktio, ctx, dframes, NULL, 64, batch, 1, dout, NULL) < 0)
+		if (odpg_pktio_recv_batch(pktio, ctx, dbuf[s % nbuf], NULL, 64, batch, 1, dout,
+					  NULL) < 0)
 			goto out;
 	odpg_ctx_sync(ctx);
 	uint64_t t2 = now_ns();
@@ -335,8 +352,9 @@ int main(int argc, char *argv[])
 	for (uint32_t i = 0; i < batch; i++)
 		if ((hout[i] & 0xffffu) != cos_of_port1 + i % num_pmr)
 			bad++;
-	printf("recv_batch: %u x %u packets (64 B, device-resident): %.1f Mpps, %u verdicts off\n",
-	       steps, batch, (double)steps * batch / sec * 1e-6, bad);
+	printf("recv_batch: %u x %u packets (64 B, device-resident, %u rotating HBM buffers): "
+	       "%.1f Mpps, %u verdicts off\n",
+	       steps, batch, nbuf, (double)steps * batch / sec * 1e-6, bad);
 
 	/* the same batches through the raw batch entry point on the same rules,
 	 * verdicts only: what recv_batch's bookkeeping costs on top */
@@ -361,9 +379,11 @@ int main(int argc, char *argv[])
 		odpg_ctx_sync(ctx);
 		uint64_t r1 = now_ns();
 
-		for (uint32_t s = 0; s < steps; s++)
+		for (uint32_t s = 0; s < steps; s++) {
+			bt.frames = dbuf[s % nbuf];
 			if (odpg_classify(ctx, tbl, &bt, &res) < 0)
 				break;
+		}
 		odpg_ctx_sync(ctx);
 		uint64_t r2 = now_ns();
 		double rsec = (double)(r2 - r1) * 1e-9;
@@ -383,7 +403,10 @@ int main(int argc, char *argv[])
 out:
 	if (ret != EXIT_SUCCESS)
 		fprintf(stderr, "Error: device part failed\n");
-	if (dframes)
+	for (uint32_t k = 0; k < NBUF_MAX; k++)
+		if (dbuf[k])
+			odpg_dev_free(ctx, dbuf[k]);
+	if (dframes && !dbuf[0])
 		odpg_dev_free(ctx, dframes);
 	if (dout)
 		odpg_dev_free(ctx, dout);

@@ -1057,6 +1057,7 @@ int oracle_classify(const odpg_rules_t *rules, const uint8_t *frames,
 	return 0;
 }
 
+/* one cache line (or more) per thread: the workers share no written line */
 typedef struct {
 	const odpg_rules_t *rules;
 	batch_t b;
@@ -1065,12 +1066,16 @@ typedef struct {
 	odpg_out_t *out;
 	uint64_t pk[4];
 	int cpu;             /* pin to this CPU, or -1 */
-} mt_arg_t;
+} __attribute__((aligned(128))) mt_arg_t;
 
 static void *mt_worker(void *p)
 {
 	mt_arg_t *a = p;
 	cls_t c = { a->rules, NULL };
+	/* the pktio counters in the thread's own registers / stack, added to
+	 * the shared block once at the end (loopback_recv likewise adds its
+	 * burst's packet and octet counts once per burst, loop.c:370-371) */
+	uint64_t pk[4] = {0, 0, 0, 0};
 
 	if (a->cpu >= 0) {
 		cpu_set_t set;
@@ -1082,7 +1087,8 @@ static void *mt_worker(void *p)
 
 	for (uint32_t r = 0; r < a->reps; r++)
 		for (uint32_t i = a->lo; i < a->hi; i++)
-			process_one(&a->b, &c, i, a->out, NULL, NULL, a->pk);
+			process_one(&a->b, &c, i, a->out, NULL, NULL, pk);
+	memcpy(a->pk, pk, sizeof(pk));
 	return NULL;
 }
 
@@ -1095,7 +1101,7 @@ int oracle_classify_mt(const odpg_rules_t *rules, const uint8_t *frames,
 		       int nthreads, uint32_t reps, const int *cpus)
 {
 	pthread_t th[256];
-	mt_arg_t args[256];
+	static mt_arg_t args[256];   /* 32 KiB: off the caller's stack */
 
 	pthread_once(&crc_once, crc_init);
 	if (nthreads < 1)
