@@ -1586,6 +1586,27 @@ static bool lean64_ok(const odpg_launch_args &a)
 	       !(a.opt & drops) && !(a.opt >> 32);
 }
 
+extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s);
+extern "C" size_t odpg_clsgf_lds(const odpg_launch_args *a);
+
+/* the lean descriptor kernel (classify_gf.hip) covers this launch: a
+ * descriptor batch, a hybrid hash-walk table in its hit-map form
+ * (TBL_XMASK) without hash-queue CoS, verdict words only, full parse with
+ * classification and no drop options */
+static bool gf_ok(const odpg_launch_args &a)
+{
+	static const bool off = getenv("ODPG_NO_GF") != nullptr;
+	const uint64_t drops = ODPG_PKTIN_DROP_IPV4_ERR | ODPG_PKTIN_DROP_IPV6_ERR |
+			       ODPG_PKTIN_DROP_UDP_ERR | ODPG_PKTIN_DROP_TCP_ERR |
+			       ODPG_PKTIN_DROP_SCTP_ERR;
+
+	return !off && a.mode == 0 && a.desc && (a.tbl_flags & TBL_XMASK) &&
+	       !(a.tbl_flags & TBL_ANY_HASHQ) && a.num_cos < ODPG_COS_NOCLS &&
+	       odpg_clsgf_lds(&a) <= odpg_lds_limit() &&
+	       !a.mark && !a.meta && !a.stats && !a.cnt.row &&
+	       a.layer >= LAYER_L4 && a.classify && !(a.opt & drops) && !(a.opt >> 32);
+}
+
 static int g_last_kernel = -1;
 
 extern "C" int odpg_last_kernel(void)
@@ -1628,8 +1649,11 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 	if (a->num == 0)
 		return 0;
 	const bool lean = lean64_ok(*a);
+	const bool gf = !lean && gf_ok(*a);
 
-	__atomic_store_n(&g_last_kernel, lean ? 1 : 0, __ATOMIC_RELAXED);
+	__atomic_store_n(&g_last_kernel, lean ? 1 : gf ? 2 : 0, __ATOMIC_RELAXED);
+	if (gf)
+		return odpg_launch_clsgf(a, s);
 	if (lean) {
 		int rc = odpg_launch_cls64(a, s);
 

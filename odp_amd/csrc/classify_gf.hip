@@ -1,0 +1,709 @@
+/* SPDX-License-Identifier: BSD-3-Clause
+ *
+ * Lean gfx950 classify kernel for descriptor (IMIX) batches: frames of any
+ * length at (offset, len) descriptors, a hybrid hash-walk table in its
+ * hit-map form (TBL_XMASK, cls_compile.cpp), verdict words only. The C3
+ * shape: IMIX 64/570/1518-byte IPv4 / IPv6 UDP / TCP traffic with the RX
+ * checksum checks and a 256-PMR DAG. Same per-packet semantics as
+ * odpg_classify_kernel (classify.hip), bit-identical results
+ * (tests/test_gf_kernel.py, tests/test_gpu_parity.py).
+ *
+ * Per packet: parse + RX checksum verdicts (_odp_packet_parse_common,
+ * odp_parse_internal.h:80-112, odp_packet.c:1906-1984), error-CoS selection
+ * and the match_pmr_cos first-match walk (odp_classification.c:1599-1701).
+ *
+ * Layout: one lane per packet, one wave per 64-packet tile, waves persistent
+ * over tiles, no workgroup barrier in the loop. A lane's first 64 frame bytes
+ * arrive as 4 x 16-byte loads straight into registers (plus the dword at
+ * byte 64), the next tile's issued while the current tile walks. A wave whose
+ * frames are all plain Eth / IPv4 (no options) or IPv6 (no extension header)
+ * UDP / TCP frames of >= 64 bytes parses them from the registers at
+ * per-lane L4 offsets 34 / 54 (v_dot2 sums for the header and pseudo-header
+ * checksums); any other wave runs the generic parse over an LDS copy of the
+ * windows. The UDP / TCP checksum bytes past the window are summed by the
+ * whole wave in balanced 64-byte units (seg_tail_sums4, pkt_parse.h).
+ *
+ * The walk: the packet's hit map (<= 256 PMRs, 8 registers) holds every
+ * PMR that matches it. Each walk group (single-word PMRs sharing slot, gate
+ * and mask) is read once per packet: its masked key word hashes
+ * collision-free to the group's entry for that value, whose map of the PMRs
+ * (of every CoS) comparing equal to it is ORed in. A level of
+ * match_pmr_cos is then the lowest set bit of the current CoS's rule range
+ * [rule_start, rule_start + nrule), the CoS's complex PMRs below that one
+ * evaluated in rule order from their LDS term records, and one LDS read of
+ * the winner's destination, mark and the destination's ranges.
+ */
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "../../include/odpg.h"
+#include "odpg_internal.h"
+#include "pkt_parse.h"
+#include "cls_match.h"
+
+#ifndef GF_BLOCK            /* threads per workgroup */
+#define GF_BLOCK 256
+#endif
+#ifndef GF_WAVES            /* waves per SIMD the launch bounds ask for */
+#define GF_WAVES 5
+#endif
+
+struct GFArgs {
+	const uint8_t *frames;
+	uint32_t num;
+	uint32_t opt;               /* ODPG_PKTIN_* (all defined bits are < 32) */
+	uint32_t nwg;               /* walk groups */
+	const uint2 *cinfo;         /* {rule_start | nrule << 16, action | ...} */
+	const uint32_t *pinfo;      /* dst | mark << 16 */
+	uint32_t num_cos, num_pmr;
+	int32_t default_cos, error_cos;
+	const dcos_t *coses;
+	const uint32_t *xm_rest;    /* TBL_XMASK: masks[num_xment][XM_WORDS], values, slot bytes */
+	uint32_t num_xment, xm_slot_bytes, num_xflat;
+	const uint32_t *xfc;        /* per CoS: first flat complex term | count << 16 */
+};
+
+typedef unsigned short gf_us2 __attribute__((ext_vector_type(2)));
+
+/* acc + w.lo * x.lo16 + w.hi * x.hi16 (one v_dot2_u32_u16) */
+__device__ __forceinline__ uint32_t gd2(uint32_t x, uint32_t w, uint32_t acc)
+{
+	return __builtin_amdgcn_udot2(__builtin_bit_cast(gf_us2, x), __builtin_bit_cast(gf_us2, w),
+				      acc, false);
+}
+
+#define GW11 0x00010001u   /* both halves */
+#define GW10 0x00000001u   /* low half (first byte pair) */
+#define GW01 0x00010000u   /* high half */
+
+/* 0xffff iff the one's-complement sum of the 16-bit halves is all-ones,
+ * as chksum_finalize folds the reference's 64-bit word sum
+ * (odp_chksum_internal.h:22-31) */
+__device__ __forceinline__ uint32_t gfold(uint32_t s)
+{
+	return oc_fold(s);
+}
+
+/* frame bytes [K, K + 4) of the window registers, K constant */
+template <int K>
+__device__ __forceinline__ uint32_t wb(const uint32_t (&f)[16])
+{
+	return fw<K>(f);
+}
+
+/* The frames the register parse takes: Eth (no SNAP / VLAN) then IPv4 with
+ * IHL 5 and tot_len within the frame, or IPv6 without extension headers and
+ * payload within the frame; then UDP with length >= 8 (IPv6: not port 4500,
+ * whose IPsec marker lies past the window) or TCP with data offset >= 5 and
+ * its 20 header bytes inside the frame; frame length >= 64. x16 is the
+ * frame's dword at byte 64 (the IPv6 TCP data-offset byte). */
+__device__ __forceinline__ bool plain_gf(const uint32_t (&f)[16], uint32_t x16, uint32_t len)
+{
+	const uint32_t et = f[3] & 0xffffu;
+	const uint32_t vb = (f[3] >> 16) & 0xffu;
+	const bool v4 = et == 0x0008u && vb == 0x45u;
+	const bool v6 = et == 0xdd86u && (vb & 0xf0u) == 0x60u;
+
+	if (len < 64u || !(v4 || v6))
+		return false;
+	if (v4) {
+		const uint32_t tot_len = swap16(f[4] & 0xffffu);
+		const uint32_t proto = f[5] >> 24;
+
+		if (tot_len > len - 14u)
+			return false;
+		if (proto == 0x11u)
+			return swap16(f[9] >> 16) >= 8u;
+		if (proto == 0x06u)
+			return ((f[11] >> 20) & 0xfu) >= 5u;
+		return false;
+	}
+	const uint32_t payload = swap16(f[4] >> 16);
+	const uint32_t nh = f[5] & 0xffu;
+
+	if (payload + 40u > len - 14u)
+		return false;
+	if (nh == 0x11u)
+		return swap16(f[14] >> 16) >= 8u && swap16(f[14] & 0xffffu) != 4500u;
+	if (nh == 0x06u)
+		return len >= 74u && ((x16 >> 20) & 0xfu) >= 5u;
+	return false;
+}
+
+/* parse_common() of a plain_gf() frame from its window registers: returns
+ * 0 / 1 (error flagged) or PARSE_PEND with the UDP / TCP checksum left for
+ * the tail bytes [64, len) (pd: the pseudo header + window part) */
+__device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t (&f)[16],
+					     uint32_t len, uint32_t opt)
+{
+	const bool v6 = (f[3] & 0xffffu) == 0xdd86u;
+	uint64_t inf = IF(IFL_L2) | IF(IFL_ETH) | IF(IFL_L3) | IF(IFL_L4) |
+		       (v6 ? IF(IFL_IPV6) : IF(IFL_IPV4));
+	uint32_t fl = 0u;
+
+	p.l2 = 0u;
+	p.l3 = 14u;
+	if (len > 1514u)
+		inf |= IF(IFL_JUMBO);
+	if (f[0] & 0x1u)
+		inf |= IF(IFL_ETH_MCAST);
+	if (f[0] == 0xffffffffu && (f[1] & 0xffffu) == 0xffffu)
+		inf |= IF(IFL_ETH_BCAST);
+
+	bool frag = false;
+	uint32_t proto, pseudo, win, ulen_raw, csum_raw, dport;
+
+	if (!v6) {
+		/* parse_ipv4 (odp_parse.c:113-169) */
+		if (opt & ODPG_PKTIN_IPV4_CHKSUM) {
+			uint32_t s = gd2(f[3], GW01, 0u);
+
+			s = gd2(f[4], GW11, s);
+			s = gd2(f[5], GW11, s);
+			s = gd2(f[6], GW11, s);
+			s = gd2(f[7], GW11, s);
+			s = gd2(f[8], GW10, s);
+			inf |= IF(IFL_L3_CHKSUM_DONE);
+			if (gfold(s) != 0xffffu) {
+				/* ip_err: no L4 offset, ip_proto 0 -> no L4 flag */
+				p.inf = inf & ~IF(IFL_L4);
+				p.fl = FB(FL_IP_ERR) | FB(FL_L3_CHKSUM_ERR);
+				p.l4 = 0xffffu;
+				return 1;
+			}
+		}
+		frag = (swap16(f[5] & 0xffffu) & 0x3fffu) != 0u;
+		const uint32_t dst_be = __builtin_bswap32(wb<30>(f));
+
+		if (frag)
+			inf |= IF(IFL_IPFRAG);
+		if (dst_be == 0xffffffffu)
+			inf |= IF(IFL_IP_BCAST);
+		if ((dst_be >> 28) == 0xeu)
+			inf |= IF(IFL_IP_MCAST);
+		proto = f[5] >> 24;
+		pseudo = gd2(f[8], GW10, gd2(f[7], GW11, gd2(f[6], GW01, 0u)));   /* bytes 26..33 */
+		win = gd2(f[8], GW01, 0u);                                      /* bytes 34..63 */
+#pragma unroll
+		for (int k = 9; k < 16; ++k)
+			win = gd2(f[k], GW11, win);
+		ulen_raw = f[9] >> 16;
+		csum_raw = f[10] & 0xffffu;
+		dport = swap16(f[9] & 0xffffu);
+		p.l4 = 34u;
+	} else {
+		/* parse_ipv6 (odp_parse.c:179-245), no extension header */
+		if (((f[9] >> 16) & 0xffu) == 0xffu)
+			inf |= IF(IFL_IP_MCAST);
+		proto = f[5] & 0xffu;
+		pseudo = gd2(f[5], GW01, 0u);                                   /* bytes 22..53 */
+#pragma unroll
+		for (int k = 6; k < 13; ++k)
+			pseudo = gd2(f[k], GW11, pseudo);
+		pseudo = gd2(f[13], GW10, pseudo);
+		win = gd2(f[15], GW11, gd2(f[14], GW11, gd2(f[13], GW01, 0u)));   /* bytes 54..63 */
+		ulen_raw = f[14] >> 16;
+		csum_raw = f[15] & 0xffffu;
+		dport = swap16(f[14] & 0xffffu);
+		p.l4 = 54u;
+	}
+	bool need = false;
+	uint32_t sum = 0u;
+	const bool udp = proto == 0x11u;
+
+	if (udp) {                                  /* parse_udp (odp_parse.c:281-322) */
+		const uint32_t udplen = swap16(ulen_raw);
+
+		inf |= IF(IFL_UDP);
+		if ((opt & ODPG_PKTIN_UDP_CHKSUM) && !frag) {
+			if (csum_raw == 0u) {
+				inf |= IF(IFL_L4_CHKSUM_DONE) | IF(IFL_UDP_CHKSUM_ZERO);
+				if (v6)
+					fl |= FB(FL_L4_CHKSUM_ERR);
+			} else {
+				sum = pseudo + ulen_raw + (0x11u << 8) + win;
+				need = true;
+			}
+		}
+		if (!v6 && dport == 4500u && udplen > 4u && wb<42>(f) != 0u)
+			inf |= IF(IFL_IPSEC) | IF(IFL_IPSEC_UDP);
+	} else {                                    /* parse_tcp (odp_parse.c:252-274) */
+		inf |= IF(IFL_TCP);
+		if ((opt & ODPG_PKTIN_TCP_CHKSUM) && !frag) {
+			sum = pseudo + swap16((len - p.l4) & 0xffffu) + (0x06u << 8) + win;
+			need = true;
+		}
+	}
+	if (need && !fl) {
+		if (len > 64u) {
+			pd.kind = udp ? 1u : 2u;
+			pd.sum = sum;
+			pd.a = 64u;
+			pd.b = len;
+			p.inf = inf;
+			p.fl = fl;
+			return PARSE_PEND;
+		}
+		/* _odp_packet_l4_chksum (odp_packet.c:1906-1984) within the window */
+		inf |= IF(IFL_L4_CHKSUM_DONE);
+		if (gfold(sum) != 0xffffu)
+			fl |= FB(FL_L4_CHKSUM_ERR) | (udp ? FB(FL_UDP_ERR) : FB(FL_TCP_ERR));
+	}
+	p.inf = inf;
+	p.fl = fl;
+	return (fl & FL_ERROR_MASK) != 0u;
+}
+
+template <int CM>
+__global__ __launch_bounds__(GF_BLOCK, GF_WAVES * 256 / GF_BLOCK) void
+odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__restrict__ xmg,
+		  const uint4 *__restrict__ xf, const odpg_desc_t *__restrict__ descs,
+		  odpg_out_t *__restrict__ out)
+{
+	/* read-only tables as restrict kernel arguments: their wave-uniform
+	 * reads compile to scalar loads */
+	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+	constexpr uint32_t RW = 16;                     /* generic-parse LDS row (dwords) */
+	uint32_t *row = smem + threadIdx.x * RW;
+	uint32_t *tb = smem + GF_BLOCK * RW;
+	/* hit-map entries (2 x uint4 each), their values, the slot bytes */
+	uint4 *xmm = (uint4 *)tb;
+	uint32_t *xmv = tb + XM_WORDS * A.num_xment;
+	uint8_t *xms = (uint8_t *)(xmv + ((A.num_xment + 3u) & ~3u));
+	uint2 *cinfo = (uint2 *)(xms + A.xm_slot_bytes);
+	/* per PMR {dst | mark << 16, the destination's rule_start | nrule << 16,
+	 * the destination's complex terms: first | count << 16, 0}: one LDS read
+	 * per walk level */
+	uint4 *pdst = (uint4 *)(cinfo + ((A.num_cos + 1u) & ~1u));
+	/* the complex PMRs' terms, per CoS in rule order (cls_compile.cpp
+	 * "xflat"): {gate, mask, value, slot | guard end << 8 | guarded << 31},
+	 * {pmr, last term of the PMR, 0, 0} */
+	uint4 *xfl = pdst + A.num_pmr;
+
+	const uint32_t lane = __lane_id();
+	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (GF_BLOCK / 64) +
+							   (threadIdx.x >> 6));
+	const uint32_t nwaves = gridDim.x * (GF_BLOCK / 64);
+	const uint32_t ntiles = (A.num + 63u) >> 6;
+	const uint32_t num = A.num;
+
+	/* the first tile's descriptors and windows are issued before the table
+	 * copy below */
+	auto load_desc = [&](uint32_t t) -> uint2 {
+		const uint32_t i = t * 64u + lane;
+
+		if (t < ntiles && i < num)
+			return *(const uint2 *)(descs + i);
+		return make_uint2(0u, 0u);
+	};
+	/* a frame's first 64 bytes (16-byte chunks holding frame bytes only: the
+	 * chunk with the last byte is masked), and its dword at byte 64 */
+	auto load_win = [&](uint32_t (&f)[16], uint32_t &x16, uint2 d) {
+		const uint8_t *g = A.frames + d.x;
+		const uint32_t len = d.y;
+
+#pragma unroll
+		for (int q = 0; q < 4; ++q) {
+			uint4 x = make_uint4(0u, 0u, 0u, 0u);
+
+			if (16u * q < len)
+				x = *(const uint4 *)(g + 16u * q);
+			f[4 * q + 0] = x.x;
+			f[4 * q + 1] = x.y;
+			f[4 * q + 2] = x.z;
+			f[4 * q + 3] = x.w;
+		}
+		x16 = len > 64u ? *(const uint32_t *)(g + 64u) : 0u;
+	};
+	uint32_t fn[16], xn = 0u;
+	uint2 dn = load_desc(gw), dnn;
+
+	load_win(fn, xn, dn);
+	dnn = load_desc(gw + nwaves);
+
+	{
+		const uint32_t nm = XM_WORDS * A.num_xment;
+
+		for (uint32_t k = threadIdx.x; k < nm; k += GF_BLOCK)
+			tb[k] = A.xm_rest[k];
+		for (uint32_t k = threadIdx.x; k < A.num_xment; k += GF_BLOCK)
+			xmv[k] = A.xm_rest[nm + k];
+		for (uint32_t k = threadIdx.x; k < A.xm_slot_bytes / 4u; k += GF_BLOCK)
+			((uint32_t *)xms)[k] = A.xm_rest[nm + A.num_xment + k];
+	}
+	for (uint32_t k = threadIdx.x; k < A.num_cos; k += GF_BLOCK)
+		cinfo[k] = A.cinfo[k];
+	for (uint32_t k = threadIdx.x; k < A.num_pmr; k += GF_BLOCK) {
+		const uint32_t pi = A.pinfo[k];
+
+		pdst[k] = make_uint4(pi, A.cinfo[pi & 0xffffu].x, A.xfc[pi & 0xffffu], 0u);
+	}
+	for (uint32_t k = threadIdx.x; k < 2u * A.num_xflat; k += GF_BLOCK)
+		xfl[k] = xf[k];
+	__syncthreads();
+
+	const uint32_t nwg = A.nwg;
+	const uint32_t opt = A.opt;
+	const bool def_valid = A.default_cos >= 0 && A.coses[A.default_cos].valid;
+	const bool def_rules = def_valid && A.coses[A.default_cos].nrule != 0u;
+
+	for (uint32_t t = gw; t < ntiles; t += nwaves) {
+		const uint32_t i = t * 64u + lane;
+		const bool live = i < num;
+		const uint2 d = dn;
+		const uint8_t *g = A.frames + d.x;
+		const uint32_t len = live ? d.y : 0u;
+		uint32_t f[16];
+		const uint32_t x16 = xn;
+
+#pragma unroll
+		for (int q = 0; q < 16; ++q) {
+			/* bytes past the frame read as zero (the reference's
+			 * undefined reads past the end: DESIGN.md deviation 1) */
+			const int nb = (int)len - 4 * q;
+
+			f[q] = nb >= 4 ? fn[q] : nb <= 0 ? 0u : fn[q] & ((1u << (8 * nb)) - 1u);
+		}
+		dn = dnn;
+
+		/* ---- parse + checksum verdicts -------------------------------- */
+		Prs p;
+		L4Pend pd = {0u, 0u, 0u, 0u};
+		int ret = 0;
+		const bool fastw = __ballot(live && !plain_gf(f, x16, len)) == 0ull;
+		Bases b;
+		uint32_t hm[XM_WORDS];
+
+		p.inf = 0ull;
+		p.fl = 0u;
+		p.l2 = p.l3 = p.l4 = 0xffffu;
+		/* the LDS row: the generic parse's window, and the complex rules'
+		 * key reads on any wave */
+#pragma unroll
+		for (int q = 0; q < 16; q += 4)
+			*(uint4 *)(row + q) = make_uint4(f[q], f[q + 1], f[q + 2], f[q + 3]);
+		auto bases = [&]() {
+			b.l2 = p.l2;
+			b.l3 = p.l3;
+			b.l4 = p.l4;
+			b.vlanx = 14u + ((p.inf & IF(IFL_VLAN_QINQ)) ? 4u : 0u);
+			b.len = len;
+			b.inf_lo = (uint32_t)p.inf;
+		};
+		/* the hit map: each walk group's masked key word, once per packet,
+		 * its entry's PMR map ORed in (a level of the walk only changes the
+		 * CoS, i.e. the rule range the map is scanned in) */
+		auto keys = [&](auto key) {
+			const bool on = live && (p.fl & FL_ERROR_MASK) == 0u;
+
+#pragma unroll
+			for (uint32_t w = 0; w < XM_WORDS; ++w)
+				hm[w] = 0u;
+			if (!__ballot(on))
+				return;
+#ifdef GF_EXP_NOHM   /* experiment builds only: cost without the hit map */
+			if (A.num != 12345u)
+				return;
+#endif
+#pragma unroll 4
+			for (uint32_t gi = 0; gi < nwg; ++gi) {
+				{
+					const uint4 g0 = wg[2u * gi];
+					const uint32_t gslot = __builtin_amdgcn_readfirstlane(g0.x);
+					const uint32_t greq = __builtin_amdgcn_readfirstlane(g0.y);
+					const uint32_t gmask = __builtin_amdgcn_readfirstlane(g0.z);
+
+					if (on && (b.inf_lo & greq) == greq) {
+						const uint32_t kv = key(gslot) & gmask;
+
+						{
+							const uint4 xg = xmg[gi];
+							const uint32_t mul = __builtin_amdgcn_readfirstlane(xg.x);
+							const uint32_t sh = __builtin_amdgcn_readfirstlane(xg.y);
+							const uint32_t soff = __builtin_amdgcn_readfirstlane(xg.z);
+							const uint32_t eb = __builtin_amdgcn_readfirstlane(xg.w);
+							const uint32_t si = xms[soff + ((kv * mul) >> sh)];
+
+							if (si != 0xffu && xmv[eb + si] == kv) {
+								const uint4 m0 = xmm[2u * (eb + si)];
+								const uint4 m1 = xmm[2u * (eb + si) + 1u];
+
+								hm[0] |= m0.x;
+								hm[1] |= m0.y;
+								hm[2] |= m0.z;
+								hm[3] |= m0.w;
+								hm[4] |= m1.x;
+								hm[5] |= m1.y;
+								hm[6] |= m1.z;
+								hm[7] |= m1.w;
+							}
+						}
+					}
+				}
+			}
+		};
+#ifdef GF_EXP_NOGEN
+		if (true) {
+#else
+		if (fastw) {
+#endif
+			if (live)
+				ret = parse_fast_gf(p, pd, f, len, opt);
+			bases();
+			const bool v6 = (b.inf_lo & (uint32_t)IF(IFL_IPV6)) != 0u;
+			const bool l4ok = b.l4 != 0xffffu;
+
+			keys([&](uint32_t slot) -> uint32_t {   /* slot wave-uniform */
+				switch (slot) {
+				case 0: return f[0];
+				case 1: return f[1];
+				case 2: return f[2];
+				case 3: return f[3];
+				case 4: return f[4];
+				case 5: return wb<14>(f);
+				case 6: return wb<14>(f);
+				case 7: return wb<18>(f);
+				case 8: return wb<22>(f);
+				case 9: return wb<26>(f);
+				case 10: return wb<30>(f);
+				case 11: return wb<34>(f);
+				case 12: return wb<38>(f);
+				case 13: return wb<42>(f);
+				case 14: return wb<46>(f);
+				case 15: return wb<50>(f);
+				case 16: return !l4ok ? 0u : v6 ? wb<54>(f) : wb<34>(f);
+				case 17: return !l4ok ? 0u : v6 ? wb<58>(f) : wb<38>(f);
+				default: return len;
+				}
+			});
+		} else {
+			Pkt<64, true> v;
+
+			v.row = row;
+			v.g = g;
+			v.len = len;
+			if (live)
+				ret = parse_common(p, v, LAYER_ALL, (uint64_t)opt, &pd);
+			bases();
+			KeySrc<64, true> key;
+
+			key.f = nullptr;
+			key.v = &v;
+			key.b = &b;
+			key.fast = false;
+			keys(key);
+		}
+
+		/* ---- checksum bytes past the window: the whole wave --------------- */
+		{
+			const uint64_t pm = __ballot(ret == PARSE_PEND);
+
+#ifdef GF_EXP_NOTAIL
+			if (false) {
+#else
+			if (pm) {
+#endif
+				const uint32_t tail = seg_tail_sums4(pm, g, pd);
+
+				if (ret == PARSE_PEND)
+					ret = finish_l4(p, pd, tail, (uint64_t)opt);
+			}
+		}
+
+		/* the next tile's windows, in flight during the walk */
+		load_win(fn, xn, dn);
+		dnn = load_desc(t + 2u * nwaves);
+
+		/* ---- CoS walk (cls_select_cos + match_pmr_cos) ------------------ */
+		const bool err = (p.fl & FL_ERROR_MASK) != 0u;
+		const bool want_cls = live && ret >= 0;
+		uint32_t cos = ODPG_COS_NOCLS;
+		bool active = false, any_match = false;
+		uint32_t mark = 0u, steps = 0u;
+
+		if (want_cls) {
+			if (err) {
+				cos = A.error_cos < 0 ? ODPG_COS_NONE : (uint32_t)A.error_cos;
+			} else if (def_valid) {
+				cos = (uint32_t)A.default_cos;
+				active = def_rules;
+			} else {
+				cos = A.default_cos < 0 ? ODPG_COS_NONE : (uint32_t)A.default_cos;
+			}
+		}
+#ifdef GF_EXP_NOWALK   /* experiment builds only: cost without the walk */
+		active = false;
+#endif
+		{
+			/* a level: the lowest set bit of the CoS's rule range
+			 * [rule_start, rule_start + nrule) in the hit map; the CoS's
+			 * complex PMRs below it, in rule order, from their term
+			 * records (gate, CUSTOM_L3 length guard, masked slot word); then
+			 * the PMR's destination, mark and the destination's ranges */
+			uint32_t crs = 0u, cxf = 0u;
+
+			if (active) {
+				crs = cinfo[cos].x;
+				cxf = A.xfc[cos];
+			}
+			while (__ballot(active)) {
+				if (active) {
+					uint32_t best = 0xffffffffu;
+					uint32_t bi = crs & 0xffffu;
+					const uint32_t end = bi + (crs >> 16);
+
+					while (bi < end) {
+						const uint32_t w = bi >> 5;
+						uint32_t x = hm[0];
+
+#pragma unroll
+						for (uint32_t k = 1; k < XM_WORDS; ++k)
+							x = w == k ? hm[k] : x;
+						x >>= bi & 31u;
+						if (end - bi < 32u)
+							x &= (1u << (end - bi)) - 1u;
+						if (x) {
+							best = bi + (uint32_t)__builtin_ctz(x);
+							break;
+						}
+						bi = (w + 1u) << 5;
+					}
+					uint32_t j = cxf & 0xffffu;
+					const uint32_t jend = j + (cxf >> 16);
+					bool acc = true;
+
+					for (; j < jend; ++j) {
+						const uint4 q = xfl[2u * j + 1u];
+
+						if (q.x >= best)
+							break;
+						const uint4 r = xfl[2u * j];
+						Pkt<64, true> v;
+
+						v.row = row;
+						v.g = g;
+						v.len = len;
+						KeySrc<64, true> key;
+
+						key.f = nullptr;
+						key.v = &v;
+						key.b = &b;
+						key.fast = false;
+						acc = acc && (b.inf_lo & r.x) == r.x &&
+						      (!(r.w >> 31) || b.len > b.l3 + ((r.w >> 8) & 0xffffu)) &&
+						      (key(r.w & 0xffu) & r.y) == r.z;
+						if (q.y) {              /* the PMR's last term */
+							if (acc) {
+								best = q.x;
+								break;
+							}
+							acc = true;
+						}
+					}
+					if (best == 0xffffffffu) {
+						active = false;
+					} else {
+						const uint4 pd2 = pdst[best];
+
+						cos = pd2.x & 0xffffu;
+						mark = pd2.x >> 16;
+						crs = pd2.y;
+						cxf = pd2.z;
+						any_match = true;
+						if (++steps >= A.num_cos) {
+							cos = ODPG_COS_LOOP;
+							active = false;
+						} else {
+							active = (crs >> 16) != 0u;   /* no rules below: done */
+						}
+					}
+				}
+			}
+		}
+
+		/* ---- verdict word (odpg.h) ------------------------------------- */
+		if (live) {
+			int cret = 0;
+			bool markv = false;
+
+			if (want_cls) {
+				if (cos == ODPG_COS_LOOP)
+					cret = -2;
+				else if (cos == ODPG_COS_NONE)
+					cret = -1;
+				else if (cos < A.num_cos && (cinfo[cos].y & 0xffu) == 1u)
+					cret = 1;
+				markv = any_match && !err && cos != ODPG_COS_LOOP && mark != 0u;
+			} else if (ret < 0) {
+				cos = ODPG_COS_PDROP;
+			}
+			uint32_t w = cos & 0xffffu;
+
+			if (cret == 1)
+				w |= ODPG_OUT_CLS_DROP;
+			if (p.inf & IF(IFL_L3_CHKSUM_DONE))
+				w |= (p.fl & FB(FL_L3_CHKSUM_ERR) ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 16;
+			if (p.inf & IF(IFL_L4_CHKSUM_DONE))
+				w |= (p.fl & FB(FL_L4_CHKSUM_ERR) ? ODPG_CHKSUM_BAD : ODPG_CHKSUM_OK) << 18;
+			if (err)
+				w |= ODPG_OUT_ERROR;
+			if (markv)
+				w |= ODPG_OUT_MARK_VALID;
+			if (ret)
+				w |= ODPG_OUT_PARSE_ERR;
+			out[i] = w;
+		}
+	}
+}
+
+/* ---- launch ----------------------------------------------------------------- */
+extern "C" uint32_t odpg_resident_grid(const void *kernel, uint32_t block, size_t lds);
+extern "C" uint32_t odpg_lds_limit(void);
+
+/* dynamic LDS of a launch: generic-parse rows + the table copy */
+extern "C" size_t odpg_clsgf_lds(const odpg_launch_args *a)
+{
+	const size_t tb = (size_t)a->num_xment * (XM_WORDS + 1u) * 4u + 12u + a->xm_slot_bytes;
+
+	return (size_t)GF_BLOCK * 16u * 4u + tb + (size_t)((a->num_cos + 1u) & ~1u) * 8u +
+	       (size_t)a->num_pmr * 16u + (size_t)a->num_xflat * 32u;
+}
+
+extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s)
+{
+	if (a->num == 0)
+		return 0;
+	GFArgs A;
+
+	A.frames = a->frames;
+	A.num = a->num;
+	A.opt = (uint32_t)a->opt;
+	A.nwg = a->num_wgroups;
+	A.cinfo = (const uint2 *)a->cinfo;
+	A.pinfo = a->pinfo;
+	A.num_cos = a->num_cos;
+	A.num_pmr = a->num_pmr;
+	A.default_cos = a->default_cos;
+	A.error_cos = a->error_cos;
+	A.coses = a->coses;
+	A.xm_rest = a->xm + 4u * a->num_wgroups;
+	A.num_xment = a->num_xment;
+	A.xm_slot_bytes = a->xm_slot_bytes;
+	A.num_xflat = a->num_xflat;
+	const uint4 *xf = (const uint4 *)(A.xm_rest + (XM_WORDS + 1u) * a->num_xment +
+					  a->xm_slot_bytes / 4u);
+
+	A.xfc = (const uint32_t *)(xf + 2u * a->num_xflat);
+
+	const size_t lds = odpg_clsgf_lds(a);
+	const uint32_t ntiles = (a->num + 63u) / 64u;
+	const uint32_t want = (ntiles + GF_BLOCK / 64u - 1u) / (GF_BLOCK / 64u);
+	uint32_t grid = odpg_resident_grid((const void *)odpg_clsgf_kernel<0>, GF_BLOCK, lds);
+
+	grid = grid < want ? grid : want;
+	hipLaunchKernelGGL((odpg_clsgf_kernel<0>), dim3(grid ? grid : 1u), dim3(GF_BLOCK), lds, s, A,
+			   (const uint4 *)a->wgroups, (const uint4 *)a->xm, xf, a->desc, a->out);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}

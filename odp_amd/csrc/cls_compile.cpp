@@ -938,6 +938,120 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		h.flags |= TBL_XWALK;
 		h.num_xlist = num_xent;
 		h.num_xwords = (uint32_t)xlist.size();
+		/* the descriptor-layout lean kernel (classify_gf.hip) evaluates
+		 * every complex rule from its xterm records */
+		bool gf = ncos < 65536;
+
+		for (uint32_t k = 0; gf && k < num_xent; k++)
+			gf = (xlist[2 * k + 1] >> 24) != 0u;
+		if (gf)
+			h.flags |= TBL_XGF;
+	}
+
+	/* TBL_XMASK (classify_gf.hip's hit-map form, <= XM_MAX_PMR PMRs): per
+	 * walk group its distinct masked values, each with the bit map of the
+	 * PMRs (of any CoS) that compare equal to it, found through a
+	 * collision-free multiplicative hash (slot = (value * mul) >> shift) and
+	 * a byte table of entry indices. A packet reads each group once and ORs
+	 * the entry's map; a walk level then finds the CoS's first matching
+	 * single-word rule as the lowest set bit of its rule range. Only the
+	 * lowest PMR per (CoS, value) is in the walk groups: a higher one of the
+	 * same key matches exactly when that one does, so never first. */
+	std::vector<uint32_t> xmg, xmmask, xmval;
+	std::vector<uint8_t> xmslot;
+	bool xm = (h.flags & TBL_XGF) && pmr.size() <= XM_MAX_PMR;
+	uint64_t rs = 0x9E3779B97F4A7C15ull;
+
+	for (size_t gi = 0; xm && gi < wgroups.size(); gi++) {
+		const dhgroup_t &g = wgroups[gi];
+		std::map<uint32_t, std::vector<uint32_t>> vm;
+
+		for (uint32_t e = 0; e < (1u << g.log2sz); e++) {
+			const dwent_t &w = wents[g.off + e];
+
+			if (w.cos_pmr == HENT_EMPTY)
+				continue;
+			std::vector<uint32_t> &m = vm[w.value];
+
+			m.resize(XM_WORDS, 0u);
+			m[(w.cos_pmr >> 16) >> 5] |= 1u << ((w.cos_pmr >> 16) & 31u);
+		}
+		if (vm.size() > 255) {
+			xm = false;
+			break;
+		}
+		uint32_t lg = 1, mul = 0;
+		bool found = false;
+
+		while ((1u << lg) < 2 * vm.size())
+			lg++;
+		for (; lg <= XM_MAX_LG && !found; lg += found ? 0 : 1) {
+			std::vector<uint8_t> used(1u << lg);
+
+			for (int t = 0; t < 4096 && !found; t++) {
+				rs ^= rs << 13;
+				rs ^= rs >> 7;
+				rs ^= rs << 17;
+				mul = (uint32_t)(rs >> 16) | 1u;
+				std::fill(used.begin(), used.end(), 0);
+				found = true;
+				for (auto &v : vm) {
+					uint8_t &u = used[(v.first * mul) >> (32u - lg)];
+
+					if (u) {
+						found = false;
+						break;
+					}
+					u = 1;
+				}
+			}
+			if (found)
+				break;
+		}
+		if (!found) {
+			xm = false;
+			break;
+		}
+		const uint32_t soff = (uint32_t)xmslot.size();
+		const uint32_t ebase = (uint32_t)xmval.size();
+		uint32_t k = 0;
+
+		xmslot.resize(soff + (1u << lg), 0xff);
+		for (auto &v : vm) {
+			xmslot[soff + ((v.first * mul) >> (32u - lg))] = (uint8_t)k++;
+			xmval.push_back(v.first);
+			xmmask.insert(xmmask.end(), v.second.begin(), v.second.end());
+		}
+		xmg.insert(xmg.end(), {mul, 32u - lg, soff, ebase});
+	}
+	/* the complex PMRs' terms flat, per CoS in rule order: {gate, mask,
+	 * value, slot | guard end << 8 | guarded << 31}, {pmr, last term of the
+	 * PMR, 0, 0}; per CoS its first flat term | count << 16 */
+	std::vector<uint32_t> xflat, xfc(ncos, 0u), xfstart(num_xent + 1, 0u);
+
+	for (uint32_t k = 0; xm && k < num_xent; k++) {
+		const uint32_t nt = xlist[2 * k + 1] >> 24, ts = xlist[2 * k + 1] & 0xffffffu;
+
+		xfstart[k] = (uint32_t)(xflat.size() / 8);
+		for (uint32_t tt = 0; tt < nt; tt++) {
+			xflat.insert(xflat.end(), xterm.begin() + 4 * (ts + tt), xterm.begin() + 4 * (ts + tt + 1));
+			xflat.insert(xflat.end(), {xlist[2 * k], tt + 1 == nt ? 1u : 0u, 0u, 0u});
+		}
+	}
+	xfstart[num_xent] = (uint32_t)(xflat.size() / 8);
+	for (uint32_t c = 0; xm && c < ncos; c++) {
+		const uint32_t st = xcos[2 * c] & 0xffffu, n = xcos[2 * c] >> 16;
+
+		xfc[c] = xfstart[st] | ((xfstart[st + n] - xfstart[st]) << 16);
+	}
+	if (xflat.size() / 8 > XM_MAX_XTERMS)
+		xm = false;
+	if (xm && !wgroups.empty()) {
+		h.flags |= TBL_XMASK;
+		h.num_xment = (uint32_t)xmval.size();
+		xmslot.resize((xmslot.size() + 15u) & ~(size_t)15u, 0xff);
+		h.xm_slot_bytes = (uint32_t)xmslot.size();
+		h.num_xflat = (uint32_t)(xflat.size() / 8);
 	}
 	const uint32_t lean_req = (1u << IFL_L2) | (1u << IFL_L3) | (1u << IFL_L4) |
 				  (1u << IFL_ETH) | (1u << IFL_VLAN) | (1u << IFL_IPV4) |
@@ -1073,7 +1187,14 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.pinfo4_off = align(h.pinfo3_off + (uint32_t)(pinfo3.size() * 4u));
 	h.xcos_off = align(h.pinfo4_off + (uint32_t)(pinfo4.size() * 4u));
 	h.xlist_off = align(h.xcos_off + (uint32_t)(xcos.size() * 4u));
-	h.blob_bytes = align(h.xlist_off + (uint32_t)(xlist.size() * 4u));
+	h.xm_off = align(h.xlist_off + (uint32_t)(xlist.size() * 4u));
+	/* TBL_XMASK region: uint4 xmg[num_wgroups] {mul, shift, slot offset,
+	 * entry base}, masks[num_xment][XM_WORDS], values[num_xment], slot
+	 * bytes (16-byte multiple), 2 x uint4 xflat[num_xflat], xfc[num_cos] */
+	const uint32_t xm_bytes = (h.flags & TBL_XMASK) ?
+		(uint32_t)(xmg.size() * 4u + xmmask.size() * 4u + xmval.size() * 4u + xmslot.size() +
+			   xflat.size() * 4u + xfc.size() * 4u) : 0u;
+	h.blob_bytes = align(h.xm_off + xm_bytes);
 	if (h.blob_bytes == 0)
 		h.blob_bytes = 64;
 	blob.assign(h.blob_bytes, 0);
@@ -1121,6 +1242,22 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		memcpy(blob.data() + h.xcos_off, xcos.data(), xcos.size() * 4u);
 	if (!xlist.empty())
 		memcpy(blob.data() + h.xlist_off, xlist.data(), xlist.size() * 4u);
+	if (h.flags & TBL_XMASK) {
+		uint8_t *o = blob.data() + h.xm_off;
+
+		memcpy(o, xmg.data(), xmg.size() * 4u);
+		o += xmg.size() * 4u;
+		memcpy(o, xmmask.data(), xmmask.size() * 4u);
+		o += xmmask.size() * 4u;
+		memcpy(o, xmval.data(), xmval.size() * 4u);
+		o += xmval.size() * 4u;
+		memcpy(o, xmslot.data(), xmslot.size());
+		o += xmslot.size();
+		if (!xflat.empty())
+			memcpy(o, xflat.data(), xflat.size() * 4u);
+		o += xflat.size() * 4u;
+		memcpy(o, xfc.data(), xfc.size() * 4u);
+	}
 	*hdr_out = h;
 	return 0;
 }

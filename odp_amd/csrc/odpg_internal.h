@@ -99,6 +99,15 @@ typedef struct dcos_s {
 			      * over a frame word (no frame-length slot) */
 #define TBL_XWALK      0x200 /* hybrid hash walk: walk groups over the single-word
                               * PMRs, xcos / xlist name the complex ones per CoS */
+#define TBL_XGF        0x800 /* TBL_XWALK with every complex PMR in xterm
+			      * records (the form classify_gf.hip evaluates) */
+#define TBL_XMASK      0x1000 /* TBL_XGF with <= XM_MAX_PMR PMRs and a collision-free
+			       * value hash per walk group: the hit-map form
+			       * (cls_compile.cpp "TBL_XMASK") */
+#define XM_MAX_PMR     256
+#define XM_WORDS       8     /* hit-map words per packet (XM_MAX_PMR / 32) */
+#define XM_MAX_LG      10    /* largest per-group slot table: 1024 bytes */
+#define XM_MAX_XTERMS  512   /* complex-PMR terms the kernel evaluates per packet */
 #define TBL_LEAN64HW   0x100 /* TBL_HASHWALK with <= 4 walk groups whose gates
 			      * the lean kernel's register parse computes: the
 			      * lean kernel's walk-group form */
@@ -293,6 +302,10 @@ typedef struct dtable_hdr_s {
 	                      *  uint4 xterm records (cls_compile.cpp) */
 	uint32_t num_xlist;
 	uint32_t num_xwords;
+	uint32_t xm_off;     /* TBL_XMASK region (cls_compile.cpp) */
+	uint32_t num_xment;
+	uint32_t xm_slot_bytes;
+	uint32_t num_xflat;
 	uint32_t blob_bytes;
 } dtable_hdr_t;
 
@@ -369,6 +382,8 @@ typedef struct odpg_launch_args {
 	const uint2_t *xcos;        /* TBL_XWALK */
 	const uint32_t *xlist;
 	uint32_t num_xlist, num_xwords;
+	const uint32_t *xm;         /* TBL_XMASK region */
+	uint32_t num_xment, xm_slot_bytes, num_xflat;
 	/* lean 64-byte kernel (classify64.hip): CoS start state, from the host
 	 * copy of the table */
 	uint32_t l64_err_cos, l64_err_act, l64_def_cos, l64_def_act, l64_def_ci, l64_def_rules;

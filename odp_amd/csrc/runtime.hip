@@ -681,6 +681,10 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.xlist = (const uint32_t *)((const uint8_t *)t->dblob + h.xlist_off);
 	a.num_xlist = h.num_xlist;
 	a.num_xwords = h.num_xwords;
+	a.xm = (const uint32_t *)((const uint8_t *)t->dblob + h.xm_off);
+	a.num_xment = h.num_xment;
+	a.xm_slot_bytes = h.xm_slot_bytes;
+	a.num_xflat = h.num_xflat;
 	{
 		/* start state of cls_select_cos (odp_classification.c:1669-1701)
 		 * for the lean kernel, as classify.hip derives it per packet */

@@ -94,3 +94,14 @@ def assert_counters(f, e, what=""):
             raise AssertionError(f"{what}: counters '{k}' differ at {bad.tolist()}: "
                                  f"{[int(f[k][tuple(b)]) for b in bad]} vs "
                                  f"{[int(e[k][tuple(b)]) for b in bad]}")
+
+
+TBL_XWALK, TBL_XGF, TBL_XMASK = 0x200, 0x800, 0x1000    # odpg_internal.h table forms
+
+
+def table_flags(rules):
+    """dtable_hdr_t.flags of the compiled image (odpg_rules_compile: a
+    16-byte image header, then the table header, flags at +12)"""
+    from odp_amd import gpu
+    img = gpu.compile_rules(rules)
+    return int.from_bytes(img[28:32], "little")

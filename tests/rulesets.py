@@ -262,3 +262,107 @@ def random_mixed_rules(cls, pktio, seed, n_cos=24, complex_share=0.3, stats=True
             if p:
                 pmrs.append(p)
     return {"coses": coses, "error": err, "pmrs": pmrs}
+
+
+def _ip_csum_fix(a):
+    """recompute the IPv4 header checksum of a (1, len) Eth/IPv4 frame array"""
+    ihl = int(a[0, 14] & 0x0F) * 4
+    a[0, 24:26] = 0
+    c = int(gen.csum(gen.ones_sum(a, 14, 14 + ihl))[0])
+    a[0, 24], a[0, 25] = c >> 8, c & 0xFF
+
+
+def _edge_frame(rng, clean):
+    lens = (64, 65, 66, 67, 70, 73, 74, 75, 80, 127, 128, 129, 191, 570, 1514, 1515, 1518, 2000)
+    v6 = rng.integers(3) == 0
+    tcp = rng.integers(2) == 0
+    proto = gen.PROTO_TCP if tcp else gen.PROTO_UDP
+    n = int(lens[rng.integers(len(lens))])
+    kind = int(rng.integers(6 if clean else 16))
+    if v6 and kind == 5 and clean:
+        kind = 0
+    dport = 4500 if kind in (5, 14) else int(rng.integers(64))
+    sport = int(rng.integers(1 << 16))
+    src, dst = (np.array([rng.integers(1 << 32)], np.uint64) for _ in range(2))
+    if v6:
+        a = gen.ipv6_frames(1, max(n, 74 if tcp else 62), src, dst, proto, sport, dport)
+    else:
+        a = gen.ipv4_frames(1, n, src, dst, proto, sport, dport)
+    l4 = 54 if v6 else 34
+    L = a.shape[1]
+    if kind == 1:                                    # bad L4 checksum
+        j = int(rng.integers(l4, L))
+        a[0, j] ^= int(rng.integers(1, 256))
+    elif kind == 2:
+        if not tcp:
+            a[0, l4 + 6:l4 + 8] = 0                  # UDP checksum 0
+        elif L > 64:
+            a[0, int(rng.integers(64, L))] ^= 0x41   # bad sum in the tail only
+    elif kind == 3:
+        if v6:
+            a[0, 38] = 0xFF                          # multicast destination
+        else:
+            a[0, 20] |= 0x20                         # more fragments
+            _ip_csum_fix(a)
+    elif kind == 4:
+        a[0, 0:6] = 0xFF if rng.integers(2) else a[0, 0:6] | 1
+        if not v6:
+            a[0, 30:34] = [0xFF] * 4 if rng.integers(2) else [224, 0, 0, 9]
+            _ip_csum_fix(a)
+    elif kind == 5:                                  # NAT-T marker present / absent
+        if rng.integers(2) and L >= 46:
+            a[0, 42:46] = 0
+    elif kind == 6:
+        if v6:
+            a[0, 18:20] = [0xFF, 0x00]               # payload past the frame
+        else:
+            a[0, 24] ^= 0x5A                         # bad IPv4 header checksum
+    elif kind == 7:
+        if v6:
+            a[0, 20] = 0                             # hop-by-hop next header
+        else:
+            a[0, 16:18] = [(L - 13) >> 8, (L - 13) & 0xFF]   # tot_len past the frame
+            _ip_csum_fix(a)
+    elif kind == 8 and not v6:                       # short tot_len, valid header
+        t = int(rng.integers(20, L - 13))
+        a[0, 16:18] = [t >> 8, t & 0xFF]
+        _ip_csum_fix(a)
+    elif kind == 9 and not v6:
+        a[0, 14] = 0x46                              # IHL 6
+        _ip_csum_fix(a)
+    elif kind == 10:
+        if tcp:
+            a[0, l4 + 12] = int(rng.integers(0, 5)) << 4   # data offset < 5
+        else:
+            a[0, l4 + 4:l4 + 6] = [0, int(rng.integers(0, 8))]   # UDP length < 8
+    elif kind == 11:
+        a = a[:, :int(rng.integers(14, L))]
+    elif kind == 12:
+        a = np.concatenate([a[:, :12], np.array([[0x81, 0, 0, 7]], np.uint8), a[:, 12:]], 1)
+    elif kind == 13:
+        for _ in range(int(rng.integers(1, 4))):
+            a[0, int(rng.integers(14, min(L, 80)))] = int(rng.integers(256))
+    elif kind == 14 and v6 and tcp:
+        a = a[:, :int(rng.integers(64, 74))]         # TCP header past the frame
+    elif kind == 15:
+        a[0, 20 if v6 else 23] = 1                   # ICMP
+        if not v6:
+            _ip_csum_fix(a)
+    return bytes(a[0])
+
+
+def imix_edge_corpus(n, seed=3):
+    """IMIX-length Eth/IPv4|IPv6/UDP|TCP frames at the edges of the lean
+    descriptor kernel's register parse (classify_gf.hip): lengths around the
+    64-byte window and 1514 (jumbo), IPv6 TCP data offset in the byte past
+    the window, bad / zero / tail-only-bad checksums, fragments, broadcast /
+    multicast, NAT-T port 4500, tot_len / payload_len edges, IHL 6, short UDP
+    length / TCP data offset, truncations, VLAN, ICMP. Half of the 64-frame
+    blocks hold register-parse frames only (whole fast waves), the others
+    every kind (generic waves)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for b0 in range(0, n, 64):
+        clean = rng.integers(2) == 0
+        out += [_edge_frame(rng, clean) for _ in range(min(64, n - b0))]
+    return out

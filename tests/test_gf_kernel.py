@@ -1,0 +1,75 @@
+"""The lean descriptor kernel (classify_gf.hip): descriptor (IMIX) batches
+under a hybrid hash-walk table in its hit-map form (TBL_XMASK), verdict
+words only, auto mode. Bit-exact against the oracle on the C3 traffic, the
+IMIX edge corpus (rulesets.imix_edge_corpus: every register-parse edge and
+the frames that must leave it), the mutation corpus and the golden frames,
+under each RX checksum option mix; and the launch really took the kernel
+(odpg_last_kernel() == 2)."""
+import numpy as np
+import pytest
+
+import oracle
+import rulesets
+from helpers import ALL_CHKSUM, TBL_XMASK, assert_same, golden_frames, pack, table_flags
+from odp_amd import _lib as L
+from odp_amd import gen
+
+OPTS = [0, L.PKTIN_IPV4_CHKSUM, L.PKTIN_UDP_CHKSUM | L.PKTIN_TCP_CHKSUM, L.PKTIN_TCP_CHKSUM,
+        ALL_CHKSUM]
+
+
+def _c3(cls, opt):
+    p = cls.loop_pktio(pktin=opt)
+    gen.build_c3_rules(cls, p, stats=False)
+    assert cls.pktio_start(p) == 0
+    return cls.pktio_rules(p)
+
+
+def test_c3_table_takes_the_gf_form(fresh_cls):
+    assert table_flags(_c3(fresh_cls, ALL_CHKSUM)) & TBL_XMASK
+
+
+def test_edge_corpus_spans_both_parses():
+    fr = rulesets.imix_edge_corpus(4096)
+    lens = np.array([len(f) for f in fr])
+    assert lens.min() < 64 and lens.max() > 1514 and np.any(lens == 64) and np.any(lens == 74)
+    v6 = sum(1 for f in fr if f[12:14] == b"\x86\xdd")
+    assert 0.2 < v6 / len(fr) < 0.45
+
+
+def _verdicts(ctx, rules, buf, n, desc, opt):
+    tbl = ctx.table(rules)
+    g = ctx.classify(tbl, buf, n, desc=desc, opt=opt, want_mark=False, want_meta=False,
+                     want_stats=False)
+    assert L.lib.odpg_last_kernel() == 2, "the launch did not take the lean descriptor kernel"
+    o = oracle.classify(rules, buf, n, desc=desc, opt=opt)
+    return g, o
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", OPTS)
+@pytest.mark.parametrize("corpus", ["c3", "edge", "mutate", "golden"])
+def test_gf_kernel_matches_oracle(gpu_ctx, fresh_cls, opt, corpus):
+    rules = _c3(fresh_cls, opt)
+    if corpus == "c3":
+        n = 64 * 1031 + 17
+        buf, desc = gen.c3_frames(n, seed=77 + opt)
+    else:
+        frames = (rulesets.imix_edge_corpus(24000, seed=opt + 1) if corpus == "edge" else
+                  rulesets.mutate_corpus(12000, seed=61) if corpus == "mutate" else
+                  golden_frames()[1])
+        buf, desc = pack(frames)
+        n = len(frames)
+    g, o = _verdicts(gpu_ctx, rules, buf, n, desc, opt)
+    assert_same({"out": g["out"]}, {"out": o["out"]}, f"gf {corpus} opt={opt:#x}")
+    if corpus == "c3":
+        assert len(np.unique(o["out"] & 0xFFFF)) > 10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 4097, 1 << 18])
+def test_gf_kernel_batch_sizes(gpu_ctx, fresh_cls, n):
+    rules = _c3(fresh_cls, ALL_CHKSUM)
+    buf, desc = gen.c3_frames(n, seed=n)
+    g, o = _verdicts(gpu_ctx, rules, buf, n, desc, ALL_CHKSUM)
+    assert_same({"out": g["out"]}, {"out": o["out"]}, f"gf n={n}")

@@ -47,6 +47,12 @@ def both(ctx, rules, buf, num, stride=0, desc=None, opt=0, layer=L.LAYER_ALL, cl
         lean = ctx.classify(tbl, buf, num, stride=stride, opt=opt, layer=layer,
                             classify=classify, want_mark=False, want_meta=False)
         assert_same(res[1], lean, f"walk vs verdict+stats (kernel {L.lib.odpg_last_kernel()})")
+    if desc is not None:
+        # verdict words only: auto mode may take the lean descriptor kernel
+        vo = ctx.classify(tbl, buf, num, desc=desc, opt=opt, layer=layer, classify=classify,
+                          want_mark=False, want_meta=False, want_stats=False)
+        assert_same({"out": res[1]["out"]}, {"out": vo["out"]},
+                    f"walk vs verdict-only (kernel {L.lib.odpg_last_kernel()})")
     # sharded counters (odpg.h): the walk and auto (lean kernel where it
     # applies), two launches each, one fold against the oracle's counts
     cnt = ctx.counters(tbl)

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
 for c in ${CFGS:-c2 c3}; do
-  timeout -k 10 400 python bench.py --config $c ${BENCH_ARGS:---e2e} > $OUT/bench_$c.json 2> $OUT/bench_$c.err
+  timeout -k 10 400 python bench.py --config $c ${BENCH_ARGS---e2e} > $OUT/bench_$c.json 2> $OUT/bench_$c.err
   rc=$?; echo "bench $c: $rc"; cat $OUT/bench_$c.json; tail -3 $OUT/bench_$c.err
   [ $rc -eq 0 ] || exit $rc
 done
