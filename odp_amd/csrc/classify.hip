@@ -1591,8 +1591,9 @@ extern "C" size_t odpg_clsgf_lds(const odpg_launch_args *a);
 
 /* the lean descriptor kernel (classify_gf.hip) covers this launch: a
  * descriptor batch, a hybrid hash-walk table in its hit-map form
- * (TBL_XMASK) without hash-queue CoS, verdict words only, full parse with
- * classification and no drop options */
+ * (TBL_XMASK) without hash-queue CoS, verdict words and the sharded pktio /
+ * per-queue counters (no CoS counters), full parse with classification and
+ * no drop options */
 static bool gf_ok(const odpg_launch_args &a)
 {
 	static const bool off = getenv("ODPG_NO_GF") != nullptr;
@@ -1603,7 +1604,7 @@ static bool gf_ok(const odpg_launch_args &a)
 	return !off && a.mode == 0 && a.desc && (a.tbl_flags & TBL_XMASK) &&
 	       !(a.tbl_flags & TBL_ANY_HASHQ) && a.num_cos < ODPG_COS_NOCLS &&
 	       odpg_clsgf_lds(&a) <= odpg_lds_limit() &&
-	       !a.mark && !a.meta && !a.stats && !a.cnt.row &&
+	       !a.mark && !a.meta && !a.stats && !(a.cnt.row && a.cnt.cos) &&
 	       a.layer >= LAYER_L4 && a.classify && !(a.opt & drops) && !(a.opt >> 32);
 }
 
@@ -1653,7 +1654,7 @@ extern "C" int odpg_launch_classify(const odpg_launch_args *a, hipStream_t s)
 
 	__atomic_store_n(&g_last_kernel, lean ? 1 : gf ? 2 : 0, __ATOMIC_RELAXED);
 	if (gf)
-		return odpg_launch_clsgf(a, s);
+		return odpg_launch_clsgf(a, s);   /* counters folded at read time */
 	if (lean) {
 		int rc = odpg_launch_cls64(a, s);
 

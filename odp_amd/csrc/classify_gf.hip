@@ -49,6 +49,9 @@
 #ifndef GF_WAVES            /* waves per SIMD the launch bounds ask for */
 #define GF_WAVES 5
 #endif
+#ifndef GF_LATE_ODD         /* odd waves sum their tails after the walk */
+#define GF_LATE_ODD 0
+#endif
 
 struct GFArgs {
 	const uint8_t *frames;
@@ -63,7 +66,15 @@ struct GFArgs {
 	const uint32_t *xm_rest;    /* TBL_XMASK: masks[num_xment][XM_WORDS], values, slot bytes */
 	uint32_t num_xment, xm_slot_bytes, num_xflat;
 	const uint32_t *xfc;        /* per CoS: first flat complex term | count << 16 */
+	const odpg_cnt_dev *cnt;    /* CM 2: the sharded counters' layout */
 };
+
+/* sharded-counter histogram bins before the CoS bins (CM 2) */
+#define GF_BIN_ERR    0u
+#define GF_BIN_PDROP  1u
+#define GF_BIN_NOCOS  2u
+#define GF_BIN_DROP   3u
+#define GF_BIN_EXTRA  4u
 
 typedef unsigned short gf_us2 __attribute__((ext_vector_type(2)));
 
@@ -256,8 +267,9 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 	return (fl & FL_ERROR_MASK) != 0u;
 }
 
+/* CM: counters of the launch, 0 none, 2 sharded counter rows (odpg.h) */
 template <int CM>
-__global__ __launch_bounds__(GF_BLOCK, GF_WAVES * 256 / GF_BLOCK) void
+__global__ __launch_bounds__(GF_BLOCK) __attribute__((amdgpu_waves_per_eu(GF_WAVES))) void
 odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__restrict__ xmg,
 		  const uint4 *__restrict__ xf, const odpg_desc_t *__restrict__ descs,
 		  odpg_out_t *__restrict__ out)
@@ -267,7 +279,11 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 	constexpr uint32_t RW = 16;                     /* generic-parse LDS row (dwords) */
 	uint32_t *row = smem + threadIdx.x * RW;
-	uint32_t *tb = smem + GF_BLOCK * RW;
+	/* CM 2: the workgroup's histogram after the rows (odpg.h "sharded
+	 * counters"): four bins, then one per CoS */
+	uint32_t *dlv = smem + GF_BLOCK * RW;
+	const uint32_t nbins = CM == 2 ? ((A.num_cos + GF_BIN_EXTRA + 3u) & ~3u) : 0u;
+	uint32_t *tb = dlv + nbins;
 	/* hit-map entries (2 x uint4 each), their values, the slot bytes */
 	uint4 *xmm = (uint4 *)tb;
 	uint32_t *xmv = tb + XM_WORDS * A.num_xment;
@@ -342,6 +358,23 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 	}
 	for (uint32_t k = threadIdx.x; k < 2u * A.num_xflat; k += GF_BLOCK)
 		xfl[k] = xf[k];
+	/* CM 2: the counter layout is read now, not behind the tile loop's
+	 * last wait; the workgroup's last wave to finish flushes the histogram */
+	__shared__ uint32_t waves_done;
+	__shared__ unsigned long long octets;
+	odpg_cnt_dev C = {};
+
+	if constexpr (CM == 2) {
+		C = *A.cnt;
+		for (uint32_t k = threadIdx.x; k < nbins; k += GF_BLOCK)
+			dlv[k] = 0u;
+		if (threadIdx.x == 0u) {
+			waves_done = 0u;
+			octets = 0ull;
+		}
+	}
+	uint32_t lane_oct = 0u;     /* octets this lane handed over (< 2^32 per lane) */
+
 	__syncthreads();
 
 	const uint32_t nwg = A.nwg;
@@ -496,8 +529,13 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 			keys(key);
 		}
 
-		/* ---- checksum bytes past the window: the whole wave --------------- */
-		{
+		/* ---- checksum bytes past the window: the whole wave. Even waves
+		 * sum them before the walk, odd waves after it (a pending lane walks
+		 * as if its L4 checksum were good; one that fails then takes the
+		 * error CoS, which error packets get without a walk): persistent
+		 * waves that start together would otherwise stream and walk in
+		 * step, leaving the memory idle while they all walk */
+		auto tails = [&]() {
 			const uint64_t pm = __ballot(ret == PARSE_PEND);
 
 #ifdef GF_EXP_NOTAIL
@@ -510,14 +548,18 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 				if (ret == PARSE_PEND)
 					ret = finish_l4(p, pd, tail, (uint64_t)opt);
 			}
-		}
+		};
+		const bool late = GF_LATE_ODD && (gw & 1u);
+
+		if (!late)
+			tails();
 
 		/* the next tile's windows, in flight during the walk */
 		load_win(fn, xn, dn);
 		dnn = load_desc(t + 2u * nwaves);
 
 		/* ---- CoS walk (cls_select_cos + match_pmr_cos) ------------------ */
-		const bool err = (p.fl & FL_ERROR_MASK) != 0u;
+		bool err = (p.fl & FL_ERROR_MASK) != 0u;
 		const bool want_cls = live && ret >= 0;
 		uint32_t cos = ODPG_COS_NOCLS;
 		bool active = false, any_match = false;
@@ -623,6 +665,17 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 			}
 		}
 
+		if (late) {
+			tails();
+			if (want_cls && !err && (p.fl & FL_ERROR_MASK)) {
+				/* cls_select_cos's error branch (no PMR walk) */
+				cos = A.error_cos < 0 ? ODPG_COS_NONE : (uint32_t)A.error_cos;
+				any_match = false;
+				mark = 0u;
+			}
+			err = (p.fl & FL_ERROR_MASK) != 0u;
+		}
+
 		/* ---- verdict word (odpg.h) ------------------------------------- */
 		if (live) {
 			int cret = 0;
@@ -654,6 +707,74 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 			if (ret)
 				w |= ODPG_OUT_PARSE_ERR;
 			out[i] = w;
+			if constexpr (CM == 2) {
+				/* one histogram add per packet carries every counter: the
+				 * CoS it is handed to error-free (_odp_cls_enq; in_packets,
+				 * in_octets), an error packet (to the error CoS; in_errors),
+				 * a parse drop (in_errors), no CoS or a CoS loop
+				 * (in_discards), a drop CoS (no counter) */
+				const uint32_t bn = ret < 0 ? GF_BIN_PDROP : err ? GF_BIN_ERR :
+						    cos >= A.num_cos ? GF_BIN_NOCOS :
+						    cret == 1 ? GF_BIN_DROP : GF_BIN_EXTRA + cos;
+
+				atomicAdd(&dlv[bn], 1u);
+				lane_oct += bn >= GF_BIN_EXTRA ? len : 0u;
+			}
+		}
+	}
+	if constexpr (CM == 2) {
+		/* loopback_recv accounting (loop.c:304-374) and the per-queue
+		 * delivery counts into this workgroup's counter row: no barrier,
+		 * each wave counts itself done after its adds, the last one of the
+		 * workgroup flushes while the others have exited */
+		const uint64_t wo = (uint64_t)wave_sum_u32(lane_oct & 0xffffu) +
+				    ((uint64_t)wave_sum_u32(lane_oct >> 16) << 16);
+
+		if (lane == 0u && wo)
+			atomicAdd(&octets, (unsigned long long)wo);
+		__threadfence_block();
+		uint32_t prev = 0u;
+
+		if (lane == 0u)
+			prev = atomicAdd(&waves_done, 1u);
+		if ((uint32_t)__builtin_amdgcn_readfirstlane((int)prev) != GF_BLOCK / 64u - 1u)
+			return;
+		__threadfence_block();
+		unsigned long long *r = (unsigned long long *)(C.rows + (size_t)blockIdx.x * C.words);
+		const uint32_t nc = A.num_cos < C.ncos ? A.num_cos : C.ncos;
+		/* without hash queues each CoS owns one column */
+		auto col = [&](uint32_t c) { return 4u + C.ncos + (C.ident ? c : C.qcol[c]); };
+		uint32_t tot = 0u;
+
+		for (uint32_t k0 = 0; k0 < nc; k0 += 64u) {
+			const uint32_t k = k0 + lane;
+			const uint32_t x = k < nc ? dlv[GF_BIN_EXTRA + k] : 0u;
+
+			if (x)
+				atomicAdd(r + col(k), (unsigned long long)x);
+			tot += x;
+		}
+		const uint32_t tp = wave_sum_u32(tot);                  /* in_packets */
+
+		if (lane == 0u) {
+			const uint32_t ne = dlv[GF_BIN_ERR], np = dlv[GF_BIN_PDROP];
+			uint32_t nd = dlv[GF_BIN_NOCOS];
+			const uint32_t ec = A.error_cos < 0 ? 0xffffffffu : (uint32_t)A.error_cos;
+
+			if (tp) {
+				atomicAdd(r + 0, (unsigned long long)tp);
+				atomicAdd(r + 1, octets);
+			}
+			/* error packets: delivered to the error CoS unless it drops;
+			 * without an error CoS they are discards too */
+			if (ne && ec < nc && (cinfo[ec].y & 0xffu) != 1u)
+				atomicAdd(r + col(ec), (unsigned long long)ne);
+			else if (ec >= nc)
+				nd += ne;
+			if (ne + np)
+				atomicAdd(r + 2, (unsigned long long)(ne + np));
+			if (nd)
+				atomicAdd(r + 3, (unsigned long long)nd);
 		}
 	}
 }
@@ -667,7 +788,9 @@ extern "C" size_t odpg_clsgf_lds(const odpg_launch_args *a)
 {
 	const size_t tb = (size_t)a->num_xment * (XM_WORDS + 1u) * 4u + 12u + a->xm_slot_bytes;
 
-	return (size_t)GF_BLOCK * 16u * 4u + tb + (size_t)((a->num_cos + 1u) & ~1u) * 8u +
+	const size_t bins = a->cnt.row ? (((size_t)a->num_cos + GF_BIN_EXTRA + 3u) & ~(size_t)3u) * 4u : 0u;
+
+	return (size_t)GF_BLOCK * 16u * 4u + bins + tb + (size_t)((a->num_cos + 1u) & ~1u) * 8u +
 	       (size_t)a->num_pmr * 16u + (size_t)a->num_xflat * 32u;
 }
 
@@ -696,14 +819,31 @@ extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s)
 					  a->xm_slot_bytes / 4u);
 
 	A.xfc = (const uint32_t *)(xf + 2u * a->num_xflat);
+	A.cnt = a->cnt.dev;
 
 	const size_t lds = odpg_clsgf_lds(a);
 	const uint32_t ntiles = (a->num + 63u) / 64u;
 	const uint32_t want = (ntiles + GF_BLOCK / 64u - 1u) / (GF_BLOCK / 64u);
-	uint32_t grid = odpg_resident_grid((const void *)odpg_clsgf_kernel<0>, GF_BLOCK, lds);
+	const uint32_t rows = a->cnt.row ? a->cnt.rows : 0xffffffffu;
 
-	grid = grid < want ? grid : want;
-	hipLaunchKernelGGL((odpg_clsgf_kernel<0>), dim3(grid ? grid : 1u), dim3(GF_BLOCK), lds, s, A,
-			   (const uint4 *)a->wgroups, (const uint4 *)a->xm, xf, a->desc, a->out);
+	/* resident grid of the instantiation launched, at most one workgroup per
+	 * counter row */
+	auto go = [&](const void *k, auto launch) {
+		uint32_t grid = odpg_resident_grid(k, GF_BLOCK, lds);
+
+		grid = grid < want ? grid : want;
+		grid = grid < rows ? grid : rows;
+		launch(grid ? grid : 1u);
+	};
+	if (a->cnt.row)
+		go((const void *)odpg_clsgf_kernel<2>, [&](uint32_t grid) {
+			hipLaunchKernelGGL((odpg_clsgf_kernel<2>), dim3(grid), dim3(GF_BLOCK), lds, s, A,
+					   (const uint4 *)a->wgroups, (const uint4 *)a->xm, xf, a->desc, a->out);
+		});
+	else
+		go((const void *)odpg_clsgf_kernel<0>, [&](uint32_t grid) {
+			hipLaunchKernelGGL((odpg_clsgf_kernel<0>), dim3(grid), dim3(GF_BLOCK), lds, s, A,
+					   (const uint4 *)a->wgroups, (const uint4 *)a->xm, xf, a->desc, a->out);
+		});
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

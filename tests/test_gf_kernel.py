@@ -73,3 +73,30 @@ def test_gf_kernel_batch_sizes(gpu_ctx, fresh_cls, n):
     buf, desc = gen.c3_frames(n, seed=n)
     g, o = _verdicts(gpu_ctx, rules, buf, n, desc, ALL_CHKSUM)
     assert_same({"out": g["out"]}, {"out": o["out"]}, f"gf n={n}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("corpus", ["c3", "edge"])
+def test_gf_kernel_sharded_counters(gpu_ctx, fresh_cls, corpus):
+    """The counted launch (sharded pktio / per-queue counters) on the lean
+    descriptor kernel: two launches, one fold, against the oracle's counts."""
+    from helpers import assert_counters, expected_counters
+    rules = _c3(fresh_cls, ALL_CHKSUM)
+    if corpus == "c3":
+        n = 64 * 517 + 9
+        buf, desc = gen.c3_frames(n, seed=5)
+    else:
+        frames = rulesets.imix_edge_corpus(20000, seed=11)
+        buf, desc = pack(frames)
+        n = len(frames)
+    tbl = gpu_ctx.table(rules)
+    o = oracle.classify(rules, buf, n, desc=desc, opt=ALL_CHKSUM)
+    cnt = gpu_ctx.counters(tbl)
+    for _ in range(2):
+        g = gpu_ctx.classify(tbl, buf, n, desc=desc, opt=ALL_CHKSUM, want_mark=False,
+                             want_meta=False, counters=cnt)
+        assert L.lib.odpg_last_kernel() == 2
+        assert np.array_equal(g["out"], o["out"])
+    want = expected_counters(o, tbl.num_cos)
+    assert_counters(cnt.fold(), {k: v * 2 for k, v in want.items()}, f"gf counters {corpus}")
+    cnt.close()
