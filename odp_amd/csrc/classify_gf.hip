@@ -267,6 +267,169 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 	return (fl & FL_ERROR_MASK) != 0u;
 }
 
+#ifndef GF_SWEEP            /* 1: one coalesced sweep of every frame byte per tile */
+#define GF_SWEEP 0
+#endif
+#ifndef GF_WIN_LATE         /* next tile's windows issued after the walk */
+#define GF_WIN_LATE 0
+#endif
+
+/* One coalesced sweep over every byte of a wave's 64 frames: the frames'
+ * 64-byte units (unit 0 the window, units 1.. the tail) numbered frame after
+ * frame and spread over the lanes, 64 units per pass, two passes in flight;
+ * each 128-byte line is requested by neighbouring lanes of one instruction,
+ * once. Unit 0 lands in its frame's LDS row (zero past the frame), the first
+ * dword of unit 1 in x16s[frame]; every other byte is summed (v_dot2) and
+ * attributed to its frame by a wave prefix sum per pass: tsum[lane] = the
+ * one's-complement partial of the lane's frame's bytes [64, len). All lanes
+ * must be active. */
+struct SwUnit {
+	uint4 q[4];
+	uint32_t pv;
+	uint32_t ou;        /* owner lane | unit << 6 | bytes of the frame it holds << 16 */
+};
+
+/* a pass's unit: its owner (binary search of the prefix sums over the lanes
+ * that can own a unit of the pass), the bytes of the owner's frame it holds,
+ * and its loads (only 16-byte chunks holding frame bytes; the one partial
+ * dword again as a dword). Every lane active: a bpermute under a partial
+ * exec mask reads inactive source lanes as 0 */
+struct SwPlan {
+	uint32_t len, nu, incl, first, total, cb_lo, cb_hi;
+};
+
+__device__ __forceinline__ void sw_plan(const SwPlan &S, uint32_t base, SwUnit &U)
+{
+	const uint32_t lane = __lane_id();
+	const uint32_t sl = min(base + lane, S.total - 1u);
+	const bool valid = base + lane < S.total;
+	const uint64_t past = __ballot(S.incl > base);
+	const uint64_t beyond = __ballot(S.incl > base + 63u);
+	const uint32_t lo = past ? (uint32_t)__builtin_ctzll(past) : 63u;
+	const uint32_t hi = beyond ? (uint32_t)__builtin_ctzll(beyond) : 63u;
+	const uint32_t span = hi > lo ? hi - lo : 0u;
+	int pp = -1;
+
+	for (uint32_t st = span ? 1u << (31 - __builtin_clz(span)) : 0u; st; st >>= 1) {
+		const uint32_t cand = (uint32_t)(pp + (int)st);
+		const uint32_t src = lo + cand < 64u ? lo + cand : 63u;
+		const uint32_t v = lane_pull(S.incl, src);
+
+		if (cand <= span && v <= sl)
+			pp = (int)cand;
+	}
+	const uint32_t o = lo + (uint32_t)(pp + 1);
+	const uint64_t a = (((uint64_t)lane_pull(S.cb_hi, o) << 32) | lane_pull(S.cb_lo, o)) +
+			   64ull * sl;
+	const uint32_t ofirst = lane_pull(S.first, o), olen = lane_pull(S.len, o);
+	const uint32_t u = sl - ofirst;
+	/* bytes of the owner's frame in the unit, capped at 65 (> 64: whole) */
+	const uint32_t rb = olen - 64u * u;
+	const uint32_t rem = valid ? (rb > 65u ? 65u : rb) : 0u;   /* >= 1 */
+	const uint32_t nw = rem >> 2;
+	const uint32_t pb = rem & 3u;
+
+	U.ou = o | (u << 6) | (rem << 16);
+	U.pv = 0u;
+	if (rem && pb && nw < 16u)
+		U.pv = *(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)(a + 4u * nw) &
+		       ((1u << (8u * pb)) - 1u);
+#pragma unroll
+	for (int j = 0; j < 4; ++j) {
+		U.q[j] = make_uint4(0u, 0u, 0u, 0u);
+		if (16u * j < rem)
+			U.q[j] = ld_g16(a + 16u * j);
+	}
+}
+
+__device__ __forceinline__ void gf_sweep(const uint8_t *frames, uint2 d, uint32_t *rows,
+					 uint32_t *x16s, uint32_t *tsum)
+{
+	const uint32_t lane = __lane_id();
+	SwPlan S;
+	uint32_t acc = 0u;
+
+	S.len = d.y;
+	S.nu = S.len ? ((S.len - 1u) >> 6) + 1u : 0u;
+	S.incl = wave_scan_u32(S.nu);
+	S.first = S.incl - S.nu;
+	S.total = (uint32_t)__builtin_amdgcn_readlane((int)S.incl, 63);
+	/* unit slot s of this lane's frame starts at cb + 64 s */
+	const uint64_t cb = (uint64_t)(uintptr_t)(frames + d.x) - 64ull * S.first;
+
+	S.cb_lo = (uint32_t)cb;
+	S.cb_hi = (uint32_t)(cb >> 32);
+	x16s[lane] = 0u;
+	if (S.len == 0u) {                               /* empty frame: zero window */
+#pragma unroll
+		for (int k = 0; k < 16; k += 4)
+			*(uint4 *)(rows + 16u * lane + k) = make_uint4(0u, 0u, 0u, 0u);
+	}
+	auto consume = [&](const SwUnit &U, uint32_t base) {
+		const uint32_t uo = U.ou & 63u, uu = (U.ou >> 6) & 0x3ffu, rem = U.ou >> 16;
+		const uint32_t nw = rem >> 2;
+		const uint32_t pb = rem & 3u;
+		uint32_t w[16];
+
+#pragma unroll
+		for (int j = 0; j < 4; ++j) {
+			w[4 * j + 0] = 4 * j + 0 < (int)nw ? U.q[j].x : 0u;
+			w[4 * j + 1] = 4 * j + 1 < (int)nw ? U.q[j].y : 0u;
+			w[4 * j + 2] = 4 * j + 2 < (int)nw ? U.q[j].z : 0u;
+			w[4 * j + 3] = 4 * j + 3 < (int)nw ? U.q[j].w : 0u;
+		}
+		uint32_t sum = 0u;
+
+		if (rem && uu == 0u) {
+			uint32_t *r = rows + 16u * uo;
+
+#pragma unroll
+			for (int k = 0; k < 16; ++k)
+				if (pb && (uint32_t)k == nw)
+					w[k] = U.pv;
+#pragma unroll
+			for (int k = 0; k < 16; k += 4)
+				*(uint4 *)(r + k) = make_uint4(w[k], w[k + 1], w[k + 2], w[k + 3]);
+		} else {
+			if (rem && uu == 1u)
+				x16s[uo] = nw ? w[0] : U.pv;
+#pragma unroll
+			for (int k = 0; k < 16; ++k)
+				sum = tail_dot2(w[k], sum);
+			sum = tail_dot2(U.pv, sum);
+		}
+		/* this lane's frame: its units of the pass are lanes [fl, ll] */
+		const uint32_t ps = wave_scan_u32(oc_fold(sum));
+		const bool in = S.nu && S.incl > base && S.first < base + 64u;
+		const uint32_t fl = in && S.first > base ? S.first - base : 0u;
+		const uint32_t ll = in ? (S.incl - 1u < base + 63u ? S.incl - 1u - base : 63u) : 0u;
+		const uint32_t hv = lane_pull(ps, ll);
+		const uint32_t lv = lane_pull(ps, fl ? fl - 1u : 0u);
+
+		acc += in ? hv - (fl ? lv : 0u) : 0u;
+	};
+	SwUnit ua, ub;
+
+	if (S.total) {                                          /* uniform */
+		sw_plan(S, 0u, ua);
+		if (64u < S.total)
+			sw_plan(S, 64u, ub);
+	}
+	for (uint32_t base = 0; base < S.total; base += 128u) {    /* uniform */
+		consume(ua, base);
+		if (base + 128u < S.total)
+			sw_plan(S, base + 128u, ua);
+		if (base + 64u < S.total) {
+			consume(ub, base + 64u);
+			if (base + 192u < S.total)
+				sw_plan(S, base + 192u, ub);
+		}
+	}
+	tsum[lane] = oc_fold(acc);
+	/* the rows written by other lanes are read next by their own lanes */
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+}
+
 /* CM: counters of the launch, 0 none, 2 sharded counter rows (odpg.h) */
 template <int CM>
 __global__ __launch_bounds__(GF_BLOCK) __attribute__((amdgpu_waves_per_eu(GF_WAVES))) void
@@ -297,6 +460,8 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 	 * "xflat"): {gate, mask, value, slot | guard end << 8 | guarded << 31},
 	 * {pmr, last term of the PMR, 0, 0} */
 	uint4 *xfl = pdst + A.num_pmr;
+	/* GF_SWEEP: the wave's x16 words and tail partials (2 x 64 dwords) */
+	uint32_t *swx = (uint32_t *)(xfl + 2u * A.num_xflat) + (threadIdx.x >> 6) * 128u;
 
 	const uint32_t lane = __lane_id();
 	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (GF_BLOCK / 64) +
@@ -333,10 +498,11 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 		}
 		x16 = len > 64u ? *(const uint32_t *)(g + 64u) : 0u;
 	};
-	uint32_t fn[16], xn = 0u;
+	uint32_t fn[16] = {}, xn = 0u;
 	uint2 dn = load_desc(gw), dnn;
 
-	load_win(fn, xn, dn);
+	if (!GF_SWEEP)
+		load_win(fn, xn, dn);
 	dnn = load_desc(gw + nwaves);
 
 	{
@@ -389,15 +555,30 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 		const uint8_t *g = A.frames + d.x;
 		const uint32_t len = live ? d.y : 0u;
 		uint32_t f[16];
-		const uint32_t x16 = xn;
+		uint32_t x16 = xn;
 
+		if constexpr (GF_SWEEP) {
+			gf_sweep(A.frames, make_uint2(d.x, len), smem + (threadIdx.x & ~63u) * RW, swx,
+				 swx + 64u);
 #pragma unroll
-		for (int q = 0; q < 16; ++q) {
-			/* bytes past the frame read as zero (the reference's
-			 * undefined reads past the end: DESIGN.md deviation 1) */
-			const int nb = (int)len - 4 * q;
+			for (int q = 0; q < 16; q += 4) {
+				const uint4 x = *(const uint4 *)(row + q);
 
-			f[q] = nb >= 4 ? fn[q] : nb <= 0 ? 0u : fn[q] & ((1u << (8 * nb)) - 1u);
+				f[q] = x.x;
+				f[q + 1] = x.y;
+				f[q + 2] = x.z;
+				f[q + 3] = x.w;
+			}
+			x16 = swx[lane];
+		} else {
+#pragma unroll
+			for (int q = 0; q < 16; ++q) {
+				/* bytes past the frame read as zero (the reference's
+				 * undefined reads past the end: DESIGN.md deviation 1) */
+				const int nb = (int)len - 4 * q;
+
+				f[q] = nb >= 4 ? fn[q] : nb <= 0 ? 0u : fn[q] & ((1u << (8 * nb)) - 1u);
+			}
 		}
 		dn = dnn;
 
@@ -536,6 +717,27 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 		 * waves that start together would otherwise stream and walk in
 		 * step, leaving the memory idle while they all walk */
 		auto tails = [&]() {
+			if constexpr (GF_SWEEP) {
+				/* the sweep's partial of [64, len), less the bytes [64, a)
+				 * when the L4 header starts past the window (generic frames:
+				 * the residue mod 0xffff is the tail's, and the pending sum
+				 * holds the nonzero protocol term, so the verdict is the
+				 * same) */
+				if (ret == PARSE_PEND) {
+					uint32_t tail = swx[64u + lane];
+
+					if (pd.a > 64u) {
+						Pkt<64, true> v;
+
+						v.row = row;
+						v.g = g;
+						v.len = len;
+						tail = oc_add(tail, 0xffffu - oc_fold(sum_range(v, 64u, pd.a)));
+					}
+					ret = finish_l4(p, pd, tail, (uint64_t)opt);
+				}
+				return;
+			}
 			const uint64_t pm = __ballot(ret == PARSE_PEND);
 
 #ifdef GF_EXP_NOTAIL
@@ -555,7 +757,8 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 			tails();
 
 		/* the next tile's windows, in flight during the walk */
-		load_win(fn, xn, dn);
+		if (!GF_SWEEP && !GF_WIN_LATE)
+			load_win(fn, xn, dn);
 		dnn = load_desc(t + 2u * nwaves);
 
 		/* ---- CoS walk (cls_select_cos + match_pmr_cos) ------------------ */
@@ -676,6 +879,11 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 			err = (p.fl & FL_ERROR_MASK) != 0u;
 		}
 
+		/* GF_WIN_LATE: the next tile's windows after the walk, so that their
+		 * lines are still in L2 when that tile's tails read the rest */
+		if (!GF_SWEEP && GF_WIN_LATE)
+			load_win(fn, xn, dn);
+
 		/* ---- verdict word (odpg.h) ------------------------------------- */
 		if (live) {
 			int cret = 0;
@@ -791,7 +999,8 @@ extern "C" size_t odpg_clsgf_lds(const odpg_launch_args *a)
 	const size_t bins = a->cnt.row ? (((size_t)a->num_cos + GF_BIN_EXTRA + 3u) & ~(size_t)3u) * 4u : 0u;
 
 	return (size_t)GF_BLOCK * 16u * 4u + bins + tb + (size_t)((a->num_cos + 1u) & ~1u) * 8u +
-	       (size_t)a->num_pmr * 16u + (size_t)a->num_xflat * 32u;
+	       (size_t)a->num_pmr * 16u + (size_t)a->num_xflat * 32u +
+	       (GF_SWEEP ? (size_t)GF_BLOCK * 2u * 4u : 0u);
 }
 
 extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s)
