@@ -38,6 +38,11 @@ import os
 import sys
 import time
 
+
+def log(msg):
+    """Progress on stderr (stdout carries only the JSON line)."""
+    print(msg, file=sys.stderr, flush=True)
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -657,6 +662,7 @@ def cpu_baseline(rules, frames, desc, n, stride, opt, args):
         _, used = oracle.classify_mt(rules, frames, n, stride=stride, desc=desc, opt=opt,
                                      nthreads=threads, reps=reps, cpus=cpus)
         rates.append(n * reps / (time.perf_counter() - t) / 1e6)
+        log(f"cpu baseline: {used} threads {rates[-1]:.1f} Mpps")
     # SURVEY.md §8(d) also asks for every core (nproc): the whole affinity
     # mask, pinned, median of 3 shorter runs
     allc = None
@@ -665,13 +671,22 @@ def cpu_baseline(rules, frames, desc, n, stride, opt, args):
     except AttributeError:
         aff = list(range(os.cpu_count() or 1))
     if len(aff) > used:
-        reps_a = max(1, int(args.cpu_seconds / 6 * one * len(aff) * 1e6 / n * 0.5))
+        # calibrated on one pass over the batch with every thread (a box may
+        # grant fewer cores than its affinity mask lists), then 3 runs of
+        # ~cpu_seconds / 6 each
+        t = time.perf_counter()
+        oracle.classify_mt(rules, frames, n, stride=stride, desc=desc, opt=opt,
+                           nthreads=len(aff), reps=1, cpus=aff)
+        cal = n / (time.perf_counter() - t)
+        reps_a = max(1, int(args.cpu_seconds / 6 * cal / n))
+        log(f"cpu baseline: all {len(aff)} CPUs, {cal / 1e6:.1f} Mpps calibration, {reps_a} passes per run")
         ar = []
         for _ in range(3):
             t = time.perf_counter()
             _, ua = oracle.classify_mt(rules, frames, n, stride=stride, desc=desc, opt=opt,
                                        nthreads=len(aff), reps=reps_a, cpus=aff)
             ar.append(n * reps_a / (time.perf_counter() - t) / 1e6)
+            log(f"cpu baseline: all cores {ar[-1]:.1f} Mpps")
         allc = {"value": round(statistics.median(ar), 2), "cores": ua,
                 "runs_mpps": [round(r, 2) for r in ar],
                 "sample": f"median of 3 runs, each {reps_a} passes x {n} pkts, {ua} threads "

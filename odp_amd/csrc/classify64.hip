@@ -57,9 +57,18 @@
 #ifndef L64_BLOCK        /* threads per workgroup */
 #define L64_BLOCK 256
 #endif
+#ifndef L64_BLOCK_HW      /* threads per workgroup of the CoS-keyed cuckoo kernels */
+#define L64_BLOCK_HW L64_BLOCK
+#endif
 #define LB L64_BLOCK
+/* a kernel's workgroup size: the cuckoo tables are one LDS copy per
+ * workgroup, so larger workgroups share it among more waves */
+#define LBH(hw) ((hw) ? L64_BLOCK_HW : L64_BLOCK)
 #ifndef L64_PP           /* two frame buffers used in turn (else one, rotated) */
 #define L64_PP 0
+#endif
+#ifndef L64_COAL         /* coalesced tile loads + swizzled LDS transpose */
+#define L64_COAL 1
 #endif
 
 struct L64Args {
@@ -242,16 +251,17 @@ __device__ __forceinline__ MGd load_mg(const dmgroup_t *g, bool single = true)
  * group is a cuckoo group over a frame word (TBL_MG_CUCKOO): no per-group
  * kind tests in the tile loop. */
 template <int NG, bool HW, int CM, bool CK>
-__global__ __launch_bounds__(LB, (CM == 2 ? L64_WAVES_CNT : HW ? L64_WAVES_HW : L64_WAVES) * 256 / LB) void
+__global__ __launch_bounds__(LBH(HW), (CM == 2 ? L64_WAVES_CNT : HW ? L64_WAVES_HW : L64_WAVES) * 256 / LBH(HW)) void
 odpg_cls64_kernel(const L64Args A)
 {
 	static_assert(!HW || NG > 0, "walk groups are hoisted");
+	constexpr uint32_t LBK = LBH(HW);
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 	constexpr uint32_t RW = 17;                     /* odd dword row stride */
 	uint32_t *row = smem + threadIdx.x * RW;        /* generic-parse LDS row */
 	/* sharded counters (CM 2): the histogram right after the rows, at a
 	 * fixed offset (its adds need no base register); the table after it */
-	uint32_t *dlv = smem + LB * RW;
+	uint32_t *dlv = smem + LBK * RW;
 	const uint32_t nbins = CM == 2 ? ((A.num_cos + BIN_EXTRA + 3u) & ~3u) : 0u;
 	uint4 *ments = (uint4 *)(dlv + nbins);
 	uint4 *pinfo4 = ments + A.num_ment;
@@ -261,15 +271,65 @@ odpg_cls64_kernel(const L64Args A)
 
 	const uint32_t lane = __lane_id();
 	/* wave-uniform (readfirstlane): buffer resources are built from it */
-	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (LB / 64) + (threadIdx.x >> 6));
-	const uint32_t nwaves = gridDim.x * (LB / 64);
+	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (LBK / 64) + (threadIdx.x >> 6));
+	const uint32_t nwaves = gridDim.x * (LBK / 64);
 	const uint32_t ntiles = (A.num + 63u) >> 6;
 	const uint32_t num = A.num;
 	uint32_t fn[16];
 
 	MGd mg[NG > 0 ? NG : 1];
+	/* L64_COAL: a tile's 4 KiB arrive as coalesced 16-byte loads, lane l
+	 * holding chunks l, l + 64, l + 128, l + 192 of the tile (each load
+	 * instruction reads 1 KiB of contiguous lines, not 64 frames' first 16
+	 * bytes), and are transposed to one frame per lane through the wave's own
+	 * 4 KiB of LDS (its generic-parse rows). Chunk c (frame c / 4, part
+	 * c % 4) of frame r sits at row r, slot (part + r + r / 4) % 4: the
+	 * ds_write_b128 lane groups (8 contiguous lanes, banks mod 32) and the
+	 * ds_read_b128 groups ({0-3, 12-15, 20-27}, ... banks mod 64) then both
+	 * touch distinct banks (MI355X_MICROARCH.md "LDS"). */
+	uint32_t *stg = smem + (threadIdx.x & ~63u) * RW;
+	const uint32_t sw_fr = lane >> 2;
+	const uint32_t sw_w = 16u * sw_fr + 4u * (((lane & 3u) + sw_fr + (sw_fr >> 2)) & 3u);
+	const uint32_t sw_c = lane + (lane >> 2);
+	auto load_raw = [&](uint32_t (&dst)[16], uint32_t t) {
+		if (t >= ntiles)
+			return;
+		const size_t lim = (size_t)num * 4u - 1u;
+		const size_t c0 = (size_t)t * 256u + lane;
+
+#pragma unroll
+		for (int q = 0; q < 4; ++q) {
+			const size_t c = c0 + 64u * q;
+			const uint4 x = ld_stream(A.frames + (c < lim ? c : lim));
+
+			dst[4 * q + 0] = x.x;
+			dst[4 * q + 1] = x.y;
+			dst[4 * q + 2] = x.z;
+			dst[4 * q + 3] = x.w;
+		}
+	};
+	/* raw chunks -> LDS -> this lane's frame (the wave's LDS ops run in
+	 * order: the next stage's writes follow this stage's reads) */
+	auto stage = [&](const uint32_t (&raw)[16], uint32_t (&f)[16]) {
+#pragma unroll
+		for (int q = 0; q < 4; ++q)
+			*(uint4 *)(stg + sw_w + 256u * q) =
+				make_uint4(raw[4 * q], raw[4 * q + 1], raw[4 * q + 2], raw[4 * q + 3]);
+#pragma unroll
+		for (int j = 0; j < 4; ++j) {
+			const uint4 x = *(const uint4 *)(stg + 16u * lane + 4u * ((j + sw_c) & 3u));
+
+			f[4 * j + 0] = x.x;
+			f[4 * j + 1] = x.y;
+			f[4 * j + 2] = x.z;
+			f[4 * j + 3] = x.w;
+		}
+	};
+	(void)stage;
 	/* the first tile's frames are issued before the table copy below */
-	{
+	if (L64_COAL) {
+		load_raw(fn, gw);
+	} else {
 		const uint32_t n0 = gw < ntiles ? min(num - gw * 64u, 64u) : 0u;
 		const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
 			(void *)(A.frames + (size_t)(gw < ntiles ? gw : 0u) * 256u), 0, (int)(n0 * 64u),
@@ -287,17 +347,17 @@ odpg_cls64_kernel(const L64Args A)
 	}
 
 	if constexpr (HW) {
-		for (uint32_t k = threadIdx.x; k < A.num_cent; k += LB)
+		for (uint32_t k = threadIdx.x; k < A.num_cent; k += LBK)
 			cents[k] = A.cents[k];
-		for (uint32_t k = threadIdx.x; k < A.num_pmr; k += LB)
+		for (uint32_t k = threadIdx.x; k < A.num_pmr; k += LBK)
 			pinfo3[k] = A.pinfo3[k];
 #pragma unroll
 		for (int g = 0; g < NG; ++g)
 			mg[g] = load_mg(A.cgroups + g, false);
 	} else {
-		for (uint32_t k = threadIdx.x; k < A.num_ment; k += LB)
+		for (uint32_t k = threadIdx.x; k < A.num_ment; k += LBK)
 			ments[k] = A.ments[k];
-		for (uint32_t k = threadIdx.x; k < A.num_pmr; k += LB)
+		for (uint32_t k = threadIdx.x; k < A.num_pmr; k += LBK)
 			pinfo4[k] = A.pinfo4[k];
 		if constexpr (NG > 0) {
 #pragma unroll
@@ -312,7 +372,7 @@ odpg_cls64_kernel(const L64Args A)
 
 	if constexpr (CM == 2) {
 		C = *A.cnt;
-		for (uint32_t k = threadIdx.x; k < A.num_cos + BIN_EXTRA; k += LB)
+		for (uint32_t k = threadIdx.x; k < A.num_cos + BIN_EXTRA; k += LBK)
 			dlv[k] = 0u;
 		if (threadIdx.x == 0u)
 			waves_done = 0u;
@@ -637,8 +697,12 @@ odpg_cls64_kernel(const L64Args A)
 		const uint32_t nk = left < 64u ? left : 64u;
 		uint64_t defer = 0ull;
 
-		if (!first)
-			load_tile(fn, t0);
+		if (!first) {
+			if (L64_COAL)
+				load_raw(fn, t0);
+			else
+				load_tile(fn, t0);
+		}
 		first = false;
 #if L64_PP
 		load_tile(fb, nk > 1u ? t0 + nwaves : NO_TILE);
@@ -651,6 +715,15 @@ odpg_cls64_kernel(const L64Args A)
 			if (tile(fb, k + 1u < nk ? t + nwaves : NO_TILE))
 				defer |= 2ull << k;
 			load_tile(fb, k + 3u < nk ? t + 3u * nwaves : NO_TILE);
+		}
+#elif L64_COAL
+		for (uint32_t k = 0; k < nk; ++k) {
+			const uint32_t t = t0 + k * nwaves;
+
+			stage(fn, fb);
+			load_raw(fn, k + 1u < nk ? t + nwaves : NO_TILE);
+			if (tile(fb, t))
+				defer |= 1ull << k;
 		}
 #else
 		for (uint32_t k = 0; k < nk; ++k) {
@@ -774,7 +847,7 @@ odpg_cls64_kernel(const L64Args A)
 
 		if (lane == 0u)
 			prev = atomicAdd(&waves_done, 1u);
-		if ((uint32_t)__builtin_amdgcn_readfirstlane((int)prev) != LB / 64u - 1u)
+		if ((uint32_t)__builtin_amdgcn_readfirstlane((int)prev) != LBK / 64u - 1u)
 			return;
 		__threadfence_block();
 		unsigned long long *r = (unsigned long long *)(C.rows + (size_t)blockIdx.x * C.words);
@@ -825,7 +898,7 @@ size_t odpg_cls64_lds(const odpg_launch_args &a)
 {
 	const bool hw = (a.tbl_flags & TBL_LEAN64HW) && !(a.tbl_flags & TBL_LEAN64);
 
-	return (size_t)LB * 17u * 4u +
+	return (size_t)LBH(hw) * 17u * 4u +
 	       (hw ? (size_t)a.num_cent * 8u + (size_t)a.num_pmr * 8u
 		   : (size_t)a.num_ment * 16u + (size_t)a.num_pmr * 16u) +
 	       (a.cnt.row ? (((size_t)a.num_cos + BIN_EXTRA + 3u) & ~(size_t)3u) * 4u : 0u);
@@ -872,7 +945,8 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	lds += L64_LDS_PAD;
 #endif
 	const uint32_t ntiles = (a->num + 63u) / 64u;
-	const uint32_t want = (ntiles + LB / 64u - 1u) / (LB / 64u);
+	const uint32_t lb = LBH(hw);
+	const uint32_t want = (ntiles + lb / 64u - 1u) / (lb / 64u);
 	const uint32_t rows = a->cnt.row ? a->cnt.rows : 0xffffffffu;
 	const int cm = a->cnt.row ? 2 : a->stats ? 1 : 0;
 	const bool ck = !hw && (a->tbl_flags & TBL_MG_CUCKOO);
@@ -880,7 +954,7 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	/* resident grid of the instantiation launched, at most one workgroup
 	 * per counter row */
 	auto go = [&](const void *k, auto launch) {
-		uint32_t grid = odpg_resident_grid(k, LB, lds);
+		uint32_t grid = odpg_resident_grid(k, lb, lds);
 
 		grid = grid < want ? grid : want;
 		grid = grid < rows ? grid : rows;
@@ -892,7 +966,7 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	};
 #define L64_LAUNCH_CM(ng, h, c, k)                                                           \
 	go((const void *)odpg_cls64_kernel<ng, h, c, k>, [&](uint32_t grid) {                 \
-		hipLaunchKernelGGL((odpg_cls64_kernel<ng, h, c, k>), dim3(grid), dim3(LB), lds, s, A); \
+		hipLaunchKernelGGL((odpg_cls64_kernel<ng, h, c, k>), dim3(grid), dim3(lb), lds, s, A); \
 	})
 #define L64_LAUNCH_K(ng, h, k)                                                                 \
 	(cm == 2 ? L64_LAUNCH_CM(ng, h, 2, k) : cm == 1 ? L64_LAUNCH_CM(ng, h, 1, k) : L64_LAUNCH_CM(ng, h, 0, k))

@@ -384,6 +384,207 @@ __global__ __launch_bounds__(FBLOCK) void odpg_l3fwd_kernel(
 		out_port[i] = drop ? -1 : dif;
 }
 
+/* ---- persistent kernel for 64-byte frames ---------------------------------
+ * The same per-packet work as odpg_l3fwd_kernel<64, false>, for stride 64:
+ * one wave per 64-packet tile, waves persistent over tiles. A tile's 4 KiB
+ * arrive as coalesced 16-byte loads (lane l: chunks l, l + 64, l + 128,
+ * l + 192), issued one tile ahead, and are transposed to one frame per lane
+ * through the wave's own LDS rows, chunk (frame r, part p) at slot
+ * (p + r + r / 4) % 4 of row r: conflict-free for the ds_write_b128 and
+ * ds_read_b128 lane groups (as classify64.hip's L64_COAL staging). Hash mode
+ * issues the next tile's loads before this tile's route search (LDS only);
+ * LPM mode after its trie walk, whose dependent global loads would otherwise
+ * wait for them (vector-memory loads retire in issue order). */
+#ifndef FWD_PBLOCK
+#define FWD_PBLOCK 256
+#endif
+#ifndef FWD_WAVES           /* waves per SIMD the launch bounds ask for */
+#define FWD_WAVES 8
+#endif
+
+template <bool LPM>
+__global__ __launch_bounds__(FWD_PBLOCK, FWD_WAVES * 256 / FWD_PBLOCK) void odpg_l3fwd64_kernel(
+	uint4 *__restrict__ frames, uint32_t num, int32_t sif, uint32_t layer,
+	const uint4 *__restrict__ rmac, uint32_t nroutes, const uint32_t *__restrict__ l1,
+	const uint32_t *__restrict__ pool, const uint4 *__restrict__ pmac,
+	int32_t *__restrict__ out_port)
+{
+	constexpr uint32_t RW = 17;                 /* odd dword row stride */
+	__shared__ __attribute__((aligned(16))) uint32_t rows[FWD_PBLOCK * RW];
+	__shared__ uint4 s_rmac[ODPG_FWD_MAX_ROUTES];
+	__shared__ uint4 s_pmac[ODPG_FWD_MAX_PORTS];
+	__shared__ uint32_t s_ivb[FWD_MAX_IV], s_iva[FWD_MAX_IV];
+
+	const uint32_t tid = threadIdx.x;
+	const uint32_t lane = __lane_id();
+	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (FWD_PBLOCK / 64) + (tid >> 6));
+	const uint32_t nwaves = gridDim.x * (FWD_PBLOCK / 64);
+	const uint32_t ntiles = (num + 63u) >> 6;
+	uint32_t *row = rows + tid * RW;
+	uint32_t *stg = rows + (tid & ~63u) * RW;
+	const uint32_t sw_fr = lane >> 2;
+	const uint32_t sw_w = 16u * sw_fr + 4u * (((lane & 3u) + sw_fr + (sw_fr >> 2)) & 3u);
+	const uint32_t sw_c = lane + (lane >> 2);
+
+	auto load_raw = [&](uint32_t (&dst)[16], uint32_t t) {
+		if (t >= ntiles)
+			return;
+		const size_t lim = (size_t)num * 4u - 1u;
+		const size_t c0 = (size_t)t * 256u + lane;
+
+#pragma unroll
+		for (int q = 0; q < 4; ++q) {
+			const size_t c = c0 + 64u * q;
+			const uint4 x = frames[c < lim ? c : lim];
+
+			dst[4 * q + 0] = x.x;
+			dst[4 * q + 1] = x.y;
+			dst[4 * q + 2] = x.z;
+			dst[4 * q + 3] = x.w;
+		}
+	};
+	auto stage = [&](const uint32_t (&raw)[16], uint32_t (&f)[16]) {
+#pragma unroll
+		for (int q = 0; q < 4; ++q)
+			*(uint4 *)(stg + sw_w + 256u * q) =
+				make_uint4(raw[4 * q], raw[4 * q + 1], raw[4 * q + 2], raw[4 * q + 3]);
+#pragma unroll
+		for (int j = 0; j < 4; ++j) {
+			const uint4 x = *(const uint4 *)(stg + 16u * lane + 4u * ((j + sw_c) & 3u));
+
+			f[4 * j + 0] = x.x;
+			f[4 * j + 1] = x.y;
+			f[4 * j + 2] = x.z;
+			f[4 * j + 3] = x.w;
+		}
+	};
+	uint32_t fn[16] = {};
+
+	load_raw(fn, gw);
+	for (uint32_t k = tid; k < nroutes && k < ODPG_FWD_MAX_ROUTES; k += FWD_PBLOCK)
+		s_rmac[k] = rmac[k];
+	for (uint32_t k = tid; k < ODPG_FWD_MAX_PORTS; k += FWD_PBLOCK)
+		s_pmac[k] = pmac[k];
+	const uint32_t niv = LPM ? 0u : l1[0];     /* uniform */
+
+	for (uint32_t k = tid; k < niv; k += FWD_PBLOCK) {
+		s_ivb[k] = l1[1u + 2u * k];
+		s_iva[k] = l1[2u + 2u * k];
+	}
+	__syncthreads();
+
+	/* the route of dst: out port and the frame's new bytes 0..11 (w1, w2:
+	 * the frame's words 1, 2, for the no-route MAC swap) */
+	auto route = [&](uint32_t dst, uint32_t w1, uint32_t w2, uint4 &mac) -> int32_t {
+		int32_t dif = sif;
+
+		if constexpr (LPM) {
+			uint32_t n = l1[dst >> 16], rest = dst & 0xffffu, bits = 16u;
+
+			while (!(n & FN_END)) {          /* at most four sub levels */
+				bits -= 4u;
+				n = pool[(n & FN_VAL) + (rest >> bits)];
+				rest &= (1u << bits) - 1u;
+			}
+			if (n & FN_VALID)
+				dif = (int32_t)(n & FN_VAL);
+			mac = s_pmac[(uint32_t)dif & (ODPG_FWD_MAX_PORTS - 1u)];
+		} else {
+			uint32_t pos = 0u;
+
+#pragma unroll
+			for (uint32_t step = 64u; step; step >>= 1) {
+				const uint32_t q = pos + step;
+
+				if (q < niv && s_ivb[q] <= dst)
+					pos = q;
+			}
+			const int32_t k = niv ? (int32_t)s_iva[pos] : -1;
+
+			if (k >= 0) {
+				mac = s_rmac[k];
+				dif = (int32_t)mac.w;
+			} else {
+				mac.x = __builtin_amdgcn_alignbyte(w2, w1, 2);
+				mac.y = (w2 >> 16) | (w1 & 0xffff0000u);
+				mac.z = w2;
+			}
+		}
+		return dif;
+	};
+
+	for (uint32_t t = gw; t < ntiles; t += nwaves) {
+		uint32_t f[16];
+
+		stage(fn, f);
+		if (!LPM)
+			load_raw(fn, t + nwaves);
+		const uint32_t i = t * 64u + lane;
+		const bool live = i < num;
+		uint4 *fr = frames + (size_t)(live ? i : 0u) * 4u;
+		const bool fast = __ballot(live && !(layer >= LAYER_L4 && plain_v4(f))) == 0ull;
+
+		if (fast) {
+			/* plain frames, no RX checksum options: parse_fast cannot flag
+			 * an error, every frame is IPv4 (drop_err_pkts keeps it) */
+			uint4 mac;
+			const int32_t dif = route(__builtin_bswap32(fw<30>(f)), f[1], f[2], mac);
+
+			if (LPM)
+				load_raw(fn, t + nwaves);
+			if (live) {
+				fr[0] = make_uint4(mac.x, mac.y, mac.z, f[3]);
+				fr[1] = make_uint4(f[4], ttl_csum_word5(f[5]),
+						   (f[6] & 0xffff0000u) | csum_update(f[6] & 0xffffu), f[7]);
+				out_port[i] = dif;
+			}
+			continue;
+		}
+		/* any other wave: the generic parse over the frame in its LDS row */
+#pragma unroll
+		for (int q = 0; q < 16; ++q)
+			row[q] = f[q];
+		Prs p;
+
+		p.inf = 0ull;
+		p.fl = 0u;
+		p.l2 = p.l3 = p.l4 = 0xffffu;
+		int ret = 0;
+		Pkt<64, false> v;
+
+		v.row = row;
+		v.g = (const uint8_t *)fr;
+		v.len = live ? 64u : 0u;
+		if (live)
+			ret = parse_common(p, v, layer, 0ull);
+		const bool drop = !live || ret < 0 || (layer == LAYER_ALL && (p.fl & FL_ERROR_MASK)) ||
+				  !(p.inf & IF(IFL_IPV4));
+		const uint32_t l3 = p.l3;
+		const uint32_t dst = drop ? 0u : __builtin_bswap32(v.rd32(l3 + 16u));
+		uint4 mac;
+		const int32_t dif = route(dst, row[1], row[2], mac);
+
+		if (LPM)
+			load_raw(fn, t + nwaves);
+		if (!drop) {
+			uint8_t *fb = (uint8_t *)fr;
+			uint32_t *w = (uint32_t *)fr;
+			const uint32_t ttl = v.u8(l3 + 8u);
+			const uint32_t cs = v.rd32(l3 + 10u) & 0xffffu;
+
+			w[0] = mac.x;
+			w[1] = mac.y;
+			w[2] = mac.z;
+			fb[l3 + 8u] = (uint8_t)(ttl - 1u);
+			*(uint16_t *)(fb + l3 + 10u) = (uint16_t)csum_update(cs);
+		}
+		if (live)
+			out_port[i] = drop ? -1 : dif;
+	}
+}
+
+extern "C" uint32_t odpg_resident_grid(const void *kernel, uint32_t block, size_t lds);
+
 /* ---- host API ------------------------------------------------------------ */
 extern "C" int odpg_fwd_create(odpg_ctx_t *ctx, const odpg_route_t *routes, uint32_t num_routes,
 			       const odpg_fwd_param_t *param, odpg_fwd_t **out)
@@ -574,6 +775,27 @@ extern "C" int odpg_l3fwd(odpg_ctx_t *ctx, const odpg_fwd_t *f, const odpg_fwd_b
 	const uint32_t grid = (b->num + FBLOCK - 1) / FBLOCK;
 	const uint32_t layer = b->error_check ? LAYER_ALL : LAYER_L4;
 
+#ifndef FWD_NONPERSIST      /* experiment builds only: the one-pass kernel at stride 64 */
+	if (b->stride == 64u) {
+		const uint32_t ntiles = (b->num + 63u) / 64u;
+		const uint32_t want = (ntiles + FWD_PBLOCK / 64u - 1u) / (FWD_PBLOCK / 64u);
+		auto go = [&](const void *k) {
+			const uint32_t g = odpg_resident_grid(k, FWD_PBLOCK, 0);
+
+			return g < want ? g : want;
+		};
+		if (f->mode == ODPG_FWD_LPM)
+			hipLaunchKernelGGL((odpg_l3fwd64_kernel<true>),
+					   dim3(go((const void *)odpg_l3fwd64_kernel<true>)), dim3(FWD_PBLOCK), 0,
+					   s, (uint4 *)b->frames, b->num, b->src_port, layer, f->d_rmac,
+					   f->nroutes, f->d_l1, f->d_pool, f->d_pmac, out_port);
+		else
+			hipLaunchKernelGGL((odpg_l3fwd64_kernel<false>),
+					   dim3(go((const void *)odpg_l3fwd64_kernel<false>)), dim3(FWD_PBLOCK), 0,
+					   s, (uint4 *)b->frames, b->num, b->src_port, layer, f->d_rmac,
+					   f->nroutes, f->d_l1, f->d_pool, f->d_pmac, out_port);
+	} else
+#endif
 	if (b->stride == 64u)
 		hipLaunchKernelGGL((odpg_l3fwd_kernel<64, false>), dim3(grid), dim3(FBLOCK), 0, s,
 				   b->frames, b->stride, b->num, b->src_port, layer, f->mode,

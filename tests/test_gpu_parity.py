@@ -250,6 +250,32 @@ def test_hash_queues(gpu_ctx, fresh_cls):
         assert q.max() < 7 and len(np.unique(q)) > 1
 
 
+def test_hash_queues_every_proto_mix(gpu_ctx, fresh_cls):
+    """Every combination of the six odp_cls_hash_proto_t bits (v4 / v6, with
+    and without UDP / TCP ports) on the mutation corpus: the queue the kernel
+    picks equals the oracle's literal packet_rss_hash + thash_softrss
+    (odp_classification.c:1751-1817, thash.h:81-99)."""
+    frames = rulesets.mutate_corpus(1500, seed=0x7E)
+    buf, desc = pack(frames)
+    bits = (fresh_cls.HASH_IPV4_UDP, fresh_cls.HASH_IPV4_TCP, fresh_cls.HASH_IPV4,
+            fresh_cls.HASH_IPV6_UDP, fresh_cls.HASH_IPV6_TCP, fresh_cls.HASH_IPV6)
+    for m in range(1, 64):
+        hp = 0
+        for k, b in enumerate(bits):
+            if m >> k & 1:
+                hp |= b
+        fresh_cls.reset()
+        p = fresh_cls.loop_pktio()
+        d = fresh_cls.cos_create("d", num_queue=32, hash_proto=hp)
+        assert d
+        fresh_cls.default_cos_set(p, d)
+        assert fresh_cls.pktio_start(p) == 0
+        rules = fresh_cls.pktio_rules(p)
+        g = gpu_ctx.classify(gpu_ctx.table(rules), buf, len(frames), desc=desc)
+        o = oracle.classify(rules, buf, len(frames), desc=desc)
+        assert np.array_equal(g["out"], o["out"]), f"hash proto mix {m:#x}"
+
+
 def test_pktio_recv_batch_counters(gpu_ctx, fresh_cls):
     """odpg_pktio_recv_batch updates odp_cls_cos_stats / odp_pktio_stats like
     loopback_recv (loop.c:304-374) and match_pmr_cos (:1621-1622)."""
