@@ -58,17 +58,23 @@
 #define L64_BLOCK 256
 #endif
 #ifndef L64_BLOCK_HW      /* threads per workgroup of the CoS-keyed cuckoo kernels */
-#define L64_BLOCK_HW L64_BLOCK
+#define L64_BLOCK_HW 1024
 #endif
 #define LB L64_BLOCK
 /* a kernel's workgroup size: the cuckoo tables are one LDS copy per
  * workgroup, so larger workgroups share it among more waves */
-#define LBH(hw) ((hw) ? L64_BLOCK_HW : L64_BLOCK)
+#ifndef L64_BLOCK_CNT     /* threads per workgroup of the sharded-counter kernels */
+#define L64_BLOCK_CNT L64_BLOCK
+#endif
+#define LBH(hw, cm) ((hw) ? L64_BLOCK_HW : (cm) == 2 ? L64_BLOCK_CNT : L64_BLOCK)
 #ifndef L64_PP           /* two frame buffers used in turn (else one, rotated) */
 #define L64_PP 0
 #endif
 #ifndef L64_COAL         /* coalesced tile loads + swizzled LDS transpose */
 #define L64_COAL 1
+#endif
+#ifndef L64_NT           /* L64_COAL: the tile loads nontemporal */
+#define L64_NT 1
 #endif
 
 struct L64Args {
@@ -251,11 +257,11 @@ __device__ __forceinline__ MGd load_mg(const dmgroup_t *g, bool single = true)
  * group is a cuckoo group over a frame word (TBL_MG_CUCKOO): no per-group
  * kind tests in the tile loop. */
 template <int NG, bool HW, int CM, bool CK>
-__global__ __launch_bounds__(LBH(HW), (CM == 2 ? L64_WAVES_CNT : HW ? L64_WAVES_HW : L64_WAVES) * 256 / LBH(HW)) void
+__global__ __launch_bounds__(LBH(HW, CM), (CM == 2 ? L64_WAVES_CNT : HW ? L64_WAVES_HW : L64_WAVES) * 256 / LBH(HW, CM)) void
 odpg_cls64_kernel(const L64Args A)
 {
 	static_assert(!HW || NG > 0, "walk groups are hoisted");
-	constexpr uint32_t LBK = LBH(HW);
+	constexpr uint32_t LBK = LBH(HW, CM);
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 	constexpr uint32_t RW = 17;                     /* odd dword row stride */
 	uint32_t *row = smem + threadIdx.x * RW;        /* generic-parse LDS row */
@@ -300,7 +306,8 @@ odpg_cls64_kernel(const L64Args A)
 #pragma unroll
 		for (int q = 0; q < 4; ++q) {
 			const size_t c = c0 + 64u * q;
-			const uint4 x = ld_stream(A.frames + (c < lim ? c : lim));
+			const uint4 x = L64_NT ? ld_nt16(A.frames + (c < lim ? c : lim))
+					       : ld_stream(A.frames + (c < lim ? c : lim));
 
 			dst[4 * q + 0] = x.x;
 			dst[4 * q + 1] = x.y;
@@ -395,6 +402,13 @@ odpg_cls64_kernel(const L64Args A)
 
 			lo |= h ? d.m2 : 0u;
 			hi |= h ? d.off : 0u;
+		} else if (d.m1 == d.m2) {
+			/* collision-free group (cls_compile.cpp build_mgroup): one read */
+			const uint4 e1 = ments[d.off + ((kvm * d.m1) >> d.sh)];
+			const bool h1 = rq & (e1.x == kvm);
+
+			lo |= h1 ? e1.y : 0u;
+			hi |= h1 ? e1.z : 0u;
 		} else {
 			const uint4 e1 = ments[d.off + ((kvm * d.m1) >> d.sh)];
 			const uint4 e2 = ments[d.off + ((kvm * d.m2) >> d.sh)];
@@ -898,7 +912,7 @@ size_t odpg_cls64_lds(const odpg_launch_args &a)
 {
 	const bool hw = (a.tbl_flags & TBL_LEAN64HW) && !(a.tbl_flags & TBL_LEAN64);
 
-	return (size_t)LBH(hw) * 17u * 4u +
+	return (size_t)LBH(hw, a.cnt.row ? 2 : 0) * 17u * 4u +
 	       (hw ? (size_t)a.num_cent * 8u + (size_t)a.num_pmr * 8u
 		   : (size_t)a.num_ment * 16u + (size_t)a.num_pmr * 16u) +
 	       (a.cnt.row ? (((size_t)a.num_cos + BIN_EXTRA + 3u) & ~(size_t)3u) * 4u : 0u);
@@ -945,7 +959,7 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	lds += L64_LDS_PAD;
 #endif
 	const uint32_t ntiles = (a->num + 63u) / 64u;
-	const uint32_t lb = LBH(hw);
+	const uint32_t lb = LBH(hw, a->cnt.row ? 2 : 0);
 	const uint32_t want = (ntiles + lb / 64u - 1u) / (lb / 64u);
 	const uint32_t rows = a->cnt.row ? a->cnt.rows : 0xffffffffu;
 	const int cm = a->cnt.row ? 2 : a->stats ? 1 : 0;

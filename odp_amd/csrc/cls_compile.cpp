@@ -342,6 +342,55 @@ static void build_mgroup(const std::map<uint32_t, uint64_t> &vals, dmgroup_t &g,
 		seed ^= seed << 17;
 		return (uint32_t)(seed >> 32) | 1u;
 	};
+	/* A collision-free single-probe hash, when one exists within the cuckoo
+	 * table's size: m1 == m2, so a lookup reads one entry (the lean kernel
+	 * tests m1 == m2 wave-uniformly; the other kernels read the same entry
+	 * twice, harmlessly). Power-of-two multipliers first: they extract a bit
+	 * field of the key, which separates structured values such as a port
+	 * range or the prefix bits of a subnet list; then random multipliers. */
+#ifndef ODPG_NO_PERFECT      /* experiment builds only: cuckoo groups */
+	{
+		uint32_t plg = 1;
+
+		while ((1u << plg) < n)
+			plg++;
+		for (; plg <= lg; plg++) {
+			const uint32_t sz = 1u << plg, sh = 32u - plg;
+
+			for (int attempt = 0; attempt < 32 + 64; attempt++) {
+				const uint32_t m = attempt < 32 ? 1u << attempt : next_mul();
+				std::vector<int> slot(sz, -1);
+				bool ok = true;
+				int k = 0;
+
+				for (auto it = vals.begin(); it != vals.end() && ok; ++it, ++k) {
+					const uint32_t pos = (it->first * m) >> sh;
+
+					if (slot[pos] >= 0)
+						ok = false;
+					else
+						slot[pos] = k;
+				}
+				if (!ok)
+					continue;
+				g.shift = sh;
+				g.m1 = m;
+				g.m2 = m;
+				g.off = (uint32_t)ents.size();
+				g.count = (uint32_t)n;
+				ents.resize(ents.size() + sz, dment_t{0u, 0u, 0u, 0u});
+				for (auto &v : vals) {
+					dment_t &e = ents[g.off + ((v.first * m) >> sh)];
+
+					e.value = v.first;
+					e.lo = (uint32_t)v.second;
+					e.hi = (uint32_t)(v.second >> 32);
+				}
+				return;
+			}
+		}
+	}
+#endif
 	for (;; lg++) {
 		const uint32_t sz = 1u << lg, sh = 32u - lg;
 

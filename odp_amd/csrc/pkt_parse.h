@@ -29,6 +29,17 @@ __device__ __forceinline__ uint4 ld_stream(const uint4 *p)
 	return *p;
 }
 
+/* nontemporal 16-byte load: for coalesced streaming only (a lane-per-frame
+ * pattern with this hint runs at 2/3 of the plain load's rate,
+ * profiles/r01/diag_stream_floor.jsonl) */
+__device__ __forceinline__ uint4 ld_nt16(const uint4 *p)
+{
+	typedef unsigned int nt_u32x4 __attribute__((ext_vector_type(4)));
+	const nt_u32x4 v = __builtin_nontemporal_load((const nt_u32x4 *)p);
+
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 #define IF(x)  (1ull << (x))
 #define FB(x)  (1u << (x))
 
