@@ -1577,7 +1577,9 @@ static bool lean64_ok(const odpg_launch_args &a)
 
 	extern size_t odpg_cls64_lds(const odpg_launch_args &a);
 
+	/* (its tile loads index the batch's 16-byte chunks in 32 bits) */
 	return !off && a.mode == 0 && !a.desc && a.stride == 64 && (mg || hw) &&
+	       a.num < (1u << 30) &&
 	       odpg_cls64_lds(a) <= odpg_lds_limit() &&
 	       !(a.tbl_flags & (TBL_GENERIC | TBL_ANY_HASHQ)) &&
 	       !a.mark && !a.meta && !(a.stats && (a.tbl_flags & TBL_ANY_STATS)) &&

@@ -241,6 +241,19 @@ __device__ __forceinline__ MGd load_mg(const dmgroup_t *g, bool single = true)
 	return d;
 }
 
+/* a 16-byte LDS table entry read as one ds_read_b128 even when a field is
+ * unused (the compiler would narrow it to ds_read_b96: 8 lane groups and
+ * 32-bank mapping, twice the LDS cycles, MI355X_MICROARCH.md "LDS") */
+__device__ __forceinline__ uint4 lds_ent(const uint4 *p)
+{
+	const uint4 e = *p;
+
+#ifndef L64_NO_B128     /* experiment builds only: let the read narrow */
+	asm volatile("" ::"v"(e.w));
+#endif
+	return e;
+}
+
 /* sharded-counter histogram bins after the CoS bins (CM 2) */
 #define BIN_ERR    0u
 #define BIN_PDROP  1u
@@ -300,14 +313,15 @@ odpg_cls64_kernel(const L64Args A)
 	auto load_raw = [&](uint32_t (&dst)[16], uint32_t t) {
 		if (t >= ntiles)
 			return;
-		const size_t lim = (size_t)num * 4u - 1u;
-		const size_t c0 = (size_t)t * 256u + lane;
+		/* chunk indices in 32 bits (launches of < 2^30 packets,
+		 * lean64_ok), clamped to the batch's last chunk */
+		const uint32_t lim = num * 4u - 1u;
+		const uint32_t c0 = t * 256u + lane;
 
 #pragma unroll
 		for (int q = 0; q < 4; ++q) {
-			const size_t c = c0 + 64u * q;
-			const uint4 x = L64_NT ? ld_nt16(A.frames + (c < lim ? c : lim))
-					       : ld_stream(A.frames + (c < lim ? c : lim));
+			const uint32_t c = min(c0 + 64u * q, lim);
+			const uint4 x = L64_NT ? ld_nt16(A.frames + c) : ld_stream(A.frames + c);
 
 			dst[4 * q + 0] = x.x;
 			dst[4 * q + 1] = x.y;
@@ -315,6 +329,7 @@ odpg_cls64_kernel(const L64Args A)
 			dst[4 * q + 3] = x.w;
 		}
 	};
+
 	/* raw chunks -> LDS -> this lane's frame (the wave's LDS ops run in
 	 * order: the next stage's writes follow this stage's reads) */
 	auto stage = [&](const uint32_t (&raw)[16], uint32_t (&f)[16]) {
@@ -404,7 +419,7 @@ odpg_cls64_kernel(const L64Args A)
 			hi |= h ? d.off : 0u;
 		} else if (d.m1 == d.m2) {
 			/* collision-free group (cls_compile.cpp build_mgroup): one read */
-			const uint4 e1 = ments[d.off + ((kvm * d.m1) >> d.sh)];
+			const uint4 e1 = lds_ent(ments + d.off + ((kvm * d.m1) >> d.sh));
 			const bool h1 = rq & (e1.x == kvm);
 
 			lo |= h1 ? e1.y : 0u;

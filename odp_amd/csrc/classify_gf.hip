@@ -273,11 +273,12 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 #ifndef GF_WIN_LATE         /* next tile's windows issued after the walk */
 #define GF_WIN_LATE 0
 #endif
-/* GF_EARLY: a tile's checksum tails are summed one tile ahead, right before
- * its windows are issued (every frame's bytes [64, len), whether or not its
- * parse will want them), so a 128-byte line shared by a window and a tail
- * unit is requested twice within a few hundred cycles instead of a tile
- * apart, when the L2 has let it go (1.24x the algorithmic reads) */
+/* GF_EARLY: a tile's checksum tails are summed one tile ahead (every
+ * frame's bytes [64, len), whether or not its parse will want them), right
+ * after its windows are issued (1) or after the current tile's walk (2), so
+ * a 128-byte line shared by a window and a tail unit is requested twice
+ * within a short time instead of a tile apart, when the L2 has let it go
+ * (0: 1.24x the algorithmic reads) */
 #ifndef GF_EARLY
 #define GF_EARLY 1
 #endif
@@ -523,10 +524,10 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 	};
 	uint32_t tn = 0u;
 
-	if (GF_EARLY && !GF_SWEEP && l4ck)
-		tn = early_tails(dn, gw);
 	if (!GF_SWEEP)
 		load_win(fn, xn, dn);
+	if (GF_EARLY && !GF_SWEEP && l4ck)
+		tn = early_tails(dn, gw);
 	dnn = load_desc(gw + nwaves);
 
 	{
@@ -800,13 +801,13 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 		if (!late)
 			tails();
 
-		/* GF_EARLY: the next tile's tails, then its windows (in flight
-		 * during the walk; issued after the tail passes, whose waits would
-		 * otherwise cover them too: vector-memory loads retire in order) */
-		if (GF_EARLY && !GF_SWEEP && l4ck)
-			tn = early_tails(dn, t + nwaves);
+		/* the next tile's windows, in flight during the walk. GF_EARLY 1:
+		 * the next tile's tails right behind them; 2: after the walk */
 		if (!GF_SWEEP && !GF_WIN_LATE)
 			load_win(fn, xn, dn);
+		if (GF_EARLY == 1 && !GF_SWEEP && l4ck)
+			tn = early_tails(dn, t + nwaves);
+		const uint2 dnext = dn;
 		dnn = load_desc(t + 2u * nwaves);
 
 		/* ---- CoS walk (cls_select_cos + match_pmr_cos) ------------------ */
@@ -915,6 +916,9 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 				}
 			}
 		}
+
+		if (GF_EARLY == 2 && !GF_SWEEP && l4ck)
+			tn = early_tails(dnext, t + nwaves);
 
 		if (late) {
 			tails();

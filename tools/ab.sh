@@ -12,5 +12,5 @@ for v in $VARIANTS; do
   ODPG_LIB="$lib" timeout -k 10 300 python bench.py --no-cpu --config $CFG --diag $DIAG \
     --steps $STEPS --warmup 5 ${BENCH_EXTRA:-} > gpurun_out/ab_${CFG}_${DIAG}${TAG:-}_$v.json 2> gpurun_out/ab_${CFG}_${DIAG}${TAG:-}_$v.err \
     || { tail -3 gpurun_out/ab_${CFG}_${DIAG}${TAG:-}_$v.err; exit 3; }
-  python -c "import json;d=json.load(open('gpurun_out/ab_${CFG}_${DIAG}${TAG:-}_$v.json'));c=d.get('with_pktio_counters') or {};print('$CFG $DIAG $v', d['value'], d['roofline']['kernel_ms'], 'counted', c.get('value'), c.get('kernel_ms'))"
+  python -c "import json;d=json.load(open('gpurun_out/ab_${CFG}_${DIAG}${TAG:-}_$v.json'));c=d.get('with_pktio_counters') or {};print('$CFG $DIAG${TAG:-} $v', d['value'], d['roofline']['kernel_ms'], 'counted', c.get('value'), c.get('kernel_ms'))"
 done

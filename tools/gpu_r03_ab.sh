@@ -1,18 +1,14 @@
 #!/bin/bash
-# C3 early tails (tails before the next windows): parity, A/B, HBM counters.
+# C2 / C1 resident-grid sweep of the lean kernel (workgroups per launch).
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
-  tests/test_gf_kernel.py tests/test_gpu_parity.py -m gpu > gpurun_out/pytest_first.log 2>&1
-rc=$?; echo "first tests: $rc"; tail -3 gpurun_out/pytest_first.log; [ $rc -eq 0 ] || exit $rc
-CFG=c3 BENCH_EXTRA="--no-cpu" VARIANTS="base exp_noearly base exp_noearly" bash tools/ab.sh || exit $?
-for v in base; do
-  lib=""; [ $v = base ] || lib=$PWD/odp_amd/lib/$v/libodpg.so
-  for c in FETCH_SIZE WRITE_SIZE; do
-    ODPG_LIB="$lib" timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc3b_$v/pmc_$c -o run \
-      -- python3 bench.py --no-cpu --no-stats --config c3 --steps 20 --warmup 2 > gpurun_out/pmc3b_${v}_$c.log 2>&1
-    rc=$?; echo "pmc $v $c: $rc"; [ $rc -eq 0 ] || exit $rc
+for r in 1 2 3; do
+  for g in 1280 1536 1792 2048; do
+    ODPG_L64_GRID=$g CFG=c2 TAG=_g${g}_$r BENCH_EXTRA="--no-cpu --no-stats" VARIANTS="exp_grid" bash tools/ab.sh || exit $?
   done
+done
+for g in 1536 2048; do
+  ODPG_L64_GRID=$g CFG=c1 TAG=_g$g BENCH_EXTRA="--no-cpu --no-stats" VARIANTS="exp_grid" bash tools/ab.sh || exit $?
 done
