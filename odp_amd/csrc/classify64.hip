@@ -985,6 +985,12 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 	auto go = [&](const void *k, auto launch) {
 		uint32_t grid = odpg_resident_grid(k, lb, lds);
 
+		/* verdict-only mask-group launches with a walk of two or more
+		 * levels leave an eighth of the resident slots empty: C2 13.2-13.6
+		 * vs 13.7-13.9 us at 7 vs 8 workgroups per CU, while the one-level
+		 * C1 runs better at 8 (12.5-12.7 vs 12.8-13.1 us) */
+		if (!hw && cm == 0 && a->l64_depth != 1u)
+			grid -= grid / 8u;
 		grid = grid < want ? grid : want;
 		grid = grid < rows ? grid : rows;
 #ifdef L64_EXP_GRIDENV   /* experiment builds only: ODPG_L64_GRID workgroups */
