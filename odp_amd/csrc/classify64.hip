@@ -66,7 +66,11 @@
 #ifndef L64_BLOCK_CNT     /* threads per workgroup of the sharded-counter kernels */
 #define L64_BLOCK_CNT L64_BLOCK
 #endif
+#ifdef L64_CNT_FIRST     /* experiment builds only: counted HW launches at L64_BLOCK_CNT */
+#define LBH(hw, cm) ((cm) == 2 ? L64_BLOCK_CNT : (hw) ? L64_BLOCK_HW : L64_BLOCK)
+#else
 #define LBH(hw, cm) ((hw) ? L64_BLOCK_HW : (cm) == 2 ? L64_BLOCK_CNT : L64_BLOCK)
+#endif
 #ifndef L64_PP           /* two frame buffers used in turn (else one, rotated) */
 #define L64_PP 0
 #endif

@@ -8,10 +8,11 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/final
 mkdir -p $OUT
+exec 3>&1   # the script's stdout, for status lines (a step's own output may be redirected)
 step() {  # name, then the command; stops the script on any failure
   local n=$1; shift
   "$@"; local rc=$?
-  echo "$n: $rc" | tee -a $OUT/status.txt
+  echo "$n: $rc" >> $OUT/status.txt; echo "$n: $rc" >&3
   [ $rc -eq 0 ] || exit $rc
 }
 if [ -z "${SKIP_TESTS:-}" ]; then
