@@ -178,9 +178,9 @@ __device__ __forceinline__ uint32_t tx_fast64(const TxArgs &A, const uint32_t *t
 		w10 = true;
 		res |= udp ? ODPG_TX_OUT_UDP : ODPG_TX_OUT_TCP;
 	}
-	if (w6)
+	if (g && w6)
 		g[6] = f[6];
-	if (w10)
+	if (g && w10)
 		g[10] = f[10];
 
 	/* get_dest_queue: ports (34..37), then the IPv4 addresses (26..33) */
@@ -218,49 +218,11 @@ __device__ __forceinline__ uint32_t tx_fast64(const TxArgs &A, const uint32_t *t
 	return res | (q & ODPG_TX_OUT_QUEUE_MASK);
 }
 
-__global__ __launch_bounds__(TX_BLOCK) void odpg_tx_kernel(const TxArgs A)
+/* one packet through loopback_fix_checksums + get_dest_queue, general
+ * form (any layout, metadata or the parse; byte-range sums and stores);
+ * row: the lane's LDS row for the parse */
+__device__ void tx_generic(const TxArgs &A, const uint32_t *tab, uint32_t *row, uint32_t i)
 {
-	__shared__ uint32_t tab[256];
-	__shared__ uint32_t rows[TX_BLOCK * TX_RW];
-	const uint32_t tid = threadIdx.x;
-
-	{
-		/* reflected Castagnoli table (arch/default/odp_hash_crc32.c) */
-		uint32_t c = tid;
-
-		for (int k = 0; k < 8; ++k)
-			c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
-		tab[tid] = c;
-	}
-	__syncthreads();
-	const uint32_t i = blockIdx.x * TX_BLOCK + tid;
-	const bool live = i < A.num;
-
-	if (A.stride == 64u && !A.desc && !A.meta) {
-		/* register fast path: a wave whose frames are all plain
-		 * Eth/IPv4 (IHL 5)/UDP|TCP 64-byte frames (the parse gives l3 14,
-		 * l4 34, IPv4 + UDP|TCP) works on the 16 frame registers and
-		 * stores back only the dwords holding the checksum fields */
-		uint32_t f[16];
-		uint4 *src = (uint4 *)(A.frames + (size_t)(live ? i : A.num - 1u) * 64u);
-
-#pragma unroll
-		for (int k = 0; k < 4; ++k) {
-			const uint4 x = src[k];
-
-			f[4 * k + 0] = x.x;
-			f[4 * k + 1] = x.y;
-			f[4 * k + 2] = x.z;
-			f[4 * k + 3] = x.w;
-		}
-		if (__ballot(live && !plain_v4(f)) == 0ull) {
-			if (live)
-				A.out[i] = tx_fast64(A, tab, f, (uint32_t *)src);
-			return;
-		}
-	}
-	if (!live)
-		return;
 	uint8_t *g;
 	uint32_t len;
 
@@ -283,8 +245,6 @@ __global__ __launch_bounds__(TX_BLOCK) void odpg_tx_kernel(const TxArgs A)
 		fl = m.flags;
 	} else {
 		/* _odp_packet_parse_common, all layers, no checksum options */
-		uint32_t *row = rows + tid * TX_RW;
-
 		for (uint32_t w = 0; w < TX_W / 4; ++w)
 			row[w] = tx_word(g, len, w);
 		Pkt<TX_W, true> v;
@@ -441,7 +401,164 @@ __global__ __launch_bounds__(TX_BLOCK) void odpg_tx_kernel(const TxArgs A)
 	A.out[i] = res | (q & ODPG_TX_OUT_QUEUE_MASK);
 }
 
+__global__ __launch_bounds__(TX_BLOCK) void odpg_tx_kernel(const TxArgs A)
+{
+	__shared__ uint32_t tab[256];
+	__shared__ uint32_t rows[TX_BLOCK * TX_RW];
+	const uint32_t tid = threadIdx.x;
+
+	{
+		/* reflected Castagnoli table (arch/default/odp_hash_crc32.c) */
+		uint32_t c = tid;
+
+		for (int k = 0; k < 8; ++k)
+			c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+		tab[tid] = c;
+	}
+	__syncthreads();
+	const uint32_t i = blockIdx.x * TX_BLOCK + tid;
+	const bool live = i < A.num;
+
+	if (A.stride == 64u && !A.desc && !A.meta) {
+		/* register fast path: a wave whose frames are all plain
+		 * Eth/IPv4 (IHL 5)/UDP|TCP 64-byte frames (the parse gives l3 14,
+		 * l4 34, IPv4 + UDP|TCP) works on the 16 frame registers and
+		 * stores back only the dwords holding the checksum fields */
+		uint32_t f[16];
+		uint4 *src = (uint4 *)(A.frames + (size_t)(live ? i : A.num - 1u) * 64u);
+
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			const uint4 x = src[k];
+
+			f[4 * k + 0] = x.x;
+			f[4 * k + 1] = x.y;
+			f[4 * k + 2] = x.z;
+			f[4 * k + 3] = x.w;
+		}
+		if (__ballot(live && !plain_v4(f)) == 0ull) {
+			if (live)
+				A.out[i] = tx_fast64(A, tab, f, (uint32_t *)src);
+			return;
+		}
+	}
+	if (live)
+		tx_generic(A, tab, rows + tid * TX_RW, i);
+}
+
+/* Stride-64 batches without metadata (the bench's and the loop device's
+ * shape): waves persistent over 64-frame tiles; a tile's 4 KiB loaded
+ * coalesced one tile ahead and transposed to a frame per lane through the
+ * wave's LDS rows, and, on waves of plain frames, the frames written back
+ * whole the same way (1 KiB of whole lines per store instruction; a
+ * partial-sector write costs more than a whole one, fwd.hip). Same swizzle
+ * as classify64.hip's L64_COAL staging. Waves with any other frame take
+ * tx_generic per lane. */
+#ifndef TX_PWAVES           /* waves per SIMD: 160 VGPRs, the generic path inlined without spills */
+#define TX_PWAVES 3
+#endif
+__global__ __launch_bounds__(TX_BLOCK, TX_PWAVES * 256 / TX_BLOCK) void odpg_tx64_kernel(const TxArgs A)
+{
+	__shared__ uint32_t tab[256];
+	__shared__ __attribute__((aligned(16))) uint32_t rows[TX_BLOCK * TX_RW];
+	const uint32_t tid = threadIdx.x;
+	const uint32_t lane = __lane_id();
+	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (TX_BLOCK / 64) + (tid >> 6));
+	const uint32_t nwaves = gridDim.x * (TX_BLOCK / 64);
+	const uint32_t num = A.num;
+	const uint32_t ntiles = (num + 63u) >> 6;
+	uint4 *frames = (uint4 *)A.frames;
+	uint32_t *stg = rows + (tid & ~63u) * TX_RW;
+	const uint32_t sw_fr = lane >> 2;
+	const uint32_t sw_w = 16u * sw_fr + 4u * (((lane & 3u) + sw_fr + (sw_fr >> 2)) & 3u);
+	const uint32_t sw_c = lane + (lane >> 2);
+	/* checksum inserts the configuration asks for: plain waves write back */
+	const bool wb = ((A.capa & A.cfg) & (ODPG_PKTOUT_IPV4_CHKSUM | ODPG_PKTOUT_UDP_CHKSUM |
+					     ODPG_PKTOUT_TCP_CHKSUM)) != 0u;
+
+	auto load_raw = [&](uint32_t (&dst)[16], uint32_t t) {
+		if (t >= ntiles)
+			return;
+		const uint32_t lim = num * 4u - 1u;       /* < 2^30 packets (launcher) */
+		const uint32_t c0 = t * 256u + lane;
+
+#pragma unroll
+		for (int q = 0; q < 4; ++q) {
+			const uint4 x = frames[min(c0 + 64u * q, lim)];
+
+			dst[4 * q + 0] = x.x;
+			dst[4 * q + 1] = x.y;
+			dst[4 * q + 2] = x.z;
+			dst[4 * q + 3] = x.w;
+		}
+	};
+	uint32_t fn[16] = {};
+
+	load_raw(fn, gw);
+	{
+		uint32_t c = tid;
+
+		for (int k = 0; k < 8; ++k)
+			c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+		tab[tid] = c;
+	}
+	__syncthreads();
+
+	for (uint32_t t = gw; t < ntiles; t += nwaves) {
+		uint32_t f[16];
+
+#pragma unroll
+		for (int q = 0; q < 4; ++q)
+			*(uint4 *)(stg + sw_w + 256u * q) =
+				make_uint4(fn[4 * q], fn[4 * q + 1], fn[4 * q + 2], fn[4 * q + 3]);
+#pragma unroll
+		for (int j = 0; j < 4; ++j) {
+			const uint4 x = *(const uint4 *)(stg + 16u * lane + 4u * ((j + sw_c) & 3u));
+
+			f[4 * j + 0] = x.x;
+			f[4 * j + 1] = x.y;
+			f[4 * j + 2] = x.z;
+			f[4 * j + 3] = x.w;
+		}
+		const uint32_t i = t * 64u + lane;
+		const bool live = i < num;
+
+		if (__ballot(live && !plain_v4(f)) == 0ull) {
+			/* the next tile's loads only here: none are in flight (no
+			 * registers held) across the generic path below */
+			load_raw(fn, t + nwaves);
+			const uint32_t r = tx_fast64(A, tab, f, nullptr);
+
+			if (live)
+				A.out[i] = r;
+			if (wb) {
+				/* the frame back through its LDS slots (dwords 6 and
+				 * 10 may have changed), then the tile's chunks in
+				 * load order */
+#pragma unroll
+				for (int j = 1; j < 3; ++j)
+					*(uint4 *)(stg + 16u * lane + 4u * ((j + sw_c) & 3u)) =
+						make_uint4(f[4 * j], f[4 * j + 1], f[4 * j + 2], f[4 * j + 3]);
+				const uint32_t cb = t * 256u + lane, nc = num * 4u;
+
+#pragma unroll
+				for (int q = 0; q < 4; ++q)
+					if (cb + 64u * q < nc)
+						frames[cb + 64u * q] = *(const uint4 *)(stg + sw_w + 256u * q);
+			}
+			continue;
+		}
+		/* the generic path reads the frame from global memory; its LDS
+		 * row is this lane's slice of the wave's staging area */
+		if (live)
+			tx_generic(A, tab, rows + tid * TX_RW, i);
+		load_raw(fn, t + nwaves);
+	}
+}
+
 } /* namespace */
+
+extern "C" uint32_t odpg_resident_grid(const void *kernel, uint32_t block, size_t lds);
 
 extern "C" int odpg_tx_prepare(odpg_ctx_t *ctx, const odpg_tx_batch_t *b,
 			       const odpg_tx_cfg_t *cfg, uint32_t *out)
@@ -464,7 +581,19 @@ extern "C" int odpg_tx_prepare(odpg_ctx_t *ctx, const odpg_tx_batch_t *b,
 	A.num_qs = cfg->num_qs;
 	A.index = cfg->index;
 	A.out = out;
+	hipStream_t s = (hipStream_t)odpg_ctx_stream(ctx);
+
+#ifndef TX_ONEPASS      /* experiment builds only: the one-pass kernel at stride 64 */
+	if (b->stride == 64u && !b->desc && !b->meta && b->num < (1u << 30)) {
+		const uint32_t want = ((b->num + 63u) / 64u + TX_BLOCK / 64u - 1u) / (TX_BLOCK / 64u);
+		uint32_t grid = odpg_resident_grid((const void *)odpg_tx64_kernel, TX_BLOCK, 0);
+
+		grid = grid < want ? grid : want;
+		hipLaunchKernelGGL(odpg_tx64_kernel, dim3(grid ? grid : 1u), dim3(TX_BLOCK), 0, s, A);
+		return hipGetLastError() == hipSuccess ? 0 : -EIO;
+	}
+#endif
 	hipLaunchKernelGGL(odpg_tx_kernel, dim3((b->num + TX_BLOCK - 1) / TX_BLOCK), dim3(TX_BLOCK),
-			   0, (hipStream_t)odpg_ctx_stream(ctx), A);
+			   0, s, A);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
