@@ -71,6 +71,12 @@
 #else
 #define LBH(hw, cm) ((hw) ? L64_BLOCK_HW : (cm) == 2 ? L64_BLOCK_CNT : L64_BLOCK)
 #endif
+#ifndef L64_MG_BARRIER   /* experiment builds only: mask-group counted flush by every wave */
+#define L64_MG_BARRIER 0
+#endif
+#ifndef L64_HW_LASTWAVE  /* experiment builds only: HW counted flush by the last wave */
+#define L64_HW_LASTWAVE 0
+#endif
 #ifndef L64_PP           /* two frame buffers used in turn (else one, rotated) */
 #define L64_PP 0
 #endif
@@ -871,26 +877,39 @@ odpg_cls64_kernel(const L64Args A)
 		if (A.num_cos != 12345u)
 			return;
 #endif
-		/* no barrier: each wave counts itself done after its histogram
-		 * adds (LDS operations of a wave complete in order; the fence
-		 * makes that explicit) and the last of the workgroup's waves
-		 * flushes while the others have already exited */
-		__threadfence_block();
-		uint32_t prev = 0u;
+		/* Mask-group tables (<= 64 PMRs, a few dozen bins): no barrier,
+		 * each wave counts itself done after its histogram adds (LDS
+		 * operations of a wave complete in order; the fence makes that
+		 * explicit) and the last of the workgroup's waves flushes while the
+		 * others have already exited. CoS-keyed tables (HW, up to 1024+
+		 * CoS, 1024-thread workgroups): a barrier, then every wave flushes a
+		 * slice of the bins (one wave alone would issue ~17 passes of 64
+		 * atomics at the kernel's tail: C4 counted 22.6 vs 16.4 us). */
+		uint32_t k_first = lane, k_step = 64u;
+		bool lead = lane == 0u;
 
-		if (lane == 0u)
-			prev = atomicAdd(&waves_done, 1u);
-		if ((uint32_t)__builtin_amdgcn_readfirstlane((int)prev) != LBK / 64u - 1u)
-			return;
-		__threadfence_block();
+		if constexpr ((HW || L64_MG_BARRIER) && !L64_HW_LASTWAVE) {
+			__syncthreads();
+			k_first = threadIdx.x;
+			k_step = LBK;
+			lead = threadIdx.x == 0u;
+		} else {
+			__threadfence_block();
+			uint32_t prev = 0u;
+
+			if (lane == 0u)
+				prev = atomicAdd(&waves_done, 1u);
+			if ((uint32_t)__builtin_amdgcn_readfirstlane((int)prev) != LBK / 64u - 1u)
+				return;
+			__threadfence_block();
+		}
 		unsigned long long *r = (unsigned long long *)(C.rows + (size_t)blockIdx.x * C.words);
 		const uint32_t nc = A.num_cos < C.ncos ? A.num_cos : C.ncos;
 		/* without hash queues each CoS owns one column; else its first */
 		auto col = [&](uint32_t c) { return 4u + C.ncos + (C.ident ? c : C.qcol[c]); };
 		uint32_t tot = 0u;
 
-		for (uint32_t k0 = 0; k0 < nc; k0 += 64u) {
-			const uint32_t k = k0 + lane;
+		for (uint32_t k = k_first; k < (nc + 63u) / 64u * 64u; k += k_step) {
 			const uint32_t x = k < nc ? dlv[BIN_EXTRA + k] : 0u;
 
 			if (x)
@@ -899,14 +918,14 @@ odpg_cls64_kernel(const L64Args A)
 		}
 		const uint32_t t = wave_sum_u32(tot);            /* in_packets, in_octets */
 
-		if (lane == 0u) {
+		if (lane == 0u && t) {
+			atomicAdd(r + 0, (unsigned long long)t);
+			atomicAdd(r + 1, (unsigned long long)t * 64ull);
+		}
+		if (lead) {
 			const uint32_t ne = dlv[BIN_ERR], np = dlv[BIN_PDROP];
 			uint32_t nd = dlv[BIN_NOCOS];
 
-			if (t) {
-				atomicAdd(r + 0, (unsigned long long)t);
-				atomicAdd(r + 1, (unsigned long long)t * 64ull);
-			}
 			if (ne && A.err_cos < nc && A.err_act != 1u)
 				atomicAdd(r + col(A.err_cos), (unsigned long long)ne);
 			else if (A.err_cos >= nc)
