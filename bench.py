@@ -55,7 +55,7 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "tx"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2x", "c3", "c4", "c5", "tx"])
     ap.add_argument("--fwd-mode", default="hash", choices=["hash", "lpm"],
                     help="c5 only: l3fwd lookup mode")
     ap.add_argument("--batch", type=int, default=1 << 20)
@@ -162,6 +162,14 @@ def main():
         nrules = 1024
         frames_fn = gen.c2_frames
         workload = "C4: 64B IPv4/UDP x 1024 PMR (32x SIP/21 -> 32x31 UDP_DPORT), raised limits"
+    elif args.config == "c2x":
+        gen.build_c2x_rules(cls, pktio)
+        nrules = 60
+        frames_fn = gen.c2x_frames
+        workload = ("C2x: 64B Eth/VLAN/QinQ IPv4 UDP|TCP + IPv6/UDP + multicast x 60 PMR over "
+                    "the other term kinds (ETHTYPE_0, DMAC, IPPROTO, IP_DSCP, VLAN_ID_0/X, "
+                    "VLAN_PCP, DIP6, CUSTOM_L3/FRAME, TCP_DPORT, UDP_S/DPORT), pktin "
+                    "ipv4+udp+tcp checksum verify (SURVEY 8(d) C2 second rule mix)")
     elif args.config == "c3":
         gen.build_c3_rules(cls, pktio)
         nrules = 256
@@ -307,7 +315,8 @@ def main():
             "metric": METRIC if args.config == "c2" else (
                 METRIC.replace("64B pkts", "IMIX pkts").replace("64 PMR", f"{nrules} PMR")
                 + " + RX checksum verify" if args.config == "c3"
-                else METRIC.replace("64 PMR", f"{nrules} PMR")),
+                else METRIC.replace("64 PMR", f"{nrules} mixed-term PMR")
+                if args.config == "c2x" else METRIC.replace("64 PMR", f"{nrules} PMR")),
             "value": round(value, 1), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",

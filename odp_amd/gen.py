@@ -269,6 +269,137 @@ def build_c4_rules(cls, pktio, n_l1=32, per_l1=31):
     return {"default": default, "l1": l1, "pmrs": pmrs}
 
 
+# ---- C2x: C2's shape over the other term kinds --------------------------------
+# "a second rule-mix variant should cover the other
+# terms (DMAC, ETHTYPE_0/X, VLAN_ID/PCP, IPPROTO, IP_DSCP, SIP6/DIP6,
+# CUSTOM_FRAME/L3) with VLAN/QinQ/IPv6 frames". 64-byte frames (68
+# algorithmic bytes per packet, as C2); QinQ + IPv6 does not fit 64 bytes, so
+# the QinQ frames carry IPv4.
+C2X_VIDS = (10, 20, 30, 40, 50, 60, 70, 80)
+
+
+def c2x_frames(n, seed=C_SEED):
+    """C2x traffic, 64 B frames with valid checksums: 35 % Eth/IPv4/UDP,
+    15 % Eth/IPv4/TCP, 15 % VLAN/IPv4/UDP (VID from 16 values, half of them
+    ruled), 5 % QinQ/IPv4/UDP, 20 % Eth/IPv6/UDP, 5 % IPv4 multicast, 5 %
+    IPv4/UDP with DSCP 10. Ports and addresses as C2."""
+    r = xorshift64(seed ^ 0xC2C2, n)
+    m16 = np.uint64(0xFFFF)
+    kind = (r % np.uint64(20)).astype(np.int64)
+    src = np.uint64(ip4("10.0.0.0")) + ((r >> np.uint64(8)) & m16)
+    dst = np.uint64(ip4("10.1.0.0")) + ((r >> np.uint64(24)) & m16)
+    sport = ((r >> np.uint64(40)) & m16).astype(np.int64)
+    dport = ((r >> np.uint64(56)) & np.uint64(63)).astype(np.int64)
+    vid = np.array(C2X_VIDS + tuple(v + 1 for v in C2X_VIDS))[(r >> np.uint64(20)) & np.uint64(15)]
+    a = np.empty((n, 64), np.uint8)
+
+    def put(sel, f):
+        idx = np.nonzero(sel)[0]
+        if len(idx):
+            a[idx] = f(idx)
+    put(kind < 7, lambda i: ipv4_frames(len(i), 64, src[i], dst[i], PROTO_UDP, sport[i], dport[i]))
+    put((kind >= 7) & (kind < 10),
+        lambda i: ipv4_frames(len(i), 64, src[i], dst[i], PROTO_TCP, sport[i], dport[i]))
+    put((kind >= 10) & (kind < 13),
+        lambda i: ipv4_frames(len(i), 64, src[i], dst[i], PROTO_UDP, sport[i], dport[i],
+                              vlan=vid[i] | (3 << 13)))
+
+    def qinq(i):
+        f = ipv4_frames(len(i), 64, src[i], dst[i], PROTO_UDP, sport[i], dport[i], vlan=vid[i])
+        # outer 0x88A8 tag in front of the 0x8100 one: the IPv4 header moves
+        # 4 bytes down and the frame loses 4 payload bytes (checksums redone)
+        g = np.zeros_like(f)
+        g[:, :12] = f[:, :12]
+        _be16(g, 12, 0x88A8)
+        _be16(g, 14, 100)
+        g[:, 16:] = f[:, 12:60]
+        o, l4 = 22, 42
+        _be16(g, o + 2, 64 - o)
+        g[:, o + 10:o + 12] = 0
+        _be16(g, o + 10, csum(ones_sum(g, o, o + 20)))
+        _be16(g, l4 + 4, 64 - l4)
+        g[:, l4 + 6:l4 + 8] = 0
+        c = csum(ones_sum(g, l4, 64, ones_sum(g, o + 12, o + 20) + PROTO_UDP + (64 - l4)))
+        _be16(g, l4 + 6, np.where(c == 0, 0xFFFF, c))
+        return g
+    put(kind == 13, qinq)
+    put((kind >= 14) & (kind < 18),
+        lambda i: ipv6_frames(len(i), 64, (r[i] >> np.uint64(8)) & m16, (r[i] >> np.uint64(24)) & m16,
+                              PROTO_UDP, sport[i], dport[i]))
+    put(kind == 18, lambda i: ipv4_frames(len(i), 64, src[i], np.uint64(ip4("239.1.0.0")) + (dst[i] & m16),
+                                          PROTO_UDP, sport[i], dport[i],
+                                          dmac=[0x01, 0x00, 0x5E, 0x01, 0x00, 0x01]))
+    put(kind == 19, lambda i: ipv4_frames(len(i), 64, src[i], dst[i], PROTO_UDP, sport[i], dport[i],
+                                          tos=10 << 2))
+    return a.reshape(-1)
+
+
+def build_c2x_rules(cls, pktio, stats=False):
+    """C2x: 62 PMRs over 63 CoS in the reference limits, every level-1 and
+    level-2 rule a different term kind than C2's (SIP_ADDR / UDP_DPORT):
+    default -> {ETHTYPE_0 VLAN, ETHTYPE_0 QinQ, ETHTYPE_0 IPv6 + IPPROTO,
+    DMAC multicast, IP_DSCP + IPPROTO, IPPROTO TCP, IPPROTO UDP} -> VLAN_ID_0,
+    VLAN_ID_X + PCP, DIP6 /120 prefixes, CUSTOM_L3, TCP_DPORT, UDP_SPORT +
+    CUSTOM_FRAME, ... -> leaves."""
+    T = cls.Term
+    q = cls.queue
+    n = [0]
+
+    def cos(name):
+        c = cls.cos_create(name, queue=q(n[0]), stats_enable=stats)
+        n[0] += 1
+        assert c, name
+        return c
+    default = cos("c2x_default")
+    assert cls.default_cos_set(pktio, default) == 0
+    l1 = {k: cos("c2x_" + k) for k in ("vlan", "qinq", "v6", "mcast", "dscp", "tcp", "udp")}
+    leaves = [cos(f"c2x_leaf_{k}") for k in range(55)]
+    pmrs = []
+
+    def pmr(terms, src, dst):
+        h = cls.pmr_create(terms, src, dst)
+        assert h, (terms, src, dst)
+        pmrs.append(h)
+    pmr([T(cls.PMR_ETHTYPE_0, b"\x81\x00", b"\xff\xff")], default, l1["vlan"])
+    pmr([T(cls.PMR_ETHTYPE_0, b"\x88\xa8", b"\xff\xff")], default, l1["qinq"])
+    pmr([T(cls.PMR_ETHTYPE_0, b"\x86\xdd", b"\xff\xff"), T(cls.PMR_IPPROTO, b"\x11", b"\xff")],
+        default, l1["v6"])
+    pmr([T(cls.PMR_DMAC, b"\x01\x00\x5e\x00\x00\x00", b"\xff\xff\xff\x80\x00\x00")],
+        default, l1["mcast"])
+    pmr([T(cls.PMR_IP_DSCP, b"\x0a", b"\x3f"), T(cls.PMR_IPPROTO, b"\x11", b"\xff")],
+        default, l1["dscp"])
+    pmr([T(cls.PMR_IPPROTO, b"\x06", b"\xff")], default, l1["tcp"])
+    pmr([T(cls.PMR_IPPROTO, b"\x11", b"\xff")], default, l1["udp"])
+    k = 0
+
+    def leaf():
+        nonlocal k
+        c = leaves[k % len(leaves)]
+        k += 1
+        return c
+    for v in C2X_VIDS:
+        pmr([T(cls.PMR_VLAN_ID_0, be_bytes(v, 2), b"\x0f\xff")], l1["vlan"], leaf())
+    for j in range(4):
+        pmr([T(cls.PMR_VLAN_ID_X, be_bytes(C2X_VIDS[j], 2), b"\x0f\xff")], l1["qinq"], leaf())
+    pmr([T(cls.PMR_VLAN_PCP_0, b"\x00", b"\x07")], l1["qinq"], leaf())
+    for j in range(8):
+        # 2001:db8:1::/120 + j << 13 .. the generator's dst low 16 bits
+        pmr([T(cls.PMR_DIP6_ADDR,
+               bytes.fromhex("20010db8000100000000000000000000")[:14] + be_bytes(j << 13, 2),
+               b"\xff" * 14 + b"\xe0\x00")], l1["v6"], leaf())
+    for j in range(8):
+        pmr([T(cls.PMR_UDP_DPORT, be_bytes(8 * j, 2), b"\xff\xf8")], l1["mcast"], leaf())
+    for j in range(8):
+        pmr([T(cls.PMR_CUSTOM_L3, be_bytes(j << 5, 1), b"\xe0", offset=13)], l1["dscp"], leaf())
+    for j in range(8):
+        pmr([T(cls.PMR_TCP_DPORT, be_bytes(c2_dport(j, 0) + 8 * j % 64, 2), b"\xff\xff")],
+            l1["tcp"], leaf())
+    for j in range(8):
+        pmr([T(cls.PMR_UDP_SPORT, be_bytes(j << 13, 2), b"\xe0\x00"),
+             T(cls.PMR_CUSTOM_FRAME, b"\x08\x00", b"\xff\xff", offset=12)], l1["udp"], leaf())
+    return {"default": default, "l1": l1, "leaves": leaves, "pmrs": pmrs}
+
+
 # ---- C3: IMIX + 256 PMR DAG + RX checksum verify ----------------------------
 IMIX_SIZES = (64, 570, 1518)       # 7:4:1, mean 353.83 B
 

@@ -146,6 +146,21 @@ def test_c2_stride64_sizes(gpu_ctx, fresh_cls, n):
     assert g["stats"][0] == n                        # every packet delivered
 
 
+@pytest.mark.parametrize("n", [255, 1 << 16])
+def test_c2x_mixed_terms(gpu_ctx, fresh_cls, n):
+    """The C2x bench workload (SURVEY 8(d)'s second C2 rule mix: VLAN / QinQ
+    / IPv6 / multicast frames against ETHTYPE, DMAC, IPPROTO, DSCP, VLAN,
+    DIP6, CUSTOM and port terms), every kernel strategy vs the oracle."""
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    gen.build_c2x_rules(fresh_cls, p, stats=True)
+    assert fresh_cls.pktio_start(p) == 0
+    fr = gen.c2x_frames(n)
+    g, o = both(gpu_ctx, fresh_cls.pktio_rules(p), fr, n, stride=64, opt=ALL_CHKSUM)
+    assert_same(g, o, f"C2x n={n}")
+    assert g["stats"][0] == n
+    assert len(np.unique(o["out"] & 0xFFFF)) > 40
+
+
 def test_c2_stride_variants(gpu_ctx, fresh_cls):
     """Same frames at strides 64 / 128 / 256 / 2048 (different kernel variants)."""
     p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)

@@ -223,6 +223,33 @@ def test_gpu_generic_frames_parity(gpu_ctx, error_check, stride):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [L.FWD_HASH, L.FWD_LPM])
+def test_gpu_stride64_mixed_waves(gpu_ctx, mode):
+    """The persistent stride-64 kernel with tiles of plain frames (register
+    path, whole frames written back through the LDS transpose) next to
+    tiles holding mutated frames (generic path per lane); ragged last tile."""
+    import rulesets
+    routes = gen.c5_routes()
+    n = 64 * 91 + 17
+    fr = gen.c5_frames(n, routes, seed=77).reshape(n, 64).copy()
+    mut = rulesets.mutate_corpus(2000, seed=29, max_len=64)
+    k = 0
+    for t in range(1, (n + 63) // 64, 3):
+        for j in range(t * 64, min(n, t * 64 + 64), 4):
+            m = np.frombuffer(bytes(mut[k % len(mut)])[:64], np.uint8)
+            fr[j, :] = 0
+            fr[j, :len(m)] = m
+            k += 1
+    fr = fr.reshape(-1)
+    for error_check in (False, True):
+        fw = gpu.Forwarder(gpu_ctx, routes, mode=mode)
+        g_out, g_fr = fw.run(fr, 64, n, src_port=2, error_check=error_check)
+        o_out, o_fr = run_oracle(routes, fr, mode=mode, sif=2, error_check=error_check)
+        np.testing.assert_array_equal(g_out, o_out)
+        np.testing.assert_array_equal(g_fr[:fr.nbytes], o_fr)
+
+
+@pytest.mark.gpu
 def test_gpu_example_pcap(gpu_ctx):
     pk = [bytes.fromhex(h) for h in GOLDEN["pcap"]["perf_udp64"]]
     buf = np.zeros((len(pk), 64), np.uint8)

@@ -208,3 +208,34 @@ def test_tx_gpu_stride64(gpu_ctx):
     assert np.array_equal(g_fr[:len(ref)], ref)
     assert np.array_equal(o_fr, ref)
     assert len(np.unique(g_out & 0xFFFF)) == 4
+
+
+@pytest.mark.gpu
+def test_tx_gpu_stride64_mixed_waves(gpu_ctx):
+    """Stride-64 batches run the persistent kernel: tiles of plain frames
+    take the register path and write whole frames back through the LDS
+    transpose, tiles with any other frame the generic path per lane. Every
+    third tile here mixes in mutated frames (VLAN, IPv6, SNAP, truncated,
+    bad headers cut to 64 bytes); the last tile is ragged."""
+    n = 64 * 97 + 33
+    fr = gen.c2_frames(n, seed=21).reshape(n, 64).copy()
+    fr[:, 24:26] = 0
+    mut = rulesets.mutate_corpus(2000, seed=23, max_len=64)
+    k = 0
+    for t in range(0, (n + 63) // 64, 3):
+        for j in range(t * 64, min(n, t * 64 + 64), 5):
+            m = np.frombuffer(bytes(mut[k % len(mut)])[:64], np.uint8)
+            fr[j, :] = 0
+            fr[j, :len(m)] = m
+            k += 1
+    fr = fr.reshape(-1)
+    for cfg, hp, qs in [(CFG_ALL, L.HASH_IPV4_UDP | L.HASH_IPV4, 4),
+                        (L.PKTOUT_TCP_CHKSUM, L.HASH_IPV6 | L.HASH_IPV6_TCP, 7),
+                        (0, 0, 3)]:
+        g_out, g_fr = gpu_ctx.tx_prepare(fr, n, stride=64, pktout_cfg=cfg, hash_proto=hp,
+                                         num_qs=qs, index=5)
+        o_out, o_fr = oracle.tx_prepare(fr, n, stride=64, pktout_cfg=cfg, hash_proto=hp,
+                                        num_qs=qs, index=5)
+        bad = np.nonzero(o_out != g_out)[0]
+        assert len(bad) == 0, (cfg, bad[:5], o_out[bad[:5]], g_out[bad[:5]])
+        assert np.array_equal(o_fr, g_fr[:len(o_fr)]), cfg
