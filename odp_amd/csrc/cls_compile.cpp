@@ -754,13 +754,25 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	 * slot compares (n > 0; n == 0: the generic compare) */
 	std::vector<uint32_t> xcos, xlist, xterm;
 	uint32_t num_xent = 0;
-	auto slotted_terms = [&](const dpmr_t &p, std::vector<uint32_t> &rec) -> bool {
+	/* one AND-chain of a PMR's terms as records: `pick` chooses, for each
+	 * alternative pair (a term with DT_ALT_NEXT and the one after it: the
+	 * IPv4 / IPv6 or AH / ESP forms of one reference term, whose gates
+	 * exclude each other), which of the two is in the chain (bit j for the
+	 * j-th pair) */
+	auto slotted_terms = [&](const dpmr_t &p, std::vector<uint32_t> &rec, uint32_t pick) -> bool {
+		uint32_t pair = 0;
+
 		for (uint32_t k = 0; k < p.nterms; k++) {
 			dterm_t t = terms[p.term_start + k];
 			uint32_t gend = 0, guarded = 0;
 
-			if (t.tflags & DT_ALT_NEXT)
-				return false;
+			if (t.tflags & DT_ALT_NEXT) {
+				if (k + 1 >= p.nterms)
+					return false;
+				if ((pick >> pair++) & 1u)
+					t = terms[p.term_start + k + 1];
+				k++;
+			}
 			if (t.tflags & DT_GUARD) {
 				/* CUSTOM_L3: frame_len > l3 + off + size (the kernel's
 				 * term_cmp guard) checked before the slot read */
@@ -772,12 +784,29 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			}
 			const dslot_t sl = slotify(t);
 
-			if (sl.slot == SLOT_NONE || sl.nw != 1 || gend > 0xffffu)
+			if (sl.slot == SLOT_NONE || sl.nw < 1 || sl.nw > 4 || gend > 0xffffu ||
+			    (guarded && sl.nw != 1))
 				return false;
-			rec.push_back(t.req);
-			rec.push_back(sl.mask[0]);
-			rec.push_back(sl.value[0]);
-			rec.push_back(sl.slot | (gend << 8) | (guarded << 31));
+			/* a term over nw consecutive key slots (SIP6 / DIP6, DMAC) is the
+			 * AND of nw single-word compares: one record per word, words
+			 * whose mask and value are both zero dropped (always equal) */
+			uint32_t nrec = 0;
+
+			for (uint32_t w = 0; w < sl.nw; w++) {
+				if (sl.mask[w] == 0u && sl.value[w] == 0u && !(w == 0u && sl.nw == 1u))
+					continue;
+				rec.push_back(t.req);
+				rec.push_back(sl.mask[w]);
+				rec.push_back(sl.value[w]);
+				rec.push_back((sl.slot + w) | (gend << 8) | (guarded << 31));
+				nrec++;
+			}
+			if (nrec == 0u) {            /* every word always equal: gate only */
+				rec.push_back(t.req);
+				rec.push_back(0u);
+				rec.push_back(0u);
+				rec.push_back(sl.slot | (gend << 8) | (guarded << 31));
+			}
 		}
 		return p.nterms > 0;
 	};
@@ -798,18 +827,38 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 
 			for (uint32_t k = 0; k < cos[c].nrule; k++) {
 				const uint32_t pi = cos[c].rule_start + k;
-				std::vector<uint32_t> rec;
 
 				if (!complex_pmr[pi])
 					continue;
-				uint32_t xw = 0;
+				/* a PMR with alternative pairs is the OR of its chains,
+				 * one xlist entry each (same PMR index, consecutive:
+				 * both kernels take the first entry that matches); up to
+				 * two pairs, else the generic compare */
+				uint32_t npair = 0;
 
-				if (slotted_terms(pmr[pi], rec) && xterm.size() / 4 < (1u << 24)) {
-					xw = (uint32_t)(xterm.size() / 4) | ((uint32_t)pmr[pi].nterms << 24);
-					xterm.insert(xterm.end(), rec.begin(), rec.end());
+				for (uint32_t k = 0; k < pmr[pi].nterms; k++)
+					if (terms[pmr[pi].term_start + k].tflags & DT_ALT_NEXT)
+						npair++;
+				std::vector<std::vector<uint32_t>> chains;
+				bool ok = npair <= 2;
+
+				for (uint32_t pick = 0; ok && pick < (1u << npair); pick++) {
+					std::vector<uint32_t> r;
+
+					ok = slotted_terms(pmr[pi], r, pick) && r.size() / 4 < 256u;
+					chains.push_back(r);
 				}
-				xlist.push_back(pi);
-				xlist.push_back(xw);
+				if (ok && xterm.size() / 4 + 64u < (1u << 24)) {
+					for (const auto &r : chains) {
+						xlist.push_back(pi);
+						xlist.push_back((uint32_t)(xterm.size() / 4) |
+								((uint32_t)(r.size() / 4) << 24));
+						xterm.insert(xterm.end(), r.begin(), r.end());
+					}
+				} else {
+					xlist.push_back(pi);
+					xlist.push_back(0u);
+				}
 			}
 			xcos[2 * c] = st | (((uint32_t)(xlist.size() / 2) - st) << 16);
 			xcos[2 * c + 1] = gm[c];
