@@ -866,10 +866,16 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 
 								/* gate, then the CUSTOM_L3 length guard,
 								 * before the slot is read */
+								/* bit 30: CUSTOM_FRAME, guard and
+								 * word from the frame start (the L2
+								 * slots whenever the parse set l2 = 0) */
+								const bool ab = (r.w >> 30) & 1u;
+								const uint32_t kw = ab && b.l2 != 0u ? v.rd32(4u * sl) : key(sl);
+
 								hit = (b.inf_lo & r.x) == r.x &&
 								      (!(r.w >> 31) ||
-								       b.len > b.l3 + ((r.w >> 8) & 0xffffu)) &&
-								      (key(sl) & r.y) == r.z;
+								       b.len > (ab ? 0u : b.l3) + ((r.w >> 8) & 0xffffu)) &&
+								      (kw & r.y) == r.z;
 							}
 							done = true;
 						} else {
@@ -1603,7 +1609,10 @@ static bool gf_ok(const odpg_launch_args &a)
 			       ODPG_PKTIN_DROP_UDP_ERR | ODPG_PKTIN_DROP_TCP_ERR |
 			       ODPG_PKTIN_DROP_SCTP_ERR;
 
-	return !off && a.mode == 0 && a.desc && (a.tbl_flags & TBL_XMASK) &&
+	/* descriptors, or a fixed stride whose offsets fit the kernel's 32 bits */
+	const bool layout = a.desc || (a.stride && (uint64_t)a.num * a.stride <= 0xffffffffull);
+
+	return !off && a.mode == 0 && layout && (a.tbl_flags & TBL_XMASK) &&
 	       !(a.tbl_flags & TBL_ANY_HASHQ) && a.num_cos < ODPG_COS_NOCLS &&
 	       odpg_clsgf_lds(&a) <= odpg_lds_limit() &&
 	       !a.mark && !a.meta && !a.stats && !(a.cnt.row && a.cnt.cos) &&

@@ -1,7 +1,8 @@
 /* SPDX-License-Identifier: BSD-3-Clause
  *
  * Lean gfx950 classify kernel for descriptor (IMIX) batches: frames of any
- * length at (offset, len) descriptors, a hybrid hash-walk table in its
+ * length at (offset, len) descriptors (or a fixed stride, the descriptor
+ * computed: the C2x launches), a hybrid hash-walk table in its
  * hit-map form (TBL_XMASK, cls_compile.cpp), verdict words only. The C3
  * shape: IMIX 64/570/1518-byte IPv4 / IPv6 UDP / TCP traffic with the RX
  * checksum checks and a 256-PMR DAG. Same per-packet semantics as
@@ -56,6 +57,7 @@
 struct GFArgs {
 	const uint8_t *frames;
 	uint32_t num;
+	uint32_t stride;            /* fixed-stride batch (descs unused), or 0 */
 	uint32_t opt;               /* ODPG_PKTIN_* (all defined bits are < 32) */
 	uint32_t nwg;               /* walk groups */
 	const uint2 *cinfo;         /* {rule_start | nrule << 16, action | ...} */
@@ -485,7 +487,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 		const uint32_t i = t * 64u + lane;
 
 		if (t < ntiles && i < num)
-			return *(const uint2 *)(descs + i);
+			return A.stride ? make_uint2(i * A.stride, A.stride) : *(const uint2 *)(descs + i);
 		return make_uint2(0u, 0u);
 	};
 	/* a frame's first 64 bytes (16-byte chunks holding frame bytes only: the
@@ -886,7 +888,8 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 						key.b = &b;
 						key.fast = false;
 						acc = acc && (b.inf_lo & r.x) == r.x &&
-						      (!(r.w >> 31) || b.len > b.l3 + ((r.w >> 8) & 0xffffu)) &&
+						      (!(r.w >> 31) ||
+						       b.len > ((r.w >> 30) & 1u ? 0u : b.l3) + ((r.w >> 8) & 0xffffu)) &&
 						      (key(r.w & 0xffu) & r.y) == r.z;
 						if (q.y) {              /* the PMR's last term */
 							if (acc) {
@@ -1063,6 +1066,7 @@ extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s)
 
 	A.frames = a->frames;
 	A.num = a->num;
+	A.stride = a->desc ? 0u : a->stride;   /* gf_ok: num * stride < 2^32 */
 	A.opt = (uint32_t)a->opt;
 	A.nwg = a->num_wgroups;
 	A.cinfo = (const uint2 *)a->cinfo;

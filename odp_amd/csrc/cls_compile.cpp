@@ -773,13 +773,21 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 					t = terms[p.term_start + k + 1];
 				k++;
 			}
+			uint32_t absolute = 0;
+
 			if (t.tflags & DT_GUARD) {
 				/* CUSTOM_L3: frame_len > l3 + off + size (the kernel's
-				 * term_cmp guard) checked before the slot read */
-				if (t.kind != DK_CMP || t.base != DB_L3 || t.off < 0)
+				 * term_cmp guard) checked before the slot read;
+				 * CUSTOM_FRAME: frame_len > off + size, the slot an
+				 * absolute frame word (the L2 slots at l2 == 0) */
+				if (t.kind != DK_CMP || (t.base != DB_L3 && t.base != DB_ABS) || t.off < 0)
 					return false;
 				gend = (uint32_t)t.off + t.size;
 				guarded = 1;
+				if (t.base == DB_ABS) {
+					absolute = 1;
+					t.base = DB_L2;
+				}
 				t.tflags &= (uint8_t)~DT_GUARD;
 			}
 			const dslot_t sl = slotify(t);
@@ -798,14 +806,14 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 				rec.push_back(t.req);
 				rec.push_back(sl.mask[w]);
 				rec.push_back(sl.value[w]);
-				rec.push_back((sl.slot + w) | (gend << 8) | (guarded << 31));
+				rec.push_back((sl.slot + w) | (gend << 8) | (absolute << 30) | (guarded << 31));
 				nrec++;
 			}
 			if (nrec == 0u) {            /* every word always equal: gate only */
 				rec.push_back(t.req);
 				rec.push_back(0u);
 				rec.push_back(0u);
-				rec.push_back(sl.slot | (gend << 8) | (guarded << 31));
+				rec.push_back(sl.slot | (gend << 8) | (absolute << 30) | (guarded << 31));
 			}
 		}
 		return p.nterms > 0;

@@ -100,3 +100,47 @@ def test_gf_kernel_sharded_counters(gpu_ctx, fresh_cls, corpus):
     want = expected_counters(o, tbl.num_cos)
     assert_counters(cnt.fold(), {k: v * 2 for k, v in want.items()}, f"gf counters {corpus}")
     cnt.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride", [64, 128, 256])
+def test_gf_kernel_fixed_stride(gpu_ctx, fresh_cls, stride):
+    """Fixed-stride batches take the same kernel (each frame's descriptor
+    computed as (i * stride, stride)): edge-corpus frames cut / padded into
+    stride slots, C3 rules, every checksum option mix; ragged last tile."""
+    frames = rulesets.imix_edge_corpus(64 * 157 + 29, seed=stride)
+    n = len(frames)
+    buf = np.zeros((n, stride), np.uint8)
+    for k, f in enumerate(frames):
+        m = np.frombuffer(bytes(f)[:stride], np.uint8)
+        buf[k, :len(m)] = m
+    buf = buf.reshape(-1)
+    for opt in (ALL_CHKSUM, L.PKTIN_UDP_CHKSUM | L.PKTIN_TCP_CHKSUM, 0):
+        fresh_cls.reset()
+        rules = _c3(fresh_cls, opt)
+        tbl = gpu_ctx.table(rules)
+        g = gpu_ctx.classify(tbl, buf, n, stride=stride, opt=opt, want_mark=False,
+                             want_meta=False, want_stats=False)
+        assert L.lib.odpg_last_kernel() == 2, "fixed stride did not take the lean descriptor kernel"
+        o = oracle.classify(rules, buf, n, stride=stride, opt=opt)
+        assert np.array_equal(g["out"], o["out"]), (stride, opt)
+
+
+@pytest.mark.gpu
+def test_c2x_takes_the_gf_kernel(gpu_ctx, fresh_cls):
+    """The C2x rule mix (multi-word DIP6 and DMAC terms, IPPROTO / DSCP
+    alternative pairs in multi-term rules, CUSTOM_FRAME) compiles to the
+    hit-map form and its 64-byte batches run the lean descriptor kernel."""
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    gen.build_c2x_rules(fresh_cls, p)
+    assert fresh_cls.pktio_start(p) == 0
+    rules = fresh_cls.pktio_rules(p)
+    assert table_flags(rules) & TBL_XMASK
+    n = 64 * 500 + 3
+    fr = gen.c2x_frames(n, seed=5)
+    tbl = gpu_ctx.table(rules)
+    g = gpu_ctx.classify(tbl, fr, n, stride=64, opt=ALL_CHKSUM, want_mark=False,
+                         want_meta=False, want_stats=False)
+    assert L.lib.odpg_last_kernel() == 2
+    o = oracle.classify(rules, fr, n, stride=64, opt=ALL_CHKSUM)
+    assert np.array_equal(g["out"], o["out"])
