@@ -21,7 +21,7 @@ if [ -z "${SKIP_TESTS:-}" ]; then
   tail -2 $OUT/pytest_gpu.log
   step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 fi
-for cfg in ${CFGS:-c2 c1 c3 c4 c5 tx}; do
+for cfg in ${CFGS:-c2 c1 c2x c3 c4 c5 tx}; do
   for c in FETCH_SIZE WRITE_SIZE; do
     step "pmc $cfg $c" timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$cfg/pmc_$c -o run \
       -- python3 bench.py --no-cpu --no-stats --config $cfg --steps 20 --warmup 2 > $OUT/pmc_${cfg}_$c.log 2>&1
