@@ -468,8 +468,8 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 	 * per walk level */
 	uint4 *pdst = (uint4 *)(cinfo + ((A.num_cos + 1u) & ~1u));
 	/* the complex PMRs' terms, per CoS in rule order (cls_compile.cpp
-	 * "xflat"): {gate, mask, value, slot | guard end << 8 | guarded << 31},
-	 * {pmr, last term of the PMR, 0, 0} */
+	 * "xflat"): {gate, mask, value, slot | guard end << 8 | absolute << 30 |
+	 * guarded << 31}, {pmr, last record of its chain, that record's index, 0} */
 	uint4 *xfl = pdst + A.num_pmr;
 	/* GF_SWEEP: the wave's x16 words and tail partials (2 x 64 dwords) */
 	uint32_t *swx = (uint32_t *)(xfl + 2u * A.num_xflat) + (threadIdx.x >> 6) * 128u;
@@ -891,11 +891,14 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 						      (!(r.w >> 31) ||
 						       b.len > ((r.w >> 30) & 1u ? 0u : b.l3) + ((r.w >> 8) & 0xffffu)) &&
 						      (key(r.w & 0xffu) & r.y) == r.z;
-						if (q.y) {              /* the PMR's last term */
+						if (q.y) {              /* the chain's last record */
 							if (acc) {
 								best = q.x;
 								break;
 							}
+							acc = true;
+						} else if (!acc) {      /* failed: on to the next chain */
+							j = q.z;
 							acc = true;
 						}
 					}

@@ -850,12 +850,28 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 				std::vector<std::vector<uint32_t>> chains;
 				bool ok = npair <= 2;
 
+				/* gates that no packet carries together: a chain needing
+				 * both never matches and is left out */
+				const uint32_t excl[][2] = {{RQ(IFL_IPV4), RQ(IFL_IPV6)},
+							    {RQ(IFL_IPSEC_AH), RQ(IFL_IPSEC_ESP)}};
+
 				for (uint32_t pick = 0; ok && pick < (1u << npair); pick++) {
 					std::vector<uint32_t> r;
 
 					ok = slotted_terms(pmr[pi], r, pick) && r.size() / 4 < 256u;
-					chains.push_back(r);
+					uint32_t req = 0;
+
+					for (size_t q = 0; q < r.size(); q += 4)
+						req |= r[q];
+					bool never = false;
+
+					for (const auto &e : excl)
+						never |= (req & e[0]) && (req & e[1]);
+					if (ok && !never)
+						chains.push_back(r);
 				}
+				if (ok && chains.empty())        /* no chain can match */
+					chains.push_back({0u, 0u, 1u, 0u});   /* (x & 0) == 1: never */
 				if (ok && xterm.size() / 4 + 64u < (1u << 24)) {
 					for (const auto &r : chains) {
 						xlist.push_back(pi);
@@ -1131,8 +1147,9 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		xmg.insert(xmg.end(), {mul, 32u - lg, soff, ebase});
 	}
 	/* the complex PMRs' terms flat, per CoS in rule order: {gate, mask,
-	 * value, slot | guard end << 8 | guarded << 31}, {pmr, last term of the
-	 * PMR, 0, 0}; per CoS its first flat term | count << 16 */
+	 * value, slot | guard end << 8 | absolute << 30 | guarded << 31}, {pmr,
+	 * last record of its chain, flat index of that record, 0}; per CoS its
+	 * first flat record | count << 16 */
 	std::vector<uint32_t> xflat, xfc(ncos, 0u), xfstart(num_xent + 1, 0u);
 
 	for (uint32_t k = 0; xm && k < num_xent; k++) {
@@ -1141,7 +1158,9 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		xfstart[k] = (uint32_t)(xflat.size() / 8);
 		for (uint32_t tt = 0; tt < nt; tt++) {
 			xflat.insert(xflat.end(), xterm.begin() + 4 * (ts + tt), xterm.begin() + 4 * (ts + tt + 1));
-			xflat.insert(xflat.end(), {xlist[2 * k], tt + 1 == nt ? 1u : 0u, 0u, 0u});
+			/* {pmr, last record of the chain, that record's flat index} */
+			xflat.insert(xflat.end(), {xlist[2 * k], tt + 1 == nt ? 1u : 0u,
+						   xfstart[k] + nt - 1u, 0u});
 		}
 	}
 	xfstart[num_xent] = (uint32_t)(xflat.size() / 8);
