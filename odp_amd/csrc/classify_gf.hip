@@ -871,11 +871,12 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 					bool acc = true;
 
 					for (; j < jend; ++j) {
+						/* both halves of the record issued together */
 						const uint4 q = xfl[2u * j + 1u];
+						const uint4 r = xfl[2u * j];
 
 						if (q.x >= best)
 							break;
-						const uint4 r = xfl[2u * j];
 						Pkt<64, true> v;
 
 						v.row = row;
