@@ -68,6 +68,7 @@ struct GFArgs {
 	const uint32_t *xm_rest;    /* TBL_XMASK: masks[num_xment][XM_WORDS], values, slot bytes */
 	uint32_t num_xment, xm_slot_bytes, num_xflat;
 	const uint32_t *xfc;        /* per CoS: first flat complex term | count << 16 */
+	uint32_t upf;               /* complex PMRs evaluated up front into the hit map */
 	const odpg_cnt_dev *cnt;    /* CM 2: the sharded counters' layout */
 };
 
@@ -685,6 +686,49 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 					}
 				}
 			}
+			/* up front (A.upf): every complex PMR's chains once per packet,
+			 * in a wave-uniform loop over the flat records (one LDS
+			 * broadcast per record, the key word by uniform slot), a match
+			 * setting the PMR's bit in the hit map; the walk then needs no
+			 * complex-rule evaluation at any level */
+			if (A.upf) {
+				bool acc = on;
+
+				for (uint32_t j = 0; j < A.num_xflat; ++j) {
+					const uint4 r = xfl[2u * j];
+					const uint4 q = xfl[2u * j + 1u];
+					const uint32_t rx = __builtin_amdgcn_readfirstlane(r.x);
+					const uint32_t ry = __builtin_amdgcn_readfirstlane(r.y);
+					const uint32_t rz = __builtin_amdgcn_readfirstlane(r.z);
+					const uint32_t rw = __builtin_amdgcn_readfirstlane(r.w);
+					const uint32_t qx = __builtin_amdgcn_readfirstlane(q.x);
+					const uint32_t qy = __builtin_amdgcn_readfirstlane(q.y);
+					const uint32_t qz = __builtin_amdgcn_readfirstlane(q.z);
+
+					acc = acc && (b.inf_lo & rx) == rx &&
+					      (!(rw >> 31) ||
+					       b.len > ((rw >> 30) & 1u ? 0u : b.l3) + ((rw >> 8) & 0xffffu)) &&
+					      (key(rw & 0xffu) & ry) == rz;
+					if (qy) {
+						const uint32_t bit = acc ? 1u << (qx & 31u) : 0u;
+
+						switch (qx >> 5) {
+						case 0: hm[0] |= bit; break;
+						case 1: hm[1] |= bit; break;
+						case 2: hm[2] |= bit; break;
+						case 3: hm[3] |= bit; break;
+						case 4: hm[4] |= bit; break;
+						case 5: hm[5] |= bit; break;
+						case 6: hm[6] |= bit; break;
+						default: hm[7] |= bit; break;
+						}
+						acc = on;
+					} else if (!__ballot(acc)) {      /* the chain failed everywhere */
+						j = qz;
+						acc = on;
+					}
+				}
+			}
 		};
 #ifdef GF_EXP_NOGEN
 		if (true) {
@@ -842,7 +886,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 
 			if (active) {
 				crs = cinfo[cos].x;
-				cxf = A.xfc[cos];
+				cxf = A.upf ? 0u : A.xfc[cos];
 			}
 			while (__ballot(active)) {
 				if (active) {
@@ -911,7 +955,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 						cos = pd2.x & 0xffffu;
 						mark = pd2.x >> 16;
 						crs = pd2.y;
-						cxf = pd2.z;
+						cxf = A.upf ? 0u : pd2.z;
 						any_match = true;
 						if (++steps >= A.num_cos) {
 							cos = ODPG_COS_LOOP;
@@ -1088,6 +1132,9 @@ extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s)
 					  a->xm_slot_bytes / 4u);
 
 	A.xfc = (const uint32_t *)(xf + 2u * a->num_xflat);
+	/* complex PMRs up front or per level (ODPG_GF_UPF=0/1 overrides) */
+	static const char *upf_env = getenv("ODPG_GF_UPF");
+	A.upf = upf_env ? (uint32_t)atoi(upf_env) : 0u;
 	A.cnt = a->cnt.dev;
 
 	const size_t lds = odpg_clsgf_lds(a);
