@@ -694,16 +694,14 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 			if (A.upf) {
 				bool acc = on;
 
+#pragma unroll 4
 				for (uint32_t j = 0; j < A.num_xflat; ++j) {
-					const uint4 r = xfl[2u * j];
-					const uint4 q = xfl[2u * j + 1u];
-					const uint32_t rx = __builtin_amdgcn_readfirstlane(r.x);
-					const uint32_t ry = __builtin_amdgcn_readfirstlane(r.y);
-					const uint32_t rz = __builtin_amdgcn_readfirstlane(r.z);
-					const uint32_t rw = __builtin_amdgcn_readfirstlane(r.w);
-					const uint32_t qx = __builtin_amdgcn_readfirstlane(q.x);
-					const uint32_t qy = __builtin_amdgcn_readfirstlane(q.y);
-					const uint32_t qz = __builtin_amdgcn_readfirstlane(q.z);
+					/* the records from global memory at a uniform index:
+					 * scalar loads straight into SGPRs */
+					const uint4 r = xf[2u * j];
+					const uint4 q = xf[2u * j + 1u];
+					const uint32_t rx = r.x, ry = r.y, rz = r.z, rw = r.w;
+					const uint32_t qx = q.x, qy = q.y, qz = q.z;
 
 					acc = acc && (b.inf_lo & rx) == rx &&
 					      (!(rw >> 31) ||
