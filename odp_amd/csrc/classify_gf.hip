@@ -50,6 +50,9 @@
 #ifndef GF_WAVES            /* waves per SIMD the launch bounds ask for */
 #define GF_WAVES 5
 #endif
+#ifndef GF_RW               /* LDS row stride per lane, dwords (16-byte multiple) */
+#define GF_RW 20
+#endif
 #ifndef GF_LATE_ODD         /* odd waves sum their tails after the walk */
 #define GF_LATE_ODD 0
 #endif
@@ -375,7 +378,7 @@ __device__ __forceinline__ void gf_sweep(const uint8_t *frames, uint2 d, uint32_
 	if (S.len == 0u) {                               /* empty frame: zero window */
 #pragma unroll
 		for (int k = 0; k < 16; k += 4)
-			*(uint4 *)(rows + 16u * lane + k) = make_uint4(0u, 0u, 0u, 0u);
+			*(uint4 *)(rows + GF_RW * lane + k) = make_uint4(0u, 0u, 0u, 0u);
 	}
 	auto consume = [&](const SwUnit &U, uint32_t base) {
 		const uint32_t uo = U.ou & 63u, uu = (U.ou >> 6) & 0x3ffu, rem = U.ou >> 16;
@@ -393,7 +396,7 @@ __device__ __forceinline__ void gf_sweep(const uint8_t *frames, uint2 d, uint32_
 		uint32_t sum = 0u;
 
 		if (rem && uu == 0u) {
-			uint32_t *r = rows + 16u * uo;
+			uint32_t *r = rows + GF_RW * uo;
 
 #pragma unroll
 			for (int k = 0; k < 16; ++k)
@@ -452,7 +455,10 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 	/* read-only tables as restrict kernel arguments: their wave-uniform
 	 * reads compile to scalar loads */
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-	constexpr uint32_t RW = 16;                     /* generic-parse LDS row (dwords) */
+	/* generic-parse LDS row (dwords): GF_RW 16 packs the rows; 20 (80 B,
+	 * still 16-byte aligned) spreads a wave's reads of one row offset over
+	 * 8 banks instead of 2 */
+	constexpr uint32_t RW = GF_RW;
 	uint32_t *row = smem + threadIdx.x * RW;
 	/* CM 2: the workgroup's histogram after the rows (odpg.h "sharded
 	 * counters"): four bins, then one per CoS */
@@ -1099,7 +1105,7 @@ extern "C" size_t odpg_clsgf_lds(const odpg_launch_args *a)
 
 	const size_t bins = a->cnt.row ? (((size_t)a->num_cos + GF_BIN_EXTRA + 3u) & ~(size_t)3u) * 4u : 0u;
 
-	return (size_t)GF_BLOCK * 16u * 4u + bins + tb + (size_t)((a->num_cos + 1u) & ~1u) * 8u +
+	return (size_t)GF_BLOCK * GF_RW * 4u + bins + tb + (size_t)((a->num_cos + 1u) & ~1u) * 8u +
 	       (size_t)a->num_pmr * 16u + (size_t)a->num_xflat * 32u +
 	       (GF_SWEEP ? (size_t)GF_BLOCK * 2u * 4u : 0u);
 }
