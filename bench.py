@@ -55,6 +55,9 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--runs", type=int, default=5,
+                    help="timed loops of exactly --steps launches each (after one warmup); "
+                         "the line reports the median run (SURVEY.md 8(d))")
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2x", "c3", "c4", "c5", "tx"])
     ap.add_argument("--fwd-mode", default="hash", choices=["hash", "lpm"],
                     help="c5 only: l3fwd lookup mode")
@@ -246,30 +249,12 @@ def main():
             dist.barrier()
 
     def timed(res):
-        """warmup, then exactly args.steps launches between barriers; returns
-        (wall seconds, mean HIP-event ms per launch on the launch stream)"""
-        for i in range(args.warmup):
-            launch(i, res)
-        barrier()
-        t0 = time.perf_counter()
-        lib.odpg_event_record(ctx.h, 0)
-        for i in range(args.steps):
-            launch(i, res)
-        lib.odpg_event_record(ctx.h, 1)
-        ctx.sync()
-        t1 = time.perf_counter()
-        barrier()
-        ev_ms = C.c_float(0)
-        L.check(lib.odpg_event_elapsed_ms(ctx.h, 0, 1, C.byref(ev_ms)), "event")
-        return t1 - t0, ev_ms.value / max(args.steps, 1)
+        return timed_runs(args, ctx, lambda i: launch(i, res), barrier, dist, dev)
 
-    wall, kernel_ms = timed(results)
-    # max wall clock over ranks
-    wall = shard.max_over_ranks(wall, dist, dev)
+    wall, kernel_ms, enq_ms, run_ms = timed(results)
     counted = None
     if not args.no_stats:
-        wall_st, kernel_ms_st = timed(results_st)
-        wall_st = shard.max_over_ranks(wall_st, dist, dev)
+        wall_st, kernel_ms_st, _, run_ms_st = timed(results_st)
         # the read-time fold, then CoS / pktio counters summed over GPUs (RCCL)
         folded = cnt.fold()
         tf0 = time.perf_counter()          # a steady-state fold (code loaded)
@@ -282,7 +267,7 @@ def main():
             # loopback_recv accounting: every packet is either delivered
             # error-free (in_packets) or counted in in_errors (error CoS /
             # parse error)
-            launches = args.warmup + args.steps
+            launches = args.warmup + args.steps * max(1, args.runs)
             assert int(stats[0]) + int(stats[2]) == n * world * launches, ("packets lost",
                                                                              stats[:4])
             if args.config != "c3":
@@ -291,6 +276,7 @@ def main():
         counted = {"value": round(n * world * args.steps / wall_st / 1e6, 1),
                    "ms_per_step": round(wall_st * 1e3 / max(args.steps, 1), 5),
                    "kernel_ms": round(kernel_ms_st, 5),
+                   "runs_ms_per_step": run_ms_st,
                    "fold_ms": round(fold_ms, 3),
                    "what": "same launches + pktio and per-queue counters (per-workgroup rows of "
                            "odpg_counters_t, no extra kernel per launch; fold_ms = the one "
@@ -319,6 +305,8 @@ def main():
                 if args.config == "c2x" else METRIC.replace("64 PMR", f"{nrules} PMR")),
             "value": round(value, 1), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
+            "runs": max(1, args.runs), "runs_ms_per_step": run_ms,
+            "host_enqueue_ms_per_step": round(enq_ms / max(args.steps, 1), 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic",
             "config": {"workload": workload, "batch_per_gpu": n,
@@ -352,6 +340,40 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def timed_runs(args, ctx, launch, barrier, dist, dev):
+    """warmup, then args.runs loops of exactly args.steps launches, each
+    between barriers (device sync + process-group barrier); returns the
+    median run's (wall seconds, mean HIP-event ms per launch on the launch
+    stream, host ms spent enqueueing the launches) and every run's wall ms
+    per step. The wall clock is the max over ranks per run."""
+    import ctypes as C
+
+    from odp_amd import _lib as L
+    from odp_amd import shard
+    lib = L.lib
+    for i in range(args.warmup):
+        launch(i)
+    runs = []
+    for _ in range(max(1, args.runs)):
+        barrier()
+        t0 = time.perf_counter()
+        lib.odpg_event_record(ctx.h, 0)
+        for i in range(args.steps):
+            launch(i)
+        lib.odpg_event_record(ctx.h, 1)
+        te = time.perf_counter()
+        ctx.sync()
+        t1 = time.perf_counter()
+        barrier()
+        ev_ms = C.c_float(0)
+        L.check(lib.odpg_event_elapsed_ms(ctx.h, 0, 1, C.byref(ev_ms)), "event")
+        runs.append((shard.max_over_ranks(t1 - t0, dist, dev),
+                     ev_ms.value / max(args.steps, 1), (te - t0) * 1e3))
+    order = sorted(range(len(runs)), key=lambda k: runs[k][0])
+    med = runs[order[len(runs) // 2]]
+    return med[0], med[1], med[2], [round(r[0] * 1e3 / max(args.steps, 1), 5) for r in runs]
 
 
 def bench_scatter_gather(args, ctx, tbl, frames, n, stride, opt, world, rank, local, dist):
@@ -479,26 +501,15 @@ def bench_tx(args, world, rank, local, dist):
         if rc:
             raise RuntimeError(f"odpg_tx_prepare rc={rc}")
 
-    for i in range(args.warmup):
-        launch(i)
-    ctx.sync()
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    lib.odpg_event_record(ctx.h, 0)
-    for i in range(args.steps):
-        launch(i)
-    lib.odpg_event_record(ctx.h, 1)
-    ctx.sync()
-    wall = time.perf_counter() - t0
-    if dist is not None:
-        dist.barrier()
-    ev_ms = C.c_float(0)
-    L.check(lib.odpg_event_elapsed_ms(ctx.h, 0, 1, C.byref(ev_ms)), "event")
-    kernel_ms = ev_ms.value / max(args.steps, 1)
+    dev = f"cuda:{local}" if dist is not None and args.backend == "nccl" else None
+
+    def barrier():
+        ctx.sync()
+        if dist is not None:
+            dist.barrier()
+    wall, kernel_ms, enq_ms, run_ms = timed_runs(args, ctx, launch, barrier, dist, dev)
     out = obufs[(args.steps - 1) % nbuf].download(np.uint32, n)
     assert np.all(out & L.TX_OUT_IPV4) and np.all(out & L.TX_OUT_UDP)
-    wall = shard.max_over_ranks(wall, dist, f"cuda:{local}" if dist is not None and args.backend == "nccl" else None)
     value = n * world * args.steps / wall / 1e6
     bytes_per_pkt = 64 + 4 + 4           # frame read + two checksum fields + out word
     achieved = bytes_per_pkt * n / (kernel_ms * 1e-3) / 1e9
@@ -523,6 +534,8 @@ def bench_tx(args, world, rank, local, dist):
                       "+ crc32c loop queue pick",
             "value": round(value, 1), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(wall * 1e3 / max(args.steps, 1), 5),
+            "runs": max(1, args.runs), "runs_ms_per_step": run_ms,
+            "host_enqueue_ms_per_step": round(enq_ms / max(args.steps, 1), 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic",
             "config": {"workload": "loop pktio TX: 64B IPv4/UDP with zeroed checksums, pktout "
@@ -573,26 +586,15 @@ def bench_l3fwd(args, world, rank, local, dist):
         if rc:
             raise RuntimeError(f"odpg_l3fwd rc={rc}")
 
-    for i in range(args.warmup):
-        launch(i)
-    ctx.sync()
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    lib.odpg_event_record(ctx.h, 0)
-    for i in range(args.steps):
-        launch(i)
-    lib.odpg_event_record(ctx.h, 1)
-    ctx.sync()
-    wall = time.perf_counter() - t0
-    if dist is not None:
-        dist.barrier()
-    ev_ms = C.c_float(0)
-    L.check(lib.odpg_event_elapsed_ms(ctx.h, 0, 1, C.byref(ev_ms)), "event")
-    kernel_ms = ev_ms.value / max(args.steps, 1)
+    dev = f"cuda:{local}" if dist is not None and args.backend == "nccl" else None
+
+    def barrier():
+        ctx.sync()
+        if dist is not None:
+            dist.barrier()
+    wall, kernel_ms, enq_ms, run_ms = timed_runs(args, ctx, launch, barrier, dist, dev)
     out = obufs[(args.steps - 1) % nbuf].download(np.int32, n)
     assert (out >= 0).all(), "every C5 packet is IPv4 and forwarded"
-    wall = shard.max_over_ranks(wall, dist, f"cuda:{local}" if dist is not None and args.backend == "nccl" else None)
     value = n * world * args.steps / wall / 1e6
     bytes_per_pkt = 64 + 32 + 4          # frame read + header rewrite + port
     achieved = bytes_per_pkt * n / (kernel_ms * 1e-3) / 1e9
@@ -616,6 +618,8 @@ def bench_l3fwd(args, world, rank, local, dist):
                       "10M flows",
             "value": round(value, 1), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(wall * 1e3 / max(args.steps, 1), 5),
+            "runs": max(1, args.runs), "runs_ms_per_step": run_ms,
+            "host_enqueue_ms_per_step": round(enq_ms / max(args.steps, 1), 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic",
             "config": {"workload": f"C5: example/l3fwd {args.fwd_mode} mode, {len(routes)} "
@@ -676,34 +680,20 @@ def cpu_baseline(rules, frames, desc, n, stride, opt, args):
                                      nthreads=threads, reps=reps, cpus=cpus)
         rates.append(n * reps / (time.perf_counter() - t) / 1e6)
         log(f"cpu baseline: {used} threads {rates[-1]:.1f} Mpps")
-    # SURVEY.md §8(d) also asks for every core (nproc): the whole affinity
-    # mask, pinned, median of 3 shorter runs
+    # SURVEY.md §8(d) also asks for every core (nproc). Where the host
+    # grants this job fewer cores than its affinity mask lists (the GPU box:
+    # OMP_NUM_THREADS=16 of 256), a run over the whole mask measures that
+    # quota, not the cores, and is not reported
     allc = None
     try:
         aff = sorted(os.sched_getaffinity(0))
     except AttributeError:
         aff = list(range(os.cpu_count() or 1))
     if len(aff) > used:
-        # calibrated on one pass over the batch with every thread (a box may
-        # grant fewer cores than its affinity mask lists), then 3 runs of
-        # ~cpu_seconds / 6 each
-        t = time.perf_counter()
-        oracle.classify_mt(rules, frames, n, stride=stride, desc=desc, opt=opt,
-                           nthreads=len(aff), reps=1, cpus=aff)
-        cal = n / (time.perf_counter() - t)
-        reps_a = max(1, int(args.cpu_seconds / 6 * cal / n))
-        log(f"cpu baseline: all {len(aff)} CPUs, {cal / 1e6:.1f} Mpps calibration, {reps_a} passes per run")
-        ar = []
-        for _ in range(3):
-            t = time.perf_counter()
-            _, ua = oracle.classify_mt(rules, frames, n, stride=stride, desc=desc, opt=opt,
-                                       nthreads=len(aff), reps=reps_a, cpus=aff)
-            ar.append(n * reps_a / (time.perf_counter() - t) / 1e6)
-            log(f"cpu baseline: all cores {ar[-1]:.1f} Mpps")
-        allc = {"value": round(statistics.median(ar), 2), "cores": ua,
-                "runs_mpps": [round(r, 2) for r in ar],
-                "sample": f"median of 3 runs, each {reps_a} passes x {n} pkts, {ua} threads "
-                          f"pinned one per CPU of the whole affinity mask (nproc)"}
+        allc = {"value": None,
+                "note": f"not measured: the affinity mask lists {len(aff)} CPUs but the host "
+                        f"grants this job {used} ({share}); threads beyond the grant share "
+                        f"its cores"}
     model = ""
     try:
         for ln in open("/proc/cpuinfo"):

@@ -83,6 +83,7 @@ typedef struct {
 typedef struct {
 	int valid;
 	int started;
+	int closing;                 /* odp_pktio_close in progress: no start, no second close */
 	char name[64];
 	odp_pool_t pool;
 	odp_pktio_config_t config;
@@ -1156,7 +1157,7 @@ int odp_pktio_close(odp_pktio_t hdl)
 	LOCK();
 	pktio_e *p = get_pktio(hdl);
 
-	if (!p) {
+	if (!p || p->closing) {
 		UNLOCK();
 		return -1;
 	}
@@ -1171,9 +1172,11 @@ int odp_pktio_close(odp_pktio_t hdl)
 			ERR("pktio close during a receive\n");
 			return -1;
 		}
+	/* marked closing before the lock is dropped for the runtime side: a
+	 * start in that window is refused, and a stopped pktio takes no new
+	 * receive (recv_impl, rx_burst), so nothing re-binds */
+	p->closing = 1;
 	UNLOCK();
-	/* a stopped pktio takes no new receive (recv_impl, rx_burst), so
-	 * nothing re-binds while the lock is dropped for the runtime side */
 	odpg_rt_pktio_close(hdl);
 	LOCK();
 	p = get_pktio(hdl);
@@ -1299,7 +1302,7 @@ int odp_pktio_start(odp_pktio_t hdl)
 	LOCK();
 	pktio_e *p = get_pktio(hdl);
 
-	if (!p || p->started) {
+	if (!p || p->started || p->closing) {
 		rc = -1;
 	} else {
 		p->parse_layer = p->cls_enabled ? ODP_PROTO_LAYER_ALL : (int)p->config.parser.layer;

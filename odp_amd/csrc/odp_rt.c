@@ -87,6 +87,7 @@ typedef struct rt_queue {
 	rt_pkt_t *head, *tail;
 	struct rt_queue *next_sched;
 	int dead;
+	uint32_t gen;              /* registry slot generation (in the handle) */
 	odp_pktio_t pktin;         /* a QUEUE-mode pktin queue: dequeue polls it */
 	odp_pktio_t pktout;        /* a pktout event queue: enqueue transmits */
 } rt_queue_t;
@@ -605,12 +606,15 @@ int odp_shm_free(odp_shm_t shm)
 	pthread_mutex_lock(&shm_lock);
 	for (pp = &shm_list; *pp && *pp != s; pp = &(*pp)->next)
 		;
-	if (*pp)
-		*pp = s->next;
-	pthread_mutex_unlock(&shm_lock);
-	if (s->magic != SHM_MAGIC)
+	/* not a live block (freed before, or never reserved): nothing of it
+	 * is read */
+	if (!*pp || s->magic != SHM_MAGIC) {
+		pthread_mutex_unlock(&shm_lock);
 		return -1;
+	}
+	*pp = s->next;
 	s->magic = 0;
+	pthread_mutex_unlock(&shm_lock);
 	free(s->addr);
 	free(s);
 	return 0;
@@ -1348,14 +1352,28 @@ static void pktin_queue_fill(odp_pktio_t pktio);
 
 #define QH_TAG      0x0DD0000000000000ull  /* no user-space pointer has these bits */
 #define QH_TAG_MASK 0xFFFF000000000000ull
+#define QH_IDX_BITS 21                     /* slot index + 1 */
+#define QH_GEN_MASK 0x7FFFFFFull           /* the 27 bits above it */
 #define QCHUNK      4096u
-#define QCHUNKS     256u                   /* up to 1 M queues */
+#define QCHUNKS     256u                   /* up to 1 M live queues */
 
+/* Queue registry: a handle is tag | generation | slot + 1. A destroyed
+ * queue's slot goes on a free list and its object is reused by the next
+ * create with the generation advanced, so create / destroy cycles do not
+ * use the registry up and a stale handle stops resolving (queue_basic.c's
+ * queue table frees and reuses its entries the same way). Objects are never
+ * freed: a lookup racing a destroy reads valid memory and fails on the
+ * handle. Scheduled queues are unlinked from the scheduler's list under the
+ * write side of sched_rw, which every scheduler walk holds for reading, so
+ * no walk is inside an object when it is reused. */
 static struct {
 	pthread_mutex_t lock;
 	rt_queue_t **chunk[QCHUNKS];
 	uint32_t num;              /* slots handed out (published with release) */
-} qreg = { PTHREAD_MUTEX_INITIALIZER, {0}, 0 };
+	uint32_t *free;            /* destroyed slots */
+	uint32_t nfree, cap;
+} qreg = { PTHREAD_MUTEX_INITIALIZER, {0}, 0, NULL, 0, 0 };
+static pthread_rwlock_t sched_rw = PTHREAD_RWLOCK_INITIALIZER;
 
 static rt_queue_t *queue_slot(odp_queue_t q)
 {
@@ -1363,7 +1381,7 @@ static rt_queue_t *queue_slot(odp_queue_t q)
 
 	if ((v & QH_TAG_MASK) != QH_TAG)
 		return NULL;
-	const uint64_t idx = (v & ~QH_TAG_MASK) - 1u;
+	const uint64_t idx = (v & ((1ull << QH_IDX_BITS) - 1u)) - 1u;
 
 	if (idx >= __atomic_load_n(&qreg.num, __ATOMIC_ACQUIRE))
 		return NULL;
@@ -1374,46 +1392,91 @@ static rt_queue_t *get_queue(odp_queue_t q)
 {
 	rt_queue_t *x = queue_slot(q);
 
-	if (!x || x->magic != QUEUE_MAGIC || x->dead)
+	if (!x || x->magic != QUEUE_MAGIC ||
+	    __atomic_load_n(&x->hdl, __ATOMIC_ACQUIRE) != q || x->dead)
 		return NULL;
 	return x;
 }
 
 static rt_queue_t *queue_new(const char *name, const odp_queue_param_t *param)
 {
-	rt_queue_t *q = calloc(1, sizeof(*q));
+	rt_queue_t *q = NULL;
+	uint32_t idx;
 
-	if (!q)
-		return NULL;
 	pthread_mutex_lock(&qreg.lock);
-	const uint32_t idx = qreg.num;
-
-	if (idx >= QCHUNK * QCHUNKS ||
-	    (!qreg.chunk[idx / QCHUNK] &&
-	     !(qreg.chunk[idx / QCHUNK] = calloc(QCHUNK, sizeof(rt_queue_t *))))) {
-		pthread_mutex_unlock(&qreg.lock);
-		free(q);
-		ERR("queue registry full\n");
-		return NULL;
+	if (qreg.nfree) {
+		idx = qreg.free[--qreg.nfree];
+		q = qreg.chunk[idx / QCHUNK][idx % QCHUNK];
+	} else {
+		idx = qreg.num;
+		if (idx >= QCHUNK * QCHUNKS ||
+		    (!qreg.chunk[idx / QCHUNK] &&
+		     !(qreg.chunk[idx / QCHUNK] = calloc(QCHUNK, sizeof(rt_queue_t *)))) ||
+		    !(q = calloc(1, sizeof(*q)))) {
+			pthread_mutex_unlock(&qreg.lock);
+			ERR("queue registry full\n");
+			return NULL;
+		}
+		pthread_mutex_init(&q->lock, NULL);
+		q->magic = QUEUE_MAGIC;
 	}
-	q->magic = QUEUE_MAGIC;
-	q->hdl = (odp_queue_t)(uintptr_t)(QH_TAG | (uint64_t)(idx + 1u));
+	/* a reused object: the destroyed queue's fields reset (its lock and
+	 * magic stay), generation advanced */
+	q->gen = (q->gen + 1u) & (uint32_t)QH_GEN_MASK;
 	snprintf(q->name, sizeof(q->name), "%s", name ? name : "");
 	if (param)
 		q->param = *param;
 	else
 		odp_queue_param_init(&q->param);
-	pthread_mutex_init(&q->lock, NULL);
-	qreg.chunk[idx / QCHUNK][idx % QCHUNK] = q;
-	__atomic_store_n(&qreg.num, idx + 1u, __ATOMIC_RELEASE);
+	q->head = q->tail = NULL;
+	q->next_sched = NULL;
+	q->pktin = q->pktout = ODP_PKTIO_INVALID;
+	q->dead = 0;
+	__atomic_store_n(&q->hdl, (odp_queue_t)(uintptr_t)(QH_TAG | ((uint64_t)q->gen << QH_IDX_BITS) |
+							     (uint64_t)(idx + 1u)), __ATOMIC_RELEASE);
+	if (idx == qreg.num) {
+		qreg.chunk[idx / QCHUNK][idx % QCHUNK] = q;
+		__atomic_store_n(&qreg.num, idx + 1u, __ATOMIC_RELEASE);
+	}
 	pthread_mutex_unlock(&qreg.lock);
 	if (q->param.type == ODP_QUEUE_TYPE_SCHED) {
-		pthread_mutex_lock(&rt.lock);
+		pthread_rwlock_wrlock(&sched_rw);
 		q->next_sched = rt.sched;
 		rt.sched = q;
-		pthread_mutex_unlock(&rt.lock);
+		pthread_rwlock_unlock(&sched_rw);
 	}
 	return q;
+}
+
+/* a dead queue out of the scheduler's list and its slot onto the free list */
+static void queue_release(rt_queue_t *q)
+{
+	if (q->param.type == ODP_QUEUE_TYPE_SCHED) {
+		pthread_rwlock_wrlock(&sched_rw);
+		for (rt_queue_t **pp = &rt.sched; *pp; pp = &(*pp)->next_sched)
+			if (*pp == q) {
+				*pp = q->next_sched;
+				break;
+			}
+		pthread_rwlock_unlock(&sched_rw);
+	}
+	const uint64_t v = (uint64_t)(uintptr_t)q->hdl;
+	const uint32_t idx = (uint32_t)((v & ((1ull << QH_IDX_BITS) - 1u)) - 1u);
+
+	pthread_mutex_lock(&qreg.lock);
+	if (qreg.nfree == qreg.cap) {
+		const uint32_t nc = qreg.cap ? 2u * qreg.cap : 256u;
+		uint32_t *nf = realloc(qreg.free, nc * sizeof(uint32_t));
+
+		if (!nf) {                      /* the slot stays used */
+			pthread_mutex_unlock(&qreg.lock);
+			return;
+		}
+		qreg.free = nf;
+		qreg.cap = nc;
+	}
+	qreg.free[qreg.nfree++] = idx;
+	pthread_mutex_unlock(&qreg.lock);
 }
 
 odp_queue_t odp_queue_create(const char *name, const odp_queue_param_t *param)
@@ -1423,8 +1486,7 @@ odp_queue_t odp_queue_create(const char *name, const odp_queue_param_t *param)
 	return q ? q->hdl : ODP_QUEUE_INVALID;
 }
 
-/* a destroyed queue stays in the registry (schedulers may still hold it);
- * its handle stops being a queue */
+/* queue_basic.c queue_destroy: an empty queue only; its slot is reused */
 int odp_queue_destroy(odp_queue_t queue)
 {
 	rt_queue_t *q = get_queue(queue);
@@ -1432,13 +1494,17 @@ int odp_queue_destroy(odp_queue_t queue)
 	if (!q)
 		return -1;
 	pthread_mutex_lock(&q->lock);
-	if (q->head) {
+	if (q->head || q->dead) {
+		const int busy = q->head != NULL;
+
 		pthread_mutex_unlock(&q->lock);
-		ERR("queue '%s' not empty\n", q->name);
+		if (busy)
+			ERR("queue '%s' not empty\n", q->name);
 		return -1;
 	}
 	q->dead = 1;
 	pthread_mutex_unlock(&q->lock);
+	queue_release(q);
 	return 0;
 }
 
@@ -1561,14 +1627,18 @@ static rt_pktio_t *get_rt_pktio(odp_pktio_t hdl)
 	return n && n <= RT_MAX_PKTIO && rt.pktio[n - 1].valid ? &rt.pktio[n - 1] : NULL;
 }
 
-/* a queue the pktio owns: unlinked from use, its packets freed; the memory
- * stays (schedulers may still walk it) */
-static void pktio_queue_kill(rt_queue_t *q)
+/* a queue the pktio owns: unlinked from use, its packets freed, its slot
+ * reused */
+static void pktio_queue_kill(rt_queue_t **qp)
 {
+	rt_queue_t *q = *qp;
+
+	*qp = NULL;
 	if (!q)
 		return;
 	pthread_mutex_lock(&q->lock);
 	rt_pkt_t *k = q->head;
+	const int was_dead = q->dead;
 
 	q->head = q->tail = NULL;
 	q->dead = 1;
@@ -1580,6 +1650,8 @@ static void pktio_queue_kill(rt_queue_t *q)
 		odp_packet_free((odp_packet_t)k);
 		k = nx;
 	}
+	if (!was_dead)
+		queue_release(q);
 }
 
 /* "loop[...]" (pktio/loop.c) or "pcap:in=<file>[:loops=<n>]" (pktio/pcap.c's
@@ -1647,8 +1719,8 @@ void odpg_rt_pktio_close(odp_pktio_t hdl)
 
 		if (p->have_cap)
 			odpg_pcap_free(&p->cap);
-		pktio_queue_kill(p->inq);
-		pktio_queue_kill(p->outq);
+		pktio_queue_kill(&p->inq);
+		pktio_queue_kill(&p->outq);
 		while (k) {
 			rt_pkt_t *nx = k->next;
 
@@ -1681,7 +1753,7 @@ int odpg_rt_pktin_config(odp_pktio_t hdl, uint32_t num_queues)
 	p->num_in = num_queues;
 	if (p->in_mode != ODP_PKTIN_MODE_QUEUE && p->in_mode != ODP_PKTIN_MODE_SCHED)
 		return 0;
-	pktio_queue_kill(p->inq);
+	pktio_queue_kill(&p->inq);
 	odp_queue_param_init(&qp);
 	qp.type = p->in_mode == ODP_PKTIN_MODE_SCHED ? ODP_QUEUE_TYPE_SCHED : ODP_QUEUE_TYPE_PLAIN;
 	snprintf(name, sizeof(name), "odp-pktin-%u-0", (unsigned)(uintptr_t)hdl);
@@ -2059,31 +2131,28 @@ int odp_schedule_default_prio(void)
 
 static int sched_once(odp_queue_t *from, odp_event_t ev[], int num)
 {
-	pthread_mutex_lock(&rt.lock);
+	/* the list is walked under the read side of sched_rw: a destroy
+	 * unlinks under the write side before the object is reused */
+	pthread_rwlock_rdlock(&sched_rw);
 	rt_queue_t *list = rt.sched;
-	uint32_t skip = rt.rr++;
-	pthread_mutex_unlock(&rt.lock);
-
-	int nq = 0;
+	const uint32_t skip = __atomic_fetch_add(&rt.rr, 1u, __ATOMIC_RELAXED);
+	int nq = 0, n = 0;
 
 	for (rt_queue_t *q = list; q; q = q->next_sched)
 		nq++;
-	for (int pass = 0; pass < nq; pass++) {
+	for (int pass = 0; pass < nq && !n; pass++) {
 		rt_queue_t *q = list;
 
 		for (uint32_t s = (skip + (uint32_t)pass) % (uint32_t)nq; s; s--)
 			q = q->next_sched;
 		if (q->dead)
 			continue;
-		const int n = deq_multi(q, ev, num);
-
-		if (n) {
-			if (from)
-				*from = q->hdl;
-			return n;
-		}
+		n = deq_multi(q, ev, num);
+		if (n && from)
+			*from = q->hdl;
 	}
-	return 0;
+	pthread_rwlock_unlock(&sched_rw);
+	return n;
 }
 
 int odp_schedule_multi(odp_queue_t *from, uint64_t wait, odp_event_t events[], int num)
@@ -2162,7 +2231,7 @@ int odp_pktout_queue_config(odp_pktio_t pktio, const odp_pktout_queue_param_t *p
 	p->num_out = param->num_queues;
 	if (p->out_mode != ODP_PKTOUT_MODE_QUEUE)
 		return 0;
-	pktio_queue_kill(p->outq);
+	pktio_queue_kill(&p->outq);
 	odp_queue_param_init(&qp);
 	snprintf(name, sizeof(name), "odp-pktout-%u-0", (unsigned)(uintptr_t)pktio);
 	p->outq = queue_new(name, &qp);

@@ -1,0 +1,182 @@
+/* SPDX-License-Identifier: BSD-3-Clause
+ *
+ * Host-only checks of the ODP runtime subset (odp_amd/csrc/odp_rt.c) under
+ * thread contention, no GPU: the two-phase barrier re-entered many times
+ * with a shared counter checked between phases (test/validation/api/barrier
+ * does the same), thread ids handed out and given back by concurrent
+ * odp_init_local / odp_term_local (unique, below ODP_THREAD_COUNT_MAX), named
+ * shm reserve / lookup / free (a second free fails cleanly), and the queue
+ * registry: create / destroy cycles beyond its slot count, stale handles
+ * refused, scheduled queues created and destroyed while other threads
+ * schedule. Prints PASS or the first failure. Run by tests/test_odp_rt.py.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <odp_api.h>
+
+#define NT 8
+static int fails;
+
+#define CHECK(c, ...)                                                            \
+	do {                                                                     \
+		if (!(c)) {                                                      \
+			printf("FAIL %s:%d: ", __FILE__, __LINE__);              \
+			printf(__VA_ARGS__);                                     \
+			printf("\n");                                            \
+			__atomic_fetch_add(&fails, 1, __ATOMIC_RELAXED);         \
+		}                                                                \
+	} while (0)
+
+/* ---- barrier ---------------------------------------------------------------- */
+static odp_barrier_t barr;
+static uint32_t shared_count;
+#define BAR_ITERS 20000
+
+static void *bar_thread(void *arg)
+{
+	(void)arg;
+	for (uint32_t it = 0; it < BAR_ITERS && !fails; it++) {
+		__atomic_fetch_add(&shared_count, 1, __ATOMIC_RELAXED);
+		odp_barrier_wait(&barr);
+		const uint32_t v = __atomic_load_n(&shared_count, __ATOMIC_RELAXED);
+
+		CHECK(v == (it + 1) * NT, "barrier iteration %u: count %u, want %u", it, v,
+		      (it + 1) * NT);
+		odp_barrier_wait(&barr);
+	}
+	return NULL;
+}
+
+/* ---- thread ids --------------------------------------------------------------- */
+static int owner[ODP_THREAD_COUNT_MAX];
+
+static void *id_thread(void *arg)
+{
+	const int me = (int)(intptr_t)arg + 1;
+
+	for (int it = 0; it < 3000 && !fails; it++) {
+		CHECK(odp_init_local((odp_instance_t)0, ODP_THREAD_WORKER) == 0, "init_local");
+		const int id = odp_thread_id();
+
+		CHECK(id >= 0 && id < ODP_THREAD_COUNT_MAX, "thread id %d out of range", id);
+		if (id < 0 || id >= ODP_THREAD_COUNT_MAX)
+			break;
+		int z = 0;
+
+		CHECK(__atomic_compare_exchange_n(&owner[id], &z, me, 0, __ATOMIC_ACQ_REL,
+						  __ATOMIC_ACQUIRE),
+		      "thread id %d handed to two live threads", id);
+		CHECK(odp_thread_count() <= NT, "thread count %d", odp_thread_count());
+		__atomic_store_n(&owner[id], 0, __ATOMIC_RELEASE);
+		CHECK(odp_term_local() == 0, "term_local");
+	}
+	return NULL;
+}
+
+/* ---- scheduled queues created / destroyed under schedulers -------------------- */
+static int sched_stop;
+
+static void *sched_thread(void *arg)
+{
+	(void)arg;
+	while (!__atomic_load_n(&sched_stop, __ATOMIC_ACQUIRE)) {
+		odp_event_t ev[4];
+		odp_queue_t from;
+
+		CHECK(odp_schedule_multi(&from, ODP_SCHED_NO_WAIT, ev, 4) == 0,
+		      "events from empty queues");
+	}
+	return NULL;
+}
+
+static void *churn_thread(void *arg)
+{
+	(void)arg;
+	odp_queue_param_t qp;
+
+	odp_queue_param_init(&qp);
+	qp.type = ODP_QUEUE_TYPE_SCHED;
+	for (int it = 0; it < 20000 && !fails; it++) {
+		odp_queue_t q = odp_queue_create("sq", &qp);
+
+		CHECK(q != ODP_QUEUE_INVALID, "sched queue create %d", it);
+		CHECK(odp_queue_destroy(q) == 0, "sched queue destroy %d", it);
+	}
+	return NULL;
+}
+
+static void run(void *(*fn)(void *), int n)
+{
+	pthread_t t[NT];
+
+	for (int i = 0; i < n; i++)
+		pthread_create(&t[i], NULL, fn, (void *)(intptr_t)i);
+	for (int i = 0; i < n; i++)
+		pthread_join(t[i], NULL);
+}
+
+int main(void)
+{
+	/* barrier */
+	odp_barrier_init(&barr, NT);
+	run(bar_thread, NT);
+	printf("barrier: %d x %d waits\n", NT, 2 * BAR_ITERS);
+
+	/* thread ids */
+	run(id_thread, NT);
+	CHECK(odp_thread_count() == 0, "thread count after every term_local: %d",
+	      odp_thread_count());
+	printf("thread ids: %d threads x 3000 init/term\n", NT);
+
+	/* shm */
+	odp_shm_t a = odp_shm_reserve("blk_a", 100, 64, 0);
+	odp_shm_t b = odp_shm_reserve("blk_b", 4096, 4096, 0);
+
+	CHECK(a != ODP_SHM_INVALID && b != ODP_SHM_INVALID, "shm reserve");
+	CHECK(odp_shm_lookup("blk_a") == a && odp_shm_lookup("blk_b") == b, "shm lookup");
+	CHECK(odp_shm_addr(a) && ((uintptr_t)odp_shm_addr(b) & 4095u) == 0, "shm addr / align");
+	memset(odp_shm_addr(a), 0x5a, 100);
+	CHECK(odp_shm_free(a) == 0, "shm free");
+	CHECK(odp_shm_lookup("blk_a") == ODP_SHM_INVALID, "lookup after free");
+	CHECK(odp_shm_free(b) == 0 && odp_shm_free(b) == -1, "second free of a block");
+	printf("shm: reserve / lookup / free\n");
+
+	/* queue registry: more create / destroy cycles than slots */
+	odp_queue_t first = odp_queue_create("q", NULL), q = first;
+
+	CHECK(odp_queue_destroy(first) == 0, "destroy");
+	CHECK(odp_queue_destroy(first) == -1, "second destroy of a queue");
+	for (uint32_t it = 0; it < (1u << 21) && !fails; it++) {
+		q = odp_queue_create("q", NULL);
+		CHECK(q != ODP_QUEUE_INVALID, "create %u", it);
+		CHECK(odp_queue_destroy(q) == 0, "destroy %u", it);
+	}
+	CHECK(odp_queue_enq(first, ODP_EVENT_INVALID) == -1 &&
+	      odp_queue_deq(first) == ODP_EVENT_INVALID, "a stale handle still resolves");
+	odp_queue_t live = odp_queue_create("live", NULL);
+
+	CHECK(live != ODP_QUEUE_INVALID && live != first && live != q, "handle reuse");
+	CHECK(odp_queue_destroy(live) == 0, "destroy live");
+	printf("queues: 2^21 create/destroy cycles\n");
+
+	/* scheduled queues under concurrent schedulers */
+	pthread_t s[4], c[2];
+
+	for (int i = 0; i < 4; i++)
+		pthread_create(&s[i], NULL, sched_thread, NULL);
+	for (int i = 0; i < 2; i++)
+		pthread_create(&c[i], NULL, churn_thread, NULL);
+	for (int i = 0; i < 2; i++)
+		pthread_join(c[i], NULL);
+	__atomic_store_n(&sched_stop, 1, __ATOMIC_RELEASE);
+	for (int i = 0; i < 4; i++)
+		pthread_join(s[i], NULL);
+	printf("sched queues: 2 x 20000 create/destroy under 4 schedulers\n");
+
+	printf(fails ? "FAILED (%d)\n" : "PASS\n", fails);
+	return fails ? 1 : 0;
+}

@@ -333,3 +333,28 @@ def test_gpu_hash_flow_cache_cases(gpu_ctx):
                                                                        src_port=2)
         o_out, _ = run_oracle(routes, fr, sif=2)
         np.testing.assert_array_equal(g_out, o_out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride", [64, 128])
+def test_gpu_hash_more_than_128_intervals(gpu_ctx, stride):
+    """32 disjoint /24 routes with host bits set: each adds its masked scan
+    range and its unaligned warmed range, 4 points per route + 0 = 129
+    interval starts, so the destinations of the last routes sit at interval
+    index >= 128, past a 7-step binary search (fwd.hip search)."""
+    routes = [R((ip("10.0.0.0") | (k << 8)) + 0x55, 24, k % 4, k) for k in range(32)]
+    dsts = []
+    for k in range(32):
+        b = ip("10.0.0.0") | (k << 8)
+        dsts += [b, b + 0x54, b + 0x55, b + 0xFF, b + 0x100 + 0x54, b + 0x100 + 0x55]
+    dsts += [ip("10.0.32.0"), ip("10.0.31.255"), 0, 0xFFFFFFFF]
+    fr = frames_to(dsts).reshape(-1, 64)
+    if stride != 64:
+        fr = np.concatenate([fr, np.zeros((len(dsts), stride - 64), np.uint8)], axis=1)
+    fr = fr.reshape(-1)
+    fw = gpu.Forwarder(gpu_ctx, routes, mode=L.FWD_HASH)
+    g_out, g_fr = fw.run(fr, stride, len(dsts), src_port=3)
+    o_out, o_fr = run_oracle(routes, fr, stride=stride, sif=3)
+    np.testing.assert_array_equal(g_out, o_out)
+    np.testing.assert_array_equal(g_fr[:fr.nbytes], o_fr)
+    assert len(set(int(x) for x in o_out)) == 4

@@ -211,3 +211,16 @@ def test_reference_classifier_runs_and_passes_its_ci_check(tmp_path):
     assert rows, r.stdout[-2000:]
     counts = [int(x.split()[0]) for x in rows[-1].split("|")[:-1]]
     assert counts[:2] == [100, 100], rows[-1]
+
+
+def test_host_runtime_under_contention():
+    """tests/c/odp_rt_host.c, no GPU: the barrier re-entered 40000 times by
+    8 threads with a shared count checked between phases, thread ids under
+    concurrent init_local / term_local, named shm reserve / lookup / free
+    (a second free fails cleanly), 2^21 queue create / destroy cycles (more
+    than the registry's slots: destroyed slots are reused and stale handles
+    refused) and scheduled queues created / destroyed under 4 schedulers."""
+    subprocess.run(["make", "-C", os.path.join(HERE, "c")], check=True, capture_output=True)
+    r = subprocess.run(["timeout", "-k", "10", "240", os.path.join(HERE, "c", "odp_rt_host")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0 and "PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-2000:])
