@@ -315,6 +315,7 @@ SIGNATURES = {
     "odpg_dev_free": (_i32, [_vp, _vp]),
     "odpg_host_alloc_pinned": (_i32, [_sz, C.POINTER(_vp)]),
     "odpg_host_free_pinned": (_i32, [_vp]),
+    "odpg_host_device_ptr": (_i32, [_vp, C.POINTER(_vp)]),
     "odpg_memcpy_h2d": (_i32, [_vp, _vp, _vp, _sz]),
     "odpg_memcpy_d2h": (_i32, [_vp, _vp, _vp, _sz]),
     "odpg_memset_dev": (_i32, [_vp, _vp, _i32, _sz]),

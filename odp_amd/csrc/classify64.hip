@@ -271,6 +271,18 @@ __device__ __forceinline__ uint4 lds_ent(const uint4 *p)
 #define BIN_DROP   3u
 #define BIN_EXTRA  4u
 
+#ifdef L64_EXP_TIMES   /* experiment builds only: per-wave start / end times */
+/* {s_memrealtime at the wave's start, at its end | tiles << 48} per wave */
+__device__ unsigned long long g_l64_times[2 * 65536];
+
+extern "C" int odpg_diag_l64_times(unsigned long long *out, uint32_t nwaves)
+{
+	if (nwaves > 65536u)
+		return -EINVAL;
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_l64_times), 16u * nwaves) == hipSuccess ? 0 : -EIO;
+}
+#endif
+
 /* ---- the kernel ------------------------------------------------------------
  * NG > 0: the table has exactly NG mask groups (HW: walk groups); their
  * descriptors are read once into scalar registers before the tile loop.
@@ -285,6 +297,10 @@ odpg_cls64_kernel(const L64Args A)
 {
 	static_assert(!HW || NG > 0, "walk groups are hoisted");
 	constexpr uint32_t LBK = LBH(HW, CM);
+#ifdef L64_EXP_TIMES
+	const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+	uint32_t n_tiles = 0u;
+#endif
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 	constexpr uint32_t RW = 17;                     /* odd dword row stride */
 	uint32_t *row = smem + threadIdx.x * RW;        /* generic-parse LDS row */
@@ -297,6 +313,12 @@ odpg_cls64_kernel(const L64Args A)
 	/* HW: cuckoo entries, pinfo3 */
 	uint2 *cents = (uint2 *)(dlv + nbins);
 	uint2 *pinfo3 = cents + A.num_cent;
+	/* CM 2: the workgroup's counter row as it stood before this launch,
+	 * read at the start (behind the first tile's loads), so that the
+	 * flush is plain stores of row + histogram, not atomics at the
+	 * kernel's common tail (the workgroup owns its row) */
+	unsigned long long *base = HW ? (unsigned long long *)(pinfo3 + A.num_pmr)
+				      : (unsigned long long *)(pinfo4 + A.num_pmr);
 
 	const uint32_t lane = __lane_id();
 	/* wave-uniform (readfirstlane): buffer resources are built from it */
@@ -402,12 +424,21 @@ odpg_cls64_kernel(const L64Args A)
 	__shared__ uint32_t waves_done;
 	odpg_cnt_dev C = {};
 
+	__shared__ uint32_t flush_tot;
+
 	if constexpr (CM == 2) {
 		C = *A.cnt;
+		const unsigned long long *r0 =
+			(const unsigned long long *)(C.rows + (size_t)blockIdx.x * C.words);
+
+		for (uint32_t k = threadIdx.x; k < C.words; k += LBK)
+			base[k] = r0[k];
 		for (uint32_t k = threadIdx.x; k < A.num_cos + BIN_EXTRA; k += LBK)
 			dlv[k] = 0u;
-		if (threadIdx.x == 0u)
+		if (threadIdx.x == 0u) {
 			waves_done = 0u;
+			flush_tot = 0u;
+		}
 	}
 	__syncthreads();
 
@@ -868,11 +899,27 @@ odpg_cls64_kernel(const L64Args A)
 				A.out[i] = w;
 		}
 		t0 += nk * nwaves;
+#ifdef L64_EXP_TIMES
+		n_tiles += nk;
+#endif
 	}
+#ifdef L64_EXP_TIMES
+	{
+		const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+
+		if (__lane_id() == 0u && gw < 65536u) {
+			g_l64_times[2u * gw] = t_start;
+			g_l64_times[2u * gw + 1u] = t_end | ((unsigned long long)n_tiles << 48);
+		}
+	}
+#endif
 	if constexpr (CM == 2) {
 		/* the workgroup's histogram into its own counter row (odpg.h
-		 * "sharded counters"): no-return atomics, one trip to L2 at the
-		 * kernel's tail (a read-modify-write would be two) */
+		 * "sharded counters"): plain stores of the row read at the start
+		 * plus the histogram (the workgroup owns the row; the launches
+		 * on the stream are ordered). No-return atomics here, ~70 per
+		 * workgroup, all reached L2 together at the kernel's common tail
+		 * (+1 us of 13.3 on C2) */
 #ifdef L64_EXP_NOFLUSH   /* experiment builds only */
 		if (A.num_cos != 12345u)
 			return;
@@ -884,7 +931,7 @@ odpg_cls64_kernel(const L64Args A)
 		 * others have already exited. CoS-keyed tables (HW, up to 1024+
 		 * CoS, 1024-thread workgroups): a barrier, then every wave flushes a
 		 * slice of the bins (one wave alone would issue ~17 passes of 64
-		 * atomics at the kernel's tail: C4 counted 22.6 vs 16.4 us). */
+		 * at the kernel's tail: C4 counted 22.6 vs 16.4 us with atomics). */
 		uint32_t k_first = lane, k_step = 64u;
 		bool lead = lane == 0u;
 
@@ -907,33 +954,40 @@ odpg_cls64_kernel(const L64Args A)
 		const uint32_t nc = A.num_cos < C.ncos ? A.num_cos : C.ncos;
 		/* without hash queues each CoS owns one column; else its first */
 		auto col = [&](uint32_t c) { return 4u + C.ncos + (C.ident ? c : C.qcol[c]); };
+		const uint32_t ne = dlv[BIN_ERR], np = dlv[BIN_PDROP];
+		/* error packets are delivered to the error CoS unless it drops;
+		 * without an error CoS they are discards too */
+		const bool edeliv = ne && A.err_cos < nc && A.err_act != 1u;
 		uint32_t tot = 0u;
 
 		for (uint32_t k = k_first; k < (nc + 63u) / 64u * 64u; k += k_step) {
 			const uint32_t x = k < nc ? dlv[BIN_EXTRA + k] : 0u;
+			const uint32_t xe = x + (edeliv && k == A.err_cos ? ne : 0u);
 
-			if (x)
-				atomicAdd(r + col(k), (unsigned long long)x);
+			if (xe)
+				r[col(k)] = base[col(k)] + xe;
 			tot += x;
 		}
-		const uint32_t t = wave_sum_u32(tot);            /* in_packets, in_octets */
+		uint32_t t = wave_sum_u32(tot);            /* in_packets, in_octets */
 
-		if (lane == 0u && t) {
-			atomicAdd(r + 0, (unsigned long long)t);
-			atomicAdd(r + 1, (unsigned long long)t * 64ull);
+		if constexpr ((HW || L64_MG_BARRIER) && !L64_HW_LASTWAVE) {
+			/* every wave flushed a slice: the in_packets total over them */
+			if (lane == 0u && t)
+				atomicAdd(&flush_tot, t);
+			__syncthreads();
+			t = flush_tot;
 		}
 		if (lead) {
-			const uint32_t ne = dlv[BIN_ERR], np = dlv[BIN_PDROP];
-			uint32_t nd = dlv[BIN_NOCOS];
+			const uint32_t nd = dlv[BIN_NOCOS] + (A.err_cos >= nc ? ne : 0u);
 
-			if (ne && A.err_cos < nc && A.err_act != 1u)
-				atomicAdd(r + col(A.err_cos), (unsigned long long)ne);
-			else if (A.err_cos >= nc)
-				nd += ne;
+			if (t) {
+				r[0] = base[0] + t;
+				r[1] = base[1] + (unsigned long long)t * 64ull;
+			}
 			if (ne + np)
-				atomicAdd(r + 2, (unsigned long long)(ne + np));
+				r[2] = base[2] + (ne + np);
 			if (nd)
-				atomicAdd(r + 3, (unsigned long long)nd);
+				r[3] = base[3] + nd;
 		}
 	} else if constexpr (CM == 1) {
 		const uint64_t v[4] = {n_pkt, (uint64_t)n_pkt * 64u, n_err, n_disc};
@@ -953,7 +1007,8 @@ size_t odpg_cls64_lds(const odpg_launch_args &a)
 	return (size_t)LBH(hw, a.cnt.row ? 2 : 0) * 17u * 4u +
 	       (hw ? (size_t)a.num_cent * 8u + (size_t)a.num_pmr * 8u
 		   : (size_t)a.num_ment * 16u + (size_t)a.num_pmr * 16u) +
-	       (a.cnt.row ? (((size_t)a.num_cos + BIN_EXTRA + 3u) & ~(size_t)3u) * 4u : 0u);
+	       (a.cnt.row ? (((size_t)a.num_cos + BIN_EXTRA + 3u) & ~(size_t)3u) * 4u +
+				    (size_t)a.cnt.words * 8u : 0u);
 }
 
 extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)

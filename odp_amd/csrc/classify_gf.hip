@@ -71,6 +71,7 @@ struct GFArgs {
 	const uint32_t *xfc;        /* lazy form: per CoS first complex record | count << 16 */
 	uint32_t num_xflat;         /* lazy form: complex records */
 	const odpg_cnt_dev *cnt;    /* CM 2: the sharded counters' layout */
+	uint32_t cnt_words;         /* CM 2: words of a counter row */
 };
 
 /* sharded-counter histogram bins before the CoS bins (CM 2) */
@@ -81,6 +82,8 @@ struct GFArgs {
 #define GF_BIN_EXTRA  4u
 
 typedef unsigned short gf_us2 __attribute__((ext_vector_type(2)));
+/* key slots 0..15 of a packet, indexed by a wave-uniform slot (v_movrels) */
+typedef uint32_t gf_kv_t __attribute__((ext_vector_type(16)));
 
 /* acc + w.lo * x.lo16 + w.hi * x.hi16 (one v_dot2_u32_u16) */
 __device__ __forceinline__ uint32_t gd2(uint32_t x, uint32_t w, uint32_t acc)
@@ -526,8 +529,12 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	const uint2 *xci = (const uint2 *)(tb + A.L.xci);
 	const uint4 *pdst = (const uint4 *)(tb + A.L.xpd);
 	const uint4 *xfl = (const uint4 *)(tb + A.L.xflat);
+	/* CM 2: the workgroup's counter row as it stood before this launch
+	 * (read at the start; the flush stores row + histogram) */
+	unsigned long long *base = (unsigned long long *)(tb + ((A.L.lds_words + 1u) & ~1u));
 	/* GF_SWEEP: the wave's x16 words and tail partials (2 x 64 dwords) */
-	uint32_t *swx = tb + A.L.lds_words + (threadIdx.x >> 6) * 128u;
+	uint32_t *swx = tb + ((A.L.lds_words + 1u) & ~1u) + (CM == 2 ? 2u * A.cnt_words : 0u) +
+			(threadIdx.x >> 6) * 128u;
 
 	const uint32_t lane = __lane_id();
 	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (GF_BLOCK / 64) +
@@ -597,6 +604,11 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 
 	if constexpr (CM == 2) {
 		C = *A.cnt;
+		const unsigned long long *r0 =
+			(const unsigned long long *)(C.rows + (size_t)blockIdx.x * C.words);
+
+		for (uint32_t k = threadIdx.x; k < C.words; k += GF_BLOCK)
+			base[k] = r0[k];
 		for (uint32_t k = threadIdx.x; k < nbins; k += GF_BLOCK)
 			dlv[k] = 0u;
 		if (threadIdx.x == 0u) {
@@ -614,6 +626,8 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	const bool def_rules = def_valid && A.coses[A.default_cos].nrule != 0u;
 	/* the chain bits (they start set, groups clear them), uniform */
 	uint32_t chain[NW];
+	/* the key slots the groups read */
+	const uint32_t kslots = xhdr[6];
 
 #pragma unroll
 	for (int w = 0; w < NW; ++w)
@@ -642,7 +656,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 				f[q + 3] = x.w;
 			}
 			x16 = swx[lane];
-		} else {
+		} else if (__ballot(live && len < 64u)) {
 #pragma unroll
 			for (int q = 0; q < 16; ++q) {
 				/* bytes past the frame read as zero (the reference's
@@ -651,6 +665,12 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 
 				f[q] = nb >= 4 ? fn[q] : nb <= 0 ? 0u : fn[q] & ((1u << (8 * nb)) - 1u);
 			}
+		} else {
+			/* no live frame shorter than the window (dead lanes' bytes
+			 * are never used) */
+#pragma unroll
+			for (int q = 0; q < 16; ++q)
+				f[q] = fn[q];
 		}
 		dn = dnn;
 
@@ -699,72 +719,12 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			b.len = len;
 			b.inf_lo = (uint32_t)p.inf;
 		};
-		/* the hit map: each group's masked key word, once per packet.
-		 * Single-word rules OR their bits in; a complex rule's chain bit
-		 * (set to start with) stays set only while every group holding one
-		 * of its records has it in the entry for the packet's key */
-		auto keys = [&](auto key) {
-			const bool on = live && (p.fl & FL_ERROR_MASK) == 0u;
+		/* the packet's key slots (odpg_internal.h "key slots"), extracted
+		 * once: slots 0..15 in a register vector the groups index by their
+		 * uniform slot, 16 / 17 (L4) and 18 (length) beside it */
+		gf_kv_t kv = {};
+		uint32_t k16 = 0u, k17 = 0u;
 
-#pragma unroll
-			for (int w = 0; w < NW; ++w)
-				hm[w] = on ? chain[w] : 0u;
-			if (!__ballot(on))
-				return;
-#ifdef GF_EXP_NOHM   /* experiment builds only: cost without the hit map */
-			if (A.num != 12345u)
-				return;
-#endif
-for (uint32_t gi = 0; gi < ngroups; ++gi) {
-				const uint4 q0 = xmg[4u * gi];
-				const uint4 q1 = xmg[4u * gi + 1u];
-				const uint32_t mul = __builtin_amdgcn_readfirstlane(q0.x);
-				const uint32_t shf = __builtin_amdgcn_readfirstlane(q0.y);
-				const uint32_t soff = __builtin_amdgcn_readfirstlane(q0.z);
-				const uint32_t eb = __builtin_amdgcn_readfirstlane(q0.w);
-				const uint32_t sg = __builtin_amdgcn_readfirstlane(q1.x);
-				const uint32_t greq = __builtin_amdgcn_readfirstlane(q1.y);
-				const uint32_t gmask = __builtin_amdgcn_readfirstlane(q1.z);
-				const uint32_t gand = __builtin_amdgcn_readfirstlane(q1.w);
-				/* CUSTOM_L3 / CUSTOM_FRAME records: frame_len > base + off
-				 * + size (term_cmp's guard) */
-				const bool gok = !(sg >> 31) ||
-						 b.len > ((sg >> 30) & 1u ? 0u : b.l3) + ((sg >> 8) & 0xffffu);
-				uint32_t h[NW];
-
-#pragma unroll
-				for (int w = 0; w < NW; ++w)
-					h[w] = 0u;
-				if (on && (b.inf_lo & greq) == greq && gok) {
-					const uint32_t kv = key(sg & 0xffu) & gmask;
-					const uint32_t si = xms[soff + ((kv * mul) >> shf)];
-
-					if (si != 0xffu) {
-						uint32_t m[NW];
-
-						xm_entry<NW>(xmm, eb + si, m);
-						if (xmv[eb + si] == kv) {
-#pragma unroll
-							for (int w = 0; w < NW; ++w)
-								h[w] = m[w];
-						}
-					}
-				}
-				if (gand) {                     /* uniform */
-					const uint4 a0 = xmg[4u * gi + 2u];
-					const uint4 a1 = xmg[4u * gi + 3u];
-					const uint32_t na[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-
-#pragma unroll
-					for (int w = 0; w < NW; ++w)
-						hm[w] = (hm[w] & (h[w] | na[w])) | (h[w] & ~chain[w]);
-				} else {
-#pragma unroll
-					for (int w = 0; w < NW; ++w)
-						hm[w] |= h[w];
-				}
-			}
-		};
 #ifdef GF_EXP_NOGEN
 		if (true) {
 #else
@@ -776,31 +736,25 @@ for (uint32_t gi = 0; gi < ngroups; ++gi) {
 			const bool v6 = (b.inf_lo & (uint32_t)IF(IFL_IPV6)) != 0u;
 			const bool l4ok = b.l4 != 0xffffu;
 
-			keys([&](uint32_t slot) -> uint32_t {   /* slot wave-uniform */
-				switch (slot) {
-				case 0: return f[0];
-				case 1: return f[1];
-				case 2: return f[2];
-				case 3: return u3;
-				case 4: return u4;
-				case 5:                         /* the innermost VLAN tag */
-					return qinq ? __builtin_amdgcn_alignbyte(u5, u4, 2) :
-						      __builtin_amdgcn_alignbyte(u4, u3, 2);
-				case 6: return wb<14>(f);
-				case 7: return wb<18>(f);
-				case 8: return wb<22>(f);
-				case 9: return wb<26>(f);
-				case 10: return wb<30>(f);
-				case 11: return wb<34>(f);
-				case 12: return wb<38>(f);
-				case 13: return wb<42>(f);
-				case 14: return wb<46>(f);
-				case 15: return wb<50>(f);
-				case 16: return !l4ok ? 0u : v6 ? wb<54>(f) : wb<34>(f);
-				case 17: return !l4ok ? 0u : v6 ? wb<58>(f) : wb<38>(f);
-				default: return len;
-				}
-			});
+			kv[0] = f[0];
+			kv[1] = f[1];
+			kv[2] = f[2];
+			kv[3] = u3;
+			kv[4] = u4;
+			/* the innermost VLAN tag */
+			kv[5] = qinq ? __builtin_amdgcn_alignbyte(u5, u4, 2) : __builtin_amdgcn_alignbyte(u4, u3, 2);
+			kv[6] = wb<14>(f);
+			kv[7] = wb<18>(f);
+			kv[8] = wb<22>(f);
+			kv[9] = wb<26>(f);
+			kv[10] = wb<30>(f);
+			kv[11] = wb<34>(f);
+			kv[12] = wb<38>(f);
+			kv[13] = wb<42>(f);
+			kv[14] = wb<46>(f);
+			kv[15] = wb<50>(f);
+			k16 = !l4ok ? 0u : v6 ? wb<54>(f) : wb<34>(f);
+			k17 = !l4ok ? 0u : v6 ? wb<58>(f) : wb<38>(f);
 		} else {
 			Pkt<64, true> v;
 
@@ -816,7 +770,74 @@ for (uint32_t gi = 0; gi < ngroups; ++gi) {
 			key.v = &v;
 			key.b = &b;
 			key.fast = false;
-			keys(key);
+			/* the slots the groups read (uniform mask) */
+#pragma unroll
+			for (uint32_t sl = 0; sl < 16u; ++sl)
+				if ((kslots >> sl) & 1u)
+					kv[sl] = key(sl);
+			if ((kslots >> 16) & 1u)
+				k16 = key(16u);
+			if ((kslots >> 17) & 1u)
+				k17 = key(17u);
+		}
+		/* the hit map: each group's masked key word, once per packet.
+		 * Single-word rules OR their bits in; a complex rule's chain bit
+		 * (set to start with) stays set only while every group holding one
+		 * of its records has it in the entry for the packet's key */
+		{
+			const bool on = live && (p.fl & FL_ERROR_MASK) == 0u;
+
+#pragma unroll
+			for (int w = 0; w < NW; ++w)
+				hm[w] = on ? chain[w] : 0u;
+#ifdef GF_EXP_NOHM   /* experiment builds only: cost without the hit map */
+			if (__ballot(on) && A.num == 12345u) {
+#else
+			if (__ballot(on)) {
+#endif
+				for (uint32_t gi = 0; gi < ngroups; ++gi) {
+					const uint4 q0 = xmg[4u * gi];
+					const uint4 q1 = xmg[4u * gi + 1u];
+					const uint32_t mul = q0.x, shf = q0.y, soff = q0.z, eb = q0.w;
+					const uint32_t sg = q1.x, greq = q1.y, gmask = q1.z, gand = q1.w;
+					const uint32_t sl = sg & 0xffu;
+					/* CUSTOM_L3 / CUSTOM_FRAME records: frame_len > base +
+					 * off + size (term_cmp's guard) */
+					const bool gok = !(sg >> 31) ||
+							 b.len > ((sg >> 30) & 1u ? 0u : b.l3) + ((sg >> 8) & 0xffffu);
+					const uint32_t key = sl < 16u ? kv[sl] : sl == 16u ? k16 :
+							     sl == 17u ? k17 : len;
+					const uint32_t kvm = key & gmask;
+					/* branch-free probe: the slot byte, then the entry's
+					 * value and bit map (entry eb + 0 read for an empty
+					 * slot) */
+					const uint32_t si = xms[soff + ((kvm * mul) >> shf)];
+					const uint32_t e = eb + (si != 0xffu ? si : 0u);
+					uint32_t m[NW];
+
+					xm_entry<NW>(xmm, e, m);
+					const bool hit = on && (b.inf_lo & greq) == greq && gok &&
+							 si != 0xffu && xmv[e] == kvm;
+
+					if (gand) {                     /* uniform */
+						const uint4 a0 = xmg[4u * gi + 2u];
+						const uint4 a1 = xmg[4u * gi + 3u];
+						const uint32_t na[8] = {a0.x, a0.y, a0.z, a0.w,
+									a1.x, a1.y, a1.z, a1.w};
+
+#pragma unroll
+						for (int w = 0; w < NW; ++w) {
+							const uint32_t h = hit ? m[w] : 0u;
+
+							hm[w] = (hm[w] & (h | na[w])) | (h & ~chain[w]);
+						}
+					} else {
+#pragma unroll
+						for (int w = 0; w < NW; ++w)
+							hm[w] |= hit ? m[w] : 0u;
+					}
+				}
+			}
 		}
 
 		/* ---- checksum bytes past the window: the whole wave. Even waves
@@ -1092,37 +1113,37 @@ for (uint32_t gi = 0; gi < ngroups; ++gi) {
 		const uint32_t nc = A.num_cos < C.ncos ? A.num_cos : C.ncos;
 		/* without hash queues each CoS owns one column */
 		auto col = [&](uint32_t c) { return 4u + C.ncos + (C.ident ? c : C.qcol[c]); };
+		const uint32_t ne = dlv[GF_BIN_ERR], np = dlv[GF_BIN_PDROP];
+		const uint32_t ec = A.error_cos < 0 ? 0xffffffffu : (uint32_t)A.error_cos;
+		/* error packets: delivered to the error CoS unless it drops;
+		 * without an error CoS they are discards too */
+		const bool edeliv = ne && ec < nc && (xci[ec].y & 0xffu) != 1u;
 		uint32_t tot = 0u;
 
+		/* plain stores of the row read at the start + the histogram (the
+		 * workgroup owns its row; launches on the stream are ordered) */
 		for (uint32_t k0 = 0; k0 < nc; k0 += 64u) {
 			const uint32_t k = k0 + lane;
 			const uint32_t x = k < nc ? dlv[GF_BIN_EXTRA + k] : 0u;
+			const uint32_t xe = x + (edeliv && k == ec ? ne : 0u);
 
-			if (x)
-				atomicAdd(r + col(k), (unsigned long long)x);
+			if (xe)
+				r[col(k)] = base[col(k)] + xe;
 			tot += x;
 		}
 		const uint32_t tp = wave_sum_u32(tot);                  /* in_packets */
 
 		if (lane == 0u) {
-			const uint32_t ne = dlv[GF_BIN_ERR], np = dlv[GF_BIN_PDROP];
-			uint32_t nd = dlv[GF_BIN_NOCOS];
-			const uint32_t ec = A.error_cos < 0 ? 0xffffffffu : (uint32_t)A.error_cos;
+			const uint32_t nd = dlv[GF_BIN_NOCOS] + (ec >= nc ? ne : 0u);
 
 			if (tp) {
-				atomicAdd(r + 0, (unsigned long long)tp);
-				atomicAdd(r + 1, octets);
+				r[0] = base[0] + tp;
+				r[1] = base[1] + octets;
 			}
-			/* error packets: delivered to the error CoS unless it drops;
-			 * without an error CoS they are discards too */
-			if (ne && ec < nc && (xci[ec].y & 0xffu) != 1u)
-				atomicAdd(r + col(ec), (unsigned long long)ne);
-			else if (ec >= nc)
-				nd += ne;
 			if (ne + np)
-				atomicAdd(r + 2, (unsigned long long)(ne + np));
+				r[2] = base[2] + (ne + np);
 			if (nd)
-				atomicAdd(r + 3, (unsigned long long)nd);
+				r[3] = base[3] + nd;
 		}
 	}
 }
@@ -1144,7 +1165,8 @@ extern "C" size_t odpg_clsgf_lds(const odpg_launch_args *a)
 	gf_layout(a, &L);
 	const size_t bins = a->cnt.row ? (((size_t)a->num_cos + GF_BIN_EXTRA + 3u) & ~(size_t)3u) * 4u : 0u;
 
-	return (size_t)GF_BLOCK * GF_RW * 4u + bins + (size_t)L.lds_words * 4u +
+	return (size_t)GF_BLOCK * GF_RW * 4u + bins + (size_t)((L.lds_words + 1u) & ~1u) * 4u +
+	       (a->cnt.row ? (size_t)a->cnt.words * 8u : 0u) +
 	       (GF_SWEEP ? (size_t)GF_BLOCK * 2u * 4u : 0u);
 }
 
@@ -1173,6 +1195,7 @@ extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s)
 	A.xlds = a->xm + XM_HDR_WORDS + XM_GROUP_WORDS * a->xm_ngroups;
 	A.xfc = A.xlds + A.L.lds_words;
 	A.cnt = a->cnt.dev;
+	A.cnt_words = a->cnt.row ? a->cnt.words : 0u;
 
 	const size_t lds = odpg_clsgf_lds(a);
 	const uint32_t ntiles = (a->num + 63u) / 64u;

@@ -9,6 +9,7 @@
  * the reference's raw-memory compare semantics: values and masks are the
  * caller's bytes (network order, except ODP_PMR_LEN which is CPU endian).
  */
+#include <stdlib.h>
 #include <string.h>
 #include <errno.h>
 #include <algorithm>
@@ -1113,7 +1114,10 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		}
 		cbit_n[c] = nbits - cbit_start[c];
 	}
-	if (xm && nbits > XM_MAX_PMR) {
+	/* ODPG_XM_LAZY=1 forces the lazy form (experiments / A-B runs) */
+	static const bool force_lazy = getenv("ODPG_XM_LAZY") && atoi(getenv("ODPG_XM_LAZY"));
+
+	if (xm && (nbits > XM_MAX_PMR || force_lazy)) {
 		/* lazy form: bit = PMR index, complex PMRs from their records */
 		and_form = false;
 		nbits = (uint32_t)pmr.size();
@@ -1310,6 +1314,10 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		xmhdr[3] = (uint32_t)xmval.size();
 		xmhdr[4] = (uint32_t)xmslot.size();
 		xmhdr[5] = (uint32_t)(xflat.size() / 8);
+		/* the key slots the groups read (the kernel extracts them once per
+		 * packet) */
+		for (auto &kv : gv)
+			xmhdr[6] |= 1u << (std::get<0>(kv.first) & 0x1fu);
 		for (uint32_t w = 0; w < XM_WORDS; w++)
 			xmhdr[8 + w] = chain_all[w];
 		h.flags |= TBL_XMASK;

@@ -1659,6 +1659,11 @@ static int recv_impl(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
 	res.counters = bd->cnt;
 	rc = device_ptrs ? odpg_classify(ctx, bd->tbl, &b, &res)
 			 : odpg_classify_host(ctx, bd->tbl, &b, &res, 0);
+	/* zero-copy (device_ptrs 2: pinned host buffers the kernel reads and
+	 * writes in place): complete before the results are read and the
+	 * binding can go */
+	if (!rc && device_ptrs == 2)
+		rc = odpg_ctx_sync(ctx);
 
 	LOCK();
 	if (--bd->refs == 0 && bd->stale) {
@@ -1686,6 +1691,13 @@ int odpg_cls_pktio_recv_meta(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *fr
 			     odpg_meta_t *meta)
 {
 	return recv_impl(hdl, ctx, frames, desc, 0, num, 0, out, NULL, meta);
+}
+
+int odpg_cls_pktio_recv_meta_zc(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
+				const odpg_desc_t *desc, uint32_t num, odpg_out_t *out,
+				odpg_meta_t *meta)
+{
+	return recv_impl(hdl, ctx, frames, desc, 0, num, 2, out, NULL, meta);
 }
 
 void odpg_cls_pktio_count(odp_pktio_t hdl, int64_t in_packets, int64_t in_octets,

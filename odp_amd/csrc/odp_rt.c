@@ -110,7 +110,10 @@ typedef struct rt_pktio {
 	rt_queue_t *outq;          /* pktout event queue (QUEUE mode) */
 	pthread_mutex_t ring_lock; /* the loop device's packets in flight */
 	rt_pkt_t *ring_head, *ring_tail;
-	uint8_t *stage;            /* loop packets gathered for one launch */
+	rt_pkt_t *ahead, *ahead_tail;  /* DIRECT mode: received (classified) packets
+				    * beyond what the last odp_pktin_recv asked for */
+	uint8_t *stage;            /* frames gathered for one launch (pinned host) */
+	uint8_t *dstage;           /* its device address: the kernel reads it in place */
 	size_t stage_cap;
 } rt_pktio_t;
 
@@ -125,12 +128,36 @@ static struct {
 	rt_pktio_t pktio[RT_MAX_PKTIO];
 	rt_queue_t *sched;         /* scheduled queues */
 	uint32_t rr;
-	/* poll buffers */
-	odpg_out_t out[RT_BURST];
-	odpg_meta_t meta[RT_BURST];
-	odpg_desc_t desc[RT_BURST];
+	/* poll buffers: pinned host memory the classify launch reads (desc)
+	 * and writes (out, meta) in place, with their device addresses */
+	odpg_out_t *out, *dout;
+	odpg_meta_t *meta, *dmeta;
+	odpg_desc_t *desc, *ddesc;
 } rt = { PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, 0, NULL, {{0}}, {{0}},
-	 NULL, 0, {0}, {{0}}, {{0}} };
+	 NULL, 0, NULL, NULL, NULL, NULL, NULL, NULL };
+
+/* pinned host memory and its device address (zero-copy launch buffers) */
+static int pinned_alloc(size_t bytes, void **host, void **dev)
+{
+	if (odpg_host_alloc_pinned(bytes, host))
+		return -1;
+	if (odpg_host_device_ptr(*host, dev)) {
+		odpg_host_free_pinned(*host);
+		*host = NULL;
+		return -1;
+	}
+	return 0;
+}
+
+static void poll_buffers_free(void)
+{
+	odpg_host_free_pinned(rt.out);
+	odpg_host_free_pinned(rt.meta);
+	odpg_host_free_pinned(rt.desc);
+	rt.out = rt.dout = NULL;
+	rt.meta = rt.dmeta = NULL;
+	rt.desc = rt.ddesc = NULL;
+}
 
 /* ---- init / threads ------------------------------------------------------- */
 /* thread ids: the lowest free id, given back at odp_term_local (odp_thread.c
@@ -162,6 +189,16 @@ int odp_init_global(odp_instance_t *instance, const odp_init_t *param, const voi
 			    "the GPU\n", rc);
 			return -1;
 		}
+		if (pinned_alloc(RT_BURST * sizeof(odpg_out_t), (void **)&rt.out, (void **)&rt.dout) ||
+		    pinned_alloc(RT_BURST * sizeof(odpg_meta_t), (void **)&rt.meta, (void **)&rt.dmeta) ||
+		    pinned_alloc(RT_BURST * sizeof(odpg_desc_t), (void **)&rt.desc, (void **)&rt.ddesc)) {
+			poll_buffers_free();
+			odpg_ctx_destroy(rt.ctx);
+			rt.ctx = NULL;
+			pthread_mutex_unlock(&rt.lock);
+			ERR("no pinned host memory for the receive buffers\n");
+			return -1;
+		}
 		rt.init = 1;
 	}
 	pthread_mutex_unlock(&rt.lock);
@@ -179,6 +216,7 @@ int odp_term_global(odp_instance_t instance)
 	pthread_mutex_lock(&rt.lock);
 	if (rt.init) {
 		odpg_ctx_destroy(rt.ctx);
+		poll_buffers_free();
 		rt.ctx = NULL;
 		rt.init = 0;
 	}
@@ -1721,13 +1759,20 @@ void odpg_rt_pktio_close(odp_pktio_t hdl)
 			odpg_pcap_free(&p->cap);
 		pktio_queue_kill(&p->inq);
 		pktio_queue_kill(&p->outq);
+		for (rt_pkt_t *x = p->ahead; x;) {
+			rt_pkt_t *nx = x->next;
+
+			odp_packet_free((odp_packet_t)x);
+			x = nx;
+		}
+		p->ahead = p->ahead_tail = NULL;
 		while (k) {
 			rt_pkt_t *nx = k->next;
 
 			odp_packet_free((odp_packet_t)k);
 			k = nx;
 		}
-		free(p->stage);
+		odpg_host_free_pinned(p->stage);
 		pthread_mutex_destroy(&p->ring_lock);
 		memset(p, 0, sizeof(*p));
 	}
@@ -1800,6 +1845,23 @@ static void cos_enq(odp_cos_t cos, odp_queue_t q, odp_packet_t run[], int num)
 	}
 }
 
+/* the pktio's pinned staging buffer, at least `need` bytes */
+static int stage_reserve(rt_pktio_t *p, size_t need)
+{
+	uint8_t *b = NULL, *db = NULL;
+
+	if (need <= p->stage_cap)
+		return 0;
+	need = need < (64u << 10) ? (64u << 10) : need;
+	if (pinned_alloc(need, (void **)&b, (void **)&db))
+		return -1;
+	odpg_host_free_pinned(p->stage);
+	p->stage = b;
+	p->dstage = db;
+	p->stage_cap = need;
+	return 0;
+}
+
 /* One burst of the pktio's input through the GPU classifier (loopback_recv,
  * pktio/loop.c:304-374; pcapif_recv_pkt + the same classify step). Packets
  * with a CoS are enqueued on its queue; with the classifier disabled
@@ -1836,17 +1898,10 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 		pthread_mutex_unlock(&p->ring_lock);
 		if (!n)
 			return 0;
-		if (need > p->stage_cap) {
-			uint8_t *b = NULL;
-
-			if (posix_memalign((void **)&b, 64, need)) {
-				for (uint32_t k = 0; k < n; k++)
-					odp_packet_free((odp_packet_t)src[k]);
-				return -1;
-			}
-			free(p->stage);
-			p->stage = b;
-			p->stage_cap = need;
+		if (stage_reserve(p, need)) {
+			for (uint32_t k = 0; k < n; k++)
+				odp_packet_free((odp_packet_t)src[k]);
+			return -1;
 		}
 		for (uint32_t k = 0; k < n; k++) {
 			memcpy(p->stage + off, src[k]->data, src[k]->len);
@@ -1854,8 +1909,9 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 			rt.desc[k].len = src[k]->len;
 			off += ALIGN64(src[k]->len);
 		}
-		frames = p->stage;
 	} else if (p->have_cap) {
+		size_t need = 0, off = 0;
+
 		if (p->pos >= p->cap.num) {
 			/* _pcapif_reopen: loops = 0 repeats forever, else the
 			 * capture is read again while ++loop_cnt < loops */
@@ -1867,12 +1923,26 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 		n = p->cap.num - first < (uint32_t)num ? p->cap.num - first : (uint32_t)num;
 		if (!n)
 			return 0;
-		memcpy(rt.desc, p->cap.desc + first, n * sizeof(odpg_desc_t));
-		frames = p->cap.frames;
+		for (uint32_t k = 0; k < n; k++)
+			need += ALIGN64(p->cap.desc[first + k].len);
+		if (stage_reserve(p, need))
+			return -1;
+		for (uint32_t k = 0; k < n; k++) {
+			const odpg_desc_t d = p->cap.desc[first + k];
+
+			memcpy(p->stage + off, p->cap.frames + d.offset, d.len);
+			rt.desc[k].offset = (uint32_t)off;
+			rt.desc[k].len = d.len;
+			off += ALIGN64(d.len);
+		}
 	} else {
 		return 0;
 	}
-	if (odpg_cls_pktio_recv_meta(hdl, rt.ctx, frames, rt.desc, n, rt.out, rt.meta)) {
+	/* zero-copy: the launch reads the staged frames and descriptors and
+	 * writes the verdicts and metadata in pinned host memory (a burst is a
+	 * few KiB: copies would cost more than the PCIe reads) */
+	frames = p->stage;
+	if (odpg_cls_pktio_recv_meta_zc(hdl, rt.ctx, p->dstage, rt.ddesc, n, rt.dout, rt.dmeta)) {
 		ERR("classify failed\n");
 		if (p->loopdev)
 			for (uint32_t k = 0; k < n; k++)
@@ -2033,10 +2103,38 @@ int odp_pktin_recv(odp_pktin_queue_t queue, odp_packet_t packets[], int num)
 		pthread_mutex_unlock(&rt.poll_lock);
 		return -1;
 	}
-	const int rc = rx_burst(p, queue.pktio, packets, num, &nret);
+	/* one launch classifies everything waiting (up to RT_BURST), as a NIC
+	 * fills its receive ring: what the caller did not ask for is handed out
+	 * by the next calls, in order, without a launch of their own */
+	if (num > 0 && !p->ahead) {
+		odp_packet_t got[RT_BURST];
+		const int rc = rx_burst(p, queue.pktio, got, RT_BURST, &nret);
 
+		if (rc < 0) {
+			pthread_mutex_unlock(&rt.poll_lock);
+			return -1;
+		}
+		for (int k = nret - 1; k >= 0; k--) {
+			rt_pkt_t *x = (rt_pkt_t *)got[k];
+
+			x->next = p->ahead;
+			p->ahead = x;
+			if (!x->next)
+				p->ahead_tail = x;
+		}
+	}
+	nret = 0;
+	while (nret < num && p->ahead) {
+		rt_pkt_t *x = p->ahead;
+
+		p->ahead = x->next;
+		x->next = NULL;
+		packets[nret++] = (odp_packet_t)x;
+	}
+	if (!p->ahead)
+		p->ahead_tail = NULL;
 	pthread_mutex_unlock(&rt.poll_lock);
-	return rc < 0 ? -1 : nret;
+	return nret;
 }
 
 /* per-queue counters: one input / output queue per pktio here, so queue 0

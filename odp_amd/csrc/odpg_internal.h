@@ -113,7 +113,8 @@ typedef struct dcos_s {
 			      * {slot | guard << 8, gate, mask, has chain members},
 			      * not-member words[8] */
 #define XM_HDR_WORDS   16    /* region header: nw, nbits, ngroups, num_xment,
-			      * slot bytes, num_xflat, 0, 0, chain bits[8] */
+			      * slot bytes, num_xflat, key slots the groups read
+			      * (bit mask), 0, chain bits[8] */
 
 /* TBL_XMASK region, after the header and the group descriptors: the part
  * every workgroup copies to LDS (word offsets, each part 16-byte aligned),

@@ -1026,8 +1026,19 @@ int odpg_host_alloc_pinned(size_t bytes, void **ptr)
 	return 0;
 }
 
+int odpg_host_device_ptr(void *host_ptr, void **dev_ptr)
+{
+	if (!host_ptr || !dev_ptr)
+		return -EINVAL;
+	if (hipHostGetDevicePointer(dev_ptr, host_ptr, 0) != hipSuccess)
+		return -EINVAL;
+	return 0;
+}
+
 int odpg_host_free_pinned(void *ptr)
 {
+	if (!ptr)
+		return 0;
 	HIPCHK(hipHostFree(ptr));
 	return 0;
 }

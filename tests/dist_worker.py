@@ -4,6 +4,9 @@ shard, sums the counter block over ranks and gathers the verdicts.
 
     --backend gloo --engine oracle   CPU (runs anywhere)
     --backend gloo --engine gpu      product path on cuda:LOCAL_RANK, gloo collectives
+    --config c2 | c4 | c5            the C2 rules, the C4 1024-PMR rules (limits
+                                     raised before any create, as bench.py does),
+                                     or example/l3fwd over the C5 routes
 """
 import argparse
 import json
@@ -26,13 +29,21 @@ def main():
     ap.add_argument("--npkt", type=int, default=40000)
     ap.add_argument("--engine", default="oracle", choices=["oracle", "gpu"])
     ap.add_argument("--out", required=True)
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"])
     a = ap.parse_args()
     dist.init_process_group("gloo")
+    if a.config == "c5":
+        return main_l3fwd(a)
     rank, world = dist.get_rank(), dist.get_world_size()
     opt = L.PKTIN_IPV4_CHKSUM | L.PKTIN_UDP_CHKSUM | L.PKTIN_TCP_CHKSUM
     cls.reset()
+    if a.config == "c4":
+        assert cls.set_limits(2048, 2048, 32) == 0
     pktio = cls.loop_pktio(pktin=opt)
-    gen.build_c2_rules(cls, pktio, stats=True)
+    if a.config == "c4":
+        gen.build_c4_rules(cls, pktio)
+    else:
+        gen.build_c2_rules(cls, pktio, stats=True)
     assert cls.pktio_start(pktio) == 0
     rules = cls.pktio_rules(pktio)
     # the table image: compiled on rank 0 only and broadcast (bench.py's
@@ -82,6 +93,48 @@ def main():
                        "scatter_gather_equal": bool(np.array_equal(
                            gathered.numpy().astype(np.uint32), allout[:per * world]))}, f)
         np.save(a.out + ".npy", allout)
+    dist.destroy_process_group()
+
+
+def main_l3fwd(a):
+    """example/l3fwd (C5 routes, hash mode) over packet shards: every rank
+    builds the forwarder from the same route list (odpg_fwd_create is a
+    deterministic host compile), forwards its shard, and the ports and
+    rewritten frames are gathered on rank 0"""
+    import torch
+    rank, world = dist.get_rank(), dist.get_world_size()
+    routes = gen.c5_routes()
+    frames = gen.c5_frames(a.npkt, routes, flows=a.npkt).reshape(a.npkt, 64)
+    start, count = shard.shard_range(a.npkt, rank, world)
+    mine = np.ascontiguousarray(frames[start:start + count]).reshape(-1)
+    from odp_amd import gpu
+    if a.engine == "gpu":
+        ndev = max(1, L.lib.odpg_device_count())
+        ctx = gpu.Context(int(os.environ.get("LOCAL_RANK", "0")) % ndev)
+        fw = gpu.Forwarder(ctx, routes, mode=L.FWD_HASH)
+        port, fr = fw.run(mine, 64, count)
+        fr = np.asarray(fr)[:mine.nbytes]
+        del fw
+        ctx.close()
+    else:
+        import oracle
+        port, fr = oracle.l3fwd(gpu.make_routes(routes), gpu.make_fwd_param(L.FWD_HASH, 4),
+                                mine, 64, count)
+    ports = shard.gather_verdicts(np.asarray(port).astype(np.uint32), dist, a.npkt, world)
+    # the rewritten frames: equal-size pieces gathered as int64 words
+    counts = [shard.shard_range(a.npkt, r, world)[1] for r in range(world)]
+    buf = np.zeros((max(counts), 64), np.uint8)
+    buf[:count] = np.asarray(fr, np.uint8).reshape(count, 64)
+    t = torch.from_numpy(buf.view(np.int64).copy())
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    allfr = np.concatenate([p.numpy().view(np.uint8).reshape(-1, 64)[:c]
+                            for p, c in zip(parts, counts)])
+    if rank == 0:
+        with open(a.out, "w") as f:
+            json.dump({"world": world, "n_out": int(len(ports))}, f)
+        np.save(a.out + ".npy", ports.astype(np.int32))
+        np.save(a.out + ".frames.npy", allfr)
     dist.destroy_process_group()
 
 
