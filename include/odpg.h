@@ -292,9 +292,6 @@ int odpg_dev_alloc(odpg_ctx_t *ctx, size_t bytes, void **ptr);
 int odpg_dev_free(odpg_ctx_t *ctx, void *ptr);
 int odpg_host_alloc_pinned(size_t bytes, void **ptr);
 int odpg_host_free_pinned(void *ptr);
-/* The device address of pinned host memory (odpg_host_alloc_pinned): kernels
- * read and write it in place over PCIe (zero-copy; small batches) */
-int odpg_host_device_ptr(void *host_ptr, void **dev_ptr);
 int odpg_memcpy_h2d(odpg_ctx_t *ctx, void *dst, const void *src, size_t bytes);
 int odpg_memcpy_d2h(odpg_ctx_t *ctx, void *dst, const void *src, size_t bytes);
 int odpg_memset_dev(odpg_ctx_t *ctx, void *dst, int value, size_t bytes);

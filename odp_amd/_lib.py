@@ -391,7 +391,14 @@ def _load():
             "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
     lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            # an older experiment build (ODPG_LIB) may lack newer entry
+            # points; the product library must export every one
+            if os.environ.get("ODPG_LIB"):
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     return lib

@@ -104,6 +104,8 @@ struct L64Args {
 	const uint4 *pinfo4;   /* mask groups: {dst | mark << 16, action, rule mask lo, hi} */
 	uint32_t def_mlo, def_mhi;   /* the default CoS's rule mask */
 	uint32_t def_cgmask;
+	uint32_t slot_n;       /* tiles per wave of each CU workgroup slot (4 bits each), 0 = round robin */
+	uint32_t ncu;          /* CUs (workgroups per slot) */
 	uint32_t err_cos;      /* error CoS, or ODPG_COS_NONE */
 	uint32_t err_act;      /* its action */
 	uint32_t def_cos;      /* CoS of error-free packets before the walk */
@@ -327,6 +329,30 @@ odpg_cls64_kernel(const L64Args A)
 	const uint32_t ntiles = (A.num + 63u) >> 6;
 	const uint32_t num = A.num;
 	uint32_t fn[16];
+	/* This wave's tiles: tw0 + k * tws, k < twn. Round robin over the
+	 * waves by default; with slot counts (A.slot_n: 4 bits per workgroup
+	 * slot of a CU, slot = blockIdx / ncu, the order workgroups are
+	 * dispatched in) a wave of slot s runs n_s tiles: the oldest waves on a
+	 * CU win the vector-memory arbitration and finish first, so giving them
+	 * more tiles keeps every wave busy until the end (the drain after the
+	 * last loads). */
+	uint32_t tw0 = gw, tws = nwaves, twn = gw < ntiles ? (ntiles - gw + nwaves - 1u) / nwaves : 0u;
+
+	if (A.slot_n) {
+		const uint32_t wpc = A.ncu * (LBK / 64);           /* waves per slot */
+		const uint32_t sl = blockIdx.x / A.ncu;
+		const uint32_t r = (blockIdx.x - sl * A.ncu) * (LBK / 64) + (threadIdx.x >> 6);
+		uint32_t b0 = 0u;
+
+		for (uint32_t q = 0; q < sl; ++q)
+			b0 += ((A.slot_n >> (4u * q)) & 15u) * wpc;
+		const uint32_t n = (A.slot_n >> (4u * sl)) & 15u;
+
+		tw0 = __builtin_amdgcn_readfirstlane(b0 + r);
+		tws = wpc;
+		/* tiles past the batch are not run */
+		twn = __builtin_amdgcn_readfirstlane(tw0 < ntiles ? min(n, (ntiles - tw0 + wpc - 1u) / wpc) : 0u);
+	}
 
 	MGd mg[NG > 0 ? NG : 1];
 	/* L64_COAL: a tile's 4 KiB arrive as coalesced 16-byte loads, lane l
@@ -382,9 +408,9 @@ odpg_cls64_kernel(const L64Args A)
 	(void)stage;
 	/* the first tile's frames are issued before the table copy below */
 	if (L64_COAL) {
-		load_raw(fn, gw);
+		load_raw(fn, twn ? tw0 : ntiles);
 	} else {
-		const uint32_t n0 = gw < ntiles ? min(num - gw * 64u, 64u) : 0u;
+		const uint32_t n0 = twn ? min(num - tw0 * 64u, 64u) : 0u;
 		const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
 			(void *)(A.frames + (size_t)(gw < ntiles ? gw : 0u) * 256u), 0, (int)(n0 * 64u),
 			0x00020000);
@@ -762,9 +788,8 @@ odpg_cls64_kernel(const L64Args A)
 	uint32_t fb[16];   /* second frame buffer (ping-pong with fn) */
 	bool first = true;
 
-	for (uint32_t t0 = gw; t0 < ntiles;) {
-		const uint32_t left = (ntiles - t0 + nwaves - 1u) / nwaves;
-		const uint32_t nk = left < 64u ? left : 64u;
+	for (uint32_t t0 = tw0, rem = twn; rem;) {
+		const uint32_t nk = rem < 64u ? rem : 64u;
 		uint64_t defer = 0ull;
 
 		if (!first) {
@@ -775,34 +800,34 @@ odpg_cls64_kernel(const L64Args A)
 		}
 		first = false;
 #if L64_PP
-		load_tile(fb, nk > 1u ? t0 + nwaves : NO_TILE);
+		load_tile(fb, nk > 1u ? t0 + tws : NO_TILE);
 		for (uint32_t k = 0; k < nk; k += 2u) {
-			const uint32_t t = t0 + k * nwaves;
+			const uint32_t t = t0 + k * tws;
 
 			if (tile(fn, t))
 				defer |= 1ull << k;
-			load_tile(fn, k + 2u < nk ? t + 2u * nwaves : NO_TILE);
-			if (tile(fb, k + 1u < nk ? t + nwaves : NO_TILE))
+			load_tile(fn, k + 2u < nk ? t + 2u * tws : NO_TILE);
+			if (tile(fb, k + 1u < nk ? t + tws : NO_TILE))
 				defer |= 2ull << k;
-			load_tile(fb, k + 3u < nk ? t + 3u * nwaves : NO_TILE);
+			load_tile(fb, k + 3u < nk ? t + 3u * tws : NO_TILE);
 		}
 #elif L64_COAL
 		for (uint32_t k = 0; k < nk; ++k) {
-			const uint32_t t = t0 + k * nwaves;
+			const uint32_t t = t0 + k * tws;
 
 			stage(fn, fb);
-			load_raw(fn, k + 1u < nk ? t + nwaves : NO_TILE);
+			load_raw(fn, k + 1u < nk ? t + tws : NO_TILE);
 			if (tile(fb, t))
 				defer |= 1ull << k;
 		}
 #else
 		for (uint32_t k = 0; k < nk; ++k) {
-			const uint32_t t = t0 + k * nwaves;
+			const uint32_t t = t0 + k * tws;
 
 #pragma unroll
 			for (int q = 0; q < 16; ++q)
 				fb[q] = fn[q];
-			load_tile(fn, k + 1u < nk ? t + nwaves : NO_TILE);
+			load_tile(fn, k + 1u < nk ? t + tws : NO_TILE);
 			if (tile(fb, t))
 				defer |= 1ull << k;
 		}
@@ -814,7 +839,7 @@ odpg_cls64_kernel(const L64Args A)
 			const uint32_t k = (uint32_t)__builtin_ctzll(defer);
 
 			defer &= defer - 1ull;
-			const uint32_t t = t0 + k * nwaves;
+			const uint32_t t = t0 + k * tws;
 			const uint32_t i = t * 64u + lane;
 			const bool live = i < num;
 			const uint4 *src = A.frames + (size_t)min(i, num - 1u) * 4u;
@@ -898,7 +923,8 @@ odpg_cls64_kernel(const L64Args A)
 			if (live)
 				A.out[i] = w;
 		}
-		t0 += nk * nwaves;
+		t0 += nk * tws;
+		rem -= nk;
 #ifdef L64_EXP_TIMES
 		n_tiles += nk;
 #endif
@@ -1075,6 +1101,32 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 		if (const char *ge = getenv("ODPG_L64_GRID"))
 			grid = (uint32_t)atoi(ge);
 #endif
+		A.slot_n = 0u;
+		A.ncu = 1u;
+		/* ODPG_L64_SLOTS="n0,n1,...": tiles per wave of each CU workgroup
+		 * slot (experiments), used when they cover the batch */
+		static const char *slots_env = getenv("ODPG_L64_SLOTS");
+		int cus = 0;
+
+		if (slots_env && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) == hipSuccess &&
+		    cus > 0 && grid % (uint32_t)cus == 0u && grid / (uint32_t)cus <= 8u) {
+			uint32_t packed = 0u, cover = 0u, ns = 0u;
+
+			for (const char *c = slots_env; *c && ns < grid / (uint32_t)cus; ns++) {
+				const uint32_t v = (uint32_t)atoi(c) & 15u;
+
+				packed |= v << (4u * ns);
+				cover += v;
+				while (*c && *c != ',')
+					c++;
+				if (*c == ',')
+					c++;
+			}
+			if (ns == grid / (uint32_t)cus && (uint64_t)cover * (uint32_t)cus * (lb / 64u) >= ntiles) {
+				A.slot_n = packed;
+				A.ncu = (uint32_t)cus;
+			}
+		}
 		launch(grid);
 	};
 #define L64_LAUNCH_CM(ng, h, c, k)                                                           \

@@ -62,6 +62,8 @@ typedef struct rt_pkt {
 	uint32_t magic;
 	uint32_t len;
 	uint32_t cap;
+	uint32_t ext;              /* data malloc'd on its own (longer than the pool's buffers) */
+	uint32_t pgen;             /* its pool's generation (rt_pool_t.gen) */
 	odp_pool_t pool;
 	odp_cos_t cos;
 	odp_pktio_t input;         /* the pktio it was received on */
@@ -74,8 +76,18 @@ typedef struct rt_pool {
 	int valid;
 	char name[ODP_POOL_NAME_LEN];
 	odp_pool_param_t param;
-	uint32_t in_use;
+	uint32_t in_use;           /* buffers out of the pool (made - free, caches count as out) */
 	pthread_mutex_t lock;
+	/* packet buffers (pool.c's buffer stack + per-thread caches): made in
+	 * chunks on demand up to param.pkt.num, a header and `buf` data bytes
+	 * each, never returned to the system before odp_pool_destroy */
+	uint32_t gen;              /* create count of this slot: thread caches check it */
+	uint32_t buf;              /* data bytes of a pooled buffer */
+	uint32_t made;             /* buffers made (pooled) or allocated (ext) */
+	rt_pkt_t **stack;          /* free pooled buffers */
+	uint32_t nfree;
+	void **chunks;
+	uint32_t nchunks;
 } rt_pool_t;
 
 typedef struct rt_queue {
@@ -247,8 +259,11 @@ int odp_init_local(odp_instance_t instance, odp_thread_type_t type)
 	return 0;
 }
 
+static void tcache_flush(void);
+
 int odp_term_local(void)
 {
+	tcache_flush();
 	if (thr_id < 0)
 		return 0;
 	pthread_mutex_lock(&thr_lock);
@@ -712,11 +727,22 @@ odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param)
 
 		if (p->valid)
 			continue;
+		const uint32_t gen = p->gen;
+
 		memset(p, 0, sizeof(*p));
-		p->valid = 1;
+		p->gen = gen + 1u;
 		snprintf(p->name, sizeof(p->name), "%s", name ? name : "");
 		p->param = *param;
+		/* a pooled buffer holds the pool's packet length (seg_len at
+		 * least); longer packets get their own allocation */
+		p->buf = param->pkt.len > param->pkt.seg_len ? param->pkt.len : param->pkt.seg_len;
+		if (p->buf < 64u)
+			p->buf = 64u;
+		p->stack = malloc((size_t)param->pkt.num * sizeof(rt_pkt_t *));
+		if (!p->stack)
+			break;
 		pthread_mutex_init(&p->lock, NULL);
+		p->valid = 1;
 		ret = (odp_pool_t)(uintptr_t)(i + 1);
 		break;
 	}
@@ -730,8 +756,16 @@ int odp_pool_destroy(odp_pool_t hdl)
 	rt_pool_t *p = get_pool(hdl);
 	int rc = p ? 0 : -1;
 
-	if (p)
+	if (p) {
 		p->valid = 0;
+		for (uint32_t c = 0; c < p->nchunks; c++)
+			free(p->chunks[c]);
+		free(p->chunks);
+		free(p->stack);
+		p->chunks = NULL;
+		p->stack = NULL;
+		p->nchunks = p->nfree = p->made = 0;
+	}
 	pthread_mutex_unlock(&rt.lock);
 	return rc;
 }
@@ -777,36 +811,124 @@ void odp_pool_print_all(void)
 	printf("\n");
 }
 
+#define PKT_HDR ((sizeof(rt_pkt_t) + 63u) & ~(size_t)63u)   /* data offset in a pooled buffer */
+
+/* per-thread buffer caches (pool.c's local cache): a few pools per thread */
+#define TC_POOLS 8
+#define TC_N     64
+static __thread struct {
+	uint32_t pool, gen, n;
+	rt_pkt_t *b[TC_N];
+} tcache[TC_POOLS];
+
+/* a chunk of pooled buffers onto the pool's stack (pool lock held) */
+static int pool_grow_locked(rt_pool_t *p)
+{
+	const uint32_t num = p->param.pkt.num;
+	uint32_t n = num - p->made < 256u ? num - p->made : 256u;
+	const size_t one = PKT_HDR + ((p->buf + 63u) & ~63u);
+
+	if (!n)
+		return -1;
+	uint8_t *c = NULL;
+	void **nc = realloc(p->chunks, (p->nchunks + 1u) * sizeof(void *));
+
+	if (!nc)
+		return -1;
+	p->chunks = nc;
+	if (posix_memalign((void **)&c, 64, one * n))
+		return -1;
+	p->chunks[p->nchunks++] = c;
+	for (uint32_t i = 0; i < n; i++) {
+		rt_pkt_t *k = (rt_pkt_t *)(c + one * i);
+
+		memset(k, 0, sizeof(*k));
+		k->data = (uint8_t *)k + PKT_HDR;
+		k->cap = p->buf;
+		p->stack[p->nfree++] = k;
+	}
+	p->made += n;
+	return 0;
+}
+
+static int tc_slot(odp_pool_t pool, const rt_pool_t *p)
+{
+	const uint32_t id = (uint32_t)(uintptr_t)pool;
+	int freeslot = -1;
+
+	for (int i = 0; i < TC_POOLS; i++) {
+		if (tcache[i].pool == id) {
+			if (tcache[i].gen == p->gen)
+				return i;
+			tcache[i].n = 0;           /* a destroyed pool's buffers */
+			tcache[i].gen = p->gen;
+			return i;
+		}
+		if (!tcache[i].pool && freeslot < 0)
+			freeslot = i;
+	}
+	if (freeslot >= 0) {
+		tcache[freeslot].pool = id;
+		tcache[freeslot].gen = p->gen;
+		tcache[freeslot].n = 0;
+	}
+	return freeslot;
+}
+
+static void pkt_init(rt_pkt_t *k, odp_pool_t pool, uint32_t len)
+{
+	k->magic = PKT_MAGIC;
+	k->pgen = get_pool(pool)->gen;
+	k->pool = pool;
+	k->len = len;
+	k->cos = ODP_COS_INVALID;
+	k->input = ODP_PKTIO_INVALID;
+	memset(&k->meta, 0, sizeof(k->meta));
+	k->meta.l2_offset = k->meta.l3_offset = k->meta.l4_offset = 0xffff;
+	k->next = NULL;
+}
+
 odp_packet_t odp_packet_alloc(odp_pool_t pool, uint32_t len)
 {
 	rt_pool_t *p = get_pool(pool);
-	rt_pkt_t *k;
+	rt_pkt_t *k = NULL;
 
 	if (!p)
 		return ODP_PACKET_INVALID;
-	pthread_mutex_lock(&p->lock);
-	if (p->in_use >= p->param.pkt.num) {
-		pthread_mutex_unlock(&p->lock);
-		return ODP_PACKET_INVALID;
-	}
-	p->in_use++;
-	pthread_mutex_unlock(&p->lock);
-	k = calloc(1, sizeof(*k));
-	if (k)
-		k->data = malloc(len ? len : 1);
-	if (!k || !k->data) {
-		if (k)
-			free(k);
+	const int ts = tc_slot(pool, p);
+
+	if (ts >= 0 && tcache[ts].n) {
+		k = tcache[ts].b[--tcache[ts].n];
+	} else {
 		pthread_mutex_lock(&p->lock);
-		p->in_use--;
+		if (!p->nfree)
+			pool_grow_locked(p);
+		if (p->nfree) {
+			k = p->stack[--p->nfree];
+			/* refill the thread's cache with up to half of it */
+			while (ts >= 0 && p->nfree && tcache[ts].n < TC_N / 2)
+				tcache[ts].b[tcache[ts].n++] = p->stack[--p->nfree];
+		}
+		p->in_use = p->made - p->nfree;
 		pthread_mutex_unlock(&p->lock);
-		return ODP_PACKET_INVALID;
+		if (!k)
+			return ODP_PACKET_INVALID;
 	}
-	k->magic = PKT_MAGIC;
-	k->pool = pool;
-	k->len = len;
-	k->cap = len;
-	k->meta.l2_offset = k->meta.l3_offset = k->meta.l4_offset = 0xffff;
+	if (len > p->buf) {
+		/* longer than the pool's buffers: one of the pool's buffers with
+		 * data of its own */
+		uint8_t *d = malloc(len);
+
+		if (!d) {
+			k->pgen = p->gen;
+			odp_packet_free((odp_packet_t)k);
+			return ODP_PACKET_INVALID;
+		}
+		k->data = d;
+		k->cap = len;
+		k->ext = 1;
+	}
+	pkt_init(k, pool, len);
 	return (odp_packet_t)k;
 }
 
@@ -817,15 +939,47 @@ void odp_packet_free(odp_packet_t pkt)
 
 	if (!k)
 		return;
-	p = get_pool(k->pool);
-	if (p) {
-		pthread_mutex_lock(&p->lock);
-		p->in_use--;
-		pthread_mutex_unlock(&p->lock);
-	}
 	k->magic = 0;
-	free(k->data);
-	free(k);
+	if (k->ext) {
+		free(k->data);
+		k->data = (uint8_t *)k + PKT_HDR;
+		k->ext = 0;
+	}
+	p = get_pool(k->pool);
+	if (!p || p->gen != k->pgen)    /* its pool was destroyed: the memory went with it */
+		return;
+	k->cap = p->buf;
+	const int ts = tc_slot(k->pool, p);
+
+	if (ts >= 0 && tcache[ts].n < TC_N) {
+		tcache[ts].b[tcache[ts].n++] = k;
+		return;
+	}
+	pthread_mutex_lock(&p->lock);
+	p->stack[p->nfree++] = k;
+	/* and half of the thread's cache back */
+	while (ts >= 0 && tcache[ts].n > TC_N / 2)
+		p->stack[p->nfree++] = tcache[ts].b[--tcache[ts].n];
+	p->in_use = p->made - p->nfree;
+	pthread_mutex_unlock(&p->lock);
+}
+
+/* a thread's cached buffers back to their pools (odp_term_local) */
+static void tcache_flush(void)
+{
+	for (int i = 0; i < TC_POOLS; i++) {
+		rt_pool_t *p = tcache[i].pool ? get_pool((odp_pool_t)(uintptr_t)tcache[i].pool) : NULL;
+
+		if (p && p->gen == tcache[i].gen && tcache[i].n) {
+			pthread_mutex_lock(&p->lock);
+			while (tcache[i].n)
+				p->stack[p->nfree++] = tcache[i].b[--tcache[i].n];
+			p->in_use = p->made - p->nfree;
+			pthread_mutex_unlock(&p->lock);
+		}
+		tcache[i].n = 0;
+		tcache[i].pool = 0;
+	}
 }
 
 void odp_packet_free_multi(const odp_packet_t pkt[], int num)

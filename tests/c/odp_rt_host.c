@@ -5,8 +5,9 @@
  * with a shared counter checked between phases (test/validation/api/barrier
  * does the same), thread ids handed out and given back by concurrent
  * odp_init_local / odp_term_local (unique, below ODP_THREAD_COUNT_MAX), named
- * shm reserve / lookup / free (a second free fails cleanly), and the queue
- * registry: create / destroy cycles beyond its slot count, stale handles
+ * shm reserve / lookup / free (a second free fails cleanly), the packet
+ * pool (buffers through per-thread caches, the num limit, long packets,
+ * destroy / re-create with a packet outstanding), and the queue registry: create / destroy cycles beyond its slot count, stale handles
  * refused, scheduled queues created and destroyed while other threads
  * schedule. Prints PASS or the first failure. Run by tests/test_odp_rt.py.
  */
@@ -73,6 +74,32 @@ static void *id_thread(void *arg)
 		CHECK(odp_thread_count() <= NT, "thread count %d", odp_thread_count());
 		__atomic_store_n(&owner[id], 0, __ATOMIC_RELEASE);
 		CHECK(odp_term_local() == 0, "term_local");
+	}
+	return NULL;
+}
+
+/* ---- packet pool: buffers through the per-thread caches ------------------------- */
+static odp_pool_t churn_pool;
+
+static void *pool_thread(void *arg)
+{
+	(void)arg;
+	odp_packet_t held[48];
+
+	for (int it = 0; it < 20000 && !fails; it++) {
+		int n = 0;
+
+		for (; n < 48; n++) {
+			held[n] = odp_packet_alloc(churn_pool, 60 + (n & 7));
+			if (held[n] == ODP_PACKET_INVALID)
+				break;
+			((uint8_t *)odp_packet_data(held[n]))[0] = (uint8_t)n;
+		}
+		for (int k = 0; k < n; k++) {
+			CHECK(((uint8_t *)odp_packet_data(held[k]))[0] == (uint8_t)k &&
+			      odp_packet_len(held[k]) == 60u + (k & 7), "packet %d overwritten", k);
+			odp_packet_free(held[k]);
+		}
 	}
 	return NULL;
 }
@@ -144,6 +171,48 @@ int main(void)
 	CHECK(odp_shm_lookup("blk_a") == ODP_SHM_INVALID, "lookup after free");
 	CHECK(odp_shm_free(b) == 0 && odp_shm_free(b) == -1, "second free of a block");
 	printf("shm: reserve / lookup / free\n");
+
+	/* packet pool: the num limit, buffers shared by threads, long packets,
+	 * destroy / re-create with a packet outstanding */
+	odp_pool_param_t pp;
+
+	odp_pool_param_init(&pp);
+	pp.type = ODP_POOL_PACKET;
+	pp.pkt.num = 1024;
+	pp.pkt.len = 128;
+	pp.pkt.seg_len = 128;
+	churn_pool = odp_pool_create("churn", &pp);
+	CHECK(churn_pool != ODP_POOL_INVALID, "pool create");
+	run(pool_thread, NT);
+	{
+		static odp_packet_t all[1100];
+		int n = 0;
+
+		/* the pool's num, less what the other threads' caches hold */
+		while (n < 1100 && (all[n] = odp_packet_alloc(churn_pool, 64)) != ODP_PACKET_INVALID)
+			n++;
+		CHECK(n <= 1024 && n >= 1024 - NT * 64, "num limit: %d packets", n);
+		odp_packet_free(all[--n]);
+		odp_packet_t big = odp_packet_alloc(churn_pool, 4000);   /* its own data */
+
+		CHECK(big != ODP_PACKET_INVALID && odp_packet_len(big) == 4000u, "long packet");
+		memset(odp_packet_data(big), 1, 4000);
+		CHECK(odp_packet_alloc(churn_pool, 64) == ODP_PACKET_INVALID, "num limit with a long packet");
+		odp_packet_free(big);
+		for (int k = 0; k < n; k++)
+			odp_packet_free(all[k]);
+		odp_packet_t stale = odp_packet_alloc(churn_pool, 64);
+
+		CHECK(odp_pool_destroy(churn_pool) == 0, "pool destroy");
+		churn_pool = odp_pool_create("churn2", &pp);
+		odp_packet_free(stale);                 /* its pool is gone: ignored */
+		odp_packet_t fresh = odp_packet_alloc(churn_pool, 64);
+
+		CHECK(fresh != ODP_PACKET_INVALID && fresh != stale, "re-created pool hands out its own");
+		odp_packet_free(fresh);
+		CHECK(odp_pool_destroy(churn_pool) == 0, "pool destroy 2");
+	}
+	printf("pool: %d threads x 20000 x 48 alloc/free, limits, re-create\n", NT);
 
 	/* queue registry: more create / destroy cycles than slots */
 	odp_queue_t first = odp_queue_create("q", NULL), q = first;

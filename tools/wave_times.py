@@ -56,13 +56,14 @@ def main():
     L.check(L.lib.odpg_diag_l64_times(raw.ctypes.data_as(C.c_void_p), 65536), "times")
     raw = raw.reshape(-1, 2)
     used = raw[:, 0] != 0
+    gws = np.nonzero(used)[0]
     st = raw[used, 0].astype(np.int64)
     en = (raw[used, 1] & ((1 << 48) - 1)).astype(np.int64)
     tiles = (raw[used, 1] >> 48).astype(np.int64)
     # only the last launch: the waves whose start lies within the last launch
     t0 = st.max() - 20000
     last = st >= t0
-    st, en, tiles = st[last], en[last], tiles[last]
+    st, en, tiles, gws = st[last], en[last], tiles[last], gws[last]
     base = st.min()
     out = {"config": a.config, "counted": a.counted, "waves": int(len(st)),
            "kernel_span_us": round((en.max() - base) / 100.0, 3),
@@ -75,6 +76,18 @@ def main():
         out["by_tiles"][int(k)] = {"waves": int(m.sum()),
                                    "end_us_p50": round(float(np.median(en[m] - base)) / 100.0, 3),
                                    "end_us_max": round(float((en[m] - base).max()) / 100.0, 3)}
+    # by XCD (workgroups go round-robin over the 8 XCDs) and by dispatch
+    # order (wave index eighths)
+    wpg = int(os.environ.get("ODPG_WAVES_PER_WG", "4"))
+    xcd = (gws // wpg) % 8
+    out["end_us_p50_by_xcd"] = [round(float(np.median(en[xcd == x] - base)) / 100.0, 3)
+                                for x in range(8)]
+    order = np.argsort(gws)
+    eighths = [slice(len(order) * k // 8, len(order) * (k + 1) // 8) for k in range(8)]
+    out["end_us_p50_by_gw_eighth"] = [round(float(np.median((en[order] - base)[e])) / 100.0, 3)
+                                      for e in eighths]
+    out["start_us_p50_by_gw_eighth"] = [round(float(np.median((st[order] - base)[e])) / 100.0, 3)
+                                        for e in eighths]
     # busy waves over time (10 ns bins): the drain's shape
     hist = []
     for t in range(0, int(en.max() - base) + 1, 50):
