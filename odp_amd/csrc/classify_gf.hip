@@ -47,9 +47,17 @@
 #ifndef GF_BLOCK            /* threads per workgroup */
 #define GF_BLOCK 256
 #endif
-#ifndef GF_WAVES            /* waves per SIMD the launch bounds ask for */
-#define GF_WAVES 5
+#ifndef GF_WAVES            /* waves per SIMD the launch bounds ask for: */
+#define GF_WAVES 5          /* verdict-only launches with 2-word hit maps */
 #endif
+#ifndef GF_WAVES_WIDE       /* wider hit maps, counted launches (C3: 100.7 vs */
+#define GF_WAVES_WIDE 4     /* 106.0 us at 5, whose VGPR budget spills) */
+#endif
+#define GF_WAVES_OF(cm, nw) ((cm) == 0 && (nw) == 2 ? GF_WAVES : GF_WAVES_WIDE)
+#ifndef GF_ZERO_MIN         /* hit maps of >= this many words: an entry's map read */
+#define GF_ZERO_MIN 2       /* after its value matched (else with it; C2x 45.1 vs */
+#endif                      /* 46.1 us, C3 106.0 vs 110.2 us) */
+#define GF_ZERO(nw) ((nw) >= GF_ZERO_MIN)
 #ifndef GF_RW               /* LDS row stride per lane, dwords (16-byte multiple) */
 #define GF_RW 20
 #endif
@@ -62,17 +70,16 @@ struct GFArgs {
 	uint32_t num;
 	uint32_t stride;            /* fixed-stride batch (descs unused), or 0 */
 	uint32_t opt;               /* ODPG_PKTIN_* (all defined bits are < 32) */
-	uint32_t nwg;               /* walk groups */
-	const uint2 *cinfo;         /* {rule_start | nrule << 16, action | ...} */
-	const uint32_t *pinfo;      /* dst | mark << 16 */
-	uint32_t num_cos, num_pmr;
+	uint32_t ngroups;           /* hit-map groups (descriptors in xmg) */
+	uint32_t num_cos;
 	int32_t default_cos, error_cos;
 	const dcos_t *coses;
-	const uint32_t *xm_rest;    /* TBL_XMASK: masks[num_xment][XM_WORDS], values, slot bytes */
-	uint32_t num_xment, xm_slot_bytes, num_xflat;
-	const uint32_t *xfc;        /* per CoS: first flat complex term | count << 16 */
-	uint32_t upf;               /* complex PMRs evaluated up front into the hit map */
+	const uint32_t *xlds;       /* the table's LDS part (xm_layout_t) */
+	xm_layout_t L;
+	const uint32_t *xfc;        /* lazy form: per CoS first complex record | count << 16 */
+	uint32_t num_xflat;         /* lazy form: complex records */
 	const odpg_cnt_dev *cnt;    /* CM 2: the sharded counters' layout */
+	uint32_t cnt_words;         /* CM 2: words of a counter row */
 };
 
 /* sharded-counter histogram bins before the CoS bins (CM 2) */
@@ -83,6 +90,8 @@ struct GFArgs {
 #define GF_BIN_EXTRA  4u
 
 typedef unsigned short gf_us2 __attribute__((ext_vector_type(2)));
+/* key slots 0..15 of a packet, indexed by a wave-uniform slot (v_movrels) */
+typedef uint32_t gf_kv_t __attribute__((ext_vector_type(16)));
 
 /* acc + w.lo * x.lo16 + w.hi * x.hi16 (one v_dot2_u32_u16) */
 __device__ __forceinline__ uint32_t gd2(uint32_t x, uint32_t w, uint32_t acc)
@@ -110,18 +119,37 @@ __device__ __forceinline__ uint32_t wb(const uint32_t (&f)[16])
 	return fw<K>(f);
 }
 
-/* The frames the register parse takes: Eth (no SNAP / VLAN) then IPv4 with
- * IHL 5 and tot_len within the frame, or IPv6 without extension headers and
- * payload within the frame; then UDP with length >= 8 (IPv6: not port 4500,
- * whose IPsec marker lies past the window) or TCP with data offset >= 5 and
- * its 20 header bytes inside the frame; frame length >= 64. x16 is the
- * frame's dword at byte 64 (the IPv6 TCP data-offset byte). */
-__device__ __forceinline__ bool plain_gf(const uint32_t (&f)[16], uint32_t x16, uint32_t len)
+/* Tag dwords of a frame (0 untagged; 1 one VLAN tag, or a QinQ outer tag
+ * alone; 2 a QinQ outer tag and a VLAN tag) and whether the outer one is a
+ * QinQ tag, as _odp_parse_eth walks them (odp_parse.c:23-106: an 0x88A8 tag,
+ * then an 0x8100 tag). */
+__device__ __forceinline__ uint32_t tag_dwords(const uint32_t (&f)[16], bool &qinq)
+{
+	const uint32_t e0 = f[3] & 0xffffu;
+
+	qinq = e0 == 0xa888u;
+	if (qinq)
+		return (f[4] & 0xffffu) == 0x0081u ? 2u : 1u;
+	return e0 == 0x0081u ? 1u : 0u;
+}
+
+/* The frames the register parse takes, on the tag-shifted window (g[k] =
+ * frame dword k + sh for k >= 3, so the L3 header sits at byte 14 as in an
+ * untagged frame; x16 stands in for the dword past the window): Eth (no
+ * SNAP) with up to two tags, then IPv4 with IHL 5 and tot_len within the
+ * frame, or IPv6 (at most one tag) without extension headers and payload
+ * within the frame; then UDP with length >= 8 (IPv6: not port 4500, whose
+ * IPsec marker lies past the window) or TCP with data offset >= 5 and its
+ * 20 header bytes inside the frame (IPv6: untagged); frame length >= 64.
+ * x16 is the frame's dword at byte 64 (the IPv6 TCP data-offset byte). */
+__device__ __forceinline__ bool plain_gf(const uint32_t (&f)[16], uint32_t x16, uint32_t len,
+					 uint32_t sh)
 {
 	const uint32_t et = f[3] & 0xffffu;
 	const uint32_t vb = (f[3] >> 16) & 0xffu;
 	const bool v4 = et == 0x0008u && vb == 0x45u;
-	const bool v6 = et == 0xdd86u && (vb & 0xf0u) == 0x60u;
+	const bool v6 = et == 0xdd86u && (vb & 0xf0u) == 0x60u && sh <= 1u;
+	const uint32_t l3 = 14u + 4u * sh;
 
 	if (len < 64u || !(v4 || v6))
 		return false;
@@ -129,7 +157,7 @@ __device__ __forceinline__ bool plain_gf(const uint32_t (&f)[16], uint32_t x16, 
 		const uint32_t tot_len = swap16(f[4] & 0xffffu);
 		const uint32_t proto = f[5] >> 24;
 
-		if (tot_len > len - 14u)
+		if (tot_len > len - l3)
 			return false;
 		if (proto == 0x11u)
 			return swap16(f[9] >> 16) >= 8u;
@@ -140,20 +168,23 @@ __device__ __forceinline__ bool plain_gf(const uint32_t (&f)[16], uint32_t x16, 
 	const uint32_t payload = swap16(f[4] >> 16);
 	const uint32_t nh = f[5] & 0xffu;
 
-	if (payload + 40u > len - 14u)
+	if (payload + 40u > len - l3)
 		return false;
 	if (nh == 0x11u)
 		return swap16(f[14] >> 16) >= 8u && swap16(f[14] & 0xffffu) != 4500u;
 	if (nh == 0x06u)
-		return len >= 74u && ((x16 >> 20) & 0xfu) >= 5u;
+		return sh == 0u && len >= 74u && ((x16 >> 20) & 0xfu) >= 5u;
 	return false;
 }
 
-/* parse_common() of a plain_gf() frame from its window registers: returns
- * 0 / 1 (error flagged) or PARSE_PEND with the UDP / TCP checksum left for
- * the tail bytes [64, len) (pd: the pseudo header + window part) */
+/* parse_common() of a plain_gf() frame from its tag-shifted window
+ * registers: returns 0 / 1 (error flagged) or PARSE_PEND with the UDP / TCP
+ * checksum left for the tail bytes [64, len) (pd: the pseudo header + window
+ * part). s14 / s15: g[14] / g[15] as the window sums take them (zero where
+ * they hold bytes past the frame's byte 64, which the tail pass sums). */
 __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t (&f)[16],
-					     uint32_t len, uint32_t opt)
+					     uint32_t s14, uint32_t s15, uint32_t len, uint32_t opt,
+					     uint32_t sh, bool qinq)
 {
 	const bool v6 = (f[3] & 0xffffu) == 0xdd86u;
 	uint64_t inf = IF(IFL_L2) | IF(IFL_ETH) | IF(IFL_L3) | IF(IFL_L4) |
@@ -161,7 +192,11 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 	uint32_t fl = 0u;
 
 	p.l2 = 0u;
-	p.l3 = 14u;
+	p.l3 = 14u + 4u * sh;
+	if (sh)
+		inf |= IF(IFL_VLAN);
+	if (qinq)
+		inf |= IF(IFL_VLAN_QINQ);
 	if (len > 1514u)
 		inf |= IF(IFL_JUMBO);
 	if (f[0] & 0x1u)
@@ -204,12 +239,13 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 		pseudo = gd2(f[8], GW10, gd2(f[7], GW11, gd2(f[6], GW01, 0u)));   /* bytes 26..33 */
 		win = gd2(f[8], GW01, 0u);                                      /* bytes 34..63 */
 #pragma unroll
-		for (int k = 9; k < 16; ++k)
+		for (int k = 9; k < 14; ++k)
 			win = gd2(f[k], GW11, win);
+		win = gd2(s15, GW11, gd2(s14, GW11, win));
 		ulen_raw = f[9] >> 16;
 		csum_raw = f[10] & 0xffffu;
 		dport = swap16(f[9] & 0xffffu);
-		p.l4 = 34u;
+		p.l4 = p.l3 + 20u;
 	} else {
 		/* parse_ipv6 (odp_parse.c:179-245), no extension header */
 		if (((f[9] >> 16) & 0xffu) == 0xffu)
@@ -220,11 +256,11 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 		for (int k = 6; k < 13; ++k)
 			pseudo = gd2(f[k], GW11, pseudo);
 		pseudo = gd2(f[13], GW10, pseudo);
-		win = gd2(f[15], GW11, gd2(f[14], GW11, gd2(f[13], GW01, 0u)));   /* bytes 54..63 */
+		win = gd2(s15, GW11, gd2(s14, GW11, gd2(f[13], GW01, 0u)));     /* bytes 54..63 */
 		ulen_raw = f[14] >> 16;
 		csum_raw = f[15] & 0xffffu;
 		dport = swap16(f[14] & 0xffffu);
-		p.l4 = 54u;
+		p.l4 = p.l3 + 40u;
 	}
 	bool need = false;
 	uint32_t sum = 0u;
@@ -445,12 +481,35 @@ __device__ __forceinline__ void gf_sweep(const uint8_t *frames, uint2 d, uint32_
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 }
 
-/* CM: counters of the launch, 0 none, 2 sharded counter rows (odpg.h) */
-template <int CM>
-__global__ __launch_bounds__(GF_BLOCK) __attribute__((amdgpu_waves_per_eu(GF_WAVES))) void
-odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__restrict__ xmg,
-		  const uint4 *__restrict__ xf, const odpg_desc_t *__restrict__ descs,
-		  odpg_out_t *__restrict__ out)
+/* the hit map's NW words of entry e (NW 2: one ds_read_b64; 4: one
+ * ds_read_b128; 8: two) */
+template <int NW>
+__device__ __forceinline__ void xm_entry(const uint32_t *xmm, uint32_t e, uint32_t (&m)[NW])
+{
+	if constexpr (NW == 2) {
+		const uint2 x = *(const uint2 *)(xmm + 2u * e);
+
+		m[0] = x.x;
+		m[1] = x.y;
+	} else {
+#pragma unroll
+		for (int q = 0; q < NW; q += 4) {
+			const uint4 x = *(const uint4 *)(xmm + NW * e + q);
+
+			m[q] = x.x;
+			m[q + 1] = x.y;
+			m[q + 2] = x.z;
+			m[q + 3] = x.w;
+		}
+	}
+}
+
+/* CM: counters of the launch, 0 none, 2 sharded counter rows (odpg.h);
+ * NW: hit-map words per packet (the table's rule bits, 2 / 4 / 8 x 32) */
+template <int CM, int NW>
+__global__ __launch_bounds__(GF_BLOCK) __attribute__((amdgpu_waves_per_eu(GF_WAVES_OF(CM, NW)))) void
+odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t *__restrict__ xhdr,
+		  const odpg_desc_t *__restrict__ descs, odpg_out_t *__restrict__ out)
 {
 	/* read-only tables as restrict kernel arguments: their wave-uniform
 	 * reads compile to scalar loads */
@@ -464,22 +523,26 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 	 * counters"): four bins, then one per CoS */
 	uint32_t *dlv = smem + GF_BLOCK * RW;
 	const uint32_t nbins = CM == 2 ? ((A.num_cos + GF_BIN_EXTRA + 3u) & ~3u) : 0u;
+	/* the table's LDS part (odpg_internal.h xm_layout_t): entry bit maps,
+	 * their values, the groups' slot bytes, per CoS {bit range, action},
+	 * per rule bit {dst | mark << 16, the destination's bit range, the
+	 * destination's complex records (lazy form): first | count << 16, 0},
+	 * the lazy form's complex records {gate, mask, value, slot | guard end <<
+	 * 8 | absolute << 30 | guarded << 31}, {pmr bit, last record of its
+	 * chain, that record's index, 0} */
 	uint32_t *tb = dlv + nbins;
-	/* hit-map entries (2 x uint4 each), their values, the slot bytes */
-	uint4 *xmm = (uint4 *)tb;
-	uint32_t *xmv = tb + XM_WORDS * A.num_xment;
-	uint8_t *xms = (uint8_t *)(xmv + ((A.num_xment + 3u) & ~3u));
-	uint2 *cinfo = (uint2 *)(xms + A.xm_slot_bytes);
-	/* per PMR {dst | mark << 16, the destination's rule_start | nrule << 16,
-	 * the destination's complex terms: first | count << 16, 0}: one LDS read
-	 * per walk level */
-	uint4 *pdst = (uint4 *)(cinfo + ((A.num_cos + 1u) & ~1u));
-	/* the complex PMRs' terms, per CoS in rule order (cls_compile.cpp
-	 * "xflat"): {gate, mask, value, slot | guard end << 8 | absolute << 30 |
-	 * guarded << 31}, {pmr, last record of its chain, that record's index, 0} */
-	uint4 *xfl = pdst + A.num_pmr;
+	const uint32_t *xmm = tb + A.L.masks;
+	const uint32_t *xmv = tb + A.L.values;
+	const uint8_t *xms = (const uint8_t *)(tb + A.L.slots);
+	const uint2 *xci = (const uint2 *)(tb + A.L.xci);
+	const uint4 *pdst = (const uint4 *)(tb + A.L.xpd);
+	const uint4 *xfl = (const uint4 *)(tb + A.L.xflat);
+	/* CM 2: the workgroup's counter row as it stood before this launch
+	 * (read at the start; the flush stores row + histogram) */
+	unsigned long long *base = (unsigned long long *)(tb + ((A.L.lds_words + 1u) & ~1u));
 	/* GF_SWEEP: the wave's x16 words and tail partials (2 x 64 dwords) */
-	uint32_t *swx = (uint32_t *)(xfl + 2u * A.num_xflat) + (threadIdx.x >> 6) * 128u;
+	uint32_t *swx = tb + ((A.L.lds_words + 1u) & ~1u) + (CM == 2 ? 2u * A.cnt_words : 0u) +
+			(threadIdx.x >> 6) * 128u;
 
 	const uint32_t lane = __lane_id();
 	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (GF_BLOCK / 64) +
@@ -539,25 +602,8 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 		tn = early_tails(dn, gw);
 	dnn = load_desc(gw + nwaves);
 
-	{
-		const uint32_t nm = XM_WORDS * A.num_xment;
-
-		for (uint32_t k = threadIdx.x; k < nm; k += GF_BLOCK)
-			tb[k] = A.xm_rest[k];
-		for (uint32_t k = threadIdx.x; k < A.num_xment; k += GF_BLOCK)
-			xmv[k] = A.xm_rest[nm + k];
-		for (uint32_t k = threadIdx.x; k < A.xm_slot_bytes / 4u; k += GF_BLOCK)
-			((uint32_t *)xms)[k] = A.xm_rest[nm + A.num_xment + k];
-	}
-	for (uint32_t k = threadIdx.x; k < A.num_cos; k += GF_BLOCK)
-		cinfo[k] = A.cinfo[k];
-	for (uint32_t k = threadIdx.x; k < A.num_pmr; k += GF_BLOCK) {
-		const uint32_t pi = A.pinfo[k];
-
-		pdst[k] = make_uint4(pi, A.cinfo[pi & 0xffffu].x, A.xfc[pi & 0xffffu], 0u);
-	}
-	for (uint32_t k = threadIdx.x; k < 2u * A.num_xflat; k += GF_BLOCK)
-		xfl[k] = xf[k];
+	for (uint32_t k = threadIdx.x; k < A.L.lds_words; k += GF_BLOCK)
+		tb[k] = A.xlds[k];
 	/* CM 2: the counter layout is read now, not behind the tile loop's
 	 * last wait; the workgroup's last wave to finish flushes the histogram */
 	__shared__ uint32_t waves_done;
@@ -566,6 +612,11 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 
 	if constexpr (CM == 2) {
 		C = *A.cnt;
+		const unsigned long long *r0 =
+			(const unsigned long long *)(C.rows + (size_t)blockIdx.x * C.words);
+
+		for (uint32_t k = threadIdx.x; k < C.words; k += GF_BLOCK)
+			base[k] = r0[k];
 		for (uint32_t k = threadIdx.x; k < nbins; k += GF_BLOCK)
 			dlv[k] = 0u;
 		if (threadIdx.x == 0u) {
@@ -577,10 +628,21 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 
 	__syncthreads();
 
-	const uint32_t nwg = A.nwg;
+	const uint32_t ngroups = A.ngroups;
 	const uint32_t opt = A.opt;
 	const bool def_valid = A.default_cos >= 0 && A.coses[A.default_cos].valid;
 	const bool def_rules = def_valid && A.coses[A.default_cos].nrule != 0u;
+	/* the chain bits (they start set, groups clear them), uniform */
+	uint32_t chain[NW];
+	/* the key slots the groups read, the groups without chain records,
+	 * the zero entry */
+	const uint32_t kslots = xhdr[6];
+	const uint32_t ngor = xhdr[7];
+	const uint32_t zent = xhdr[3];
+
+#pragma unroll
+	for (int w = 0; w < NW; ++w)
+		chain[w] = xhdr[8 + w];
 
 	for (uint32_t t = gw; t < ntiles; t += nwaves) {
 		const uint32_t i = t * 64u + lane;
@@ -605,7 +667,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 				f[q + 3] = x.w;
 			}
 			x16 = swx[lane];
-		} else {
+		} else if (__ballot(live && len < 64u)) {
 #pragma unroll
 			for (int q = 0; q < 16; ++q) {
 				/* bytes past the frame read as zero (the reference's
@@ -614,6 +676,12 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 
 				f[q] = nb >= 4 ? fn[q] : nb <= 0 ? 0u : fn[q] & ((1u << (8 * nb)) - 1u);
 			}
+		} else {
+			/* no live frame shorter than the window (dead lanes' bytes
+			 * are never used) */
+#pragma unroll
+			for (int q = 0; q < 16; ++q)
+				f[q] = fn[q];
 		}
 		dn = dnn;
 
@@ -621,18 +689,39 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 		Prs p;
 		L4Pend pd = {0u, 0u, 0u, 0u};
 		int ret = 0;
-		const bool fastw = __ballot(live && !plain_gf(f, x16, len)) == 0ull;
 		Bases b;
-		uint32_t hm[XM_WORDS];
+		uint32_t hm[NW];
 
 		p.inf = 0ull;
 		p.fl = 0u;
 		p.l2 = p.l3 = p.l4 = 0xffffu;
-		/* the LDS row: the generic parse's window, and the complex rules'
-		 * key reads on any wave */
+		/* the LDS row: the generic parse's window, and the key reads of
+		 * the generic waves (unshifted frame bytes) */
 #pragma unroll
 		for (int q = 0; q < 16; q += 4)
 			*(uint4 *)(row + q) = make_uint4(f[q], f[q + 1], f[q + 2], f[q + 3]);
+		/* VLAN / QinQ frames: the window shifted by the tag dwords, so that
+		 * the register parse reads their L3 / L4 headers at the untagged
+		 * offsets; the L2 words and the VLAN tag are read from u3..u5 */
+		const uint32_t u3 = f[3], u4 = f[4], u5 = f[5];
+		bool qinq = false;
+		const uint32_t sh = live ? tag_dwords(f, qinq) : 0u;
+		uint32_t s14 = f[14], s15 = f[15];
+
+		if (__ballot(sh != 0u)) {
+#pragma unroll
+			for (int k = 3; k < 16; ++k) {
+				const uint32_t n1 = k + 1 < 16 ? f[k + 1] : x16;
+				const uint32_t n2 = k + 2 < 16 ? f[k + 2] : k + 2 == 16 ? x16 : 0u;
+
+				f[k] = sh == 0u ? f[k] : sh == 1u ? n1 : n2;
+			}
+			/* the bytes past the frame's byte 64 are the tail pass's */
+			s14 = sh == 2u ? 0u : f[14];
+			s15 = sh != 0u ? 0u : f[15];
+		}
+		const bool fastw = __ballot(live && !plain_gf(f, x16, len, sh)) == 0ull;
+
 		auto bases = [&]() {
 			b.l2 = p.l2;
 			b.l3 = p.l3;
@@ -641,133 +730,42 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 			b.len = len;
 			b.inf_lo = (uint32_t)p.inf;
 		};
-		/* the hit map: each walk group's masked key word, once per packet,
-		 * its entry's PMR map ORed in (a level of the walk only changes the
-		 * CoS, i.e. the rule range the map is scanned in) */
-		auto keys = [&](auto key) {
-			const bool on = live && (p.fl & FL_ERROR_MASK) == 0u;
+		/* the packet's key slots (odpg_internal.h "key slots"), extracted
+		 * once: slots 0..15 in a register vector the groups index by their
+		 * uniform slot, 16 / 17 (L4) and 18 (length) beside it */
+		gf_kv_t kv = {};
+		uint32_t k16 = 0u, k17 = 0u;
 
-#pragma unroll
-			for (uint32_t w = 0; w < XM_WORDS; ++w)
-				hm[w] = 0u;
-			if (!__ballot(on))
-				return;
-#ifdef GF_EXP_NOHM   /* experiment builds only: cost without the hit map */
-			if (A.num != 12345u)
-				return;
-#endif
-#pragma unroll 4
-			for (uint32_t gi = 0; gi < nwg; ++gi) {
-				{
-					const uint4 g0 = wg[2u * gi];
-					const uint32_t gslot = __builtin_amdgcn_readfirstlane(g0.x);
-					const uint32_t greq = __builtin_amdgcn_readfirstlane(g0.y);
-					const uint32_t gmask = __builtin_amdgcn_readfirstlane(g0.z);
-
-					if (on && (b.inf_lo & greq) == greq) {
-						const uint32_t kv = key(gslot) & gmask;
-
-						{
-							const uint4 xg = xmg[gi];
-							const uint32_t mul = __builtin_amdgcn_readfirstlane(xg.x);
-							const uint32_t sh = __builtin_amdgcn_readfirstlane(xg.y);
-							const uint32_t soff = __builtin_amdgcn_readfirstlane(xg.z);
-							const uint32_t eb = __builtin_amdgcn_readfirstlane(xg.w);
-							const uint32_t si = xms[soff + ((kv * mul) >> sh)];
-
-							if (si != 0xffu && xmv[eb + si] == kv) {
-								const uint4 m0 = xmm[2u * (eb + si)];
-								const uint4 m1 = xmm[2u * (eb + si) + 1u];
-
-								hm[0] |= m0.x;
-								hm[1] |= m0.y;
-								hm[2] |= m0.z;
-								hm[3] |= m0.w;
-								hm[4] |= m1.x;
-								hm[5] |= m1.y;
-								hm[6] |= m1.z;
-								hm[7] |= m1.w;
-							}
-						}
-					}
-				}
-			}
-			/* up front (A.upf): every complex PMR's chains once per packet,
-			 * in a wave-uniform loop over the flat records (one LDS
-			 * broadcast per record, the key word by uniform slot), a match
-			 * setting the PMR's bit in the hit map; the walk then needs no
-			 * complex-rule evaluation at any level */
-			if (A.upf) {
-				bool acc = on;
-
-#pragma unroll 4
-				for (uint32_t j = 0; j < A.num_xflat; ++j) {
-					/* the records from global memory at a uniform index:
-					 * scalar loads straight into SGPRs */
-					const uint4 r = xf[2u * j];
-					const uint4 q = xf[2u * j + 1u];
-					const uint32_t rx = r.x, ry = r.y, rz = r.z, rw = r.w;
-					const uint32_t qx = q.x, qy = q.y, qz = q.z;
-
-					acc = acc && (b.inf_lo & rx) == rx &&
-					      (!(rw >> 31) ||
-					       b.len > ((rw >> 30) & 1u ? 0u : b.l3) + ((rw >> 8) & 0xffffu)) &&
-					      (key(rw & 0xffu) & ry) == rz;
-					if (qy) {
-						const uint32_t bit = acc ? 1u << (qx & 31u) : 0u;
-
-						switch (qx >> 5) {
-						case 0: hm[0] |= bit; break;
-						case 1: hm[1] |= bit; break;
-						case 2: hm[2] |= bit; break;
-						case 3: hm[3] |= bit; break;
-						case 4: hm[4] |= bit; break;
-						case 5: hm[5] |= bit; break;
-						case 6: hm[6] |= bit; break;
-						default: hm[7] |= bit; break;
-						}
-						acc = on;
-					} else if (!__ballot(acc)) {      /* the chain failed everywhere */
-						j = qz;
-						acc = on;
-					}
-				}
-			}
-		};
 #ifdef GF_EXP_NOGEN
 		if (true) {
 #else
 		if (fastw) {
 #endif
 			if (live)
-				ret = parse_fast_gf(p, pd, f, len, opt);
+				ret = parse_fast_gf(p, pd, f, s14, s15, len, opt, sh, qinq);
 			bases();
 			const bool v6 = (b.inf_lo & (uint32_t)IF(IFL_IPV6)) != 0u;
 			const bool l4ok = b.l4 != 0xffffu;
 
-			keys([&](uint32_t slot) -> uint32_t {   /* slot wave-uniform */
-				switch (slot) {
-				case 0: return f[0];
-				case 1: return f[1];
-				case 2: return f[2];
-				case 3: return f[3];
-				case 4: return f[4];
-				case 5: return wb<14>(f);
-				case 6: return wb<14>(f);
-				case 7: return wb<18>(f);
-				case 8: return wb<22>(f);
-				case 9: return wb<26>(f);
-				case 10: return wb<30>(f);
-				case 11: return wb<34>(f);
-				case 12: return wb<38>(f);
-				case 13: return wb<42>(f);
-				case 14: return wb<46>(f);
-				case 15: return wb<50>(f);
-				case 16: return !l4ok ? 0u : v6 ? wb<54>(f) : wb<34>(f);
-				case 17: return !l4ok ? 0u : v6 ? wb<58>(f) : wb<38>(f);
-				default: return len;
-				}
-			});
+			kv[0] = f[0];
+			kv[1] = f[1];
+			kv[2] = f[2];
+			kv[3] = u3;
+			kv[4] = u4;
+			/* the innermost VLAN tag */
+			kv[5] = qinq ? __builtin_amdgcn_alignbyte(u5, u4, 2) : __builtin_amdgcn_alignbyte(u4, u3, 2);
+			kv[6] = wb<14>(f);
+			kv[7] = wb<18>(f);
+			kv[8] = wb<22>(f);
+			kv[9] = wb<26>(f);
+			kv[10] = wb<30>(f);
+			kv[11] = wb<34>(f);
+			kv[12] = wb<38>(f);
+			kv[13] = wb<42>(f);
+			kv[14] = wb<46>(f);
+			kv[15] = wb<50>(f);
+			k16 = !l4ok ? 0u : v6 ? wb<54>(f) : wb<34>(f);
+			k17 = !l4ok ? 0u : v6 ? wb<58>(f) : wb<38>(f);
 		} else {
 			Pkt<64, true> v;
 
@@ -783,7 +781,92 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 			key.v = &v;
 			key.b = &b;
 			key.fast = false;
-			keys(key);
+			/* the slots the groups read (uniform mask) */
+#pragma unroll
+			for (uint32_t sl = 0; sl < 16u; ++sl)
+				if ((kslots >> sl) & 1u)
+					kv[sl] = key(sl);
+			if ((kslots >> 16) & 1u)
+				k16 = key(16u);
+			if ((kslots >> 17) & 1u)
+				k17 = key(17u);
+		}
+		/* the hit map: each group's masked key word, once per packet.
+		 * Single-word rules OR their bits in; a complex rule's chain bit
+		 * (set to start with) stays set only while every group holding one
+		 * of its records has it in the entry for the packet's key. The
+		 * groups without chain records come first (xhdr[7] of them), each
+		 * kind in a loop of its own */
+		{
+			const bool on = live && (p.fl & FL_ERROR_MASK) == 0u;
+
+#pragma unroll
+			for (int w = 0; w < NW; ++w)
+				hm[w] = on ? chain[w] : 0u;
+			/* a group's probe: the masked key word hashed to the group's
+			 * slot byte, the entry's value compared; m = the entry's bit
+			 * map on a hit, zero on a miss */
+			auto probe = [&](uint32_t gi, uint32_t (&m)[NW]) {
+				const uint4 q0 = xmg[4u * gi];
+				const uint4 q1 = xmg[4u * gi + 1u];
+				const uint32_t mul = q0.x, shf = q0.y, soff = q0.z, eb = q0.w;
+				const uint32_t sg = q1.x, greq = q1.y, gmask = q1.z;
+				const uint32_t sl = sg & 0xffu;
+				/* CUSTOM_L3 / CUSTOM_FRAME records: frame_len > base +
+				 * off + size (term_cmp's guard) */
+				const bool gok = !(sg >> 31) ||
+						 b.len > ((sg >> 30) & 1u ? 0u : b.l3) + ((sg >> 8) & 0xffffu);
+				const uint32_t key = sl < 16u ? kv[sl] : sl == 16u ? k16 :
+						     sl == 17u ? k17 : len;
+				const uint32_t kvm = key & gmask;
+				const uint32_t si = xms[soff + ((kvm * mul) >> shf)];
+				const uint32_t e = eb + (si != 0xffu ? si : 0u);
+
+				if constexpr (GF_ZERO(NW)) {
+					/* wide maps: the entry's map read once the value
+					 * matched, the zero entry past the last on a miss */
+					const bool hit = on && (b.inf_lo & greq) == greq && gok &&
+							 si != 0xffu && xmv[e] == kvm;
+
+					xm_entry<NW>(xmm, hit ? e : zent, m);
+				} else {
+					/* the value and the map read together (entry eb +
+					 * 0 for an empty slot), the map dropped on a miss */
+					xm_entry<NW>(xmm, e, m);
+					const bool hit = on && (b.inf_lo & greq) == greq && gok &&
+							 si != 0xffu && xmv[e] == kvm;
+
+#pragma unroll
+					for (int w = 0; w < NW; ++w)
+						m[w] = hit ? m[w] : 0u;
+				}
+			};
+#ifdef GF_EXP_NOHM   /* experiment builds only: cost without the hit map */
+			if (__ballot(on) && A.num == 12345u) {
+#else
+			if (__ballot(on)) {
+#endif
+				for (uint32_t gi = 0; gi < ngor; ++gi) {
+					uint32_t m[NW];
+
+					probe(gi, m);
+#pragma unroll
+					for (int w = 0; w < NW; ++w)
+						hm[w] |= m[w];
+				}
+				for (uint32_t gi = ngor; gi < ngroups; ++gi) {
+					uint32_t m[NW];
+
+					probe(gi, m);
+					const uint4 a0 = xmg[4u * gi + 2u];
+					const uint4 a1 = xmg[4u * gi + 3u];
+					const uint32_t na[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+
+#pragma unroll
+					for (int w = 0; w < NW; ++w)
+						hm[w] = (hm[w] & (m[w] | na[w])) | (m[w] & ~chain[w]);
+				}
+			}
 		}
 
 		/* ---- checksum bytes past the window: the whole wave. Even waves
@@ -881,16 +964,16 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 		active = false;
 #endif
 		{
-			/* a level: the lowest set bit of the CoS's rule range
-			 * [rule_start, rule_start + nrule) in the hit map; the CoS's
-			 * complex PMRs below it, in rule order, from their term
-			 * records (gate, CUSTOM_L3 length guard, masked slot word); then
-			 * the PMR's destination, mark and the destination's ranges */
+			/* a level: the lowest set bit of the CoS's bit range [start,
+			 * start + n) in the hit map; (lazy form) the CoS's complex PMRs
+			 * below it, in rule order, from their term records (gate,
+			 * CUSTOM_L3 length guard, masked slot word); then the bit's PMR
+			 * destination, mark and the destination's bit range */
 			uint32_t crs = 0u, cxf = 0u;
 
 			if (active) {
-				crs = cinfo[cos].x;
-				cxf = A.upf ? 0u : A.xfc[cos];
+				crs = xci[cos].x;
+				cxf = A.num_xflat ? A.xfc[cos] : 0u;
 			}
 			while (__ballot(active)) {
 				if (active) {
@@ -903,7 +986,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 						uint32_t x = hm[0];
 
 #pragma unroll
-						for (uint32_t k = 1; k < XM_WORDS; ++k)
+						for (uint32_t k = 1; k < NW; ++k)
 							x = w == k ? hm[k] : x;
 						x >>= bi & 31u;
 						if (end - bi < 32u)
@@ -959,7 +1042,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 						cos = pd2.x & 0xffffu;
 						mark = pd2.x >> 16;
 						crs = pd2.y;
-						cxf = A.upf ? 0u : pd2.z;
+						cxf = pd2.z;
 						any_match = true;
 						if (++steps >= A.num_cos) {
 							cos = ODPG_COS_LOOP;
@@ -1001,7 +1084,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 					cret = -2;
 				else if (cos == ODPG_COS_NONE)
 					cret = -1;
-				else if (cos < A.num_cos && (cinfo[cos].y & 0xffu) == 1u)
+				else if (cos < A.num_cos && (xci[cos].y & 0xffu) == 1u)
 					cret = 1;
 				markv = any_match && !err && cos != ODPG_COS_LOOP && mark != 0u;
 			} else if (ret < 0) {
@@ -1059,37 +1142,37 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 		const uint32_t nc = A.num_cos < C.ncos ? A.num_cos : C.ncos;
 		/* without hash queues each CoS owns one column */
 		auto col = [&](uint32_t c) { return 4u + C.ncos + (C.ident ? c : C.qcol[c]); };
+		const uint32_t ne = dlv[GF_BIN_ERR], np = dlv[GF_BIN_PDROP];
+		const uint32_t ec = A.error_cos < 0 ? 0xffffffffu : (uint32_t)A.error_cos;
+		/* error packets: delivered to the error CoS unless it drops;
+		 * without an error CoS they are discards too */
+		const bool edeliv = ne && ec < nc && (xci[ec].y & 0xffu) != 1u;
 		uint32_t tot = 0u;
 
+		/* plain stores of the row read at the start + the histogram (the
+		 * workgroup owns its row; launches on the stream are ordered) */
 		for (uint32_t k0 = 0; k0 < nc; k0 += 64u) {
 			const uint32_t k = k0 + lane;
 			const uint32_t x = k < nc ? dlv[GF_BIN_EXTRA + k] : 0u;
+			const uint32_t xe = x + (edeliv && k == ec ? ne : 0u);
 
-			if (x)
-				atomicAdd(r + col(k), (unsigned long long)x);
+			if (xe)
+				r[col(k)] = base[col(k)] + xe;
 			tot += x;
 		}
 		const uint32_t tp = wave_sum_u32(tot);                  /* in_packets */
 
 		if (lane == 0u) {
-			const uint32_t ne = dlv[GF_BIN_ERR], np = dlv[GF_BIN_PDROP];
-			uint32_t nd = dlv[GF_BIN_NOCOS];
-			const uint32_t ec = A.error_cos < 0 ? 0xffffffffu : (uint32_t)A.error_cos;
+			const uint32_t nd = dlv[GF_BIN_NOCOS] + (ec >= nc ? ne : 0u);
 
 			if (tp) {
-				atomicAdd(r + 0, (unsigned long long)tp);
-				atomicAdd(r + 1, octets);
+				r[0] = base[0] + tp;
+				r[1] = base[1] + octets;
 			}
-			/* error packets: delivered to the error CoS unless it drops;
-			 * without an error CoS they are discards too */
-			if (ne && ec < nc && (cinfo[ec].y & 0xffu) != 1u)
-				atomicAdd(r + col(ec), (unsigned long long)ne);
-			else if (ec >= nc)
-				nd += ne;
 			if (ne + np)
-				atomicAdd(r + 2, (unsigned long long)(ne + np));
+				r[2] = base[2] + (ne + np);
 			if (nd)
-				atomicAdd(r + 3, (unsigned long long)nd);
+				r[3] = base[3] + nd;
 		}
 	}
 }
@@ -1098,15 +1181,21 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ wg, const uint4 *__r
 extern "C" uint32_t odpg_resident_grid(const void *kernel, uint32_t block, size_t lds);
 extern "C" uint32_t odpg_lds_limit(void);
 
-/* dynamic LDS of a launch: generic-parse rows + the table copy */
+static void gf_layout(const odpg_launch_args *a, xm_layout_t *L)
+{
+	xm_layout_of(a->xm_nw, a->num_xment, a->xm_slot_bytes, a->num_cos, a->xm_nbits, a->num_xflat, L);
+}
+
+/* dynamic LDS of a launch: generic-parse rows + the table's LDS part */
 extern "C" size_t odpg_clsgf_lds(const odpg_launch_args *a)
 {
-	const size_t tb = (size_t)a->num_xment * (XM_WORDS + 1u) * 4u + 12u + a->xm_slot_bytes;
+	xm_layout_t L;
 
+	gf_layout(a, &L);
 	const size_t bins = a->cnt.row ? (((size_t)a->num_cos + GF_BIN_EXTRA + 3u) & ~(size_t)3u) * 4u : 0u;
 
-	return (size_t)GF_BLOCK * GF_RW * 4u + bins + tb + (size_t)((a->num_cos + 1u) & ~1u) * 8u +
-	       (size_t)a->num_pmr * 16u + (size_t)a->num_xflat * 32u +
+	return (size_t)GF_BLOCK * GF_RW * 4u + bins + (size_t)((L.lds_words + 1u) & ~1u) * 4u +
+	       (a->cnt.row ? (size_t)a->cnt.words * 8u : 0u) +
 	       (GF_SWEEP ? (size_t)GF_BLOCK * 2u * 4u : 0u);
 }
 
@@ -1114,32 +1203,28 @@ extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s)
 {
 	if (a->num == 0)
 		return 0;
+	if (a->xm_nw != 2u && a->xm_nw != 4u && a->xm_nw != 8u)
+		return -EINVAL;
 	GFArgs A;
 
 	A.frames = a->frames;
 	A.num = a->num;
 	A.stride = a->desc ? 0u : a->stride;   /* gf_ok: num * stride < 2^32 */
 	A.opt = (uint32_t)a->opt;
-	A.nwg = a->num_wgroups;
-	A.cinfo = (const uint2 *)a->cinfo;
-	A.pinfo = a->pinfo;
+	A.ngroups = a->xm_ngroups;
 	A.num_cos = a->num_cos;
-	A.num_pmr = a->num_pmr;
 	A.default_cos = a->default_cos;
 	A.error_cos = a->error_cos;
 	A.coses = a->coses;
-	A.xm_rest = a->xm + 4u * a->num_wgroups;
-	A.num_xment = a->num_xment;
-	A.xm_slot_bytes = a->xm_slot_bytes;
 	A.num_xflat = a->num_xflat;
-	const uint4 *xf = (const uint4 *)(A.xm_rest + (XM_WORDS + 1u) * a->num_xment +
-					  a->xm_slot_bytes / 4u);
+	gf_layout(a, &A.L);
+	const uint32_t *xhdr = a->xm;
+	const uint4 *xmg = (const uint4 *)(a->xm + XM_HDR_WORDS);
 
-	A.xfc = (const uint32_t *)(xf + 2u * a->num_xflat);
-	/* complex PMRs up front or per level (ODPG_GF_UPF=0/1 overrides) */
-	static const char *upf_env = getenv("ODPG_GF_UPF");
-	A.upf = upf_env ? (uint32_t)atoi(upf_env) : 0u;
+	A.xlds = a->xm + XM_HDR_WORDS + XM_GROUP_WORDS * a->xm_ngroups;
+	A.xfc = A.xlds + A.L.lds_words;
 	A.cnt = a->cnt.dev;
+	A.cnt_words = a->cnt.row ? a->cnt.words : 0u;
 
 	const size_t lds = odpg_clsgf_lds(a);
 	const uint32_t ntiles = (a->num + 63u) / 64u;
@@ -1148,22 +1233,20 @@ extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s)
 
 	/* resident grid of the instantiation launched, at most one workgroup per
 	 * counter row */
-	auto go = [&](const void *k, auto launch) {
-		uint32_t grid = odpg_resident_grid(k, GF_BLOCK, lds);
+	auto go = [&](auto kern) {
+		uint32_t grid = odpg_resident_grid((const void *)kern, GF_BLOCK, lds);
 
 		grid = grid < want ? grid : want;
 		grid = grid < rows ? grid : rows;
-		launch(grid ? grid : 1u);
+		hipLaunchKernelGGL(kern, dim3(grid ? grid : 1u), dim3(GF_BLOCK), lds, s, A, xmg, xhdr,
+				   a->desc, a->out);
 	};
-	if (a->cnt.row)
-		go((const void *)odpg_clsgf_kernel<2>, [&](uint32_t grid) {
-			hipLaunchKernelGGL((odpg_clsgf_kernel<2>), dim3(grid), dim3(GF_BLOCK), lds, s, A,
-					   (const uint4 *)a->wgroups, (const uint4 *)a->xm, xf, a->desc, a->out);
-		});
-	else
-		go((const void *)odpg_clsgf_kernel<0>, [&](uint32_t grid) {
-			hipLaunchKernelGGL((odpg_clsgf_kernel<0>), dim3(grid), dim3(GF_BLOCK), lds, s, A,
-					   (const uint4 *)a->wgroups, (const uint4 *)a->xm, xf, a->desc, a->out);
-		});
+	const bool cm = a->cnt.row != nullptr;
+
+	switch (a->xm_nw) {
+	case 2: cm ? go(odpg_clsgf_kernel<2, 2>) : go(odpg_clsgf_kernel<0, 2>); break;
+	case 4: cm ? go(odpg_clsgf_kernel<2, 4>) : go(odpg_clsgf_kernel<0, 4>); break;
+	default: cm ? go(odpg_clsgf_kernel<2, 8>) : go(odpg_clsgf_kernel<0, 8>); break;
+	}
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -9,6 +9,7 @@
  * the reference's raw-memory compare semantics: values and masks are the
  * caller's bytes (network order, except ODP_PMR_LEN which is CPU endian).
  */
+#include <stdlib.h>
 #include <string.h>
 #include <errno.h>
 #include <algorithm>
@@ -1070,34 +1071,135 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			h.flags |= TBL_XGF;
 	}
 
-	/* TBL_XMASK (classify_gf.hip's hit-map form, <= XM_MAX_PMR PMRs): per
-	 * walk group its distinct masked values, each with the bit map of the
-	 * PMRs (of any CoS) that compare equal to it, found through a
-	 * collision-free multiplicative hash (slot = (value * mul) >> shift) and
-	 * a byte table of entry indices. A packet reads each group once and ORs
-	 * the entry's map; a walk level then finds the CoS's first matching
-	 * single-word rule as the lowest set bit of its rule range. Only the
-	 * lowest PMR per (CoS, value) is in the walk groups: a higher one of the
-	 * same key matches exactly when that one does, so never first. */
-	std::vector<uint32_t> xmg, xmmask, xmval;
-	std::vector<uint8_t> xmslot;
-	bool xm = (h.flags & TBL_XGF) && pmr.size() <= XM_MAX_PMR;
-	uint64_t rs = 0x9E3779B97F4A7C15ull;
+	/* TBL_XMASK (classify_gf.hip's hit-map form). A packet's hit map holds
+	 * one bit per "rule bit": the rule bits of a CoS are contiguous and in
+	 * rule order, so a level of match_pmr_cos is the lowest set bit of the
+	 * CoS's bit range. A single-word PMR (or an IPv4 / IPv6 alternative pair
+	 * of them) has one bit, set when any of its groups' entries for the
+	 * packet's key holds it (OR). A complex PMR has one bit per AND-chain of
+	 * its terms (the chains of one PMR consecutive, so the lowest set one is
+	 * the PMR's first match); a chain's bit starts set and is cleared by
+	 * every group holding one of its records whose entry for the packet's
+	 * key does not hold it (AND): hm = (hm & (h | ~A)) | (h & ~CH), A the
+	 * group's chain members, CH every chain bit. Groups are keyed by (slot
+	 * and guard, gate, mask); each has a collision-free multiplicative hash
+	 * of its distinct masked values (slot = (value * mul) >> shift) into a
+	 * byte table of entry indices, each entry {value, bit map}. Only the
+	 * lowest PMR per (CoS, value) of a single-word group is entered: a
+	 * higher one of the same key matches exactly when that one does.
+	 * When the chain bits do not fit XM_MAX_PMR, the bits are the PMR
+	 * indices and the complex PMRs are evaluated per level from their
+	 * records (xflat, in rule order per CoS) instead. */
+	bool xm = (h.flags & TBL_XGF) != 0;
+	std::vector<uint32_t> bit_of(pmr.size(), 0u), chain_bit(num_xent, 0u);
+	std::vector<uint32_t> cbit_start(ncos, 0u), cbit_n(ncos, 0u);
+	uint32_t nbits = 0;
+	bool and_form = xm;
+
+	for (uint32_t c = 0; xm && c < ncos; c++) {
+		const uint32_t st = xcos[2 * c] & 0xffffu, n = xcos[2 * c] >> 16;
+		uint32_t k2 = st;
+
+		cbit_start[c] = nbits;
+		for (uint32_t k = 0; k < cos[c].nrule; k++) {
+			const uint32_t pi = cos[c].rule_start + k;
+
+			bit_of[pi] = nbits;
+			if (!complex_pmr[pi]) {
+				nbits++;
+				continue;
+			}
+			while (k2 < st + n && xlist[2 * k2] == pi)
+				chain_bit[k2++] = nbits++;
+		}
+		cbit_n[c] = nbits - cbit_start[c];
+	}
+	/* ODPG_XM_LAZY=1 forces the lazy form (experiments / A-B runs) */
+	static const bool force_lazy = getenv("ODPG_XM_LAZY") && atoi(getenv("ODPG_XM_LAZY"));
+
+	if (xm && (nbits > XM_MAX_PMR || force_lazy)) {
+		/* lazy form: bit = PMR index, complex PMRs from their records */
+		and_form = false;
+		nbits = (uint32_t)pmr.size();
+		for (uint32_t c = 0; c < ncos; c++) {
+			cbit_start[c] = cos[c].rule_start;
+			cbit_n[c] = cos[c].nrule;
+		}
+		for (size_t pi = 0; pi < pmr.size(); pi++)
+			bit_of[pi] = (uint32_t)pi;
+	}
+	if (nbits > XM_MAX_PMR)
+		xm = false;
+	typedef std::tuple<uint32_t, uint32_t, uint32_t> gkey_t;   /* slot | guard, gate, mask */
+	typedef std::vector<uint32_t> bm_t;                          /* XM_WORDS */
+	std::map<gkey_t, std::map<uint32_t, bm_t>> gv;
+	std::map<gkey_t, bm_t> gand;
+	bm_t chain_all(XM_WORDS, 0u);
+	auto setb = [](bm_t &m, uint32_t b) {
+		m.resize(XM_WORDS, 0u);
+		m[b >> 5] |= 1u << (b & 31u);
+	};
 
 	for (size_t gi = 0; xm && gi < wgroups.size(); gi++) {
 		const dhgroup_t &g = wgroups[gi];
-		std::map<uint32_t, std::vector<uint32_t>> vm;
+		auto &vm = gv[std::make_tuple(g.slot, g.req, g.mask)];
 
 		for (uint32_t e = 0; e < (1u << g.log2sz); e++) {
 			const dwent_t &w = wents[g.off + e];
 
-			if (w.cos_pmr == HENT_EMPTY)
-				continue;
-			std::vector<uint32_t> &m = vm[w.value];
-
-			m.resize(XM_WORDS, 0u);
-			m[(w.cos_pmr >> 16) >> 5] |= 1u << ((w.cos_pmr >> 16) & 31u);
+			if (w.cos_pmr != HENT_EMPTY)
+				setb(vm[w.value], bit_of[w.cos_pmr >> 16]);
 		}
+	}
+	for (uint32_t k = 0; xm && and_form && k < num_xent; k++) {
+		const uint32_t nt = xlist[2 * k + 1] >> 24, ts = xlist[2 * k + 1] & 0xffffffu;
+		std::map<gkey_t, uint32_t> recs;
+		bool dead = false;
+
+		for (uint32_t tt = 0; tt < nt; tt++) {
+			const uint32_t *r = &xterm[4 * (ts + tt)];
+			const gkey_t key = std::make_tuple(r[3], r[0], r[1]);
+			auto it = recs.find(key);
+
+			/* bits outside the mask, or two values for one masked word:
+			 * the chain never matches */
+			if ((r[2] & ~r[1]) || (it != recs.end() && it->second != r[2]))
+				dead = true;
+			recs[key] = r[2];
+		}
+		if (dead)
+			continue;
+		for (auto &kv : recs) {
+			setb(gv[kv.first][kv.second], chain_bit[k]);
+			setb(gand[kv.first], chain_bit[k]);
+		}
+		setb(chain_all, chain_bit[k]);
+	}
+	if (gv.empty() || gv.size() > XM_MAX_GROUPS)
+		xm = false;
+	const uint32_t nw = nbits <= 64u ? 2u : nbits <= 128u ? 4u : 8u;
+	std::vector<uint32_t> xmg, xmmask, xmval;
+	std::vector<uint8_t> xmslot;
+	uint64_t rs = 0x9E3779B97F4A7C15ull;
+
+	/* the groups without chain records first (their entries only OR bits
+	 * in), then the AND-chain groups: the kernel runs each kind in a loop
+	 * of its own (the hit map's result does not depend on group order) */
+	std::vector<decltype(gv.begin())> gorder;
+	uint32_t ngor = 0;
+
+	for (auto git = gv.begin(); git != gv.end(); ++git)
+		if (!gand.count(git->first)) {
+			gorder.push_back(git);
+			ngor++;
+		}
+	for (auto git = gv.begin(); git != gv.end(); ++git)
+		if (gand.count(git->first))
+			gorder.push_back(git);
+	for (size_t go = 0; xm && go < gorder.size(); ++go) {
+		const auto git = gorder[go];
+		const auto &vm = git->second;
+
 		if (vm.size() > 255) {
 			xm = false;
 			break;
@@ -1142,41 +1244,105 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		for (auto &v : vm) {
 			xmslot[soff + ((v.first * mul) >> (32u - lg))] = (uint8_t)k++;
 			xmval.push_back(v.first);
-			xmmask.insert(xmmask.end(), v.second.begin(), v.second.end());
+			bm_t m = v.second;
+
+			m.resize(XM_WORDS, 0u);
+			xmmask.insert(xmmask.end(), m.begin(), m.begin() + nw);
 		}
-		xmg.insert(xmg.end(), {mul, 32u - lg, soff, ebase});
+		auto ait = gand.find(git->first);
+		bm_t a = ait == gand.end() ? bm_t(XM_WORDS, 0u) : ait->second;
+
+		a.resize(XM_WORDS, 0u);
+		xmg.insert(xmg.end(), {mul, 32u - lg, soff, ebase, std::get<0>(git->first),
+				       std::get<1>(git->first), std::get<2>(git->first),
+				       ait == gand.end() ? 0u : 1u});
+		for (uint32_t w = 0; w < XM_WORDS; w++)
+			xmg.push_back(~a[w]);
 	}
-	/* the complex PMRs' terms flat, per CoS in rule order: {gate, mask,
-	 * value, slot | guard end << 8 | absolute << 30 | guarded << 31}, {pmr,
-	 * last record of its chain, flat index of that record, 0}; per CoS its
-	 * first flat record | count << 16 */
+	/* lazy form: the complex PMRs' terms flat, per CoS in rule order:
+	 * {gate, mask, value, slot | guard end << 8 | absolute << 30 | guarded <<
+	 * 31}, {pmr, last record of its chain, flat index of that record, 0}; per
+	 * CoS its first flat record | count << 16 */
 	std::vector<uint32_t> xflat, xfc(ncos, 0u), xfstart(num_xent + 1, 0u);
 
-	for (uint32_t k = 0; xm && k < num_xent; k++) {
+	for (uint32_t k = 0; xm && !and_form && k < num_xent; k++) {
 		const uint32_t nt = xlist[2 * k + 1] >> 24, ts = xlist[2 * k + 1] & 0xffffffu;
 
 		xfstart[k] = (uint32_t)(xflat.size() / 8);
 		for (uint32_t tt = 0; tt < nt; tt++) {
 			xflat.insert(xflat.end(), xterm.begin() + 4 * (ts + tt), xterm.begin() + 4 * (ts + tt + 1));
-			/* {pmr, last record of the chain, that record's flat index} */
 			xflat.insert(xflat.end(), {xlist[2 * k], tt + 1 == nt ? 1u : 0u,
 						   xfstart[k] + nt - 1u, 0u});
 		}
 	}
 	xfstart[num_xent] = (uint32_t)(xflat.size() / 8);
-	for (uint32_t c = 0; xm && c < ncos; c++) {
+	for (uint32_t c = 0; xm && !and_form && c < ncos; c++) {
 		const uint32_t st = xcos[2 * c] & 0xffffu, n = xcos[2 * c] >> 16;
 
 		xfc[c] = xfstart[st] | ((xfstart[st + n] - xfstart[st]) << 16);
 	}
 	if (xflat.size() / 8 > XM_MAX_XTERMS)
 		xm = false;
-	if (xm && !wgroups.empty()) {
+	std::vector<uint32_t> xmlds, xmhdr;
+
+	if (xm) {
+		xmslot.resize((xmslot.size() + 15u) & ~(size_t)15u, 0xff);
+		xm_layout_t L;
+
+		xm_layout_of(nw, (uint32_t)xmval.size(), (uint32_t)xmslot.size(), ncos, nbits,
+			     (uint32_t)(xflat.size() / 8), &L);
+		xmlds.assign(L.lds_words, 0u);
+		std::copy(xmmask.begin(), xmmask.end(), xmlds.begin() + L.masks);
+		std::copy(xmval.begin(), xmval.end(), xmlds.begin() + L.values);
+		memcpy(xmlds.data() + L.slots, xmslot.data(), xmslot.size());
+		for (uint32_t c = 0; c < ncos; c++) {
+			xmlds[L.xci + 2 * c] = cbit_start[c] | (cbit_n[c] << 16);
+			xmlds[L.xci + 2 * c + 1] = cos[c].action | ((uint32_t)cos[c].num_queue << 8) |
+						   ((uint32_t)cos[c].stats << 16) |
+						   ((uint32_t)cos[c].hash_proto << 24);
+		}
+		/* per rule bit: its PMR's destination and mark, the destination's
+		 * bit range and (lazy form) complex records */
+		for (size_t pi = 0; pi < pmr.size(); pi++) {
+			const uint32_t d = pmr[pi].dst;
+			const uint32_t c = src_cos[pi];
+			const uint32_t b0 = bit_of[pi];
+			uint32_t b1 = b0 + 1u;
+
+			/* the PMR's bits: up to the next PMR's first bit (or its
+			 * CoS's end) */
+			if (pi + 1 < pmr.size() && src_cos[pi + 1] == c)
+				b1 = bit_of[pi + 1];
+			else
+				b1 = cbit_start[c] + cbit_n[c];
+			for (uint32_t b = b0; b < b1; b++) {
+				xmlds[L.xpd + 4 * b] = (d & 0xffffu) | ((pmr[pi].mark & 0xffffu) << 16);
+				xmlds[L.xpd + 4 * b + 1] = cbit_start[d] | (cbit_n[d] << 16);
+				xmlds[L.xpd + 4 * b + 2] = xfc[d];
+			}
+		}
+		std::copy(xflat.begin(), xflat.end(), xmlds.begin() + L.xflat);
+		xmhdr.assign(XM_HDR_WORDS, 0u);
+		xmhdr[0] = nw;
+		xmhdr[1] = nbits;
+		xmhdr[2] = (uint32_t)gv.size();
+		xmhdr[3] = (uint32_t)xmval.size();
+		xmhdr[4] = (uint32_t)xmslot.size();
+		xmhdr[5] = (uint32_t)(xflat.size() / 8);
+		/* the key slots the groups read (the kernel extracts them once per
+		 * packet) */
+		for (auto &kv : gv)
+			xmhdr[6] |= 1u << (std::get<0>(kv.first) & 0x1fu);
+		xmhdr[7] = ngor;
+		for (uint32_t w = 0; w < XM_WORDS; w++)
+			xmhdr[8 + w] = chain_all[w];
 		h.flags |= TBL_XMASK;
 		h.num_xment = (uint32_t)xmval.size();
-		xmslot.resize((xmslot.size() + 15u) & ~(size_t)15u, 0xff);
 		h.xm_slot_bytes = (uint32_t)xmslot.size();
 		h.num_xflat = (uint32_t)(xflat.size() / 8);
+		h.xm_nw = nw;
+		h.xm_nbits = nbits;
+		h.xm_ngroups = (uint32_t)gv.size();
 	}
 	const uint32_t lean_req = (1u << IFL_L2) | (1u << IFL_L3) | (1u << IFL_L4) |
 				  (1u << IFL_ETH) | (1u << IFL_VLAN) | (1u << IFL_IPV4) |
@@ -1313,12 +1479,10 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	h.xcos_off = align(h.pinfo4_off + (uint32_t)(pinfo4.size() * 4u));
 	h.xlist_off = align(h.xcos_off + (uint32_t)(xcos.size() * 4u));
 	h.xm_off = align(h.xlist_off + (uint32_t)(xlist.size() * 4u));
-	/* TBL_XMASK region: uint4 xmg[num_wgroups] {mul, shift, slot offset,
-	 * entry base}, masks[num_xment][XM_WORDS], values[num_xment], slot
-	 * bytes (16-byte multiple), 2 x uint4 xflat[num_xflat], xfc[num_cos] */
+	/* TBL_XMASK region: header (XM_HDR_WORDS), group descriptors
+	 * (XM_GROUP_WORDS each), the LDS part (xm_layout_t), xfc[num_cos] */
 	const uint32_t xm_bytes = (h.flags & TBL_XMASK) ?
-		(uint32_t)(xmg.size() * 4u + xmmask.size() * 4u + xmval.size() * 4u + xmslot.size() +
-			   xflat.size() * 4u + xfc.size() * 4u) : 0u;
+		(uint32_t)((xmhdr.size() + xmg.size() + xmlds.size() + xfc.size()) * 4u) : 0u;
 	h.blob_bytes = align(h.xm_off + xm_bytes);
 	if (h.blob_bytes == 0)
 		h.blob_bytes = 64;
@@ -1370,18 +1534,11 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	if (h.flags & TBL_XMASK) {
 		uint8_t *o = blob.data() + h.xm_off;
 
-		memcpy(o, xmg.data(), xmg.size() * 4u);
-		o += xmg.size() * 4u;
-		memcpy(o, xmmask.data(), xmmask.size() * 4u);
-		o += xmmask.size() * 4u;
-		memcpy(o, xmval.data(), xmval.size() * 4u);
-		o += xmval.size() * 4u;
-		memcpy(o, xmslot.data(), xmslot.size());
-		o += xmslot.size();
-		if (!xflat.empty())
-			memcpy(o, xflat.data(), xflat.size() * 4u);
-		o += xflat.size() * 4u;
-		memcpy(o, xfc.data(), xfc.size() * 4u);
+		for (const std::vector<uint32_t> *v : {&xmhdr, &xmg, &xmlds, &xfc}) {
+			if (!v->empty())
+				memcpy(o, v->data(), v->size() * 4u);
+			o += v->size() * 4u;
+		}
 	}
 	*hdr_out = h;
 	return 0;

@@ -337,7 +337,7 @@ __global__ __launch_bounds__(FBLOCK) void odpg_l3fwd_kernel(
 		uint32_t pos = 0u;
 
 #pragma unroll
-		for (uint32_t step = 64u; step; step >>= 1) {
+		for (uint32_t step = 128u; step; step >>= 1) {   /* reaches index 255 >= FWD_MAX_IV - 1 */
 			const uint32_t q = pos + step;
 
 			if (q < niv && s_ivb[q] <= dst)
@@ -503,7 +503,7 @@ __global__ __launch_bounds__(FWD_PBLOCK, FWD_WAVES * 256 / FWD_PBLOCK) void odpg
 			uint32_t pos = 0u;
 
 #pragma unroll
-			for (uint32_t step = 64u; step; step >>= 1) {
+			for (uint32_t step = 128u; step; step >>= 1) {   /* reaches index 255 >= FWD_MAX_IV - 1 */
 				const uint32_t q = pos + step;
 
 				if (q < niv && s_ivb[q] <= dst)

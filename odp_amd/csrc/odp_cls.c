@@ -83,6 +83,7 @@ typedef struct {
 typedef struct {
 	int valid;
 	int started;
+	int closing;                 /* odp_pktio_close in progress: no start, no second close */
 	char name[64];
 	odp_pool_t pool;
 	odp_pktio_config_t config;
@@ -1156,7 +1157,7 @@ int odp_pktio_close(odp_pktio_t hdl)
 	LOCK();
 	pktio_e *p = get_pktio(hdl);
 
-	if (!p) {
+	if (!p || p->closing) {
 		UNLOCK();
 		return -1;
 	}
@@ -1171,9 +1172,11 @@ int odp_pktio_close(odp_pktio_t hdl)
 			ERR("pktio close during a receive\n");
 			return -1;
 		}
+	/* marked closing before the lock is dropped for the runtime side: a
+	 * start in that window is refused, and a stopped pktio takes no new
+	 * receive (recv_impl, rx_burst), so nothing re-binds */
+	p->closing = 1;
 	UNLOCK();
-	/* a stopped pktio takes no new receive (recv_impl, rx_burst), so
-	 * nothing re-binds while the lock is dropped for the runtime side */
 	odpg_rt_pktio_close(hdl);
 	LOCK();
 	p = get_pktio(hdl);
@@ -1299,7 +1302,7 @@ int odp_pktio_start(odp_pktio_t hdl)
 	LOCK();
 	pktio_e *p = get_pktio(hdl);
 
-	if (!p || p->started) {
+	if (!p || p->started || p->closing) {
 		rc = -1;
 	} else {
 		p->parse_layer = p->cls_enabled ? ODP_PROTO_LAYER_ALL : (int)p->config.parser.layer;
@@ -1656,6 +1659,11 @@ static int recv_impl(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
 	res.counters = bd->cnt;
 	rc = device_ptrs ? odpg_classify(ctx, bd->tbl, &b, &res)
 			 : odpg_classify_host(ctx, bd->tbl, &b, &res, 0);
+	/* zero-copy (device_ptrs 2: pinned host buffers the kernel reads and
+	 * writes in place): complete before the results are read and the
+	 * binding can go */
+	if (!rc && device_ptrs == 2)
+		rc = odpg_ctx_sync(ctx);
 
 	LOCK();
 	if (--bd->refs == 0 && bd->stale) {
@@ -1683,6 +1691,13 @@ int odpg_cls_pktio_recv_meta(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *fr
 			     odpg_meta_t *meta)
 {
 	return recv_impl(hdl, ctx, frames, desc, 0, num, 0, out, NULL, meta);
+}
+
+int odpg_cls_pktio_recv_meta_zc(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
+				const odpg_desc_t *desc, uint32_t num, odpg_out_t *out,
+				odpg_meta_t *meta)
+{
+	return recv_impl(hdl, ctx, frames, desc, 0, num, 2, out, NULL, meta);
 }
 
 void odpg_cls_pktio_count(odp_pktio_t hdl, int64_t in_packets, int64_t in_octets,

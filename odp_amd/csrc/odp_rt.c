@@ -221,10 +221,30 @@ int odp_init_global(odp_instance_t *instance, const odp_init_t *param, const voi
 
 static void parse_release(void);
 
+/* ODP_RT_PROF=1: receive-burst counts and times, printed by odp_term_global */
+static struct {
+	int on;
+	uint64_t bursts, pkts, stage_ns, gpu_ns, post_ns;
+} rxprof = { -1, 0, 0, 0, 0, 0 };
+
+static uint64_t prof_ns(void)
+{
+	struct timespec ts;
+
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
 int odp_term_global(odp_instance_t instance)
 {
 	(void)instance;
 	parse_release();
+	if (rxprof.on > 0 && rxprof.bursts)
+		fprintf(stderr, "odp_rt: %llu receive bursts, %.1f packets each; per burst: "
+			"staging %.2f us, GPU %.2f us, delivery %.2f us\n",
+			(unsigned long long)rxprof.bursts, (double)rxprof.pkts / rxprof.bursts,
+			rxprof.stage_ns / 1e3 / rxprof.bursts, rxprof.gpu_ns / 1e3 / rxprof.bursts,
+			rxprof.post_ns / 1e3 / rxprof.bursts);
 	pthread_mutex_lock(&rt.lock);
 	if (rt.init) {
 		odpg_ctx_destroy(rt.ctx);
@@ -2037,6 +2057,8 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 		num = RT_BURST;
 	if (num <= 0 || !rt.init || !odpg_cls_pktio_started(hdl))
 		return 0;
+	const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
+
 	if (p->loopdev) {
 		size_t need = 0, off = 0;
 
@@ -2096,6 +2118,10 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 	 * writes the verdicts and metadata in pinned host memory (a burst is a
 	 * few KiB: copies would cost more than the PCIe reads) */
 	frames = p->stage;
+	if (rxprof.on < 0)
+		rxprof.on = getenv("ODP_RT_PROF") && atoi(getenv("ODP_RT_PROF"));
+	const uint64_t t1 = rxprof.on ? prof_ns() : 0;
+
 	if (odpg_cls_pktio_recv_meta_zc(hdl, rt.ctx, p->dstage, rt.ddesc, n, rt.dout, rt.dmeta)) {
 		ERR("classify failed\n");
 		if (p->loopdev)
@@ -2103,6 +2129,8 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 				odp_packet_free((odp_packet_t)src[k]);
 		return -1;
 	}
+	const uint64_t t2 = rxprof.on ? prof_ns() : 0;
+
 	if (!p->loopdev)
 		p->pos += n;
 	for (uint32_t k = 0; k < n; k++) {
@@ -2162,6 +2190,15 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 		run[nrun++] = pkt;
 	}
 	cos_enq(run_cos, run_q, run, nrun);
+	if (rxprof.on) {            /* the callers hold rt.poll_lock */
+		const uint64_t t3 = prof_ns();
+
+		rxprof.bursts++;
+		rxprof.pkts += n;
+		rxprof.stage_ns += t1 - t0;
+		rxprof.gpu_ns += t2 - t1;
+		rxprof.post_ns += t3 - t2;
+	}
 	return (int)n;
 }
 

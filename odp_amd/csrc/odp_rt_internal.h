@@ -27,6 +27,11 @@ int  odpg_rt_pktin_config(odp_pktio_t pktio, uint32_t num_queues);
 int odpg_cls_pktio_recv_meta(odp_pktio_t pktio, odpg_ctx_t *ctx, const uint8_t *frames,
 			     const odpg_desc_t *desc, uint32_t num, odpg_out_t *out,
 			     odpg_meta_t *meta);
+/* the same on pinned host buffers read and written in place by the kernel
+ * (zero-copy), complete on return */
+int odpg_cls_pktio_recv_meta_zc(odp_pktio_t pktio, odpg_ctx_t *ctx, const uint8_t *frames,
+			     const odpg_desc_t *desc, uint32_t num, odpg_out_t *out,
+			     odpg_meta_t *meta);
 /* the pktio is started (with the classifier enabled) */
 int odpg_cls_pktio_started(odp_pktio_t pktio);
 int odpg_cls_pktio_classifies(odp_pktio_t pktio);

@@ -108,6 +108,48 @@ typedef struct dcos_s {
 #define XM_WORDS       8     /* hit-map words per packet (XM_MAX_PMR / 32) */
 #define XM_MAX_LG      10    /* largest per-group slot table: 1024 bytes */
 #define XM_MAX_XTERMS  512   /* complex-PMR terms the kernel evaluates per packet */
+#define XM_MAX_GROUPS  64    /* groups read per packet */
+#define XM_GROUP_WORDS 16    /* xmg descriptor: {mul, shift, slot offset, entry base},
+			      * {slot | guard << 8, gate, mask, has chain members},
+			      * not-member words[8] */
+#define XM_HDR_WORDS   16    /* region header: nw, nbits, ngroups, num_xment,
+			      * slot bytes, num_xflat, key slots the groups read
+			      * (bit mask), groups without chain members (they
+			      * come first), chain bits[8] */
+
+/* TBL_XMASK region, after the header and the group descriptors: the part
+ * every workgroup copies to LDS (word offsets, each part 16-byte aligned),
+ * then xfc[num_cos]. Shared by cls_compile.cpp and classify_gf.hip. */
+typedef struct xm_layout_s {
+	uint32_t masks;     /* [num_xment + 1..4][nw] entry bit maps (zero past the last) */
+	uint32_t values;    /* [num_xment] masked key values */
+	uint32_t slots;     /* per-group byte tables of entry indices */
+	uint32_t xci;       /* uint2 [num_cos]: {bit start | bits << 16, cinfo.y} */
+	uint32_t xpd;       /* uint4 [nbits]: {dst | mark << 16, dst's xci.x, dst's
+			     * xfc, 0} */
+	uint32_t xflat;     /* 2 x uint4 [num_xflat]: per-level complex records */
+	uint32_t lds_words; /* end of the LDS part */
+} xm_layout_t;
+
+static inline
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+void xm_layout_of(uint32_t nw, uint32_t num_xment, uint32_t slot_bytes, uint32_t num_cos,
+		  uint32_t nbits, uint32_t num_xflat, xm_layout_t *L)
+{
+	/* at least one zero entry past the last (index num_xment: a probe's
+	 * bit map on a miss) */
+	const uint32_t nx = (num_xment + 4u) & ~3u;
+
+	L->masks = 0u;
+	L->values = L->masks + nx * nw;
+	L->slots = L->values + nx;
+	L->xci = L->slots + ((slot_bytes + 15u) & ~15u) / 4u;
+	L->xpd = L->xci + 2u * ((num_cos + 1u) & ~1u);
+	L->xflat = L->xpd + 4u * nbits;
+	L->lds_words = L->xflat + 8u * num_xflat;
+}
 #define TBL_LEAN64HW   0x100 /* TBL_HASHWALK with <= 4 walk groups whose gates
 			      * the lean kernel's register parse computes: the
 			      * lean kernel's walk-group form */
@@ -307,6 +349,9 @@ typedef struct dtable_hdr_s {
 	uint32_t xm_slot_bytes;
 	uint32_t num_xflat;
 	uint32_t blob_bytes;
+	uint32_t xm_nw;      /* TBL_XMASK hit-map words per packet (2, 4 or 8) */
+	uint32_t xm_nbits;   /* rule bits (chains of the complex PMRs have their own) */
+	uint32_t xm_ngroups; /* groups read per packet */
 } dtable_hdr_t;
 
 typedef struct uint2_s { uint32_t x, y; } uint2_t;
@@ -384,6 +429,7 @@ typedef struct odpg_launch_args {
 	uint32_t num_xlist, num_xwords;
 	const uint32_t *xm;         /* TBL_XMASK region */
 	uint32_t num_xment, xm_slot_bytes, num_xflat;
+	uint32_t xm_nw, xm_nbits, xm_ngroups;
 	/* lean 64-byte kernel (classify64.hip): CoS start state, from the host
 	 * copy of the table */
 	uint32_t l64_err_cos, l64_err_act, l64_def_cos, l64_def_act, l64_def_ci, l64_def_rules;

@@ -685,6 +685,9 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.num_xment = h.num_xment;
 	a.xm_slot_bytes = h.xm_slot_bytes;
 	a.num_xflat = h.num_xflat;
+	a.xm_nw = h.xm_nw;
+	a.xm_nbits = h.xm_nbits;
+	a.xm_ngroups = h.xm_ngroups;
 	{
 		/* start state of cls_select_cos (odp_classification.c:1669-1701)
 		 * for the lean kernel, as classify.hip derives it per packet */
@@ -1023,8 +1026,19 @@ int odpg_host_alloc_pinned(size_t bytes, void **ptr)
 	return 0;
 }
 
+int odpg_host_device_ptr(void *host_ptr, void **dev_ptr)
+{
+	if (!host_ptr || !dev_ptr)
+		return -EINVAL;
+	if (hipHostGetDevicePointer(dev_ptr, host_ptr, 0) != hipSuccess)
+		return -EINVAL;
+	return 0;
+}
+
 int odpg_host_free_pinned(void *ptr)
 {
+	if (!ptr)
+		return 0;
 	HIPCHK(hipHostFree(ptr));
 	return 0;
 }

@@ -28,7 +28,7 @@ COS_NONE, COS_LOOP = 0xFFFF, 0xFFFD
 
 def xm_layout(nw, num_xment, slot_bytes, num_cos, nbits, num_xflat):
     """odpg_internal.h xm_layout_of (word offsets)"""
-    nx = (num_xment + 3) & ~3
+    nx = (num_xment + 4) & ~3     # at least one zero entry (a miss's bit map)
     L = {"masks": 0}
     L["values"] = nx * nw
     L["slots"] = L["values"] + nx
