@@ -292,6 +292,9 @@ int odpg_dev_alloc(odpg_ctx_t *ctx, size_t bytes, void **ptr);
 int odpg_dev_free(odpg_ctx_t *ctx, void *ptr);
 int odpg_host_alloc_pinned(size_t bytes, void **ptr);
 int odpg_host_free_pinned(void *ptr);
+/* The device address of pinned host memory (odpg_host_alloc_pinned): kernels
+ * read and write it in place over PCIe (zero-copy; small batches) */
+int odpg_host_device_ptr(void *host_ptr, void **dev_ptr);
 int odpg_memcpy_h2d(odpg_ctx_t *ctx, void *dst, const void *src, size_t bytes);
 int odpg_memcpy_d2h(odpg_ctx_t *ctx, void *dst, const void *src, size_t bytes);
 int odpg_memset_dev(odpg_ctx_t *ctx, void *dst, int value, size_t bytes);
@@ -299,6 +302,17 @@ int odpg_memset_dev(odpg_ctx_t *ctx, void *dst, int value, size_t bytes);
 /* Timing on the context stream (HIP events), for benchmarks. */
 int odpg_event_record(odpg_ctx_t *ctx, int slot);
 int odpg_event_elapsed_ms(odpg_ctx_t *ctx, int slot_a, int slot_b, float *ms);
+
+/* Completion fences on the context stream (a HIP event without timing):
+ * record after an asynchronous launch, then poll (1 done, 0 pending, < 0
+ * error) or wait. The runtime's receive path keeps several bursts in
+ * flight with them (odp_rt.c "receive pipeline"). */
+typedef struct odpg_fence_s odpg_fence_t;
+int  odpg_fence_create(odpg_ctx_t *ctx, odpg_fence_t **fence);
+int  odpg_fence_record(odpg_ctx_t *ctx, odpg_fence_t *fence);
+int  odpg_fence_query(odpg_fence_t *fence);
+int  odpg_fence_wait(odpg_fence_t *fence);
+void odpg_fence_destroy(odpg_fence_t *fence);
 
 /* Diagnostic streaming floor (not a classification entry point): read npkt
  * 64-byte frames at src, write one u32 per frame to out, with access pattern

@@ -321,6 +321,11 @@ SIGNATURES = {
     "odpg_memset_dev": (_i32, [_vp, _vp, _i32, _sz]),
     "odpg_event_record": (_i32, [_vp, _i32]),
     "odpg_event_elapsed_ms": (_i32, [_vp, _i32, _i32, C.POINTER(C.c_float)]),
+    "odpg_fence_create": (_i32, [_vp, C.POINTER(_vp)]),
+    "odpg_fence_record": (_i32, [_vp, _vp]),
+    "odpg_fence_query": (_i32, [_vp]),
+    "odpg_fence_wait": (_i32, [_vp]),
+    "odpg_fence_destroy": (None, [_vp]),
     "odpg_diag_stream": (_i32, [_vp, _vp, _u32, _vp, _i32, _u32]),
     # include/odp_cls.h
     "odp_cls_capability": (_i32, [C.POINTER(odp_cls_capability_t)]),

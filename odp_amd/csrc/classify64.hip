@@ -454,8 +454,8 @@ odpg_cls64_kernel(const L64Args A)
 
 	if constexpr (CM == 2) {
 		C = *A.cnt;
-		const unsigned long long *r0 =
-			(const unsigned long long *)(C.rows + (size_t)blockIdx.x * C.words);
+		const __attribute__((address_space(1))) unsigned long long *r0 =
+			(const __attribute__((address_space(1))) unsigned long long *)(uintptr_t)(C.rows + (size_t)blockIdx.x * C.words);
 
 		for (uint32_t k = threadIdx.x; k < C.words; k += LBK)
 			base[k] = r0[k];
@@ -976,24 +976,41 @@ odpg_cls64_kernel(const L64Args A)
 				return;
 			__threadfence_block();
 		}
-		unsigned long long *r = (unsigned long long *)(C.rows + (size_t)blockIdx.x * C.words);
+		/* global (not flat) pointers: a flat store counts on the LDS counter
+		 * too, so every histogram read would wait for the stores before it */
+		__attribute__((address_space(1))) unsigned long long *r =
+			(__attribute__((address_space(1))) unsigned long long *)(uintptr_t)(C.rows + (size_t)blockIdx.x * C.words);
+		const __attribute__((address_space(1))) uint32_t *qc =
+			(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)C.qcol;
 		const uint32_t nc = A.num_cos < C.ncos ? A.num_cos : C.ncos;
 		/* without hash queues each CoS owns one column; else its first */
-		auto col = [&](uint32_t c) { return 4u + C.ncos + (C.ident ? c : C.qcol[c]); };
+		auto col = [&](uint32_t c) { return 4u + C.ncos + qc[c]; };
 		const uint32_t ne = dlv[BIN_ERR], np = dlv[BIN_PDROP];
 		/* error packets are delivered to the error CoS unless it drops;
 		 * without an error CoS they are discards too */
 		const bool edeliv = ne && A.err_cos < nc && A.err_act != 1u;
 		uint32_t tot = 0u;
 
-		for (uint32_t k = k_first; k < (nc + 63u) / 64u * 64u; k += k_step) {
-			const uint32_t x = k < nc ? dlv[BIN_EXTRA + k] : 0u;
-			const uint32_t xe = x + (edeliv && k == A.err_cos ? ne : 0u);
+		/* the identity case (no hash queues) in a loop of its own without
+		 * loads: a load there would wait for every store before it */
+		auto flush_cols = [&](auto cf) {
+			for (uint32_t k = k_first; k < (nc + 63u) / 64u * 64u; k += k_step) {
+				const uint32_t x = k < nc ? dlv[BIN_EXTRA + k] : 0u;
+				const uint32_t xe = x + (edeliv && k == A.err_cos ? ne : 0u);
 
-			if (xe)
-				r[col(k)] = base[col(k)] + xe;
-			tot += x;
-		}
+				if (xe) {
+					const uint32_t cc = cf(k);
+
+					r[cc] = base[cc] + xe;
+				}
+				tot += x;
+			}
+		};
+
+		if (C.ident)
+			flush_cols([&](uint32_t k) { return 4u + C.ncos + k; });
+		else
+			flush_cols(col);
 		uint32_t t = wave_sum_u32(tot);            /* in_packets, in_octets */
 
 		if constexpr ((HW || L64_MG_BARRIER) && !L64_HW_LASTWAVE) {

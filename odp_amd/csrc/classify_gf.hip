@@ -312,6 +312,12 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 #ifndef GF_SWEEP            /* 1: one coalesced sweep of every frame byte per tile */
 #define GF_SWEEP 0
 #endif
+#ifndef GF_PAIR             /* chain-free groups probed two at a time */
+#define GF_PAIR 0
+#endif
+#ifndef GF_MARKS            /* tail-pass owners from an LDS mark map (else a */
+#define GF_MARKS 1          /* binary search of bpermutes) */
+#endif
 #ifndef GF_WIN_LATE         /* next tile's windows issued after the walk */
 #define GF_WIN_LATE 0
 #endif
@@ -543,6 +549,11 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	/* GF_SWEEP: the wave's x16 words and tail partials (2 x 64 dwords) */
 	uint32_t *swx = tb + ((A.L.lds_words + 1u) & ~1u) + (CM == 2 ? 2u * A.cnt_words : 0u) +
 			(threadIdx.x >> 6) * 128u;
+	/* GF_MARKS: the wave's 64-dword scratch of the tail pass's owner map
+	 * (seg_tail_sums4) */
+	uint32_t *marks = GF_MARKS ? tb + ((A.L.lds_words + 1u) & ~1u) + (CM == 2 ? 2u * A.cnt_words : 0u) +
+					     (GF_SWEEP ? GF_BLOCK * 2u : 0u) + (threadIdx.x >> 6) * 64u
+				   : nullptr;
 
 	const uint32_t lane = __lane_id();
 	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (GF_BLOCK / 64) +
@@ -592,7 +603,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			return 0u;
 		const L4Pend q = {0u, 0u, 64u, len};
 
-		return seg_tail_sums4(m, A.frames + d.x, q);
+		return seg_tail_sums4(m, A.frames + d.x, q, marks);
 	};
 	uint32_t tn = 0u;
 
@@ -612,8 +623,8 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 
 	if constexpr (CM == 2) {
 		C = *A.cnt;
-		const unsigned long long *r0 =
-			(const unsigned long long *)(C.rows + (size_t)blockIdx.x * C.words);
+		const __attribute__((address_space(1))) unsigned long long *r0 =
+			(const __attribute__((address_space(1))) unsigned long long *)(uintptr_t)(C.rows + (size_t)blockIdx.x * C.words);
 
 		for (uint32_t k = threadIdx.x; k < C.words; k += GF_BLOCK)
 			base[k] = r0[k];
@@ -846,7 +857,21 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 #else
 			if (__ballot(on)) {
 #endif
-				for (uint32_t gi = 0; gi < ngor; ++gi) {
+				uint32_t gi0 = 0;
+
+				if constexpr (GF_PAIR) {
+					/* two probes' LDS round trips in flight together */
+					for (; gi0 + 1u < ngor; gi0 += 2u) {
+						uint32_t m[NW], m2[NW];
+
+						probe(gi0, m);
+						probe(gi0 + 1u, m2);
+#pragma unroll
+						for (int w = 0; w < NW; ++w)
+							hm[w] |= m[w] | m2[w];
+					}
+				}
+				for (uint32_t gi = gi0; gi < ngor; ++gi) {
 					uint32_t m[NW];
 
 					probe(gi, m);
@@ -923,7 +948,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 #else
 			if (pm) {
 #endif
-				const uint32_t tail = seg_tail_sums4(pm, g, pd);
+				const uint32_t tail = seg_tail_sums4(pm, g, pd, marks);
 
 				if (ret == PARSE_PEND)
 					ret = finish_l4(p, pd, tail, (uint64_t)opt);
@@ -1115,7 +1140,9 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 						    cos >= A.num_cos ? GF_BIN_NOCOS :
 						    cret == 1 ? GF_BIN_DROP : GF_BIN_EXTRA + cos;
 
+#ifndef GF_EXP_NOBIN      /* experiment builds only: cost of the histogram adds */
 				atomicAdd(&dlv[bn], 1u);
+#endif
 				lane_oct += bn >= GF_BIN_EXTRA ? len : 0u;
 			}
 		}
@@ -1125,6 +1152,10 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		 * delivery counts into this workgroup's counter row: no barrier,
 		 * each wave counts itself done after its adds, the last one of the
 		 * workgroup flushes while the others have exited */
+#ifdef GF_EXP_NOFLUSH      /* experiment builds only: cost of the flush */
+		if (A.num != 12345u)
+			return;
+#endif
 		const uint64_t wo = (uint64_t)wave_sum_u32(lane_oct & 0xffffu) +
 				    ((uint64_t)wave_sum_u32(lane_oct >> 16) << 16);
 
@@ -1138,10 +1169,15 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		if ((uint32_t)__builtin_amdgcn_readfirstlane((int)prev) != GF_BLOCK / 64u - 1u)
 			return;
 		__threadfence_block();
-		unsigned long long *r = (unsigned long long *)(C.rows + (size_t)blockIdx.x * C.words);
+		/* global (not flat) pointers: a flat store counts on the LDS counter
+		 * too, so every histogram read would wait for the stores before it */
+		__attribute__((address_space(1))) unsigned long long *r =
+			(__attribute__((address_space(1))) unsigned long long *)(uintptr_t)(C.rows + (size_t)blockIdx.x * C.words);
+		const __attribute__((address_space(1))) uint32_t *qc =
+			(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)C.qcol;
 		const uint32_t nc = A.num_cos < C.ncos ? A.num_cos : C.ncos;
 		/* without hash queues each CoS owns one column */
-		auto col = [&](uint32_t c) { return 4u + C.ncos + (C.ident ? c : C.qcol[c]); };
+		auto col = [&](uint32_t c) { return 4u + C.ncos + qc[c]; };
 		const uint32_t ne = dlv[GF_BIN_ERR], np = dlv[GF_BIN_PDROP];
 		const uint32_t ec = A.error_cos < 0 ? 0xffffffffu : (uint32_t)A.error_cos;
 		/* error packets: delivered to the error CoS unless it drops;
@@ -1151,15 +1187,27 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 
 		/* plain stores of the row read at the start + the histogram (the
 		 * workgroup owns its row; launches on the stream are ordered) */
-		for (uint32_t k0 = 0; k0 < nc; k0 += 64u) {
-			const uint32_t k = k0 + lane;
-			const uint32_t x = k < nc ? dlv[GF_BIN_EXTRA + k] : 0u;
-			const uint32_t xe = x + (edeliv && k == ec ? ne : 0u);
+		/* the identity case (no hash queues) in a loop of its own without
+		 * loads: a load there would wait for every store before it */
+		auto flush_cols = [&](auto cf) {
+			for (uint32_t k0 = 0; k0 < nc; k0 += 64u) {
+				const uint32_t k = k0 + lane;
+				const uint32_t x = k < nc ? dlv[GF_BIN_EXTRA + k] : 0u;
+				const uint32_t xe = x + (edeliv && k == ec ? ne : 0u);
 
-			if (xe)
-				r[col(k)] = base[col(k)] + xe;
-			tot += x;
-		}
+				if (xe) {
+					const uint32_t cc = cf(k);
+
+					r[cc] = base[cc] + xe;
+				}
+				tot += x;
+			}
+		};
+
+		if (C.ident)
+			flush_cols([&](uint32_t k) { return 4u + C.ncos + k; });
+		else
+			flush_cols(col);
 		const uint32_t tp = wave_sum_u32(tot);                  /* in_packets */
 
 		if (lane == 0u) {
@@ -1196,7 +1244,7 @@ extern "C" size_t odpg_clsgf_lds(const odpg_launch_args *a)
 
 	return (size_t)GF_BLOCK * GF_RW * 4u + bins + (size_t)((L.lds_words + 1u) & ~1u) * 4u +
 	       (a->cnt.row ? (size_t)a->cnt.words * 8u : 0u) +
-	       (GF_SWEEP ? (size_t)GF_BLOCK * 2u * 4u : 0u);
+	       (GF_SWEEP ? (size_t)GF_BLOCK * 2u * 4u : 0u) + (GF_MARKS ? (size_t)GF_BLOCK * 4u : 0u);
 }
 
 extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s)

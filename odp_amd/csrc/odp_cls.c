@@ -1325,6 +1325,8 @@ int odp_pktio_stop(odp_pktio_t hdl)
 	else
 		p->started = 0;
 	UNLOCK();
+	if (!rc)
+		odpg_rt_pktio_drain(hdl);
 	return rc;
 }
 
@@ -1616,26 +1618,57 @@ static bind_t *bind_get_locked(pktio_e *p, odpg_ctx_t *ctx, int *rc)
 	return b;
 }
 
+/* a receive's hold on its binding (the launch's table and counters) */
+typedef struct recv_tok {
+	pktio_e *p;
+	bind_t *bd;
+} recv_tok_t;
+
+static void recv_release(pktio_e *p, bind_t *bd)
+{
+	LOCK();
+	if (--bd->refs == 0 && bd->stale) {
+		bind_t **pp = &p->binds;
+
+		while (*pp != bd)
+			pp = &(*pp)->next;
+		bind_fold_locked(p, bd);
+		*pp = bd->next;
+		bind_free(bd);
+	}
+	UNLOCK();
+}
+
+/* device_ptrs: 0 host buffers (staged copies), 1 device buffers, 2 pinned
+ * host buffers the kernel reads and writes in place (zero-copy). With a
+ * fence (zero-copy only) the launch is left running: the fence is recorded
+ * behind it and *tok holds the binding until odpg_cls_pktio_recv_end */
 static int recv_impl(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
 		     const odpg_desc_t *desc, uint32_t stride, uint32_t num,
-		     int device_ptrs, odpg_out_t *out, uint16_t *mark, odpg_meta_t *meta)
+		     int device_ptrs, odpg_out_t *out, uint16_t *mark, odpg_meta_t *meta,
+		     odpg_fence_t *fence, recv_tok_t **tok)
 {
 	int rc = 0;
 	odpg_batch_t b;
 	odpg_result_t res;
 	bind_t *bd;
+	recv_tok_t *t = NULL;
 
-	if (!ctx || !out)
+	if (!ctx || !out || (fence && (device_ptrs != 2 || !tok)))
 		return -EINVAL;
+	if (fence && !(t = malloc(sizeof(*t))))
+		return -ENOMEM;
 	LOCK();
 	pktio_e *p = get_pktio(hdl);
 
 	if (!p || !p->started) {
 		UNLOCK();
+		free(t);
 		return -EINVAL;
 	}
 	if (!(bd = bind_get_locked(p, ctx, &rc))) {
 		UNLOCK();
+		free(t);
 		return rc;
 	}
 	bd->refs++;
@@ -1659,45 +1692,65 @@ static int recv_impl(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
 	res.counters = bd->cnt;
 	rc = device_ptrs ? odpg_classify(ctx, bd->tbl, &b, &res)
 			 : odpg_classify_host(ctx, bd->tbl, &b, &res, 0);
-	/* zero-copy (device_ptrs 2: pinned host buffers the kernel reads and
-	 * writes in place): complete before the results are read and the
-	 * binding can go */
-	if (!rc && device_ptrs == 2)
-		rc = odpg_ctx_sync(ctx);
-
-	LOCK();
-	if (--bd->refs == 0 && bd->stale) {
-		bind_t **pp = &p->binds;
-
-		while (*pp != bd)
-			pp = &(*pp)->next;
-		bind_fold_locked(p, bd);
-		*pp = bd->next;
-		bind_free(bd);
+	if (!rc && fence)
+		rc = odpg_fence_record(ctx, fence);
+	if (!rc && fence) {
+		t->p = p;
+		t->bd = bd;
+		*tok = t;
+		return 0;
 	}
-	UNLOCK();
+	/* zero-copy: complete before the results are read and the binding
+	 * can go */
+	if (fence)
+		odpg_ctx_sync(ctx);
+	else if (!rc && device_ptrs == 2)
+		rc = odpg_ctx_sync(ctx);
+	free(t);
+	recv_release(p, bd);
 	return rc;
+}
+
+int odpg_cls_pktio_recv_start_zc(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
+				 const odpg_desc_t *desc, uint32_t num, odpg_out_t *out,
+				 odpg_meta_t *meta, odpg_fence_t *fence, void **token)
+{
+	if (!fence || !token)
+		return -EINVAL;
+	return recv_impl(hdl, ctx, frames, desc, 0, num, 2, out, NULL, meta, fence,
+			 (recv_tok_t **)token);
+}
+
+void odpg_cls_pktio_recv_end(void *token)
+{
+	recv_tok_t *t = token;
+
+	if (!t)
+		return;
+	recv_release(t->p, t->bd);
+	free(t);
 }
 
 int odpg_pktio_recv_batch(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
 			  const odpg_desc_t *desc, uint32_t stride, uint32_t num,
 			  int device_ptrs, odpg_out_t *out, uint16_t *mark)
 {
-	return recv_impl(hdl, ctx, frames, desc, stride, num, device_ptrs, out, mark, NULL);
+	return recv_impl(hdl, ctx, frames, desc, stride, num, device_ptrs, out, mark, NULL, NULL,
+			 NULL);
 }
 
 int odpg_cls_pktio_recv_meta(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
 			     const odpg_desc_t *desc, uint32_t num, odpg_out_t *out,
 			     odpg_meta_t *meta)
 {
-	return recv_impl(hdl, ctx, frames, desc, 0, num, 0, out, NULL, meta);
+	return recv_impl(hdl, ctx, frames, desc, 0, num, 0, out, NULL, meta, NULL, NULL);
 }
 
 int odpg_cls_pktio_recv_meta_zc(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t *frames,
 				const odpg_desc_t *desc, uint32_t num, odpg_out_t *out,
 				odpg_meta_t *meta)
 {
-	return recv_impl(hdl, ctx, frames, desc, 0, num, 2, out, NULL, meta);
+	return recv_impl(hdl, ctx, frames, desc, 0, num, 2, out, NULL, meta, NULL, NULL);
 }
 
 void odpg_cls_pktio_count(odp_pktio_t hdl, int64_t in_packets, int64_t in_octets,

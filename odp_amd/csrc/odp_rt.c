@@ -54,6 +54,7 @@
 #define RT_MAX_PKTIO 64
 #define RT_MAX_POOL  64
 #define RT_BURST     1024
+#define RT_INFLIGHT  4              /* receive bursts in flight per pktio */
 
 /* ---- objects -------------------------------------------------------------- */
 #define PKT_MAGIC 0x504b5452u
@@ -105,6 +106,19 @@ typedef struct rt_queue {
 } rt_queue_t;
 #define QUEUE_MAGIC 0x51554555u
 
+/* a receive burst's buffers (odp_rt.c "receive pipeline") */
+typedef struct rx_slot {
+	uint32_t n;                /* frames in the burst */
+	rt_pkt_t *src[RT_BURST];   /* loop device: the transmitted packets */
+	uint8_t *stage, *dstage;   /* frames (pinned host, and its device address) */
+	size_t stage_cap;
+	odpg_desc_t *desc, *ddesc;
+	odpg_out_t *out, *dout;
+	odpg_meta_t *meta, *dmeta;
+	odpg_fence_t *fence;       /* behind the burst's launch */
+	void *token;               /* the launch's binding (odpg_cls_pktio_recv_end) */
+} rx_slot_t;
+
 typedef struct rt_pktio {
 	int valid;
 	int in_mode;               /* odp_pktin_mode_t */
@@ -122,11 +136,11 @@ typedef struct rt_pktio {
 	rt_queue_t *outq;          /* pktout event queue (QUEUE mode) */
 	pthread_mutex_t ring_lock; /* the loop device's packets in flight */
 	rt_pkt_t *ring_head, *ring_tail;
+	uint32_t ring_n;           /* packets on the ring */
 	rt_pkt_t *ahead, *ahead_tail;  /* DIRECT mode: received (classified) packets
 				    * beyond what the last odp_pktin_recv asked for */
-	uint8_t *stage;            /* frames gathered for one launch (pinned host) */
-	uint8_t *dstage;           /* its device address: the kernel reads it in place */
-	size_t stage_cap;
+	struct rx_slot *slot[RT_INFLIGHT];  /* receive bursts ("receive pipeline") */
+	uint32_t rx_head, rx_count;  /* the bursts in flight: slots rx_head.. */
 } rt_pktio_t;
 
 #define LOOP_MTU 65535u            /* LOOP_MTU_MAX (pktio/loop.c:45) */
@@ -140,13 +154,8 @@ static struct {
 	rt_pktio_t pktio[RT_MAX_PKTIO];
 	rt_queue_t *sched;         /* scheduled queues */
 	uint32_t rr;
-	/* poll buffers: pinned host memory the classify launch reads (desc)
-	 * and writes (out, meta) in place, with their device addresses */
-	odpg_out_t *out, *dout;
-	odpg_meta_t *meta, *dmeta;
-	odpg_desc_t *desc, *ddesc;
 } rt = { PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, 0, NULL, {{0}}, {{0}},
-	 NULL, 0, NULL, NULL, NULL, NULL, NULL, NULL };
+	 NULL, 0 };
 
 /* pinned host memory and its device address (zero-copy launch buffers) */
 static int pinned_alloc(size_t bytes, void **host, void **dev)
@@ -161,15 +170,6 @@ static int pinned_alloc(size_t bytes, void **host, void **dev)
 	return 0;
 }
 
-static void poll_buffers_free(void)
-{
-	odpg_host_free_pinned(rt.out);
-	odpg_host_free_pinned(rt.meta);
-	odpg_host_free_pinned(rt.desc);
-	rt.out = rt.dout = NULL;
-	rt.meta = rt.dmeta = NULL;
-	rt.desc = rt.ddesc = NULL;
-}
 
 /* ---- init / threads ------------------------------------------------------- */
 /* thread ids: the lowest free id, given back at odp_term_local (odp_thread.c
@@ -187,40 +187,6 @@ void odp_init_param_init(odp_init_t *param)
 	param->mem_model = ODP_MEM_MODEL_THREAD;
 }
 
-int odp_init_global(odp_instance_t *instance, const odp_init_t *param, const void *platform)
-{
-	(void)param;
-	(void)platform;
-	pthread_mutex_lock(&rt.lock);
-	if (!rt.init) {
-		int rc = odpg_ctx_create(0, NULL, &rt.ctx);
-
-		if (rc) {
-			pthread_mutex_unlock(&rt.lock);
-			ERR("no MI355X context (odpg_ctx_create: %d): the classifier runs only on "
-			    "the GPU\n", rc);
-			return -1;
-		}
-		if (pinned_alloc(RT_BURST * sizeof(odpg_out_t), (void **)&rt.out, (void **)&rt.dout) ||
-		    pinned_alloc(RT_BURST * sizeof(odpg_meta_t), (void **)&rt.meta, (void **)&rt.dmeta) ||
-		    pinned_alloc(RT_BURST * sizeof(odpg_desc_t), (void **)&rt.desc, (void **)&rt.ddesc)) {
-			poll_buffers_free();
-			odpg_ctx_destroy(rt.ctx);
-			rt.ctx = NULL;
-			pthread_mutex_unlock(&rt.lock);
-			ERR("no pinned host memory for the receive buffers\n");
-			return -1;
-		}
-		rt.init = 1;
-	}
-	pthread_mutex_unlock(&rt.lock);
-	if (instance)
-		*instance = (odp_instance_t)(uintptr_t)&rt;
-	return 0;
-}
-
-static void parse_release(void);
-
 /* ODP_RT_PROF=1: receive-burst counts and times, printed by odp_term_global */
 static struct {
 	int on;
@@ -235,20 +201,51 @@ static uint64_t prof_ns(void)
 	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
+int odp_init_global(odp_instance_t *instance, const odp_init_t *param, const void *platform)
+{
+	(void)param;
+	(void)platform;
+	if (rxprof.on < 0)
+		rxprof.on = getenv("ODP_RT_PROF") && atoi(getenv("ODP_RT_PROF"));
+	pthread_mutex_lock(&rt.lock);
+	if (!rt.init) {
+		int rc = odpg_ctx_create(0, NULL, &rt.ctx);
+
+		if (rc) {
+			pthread_mutex_unlock(&rt.lock);
+			ERR("no MI355X context (odpg_ctx_create: %d): the classifier runs only on "
+			    "the GPU\n", rc);
+			return -1;
+		}
+		rt.init = 1;
+	}
+	pthread_mutex_unlock(&rt.lock);
+	if (instance)
+		*instance = (odp_instance_t)(uintptr_t)&rt;
+	return 0;
+}
+
+static void parse_release(void);
+
+static void rx_release(rt_pktio_t *p);
+
 int odp_term_global(odp_instance_t instance)
 {
 	(void)instance;
 	parse_release();
 	if (rxprof.on > 0 && rxprof.bursts)
 		fprintf(stderr, "odp_rt: %llu receive bursts, %.1f packets each; per burst: "
-			"staging %.2f us, GPU %.2f us, delivery %.2f us\n",
+			"staging %.2f us, launch (+ GPU wait in DIRECT mode) %.2f us, delivery %.2f us\n",
 			(unsigned long long)rxprof.bursts, (double)rxprof.pkts / rxprof.bursts,
 			rxprof.stage_ns / 1e3 / rxprof.bursts, rxprof.gpu_ns / 1e3 / rxprof.bursts,
 			rxprof.post_ns / 1e3 / rxprof.bursts);
+	pthread_mutex_lock(&rt.poll_lock);
+	for (int i = 0; i < RT_MAX_PKTIO; i++)
+		rx_release(&rt.pktio[i]);
+	pthread_mutex_unlock(&rt.poll_lock);
 	pthread_mutex_lock(&rt.lock);
 	if (rt.init) {
 		odpg_ctx_destroy(rt.ctx);
-		poll_buffers_free();
 		rt.ctx = NULL;
 		rt.init = 0;
 	}
@@ -1946,7 +1943,7 @@ void odpg_rt_pktio_close(odp_pktio_t hdl)
 			odp_packet_free((odp_packet_t)k);
 			k = nx;
 		}
-		odpg_host_free_pinned(p->stage);
+		rx_release(p);
 		pthread_mutex_destroy(&p->ring_lock);
 		memset(p, 0, sizeof(*p));
 	}
@@ -2019,75 +2016,126 @@ static void cos_enq(odp_cos_t cos, odp_queue_t q, odp_packet_t run[], int num)
 	}
 }
 
-/* the pktio's pinned staging buffer, at least `need` bytes */
-static int stage_reserve(rt_pktio_t *p, size_t need)
+/* ---- receive pipeline ----------------------------------------------------------
+ * A receive burst: the frames waiting on the loop device (or the next ones of
+ * the capture) gathered into a slot's pinned staging buffer, classified by one
+ * zero-copy launch (the kernel reads the frames and descriptors and writes the
+ * verdicts and parse metadata in place over PCIe: a burst is a few KiB), then
+ * delivered (loopback_recv's post-classification steps: CoS queues, pools,
+ * discards). The event-queue modes keep up to RT_INFLIGHT bursts in flight per
+ * pktio: a poll delivers the bursts whose fence has completed, oldest first,
+ * and launches the frames that have arrived meanwhile, without waiting for
+ * the GPU. DIRECT mode (odp_pktin_recv) launches and waits. */
+static rx_slot_t *slot_get(rt_pktio_t *p, uint32_t i)
+{
+	rx_slot_t *s = p->slot[i];
+
+	if (s)
+		return s;
+	if (!(s = calloc(1, sizeof(*s))))
+		return NULL;
+	if (pinned_alloc(RT_BURST * sizeof(odpg_desc_t), (void **)&s->desc, (void **)&s->ddesc) ||
+	    pinned_alloc(RT_BURST * sizeof(odpg_out_t), (void **)&s->out, (void **)&s->dout) ||
+	    pinned_alloc(RT_BURST * sizeof(odpg_meta_t), (void **)&s->meta, (void **)&s->dmeta) ||
+	    odpg_fence_create(rt.ctx, &s->fence)) {
+		odpg_host_free_pinned(s->desc);
+		odpg_host_free_pinned(s->out);
+		odpg_host_free_pinned(s->meta);
+		free(s);
+		ERR("no pinned host memory for a receive burst\n");
+		return NULL;
+	}
+	p->slot[i] = s;
+	return s;
+}
+
+static void slots_free(rt_pktio_t *p)
+{
+	for (uint32_t i = 0; i < RT_INFLIGHT; i++) {
+		rx_slot_t *s = p->slot[i];
+
+		if (!s)
+			continue;
+		odpg_fence_destroy(s->fence);
+		odpg_host_free_pinned(s->desc);
+		odpg_host_free_pinned(s->out);
+		odpg_host_free_pinned(s->meta);
+		odpg_host_free_pinned(s->stage);
+		free(s);
+		p->slot[i] = NULL;
+	}
+	p->rx_head = p->rx_count = 0;
+}
+
+static void rx_drop(struct rx_slot *s);
+
+/* the bursts in flight waited for and dropped, the slots freed (close,
+ * termination) */
+static void rx_release(rt_pktio_t *p)
+{
+	while (p->rx_count) {
+		rx_slot_t *s = p->slot[p->rx_head];
+
+		odpg_fence_wait(s->fence);
+		odpg_cls_pktio_recv_end(s->token);
+		s->token = NULL;
+		rx_drop(s);
+		p->rx_head = (p->rx_head + 1u) % RT_INFLIGHT;
+		p->rx_count--;
+	}
+	slots_free(p);
+}
+
+/* the slot's pinned staging buffer, at least `need` bytes */
+static int stage_reserve(rx_slot_t *s, size_t need)
 {
 	uint8_t *b = NULL, *db = NULL;
 
-	if (need <= p->stage_cap)
+	if (need <= s->stage_cap)
 		return 0;
 	need = need < (64u << 10) ? (64u << 10) : need;
 	if (pinned_alloc(need, (void **)&b, (void **)&db))
 		return -1;
-	odpg_host_free_pinned(p->stage);
-	p->stage = b;
-	p->dstage = db;
-	p->stage_cap = need;
+	odpg_host_free_pinned(s->stage);
+	s->stage = b;
+	s->dstage = db;
+	s->stage_cap = need;
 	return 0;
 }
 
-/* One burst of the pktio's input through the GPU classifier (loopback_recv,
- * pktio/loop.c:304-374; pcapif_recv_pkt + the same classify step). Packets
- * with a CoS are enqueued on its queue; with the classifier disabled
- * (ODPG_COS_NOCLS) they are returned in pkts[]. *nret = packets returned.
- * Returns the frames taken from the input (0: none waiting), or -1.
- * Caller holds rt.poll_lock (the launch buffers are shared). */
-static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num, int *nret)
+/* up to `num` waiting frames into the slot; returns how many (0: none, or
+ * no staging memory: the loop device's frames are then dropped) */
+static uint32_t rx_stage(rt_pktio_t *p, rx_slot_t *s, uint32_t num)
 {
-	rt_pkt_t *src[RT_BURST];
-	odp_packet_t run[RT_BURST];
-	const uint8_t *frames;
-	uint32_t n = 0, first = 0;
-	int nrun = 0;
-	odp_cos_t run_cos = ODP_COS_INVALID;
-	odp_queue_t run_q = ODP_QUEUE_INVALID;
-
-	*nret = 0;
-	if (num > RT_BURST)
-		num = RT_BURST;
-	if (num <= 0 || !rt.init || !odpg_cls_pktio_started(hdl))
-		return 0;
-	const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
+	uint32_t n = 0;
+	size_t need = 0, off = 0;
 
 	if (p->loopdev) {
-		size_t need = 0, off = 0;
-
 		pthread_mutex_lock(&p->ring_lock);
-		while (n < (uint32_t)num && p->ring_head) {
-			src[n] = p->ring_head;
+		while (n < num && p->ring_head) {
+			s->src[n] = p->ring_head;
 			p->ring_head = p->ring_head->next;
-			need += ALIGN64(src[n]->len);
+			need += ALIGN64(s->src[n]->len);
 			n++;
 		}
 		if (!p->ring_head)
 			p->ring_tail = NULL;
+		p->ring_n -= n;
 		pthread_mutex_unlock(&p->ring_lock);
 		if (!n)
 			return 0;
-		if (stage_reserve(p, need)) {
+		if (stage_reserve(s, need)) {
 			for (uint32_t k = 0; k < n; k++)
-				odp_packet_free((odp_packet_t)src[k]);
-			return -1;
+				odp_packet_free((odp_packet_t)s->src[k]);
+			return 0;
 		}
 		for (uint32_t k = 0; k < n; k++) {
-			memcpy(p->stage + off, src[k]->data, src[k]->len);
-			rt.desc[k].offset = (uint32_t)off;
-			rt.desc[k].len = src[k]->len;
-			off += ALIGN64(src[k]->len);
+			memcpy(s->stage + off, s->src[k]->data, s->src[k]->len);
+			s->desc[k].offset = (uint32_t)off;
+			s->desc[k].len = s->src[k]->len;
+			off += ALIGN64(s->src[k]->len);
 		}
 	} else if (p->have_cap) {
-		size_t need = 0, off = 0;
-
 		if (p->pos >= p->cap.num) {
 			/* _pcapif_reopen: loops = 0 repeats forever, else the
 			 * capture is read again while ++loop_cnt < loops */
@@ -2095,48 +2143,65 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 				return 0;
 			p->pos = 0;
 		}
-		first = p->pos;
-		n = p->cap.num - first < (uint32_t)num ? p->cap.num - first : (uint32_t)num;
+		const uint32_t first = p->pos;
+
+		n = p->cap.num - first < num ? p->cap.num - first : num;
 		if (!n)
 			return 0;
 		for (uint32_t k = 0; k < n; k++)
 			need += ALIGN64(p->cap.desc[first + k].len);
-		if (stage_reserve(p, need))
-			return -1;
+		if (stage_reserve(s, need))
+			return 0;
 		for (uint32_t k = 0; k < n; k++) {
 			const odpg_desc_t d = p->cap.desc[first + k];
 
-			memcpy(p->stage + off, p->cap.frames + d.offset, d.len);
-			rt.desc[k].offset = (uint32_t)off;
-			rt.desc[k].len = d.len;
+			memcpy(s->stage + off, p->cap.frames + d.offset, d.len);
+			s->desc[k].offset = (uint32_t)off;
+			s->desc[k].len = d.len;
+			s->src[k] = NULL;
 			off += ALIGN64(d.len);
 		}
-	} else {
-		return 0;
+		p->pos += n;
 	}
-	/* zero-copy: the launch reads the staged frames and descriptors and
-	 * writes the verdicts and metadata in pinned host memory (a burst is a
-	 * few KiB: copies would cost more than the PCIe reads) */
-	frames = p->stage;
-	if (rxprof.on < 0)
-		rxprof.on = getenv("ODP_RT_PROF") && atoi(getenv("ODP_RT_PROF"));
-	const uint64_t t1 = rxprof.on ? prof_ns() : 0;
+	s->n = n;
+	return n;
+}
 
-	if (odpg_cls_pktio_recv_meta_zc(hdl, rt.ctx, p->dstage, rt.ddesc, n, rt.dout, rt.dmeta)) {
+static void rx_drop(rx_slot_t *s)
+{
+	for (uint32_t k = 0; k < s->n; k++)
+		if (s->src[k])
+			odp_packet_free((odp_packet_t)s->src[k]);
+	s->n = 0;
+}
+
+static int rx_launch(odp_pktio_t hdl, rx_slot_t *s)
+{
+	if (odpg_cls_pktio_recv_start_zc(hdl, rt.ctx, s->dstage, s->ddesc, s->n, s->dout, s->dmeta,
+					 s->fence, &s->token)) {
 		ERR("classify failed\n");
-		if (p->loopdev)
-			for (uint32_t k = 0; k < n; k++)
-				odp_packet_free((odp_packet_t)src[k]);
+		rx_drop(s);
 		return -1;
 	}
-	const uint64_t t2 = rxprof.on ? prof_ns() : 0;
+	return 0;
+}
 
-	if (!p->loopdev)
-		p->pos += n;
-	for (uint32_t k = 0; k < n; k++) {
-		const uint32_t w = rt.out[k];
-		const uint32_t len = rt.desc[k].len;
-		rt_pkt_t *have = p->loopdev ? src[k] : NULL;
+/* a completed burst: verdicts to CoS queues and pools; packets without a
+ * CoS queue go to pkts[] */
+static void rx_deliver(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, odp_packet_t pkts[],
+		       int *nret)
+{
+	odp_packet_t run[RT_BURST];
+	int nrun = 0;
+	odp_cos_t run_cos = ODP_COS_INVALID;
+	odp_queue_t run_q = ODP_QUEUE_INVALID;
+
+	odpg_cls_pktio_recv_end(s->token);
+	s->token = NULL;
+	for (uint32_t k = 0; k < s->n; k++) {
+		const uint32_t w = s->out[k];
+		const uint32_t len = s->desc[k].len;
+		rt_pkt_t *have = s->src[k];
 		odp_cos_t cos = ODP_COS_INVALID;
 		odp_queue_t q = ODP_QUEUE_INVALID;
 		odp_pool_t pool = p->pool;
@@ -2158,7 +2223,7 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 			/* into the CoS's pool (_odp_pktio_packet_to_pool) */
 			pkt = odp_packet_alloc(pool, len);
 			if (pkt != ODP_PACKET_INVALID)
-				memcpy(PK(pkt)->data, frames + rt.desc[k].offset, len);
+				memcpy(PK(pkt)->data, s->stage + s->desc[k].offset, len);
 			if (have)
 				odp_packet_free((odp_packet_t)have);
 			if (pkt == ODP_PACKET_INVALID) {
@@ -2173,7 +2238,7 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 				continue;
 			}
 		}
-		PK(pkt)->meta = rt.meta[k];
+		PK(pkt)->meta = s->meta[k];
 		PK(pkt)->cos = cos;
 		PK(pkt)->input = hdl;
 		if (q == ODP_QUEUE_INVALID) {
@@ -2190,29 +2255,121 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 		run[nrun++] = pkt;
 	}
 	cos_enq(run_cos, run_q, run, nrun);
-	if (rxprof.on) {            /* the callers hold rt.poll_lock */
-		const uint64_t t3 = prof_ns();
+	s->n = 0;
+}
 
-		rxprof.bursts++;
-		rxprof.pkts += n;
-		rxprof.stage_ns += t1 - t0;
-		rxprof.gpu_ns += t2 - t1;
-		rxprof.post_ns += t3 - t2;
-	}
+static void prof_add(uint64_t bursts, uint64_t pkts, uint64_t t0, uint64_t t1, uint64_t t2,
+		     uint64_t t3)
+{
+	rxprof.bursts += bursts;
+	rxprof.pkts += pkts;
+	rxprof.stage_ns += t1 - t0;
+	rxprof.gpu_ns += t2 - t1;
+	rxprof.post_ns += t3 - t2;
+}
+
+/* DIRECT mode: one burst, launched and waited for. Returns the frames taken
+ * (< 0 on a failed launch); *nret packets without a CoS queue in pkts[] */
+static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num, int *nret)
+{
+	rx_slot_t *s;
+
+	*nret = 0;
+	if (num > RT_BURST)
+		num = RT_BURST;
+	if (num <= 0 || !rt.init || !odpg_cls_pktio_started(hdl) || !(s = slot_get(p, 0)))
+		return 0;
+	const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
+	const uint32_t n = rx_stage(p, s, (uint32_t)num);
+
+	if (!n)
+		return 0;
+	const uint64_t t1 = rxprof.on > 0 ? prof_ns() : 0;
+
+	if (rx_launch(hdl, s))
+		return -1;
+	odpg_fence_wait(s->fence);
+	const uint64_t t2 = rxprof.on > 0 ? prof_ns() : 0;
+
+	rx_deliver(p, hdl, s, pkts, nret);
+	if (rxprof.on > 0)
+		prof_add(1, n, t0, t1, t2, prof_ns());
 	return (int)n;
 }
 
-/* a burst of a QUEUE / SCHED mode pktio onto its pktin event queue */
-static int rx_to_inq(rt_pktio_t *p, odp_pktio_t hdl)
+/* a delivered burst's packets without a CoS queue onto the pktin event queue */
+static void to_inq(rt_pktio_t *p, odp_packet_t pkts[], int nret)
 {
-	odp_packet_t pkts[RT_BURST];
-	int nret;
-	const int took = rx_burst(p, hdl, pkts, RT_BURST, &nret);
-
 	if (nret > 0 && (!p->inq || odp_queue_enq_multi(p->inq->hdl, (const odp_event_t *)pkts,
 							 nret) != nret))
 		odp_packet_free_multi(pkts, nret);
-	return took;
+}
+
+/* QUEUE / SCHED mode: deliver the completed bursts (all of them with
+ * `drain`, waiting), then launch what has arrived. A new burst waits for
+ * RT_BURST / 4 frames while another is in flight, so that launches stay
+ * few at high rates and latency stays one launch at low ones. Returns the
+ * frames delivered or launched (0: nothing to do) */
+static int rx_to_inq(rt_pktio_t *p, odp_pktio_t hdl, int drain)
+{
+	odp_packet_t pkts[RT_BURST];
+	int got = 0;
+
+	if (!rt.init)
+		return 0;
+	while (p->rx_count) {
+		rx_slot_t *s = p->slot[p->rx_head];
+		int nret = 0;
+
+		if (drain)
+			odpg_fence_wait(s->fence);
+		else if (odpg_fence_query(s->fence) == 0)
+			break;
+		const uint64_t t2 = rxprof.on > 0 ? prof_ns() : 0;
+
+		got += (int)s->n;
+		rx_deliver(p, hdl, s, pkts, &nret);
+		to_inq(p, pkts, nret);
+		if (rxprof.on > 0)
+			prof_add(0, 0, 0, 0, t2, prof_ns());
+		p->rx_head = (p->rx_head + 1u) % RT_INFLIGHT;
+		p->rx_count--;
+	}
+	while (!drain && p->rx_count < RT_INFLIGHT && odpg_cls_pktio_started(hdl)) {
+		if (p->loopdev && p->rx_count &&
+		    __atomic_load_n(&p->ring_n, __ATOMIC_RELAXED) < RT_BURST / 4u)
+			break;
+		rx_slot_t *s = slot_get(p, (p->rx_head + p->rx_count) % RT_INFLIGHT);
+
+		if (!s)
+			break;
+		const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
+		const uint32_t n = rx_stage(p, s, RT_BURST);
+
+		if (!n)
+			break;
+		const uint64_t t1 = rxprof.on > 0 ? prof_ns() : 0;
+
+		if (rx_launch(hdl, s))
+			break;
+		if (rxprof.on > 0)
+			prof_add(1, n, t0, t1, prof_ns(), prof_ns());
+		p->rx_count++;
+		got += (int)n;
+	}
+	return got;
+}
+
+/* odp_pktio_stop: the bursts in flight are delivered (they were received
+ * before the stop) */
+void odpg_rt_pktio_drain(odp_pktio_t hdl)
+{
+	pthread_mutex_lock(&rt.poll_lock);
+	rt_pktio_t *p = get_rt_pktio(hdl);
+
+	if (p)
+		rx_to_inq(p, hdl, 1);
+	pthread_mutex_unlock(&rt.poll_lock);
 }
 
 static void pktin_queue_fill(odp_pktio_t hdl)
@@ -2221,7 +2378,7 @@ static void pktin_queue_fill(odp_pktio_t hdl)
 	rt_pktio_t *p = get_rt_pktio(hdl);
 
 	if (p && p->in_mode == ODP_PKTIN_MODE_QUEUE)
-		rx_to_inq(p, hdl);
+		rx_to_inq(p, hdl, 0);
 	pthread_mutex_unlock(&rt.poll_lock);
 }
 
@@ -2238,7 +2395,7 @@ static int poll_input(void)
 
 		if (!p->valid || p->in_mode != ODP_PKTIN_MODE_SCHED)
 			continue;
-		const int took = rx_to_inq(p, (odp_pktio_t)(uintptr_t)(i + 1));
+		const int took = rx_to_inq(p, (odp_pktio_t)(uintptr_t)(i + 1), 0);
 
 		if (took > 0)
 			got += took;
@@ -2600,6 +2757,7 @@ static int pktout_send_impl(odp_pktio_t pktio, const odp_packet_t packets[], int
 				p->ring_head = k;
 			p->ring_tail = k;
 		}
+		p->ring_n += (uint32_t)n;
 		pthread_mutex_unlock(&p->ring_lock);
 	} else {
 		odp_packet_free_multi(packets, n);

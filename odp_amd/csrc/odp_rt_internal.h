@@ -18,6 +18,8 @@
 int  odpg_rt_pktio_open(odp_pktio_t pktio, const char *name, odp_pool_t pool,
 			const odp_pktio_param_t *param);
 void odpg_rt_pktio_close(odp_pktio_t pktio);
+/* odp_rt.c: odp_pktio_stop delivers the receive bursts still in flight */
+void odpg_rt_pktio_drain(odp_pktio_t pktio);
 /* odp_rt.c: odp_pktin_queue_config's input queues (the event queue of
  * SCHED / QUEUE mode); 0 or -1 (too many queues) */
 int  odpg_rt_pktin_config(odp_pktio_t pktio, uint32_t num_queues);
@@ -32,6 +34,14 @@ int odpg_cls_pktio_recv_meta(odp_pktio_t pktio, odpg_ctx_t *ctx, const uint8_t *
 int odpg_cls_pktio_recv_meta_zc(odp_pktio_t pktio, odpg_ctx_t *ctx, const uint8_t *frames,
 			     const odpg_desc_t *desc, uint32_t num, odpg_out_t *out,
 			     odpg_meta_t *meta);
+/* its asynchronous form: launches, records `fence` behind the launch and
+ * returns a token holding the pktio's binding; the results are valid once
+ * the fence has completed, and odpg_cls_pktio_recv_end(token) then lets the
+ * binding go (every started receive must be ended) */
+int odpg_cls_pktio_recv_start_zc(odp_pktio_t pktio, odpg_ctx_t *ctx, const uint8_t *frames,
+				 const odpg_desc_t *desc, uint32_t num, odpg_out_t *out,
+				 odpg_meta_t *meta, odpg_fence_t *fence, void **token);
+void odpg_cls_pktio_recv_end(void *token);
 /* the pktio is started (with the classifier enabled) */
 int odpg_cls_pktio_started(odp_pktio_t pktio);
 int odpg_cls_pktio_classifies(odp_pktio_t pktio);

@@ -821,6 +821,19 @@ __device__ __forceinline__ uint32_t seg_tail_sums(uint64_t m, const uint8_t *g, 
 	return mine ? oc_fold(acc) : 0u;
 }
 
+/* inclusive prefix max over the 64 lanes (wave_scan_u32's DPP steps with
+ * max); every lane must be active */
+__device__ __forceinline__ uint32_t wave_max_scan_u32(uint32_t x)
+{
+	x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true));
+	x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true));
+	x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true));
+	x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true));
+	x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+	x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+	return x;
+}
+
 /* lane `src`'s value of v (ds_bpermute; every lane active) */
 __device__ __forceinline__ uint32_t lane_pull(uint32_t v, uint32_t src)
 {
@@ -1191,7 +1204,40 @@ __device__ __forceinline__ uint32_t sweep_frames(const uint8_t *g, uint32_t len,
 #ifndef SEG4_PIPE
 #define SEG4_PIPE 1
 #endif
-__device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g, const L4Pend &pd)
+#ifndef SEG4_TAILW          /* last units by whole-word compares (unit_sum_head) */
+#define SEG4_TAILW 1
+#endif
+
+/* sum of bytes [0, re) of the 64-byte unit at addr (16-byte aligned),
+ * 1 <= re <= 64, as 16-bit halves: words below re / 4 by a compare each,
+ * the word holding the last byte read again as a dword and masked (its 16
+ * bytes were just loaded). unit_sum_masked's result for lead 0 at a third
+ * of its instructions. */
+__device__ __forceinline__ uint32_t unit_sum_head(uint64_t addr, uint32_t re)
+{
+	const uint32_t nw = re >> 2, pb = re & 3u;
+	uint32_t acc = 0u;
+
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		uint4 q = make_uint4(0u, 0u, 0u, 0u);
+
+		if (16u * k < re)
+			q = ld_g16(addr + 16u * k);
+		acc = tail_dot2(4 * k + 0 < (int)nw ? q.x : 0u, acc);
+		acc = tail_dot2(4 * k + 1 < (int)nw ? q.y : 0u, acc);
+		acc = tail_dot2(4 * k + 2 < (int)nw ? q.z : 0u, acc);
+		acc = tail_dot2(4 * k + 3 < (int)nw ? q.w : 0u, acc);
+	}
+	if (pb) {
+		const uint32_t w = *(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)(addr + 4u * nw);
+
+		acc = tail_dot2(w & ((1u << (8u * pb)) - 1u), acc);
+	}
+	return acc;
+}
+__device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g, const L4Pend &pd,
+						uint32_t *marks = nullptr)
 {
 #ifdef ODPG_EXP_NOTAIL
 	return 0u;
@@ -1209,11 +1255,21 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 
 	/* the lane's own units: last (masked to b, and to a when it is the
 	 * first), then the first when it carries a lead */
+#ifdef SEG4_EXP_NOOWN       /* experiment builds only: cost of the own units */
+	if (mine && pd.b == 12345u) {
+#else
 	if (mine) {
+#endif
 		const uint32_t lu = nu - 1u;
 
-		own = unit_sum_masked(gb + 64ull * lu, lu ? 0 : (int)lead,
-				      (int)(pd.b - c0 - 64u * lu));
+		/* every last unit starting at its first byte (C3's early tails
+		 * always): whole words by a compare each, the partial one read
+		 * again as a dword (a cache hit) */
+		if (SEG4_TAILW && !__ballot(mine && lead != 0u && lu == 0u))
+			own = unit_sum_head(gb + 64ull * lu, pd.b - c0 - 64u * lu);
+		else
+			own = unit_sum_masked(gb + 64ull * lu, lu ? 0 : (int)lead,
+					      (int)(pd.b - c0 - 64u * lu));
 		if (own_first)
 			own = oc_add(own, unit_sum_masked(gb, (int)lead, 64));
 	}
@@ -1230,6 +1286,33 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 	 * search of incl over the lanes that can own a slot of the pass */
 	auto owner = [&](uint32_t base) -> uint64_t {
 		const uint32_t slot = min(base + lane, total - 1u);
+#ifdef SEG4_EXP_NOOWNER     /* experiment builds only: cost of the owner search */
+		return (((uint64_t)cb_hi << 32) | cb_lo) + 64ull * slot;
+#endif
+		if (marks) {
+			/* with a wave's 64-dword LDS scratch: every frame with a
+			 * slot in the pass marks the lane of its first one (the
+			 * frame running into the pass marks lane 0) with its own
+			 * lane + 1, and a prefix max spreads the marks over the
+			 * frame's lanes (one LDS round trip instead of the
+			 * search's dependent bpermutes; LDS operations of a wave
+			 * complete in order) */
+			const bool in = ni && incl > base && first < base + 64u;
+			/* volatile: lanes read what other lanes wrote, which the
+			 * compiler's per-thread view would forward or drop */
+			volatile __attribute__((address_space(3))) uint32_t *mk =
+				(volatile __attribute__((address_space(3))) uint32_t *)marks;
+
+			mk[lane] = 0u;
+			__builtin_amdgcn_wave_barrier();
+			if (in)
+				mk[first > base ? first - base : 0u] = lane + 1u;
+			__builtin_amdgcn_wave_barrier();
+			const uint32_t o = wave_max_scan_u32(mk[lane]) - 1u;
+
+			return (((uint64_t)lane_pull(cb_hi, o) << 32) | lane_pull(cb_lo, o)) +
+			       64ull * slot;
+		}
 		const uint64_t past = __ballot(incl > base);
 		const uint64_t beyond = __ballot(incl > base + 63u);
 		const uint32_t lo = past ? (uint32_t)__builtin_ctzll(past) : 63u;
@@ -1262,6 +1345,10 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 			s = tail_dot2(q[k].z, s);
 			s = tail_dot2(q[k].w, s);
 		}
+#ifdef SEG4_EXP_NOSCAN      /* experiment builds only: cost of the pass attribution */
+		acc += s;
+		return;
+#endif
 		const uint32_t ps = wave_scan_u32(base + lane < total ? oc_fold(s) : 0u);
 		const bool in = ni && incl > base && first < base + 64u;
 		const uint32_t fl = in && first > base ? first - base : 0u;

@@ -10,6 +10,7 @@
 #include <string.h>
 #include <stdlib.h>
 #include <mutex>
+#include <new>
 #include <vector>
 
 #include "../../include/odpg.h"
@@ -1075,6 +1076,63 @@ int odpg_event_record(odpg_ctx_t *c, int slot)
 		return -EINVAL;
 	HIPCHK(hipEventRecord(c->ev[slot], c->stream));
 	return 0;
+}
+
+struct odpg_fence_s {
+	hipEvent_t ev;
+	int device;
+};
+
+int odpg_fence_create(odpg_ctx_t *c, odpg_fence_t **fence)
+{
+	if (!c || !fence)
+		return -EINVAL;
+	odpg_fence_t *f = new (std::nothrow) odpg_fence_t;
+
+	if (!f)
+		return -ENOMEM;
+	f->device = c->device;
+	hipSetDevice(c->device);
+	if (hipEventCreateWithFlags(&f->ev, hipEventDisableTiming) != hipSuccess) {
+		delete f;
+		return -EIO;
+	}
+	*fence = f;
+	return 0;
+}
+
+int odpg_fence_record(odpg_ctx_t *c, odpg_fence_t *f)
+{
+	if (!c || !f || f->device != c->device)
+		return -EINVAL;
+	HIPCHK(hipEventRecord(f->ev, c->stream));
+	return 0;
+}
+
+int odpg_fence_query(odpg_fence_t *f)
+{
+	if (!f)
+		return -EINVAL;
+	const hipError_t e = hipEventQuery(f->ev);
+
+	return e == hipSuccess ? 1 : e == hipErrorNotReady ? 0 : -EIO;
+}
+
+int odpg_fence_wait(odpg_fence_t *f)
+{
+	if (!f)
+		return -EINVAL;
+	HIPCHK(hipEventSynchronize(f->ev));
+	return 0;
+}
+
+void odpg_fence_destroy(odpg_fence_t *f)
+{
+	if (!f)
+		return;
+	hipSetDevice(f->device);
+	hipEventDestroy(f->ev);
+	delete f;
 }
 
 int odpg_event_elapsed_ms(odpg_ctx_t *c, int a, int b, float *ms)

@@ -6,6 +6,7 @@ numpy arrays in and out of HBM through the library's own helpers.
 from __future__ import annotations
 
 import ctypes as C
+import sys
 
 import numpy as np
 
@@ -39,10 +40,13 @@ class DeviceBuffer:
 
     def free(self):
         if self.ptr:
-            lib.odpg_dev_free(self.ctx.h, self.ptr)
+            if self.ctx.h:
+                lib.odpg_dev_free(self.ctx.h, self.ptr)
             self.ptr = None
 
     def __del__(self):
+        if sys.is_finalizing():   # the HIP runtime may be torn down already
+            return
         try:
             self.free()
         except Exception:
@@ -75,6 +79,8 @@ class Table:
         self.has_cycle = bool(lib.odpg_table_has_cycle(self.h))
 
     def __del__(self):
+        if sys.is_finalizing():   # the HIP runtime may be torn down already
+            return
         try:
             if self.h:
                 lib.odpg_table_destroy(self.h)
@@ -91,6 +97,7 @@ class Counters:
         h = C.c_void_p()
         L.check(lib.odpg_counters_create(ctx.h, table.h, C.byref(h)), "odpg_counters_create")
         self.h = h.value
+        self.ctx = ctx          # counters are destroyed before their context
         self.num_cos = table.num_cos
         self.words = 4 + self.num_cos + self.num_cos * L.COS_QUEUE_MAX
 
@@ -107,10 +114,13 @@ class Counters:
 
     def close(self):
         if self.h:
-            lib.odpg_counters_destroy(self.h)
+            if self.ctx.h:      # after the context: leaked to process exit
+                lib.odpg_counters_destroy(self.h)
             self.h = None
 
     def __del__(self):
+        if sys.is_finalizing():   # the HIP runtime may be torn down already
+            return
         try:
             self.close()
         except Exception:
@@ -133,6 +143,8 @@ class Context:
             self.h = None
 
     def __del__(self):
+        if sys.is_finalizing():   # the HIP runtime may be torn down already
+            return
         try:
             self.close()
         except Exception:
@@ -277,6 +289,8 @@ class Forwarder:
         self.h = h.value
 
     def __del__(self):
+        if sys.is_finalizing():   # the HIP runtime may be torn down already
+            return
         try:
             if self.h:
                 lib.odpg_fwd_destroy(self.h)
