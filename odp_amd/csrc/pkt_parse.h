@@ -1204,8 +1204,8 @@ __device__ __forceinline__ uint32_t sweep_frames(const uint8_t *g, uint32_t len,
 #ifndef SEG4_PIPE
 #define SEG4_PIPE 1
 #endif
-#ifndef SEG4_TAILW          /* last units by whole-word compares (unit_sum_head) */
-#define SEG4_TAILW 1
+#ifndef SEG4_TAILW          /* last units by whole-word compares (unit_sum_head): */
+#define SEG4_TAILW 0        /* fewer VALU but a dependent reload; C3 +1.5 us */
 #endif
 
 /* sum of bytes [0, re) of the 64-byte unit at addr (16-byte aligned),
