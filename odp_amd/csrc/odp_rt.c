@@ -2331,7 +2331,7 @@ static int rx_to_inq(rt_pktio_t *p, odp_pktio_t hdl, int drain)
 		rx_deliver(p, hdl, s, pkts, &nret);
 		to_inq(p, pkts, nret);
 		if (rxprof.on > 0)
-			prof_add(0, 0, 0, 0, t2, prof_ns());
+			prof_add(0, 0, t2, t2, t2, prof_ns());
 		p->rx_head = (p->rx_head + 1u) % RT_INFLIGHT;
 		p->rx_count--;
 	}
@@ -2352,8 +2352,11 @@ static int rx_to_inq(rt_pktio_t *p, odp_pktio_t hdl, int drain)
 
 		if (rx_launch(hdl, s))
 			break;
-		if (rxprof.on > 0)
-			prof_add(1, n, t0, t1, prof_ns(), prof_ns());
+		if (rxprof.on > 0) {
+			const uint64_t t2 = prof_ns();
+
+			prof_add(1, n, t0, t1, t2, t2);
+		}
 		p->rx_count++;
 		got += (int)n;
 	}

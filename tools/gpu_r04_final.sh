@@ -50,6 +50,18 @@ if [ "${EXTRAS:-1}" = 1 ]; then
   step "bench default" timeout -k 10 600 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err
   cat $OUT/bench_default.json
   step "odp_bench_cls_gpu" timeout -k 10 300 odp_amd/lib/odp_bench_cls_gpu > $OUT/odp_bench_cls_gpu.txt 2>&1
+  # C5 with only the rewritten 32 bytes of each frame stored (experiment
+  # build FWD_COALW=1): its HBM traffic and time against the full-sector store
+  if [ -f odp_amd/lib/exp_fwd32/libodpg.so ]; then
+    for c in FETCH_SIZE WRITE_SIZE; do
+      step "pmc c5w32 $c" env ODPG_LIB=odp_amd/lib/exp_fwd32/libodpg.so timeout -k 10 300 rocprofv3 --pmc $c \
+        --output-format csv -d $OUT/pmc_c5w32/pmc_$c -o run \
+        -- python3 bench.py --no-cpu --no-stats --config c5 --steps 20 --warmup 2 --runs 1 > $OUT/pmc_c5w32_$c.log 2>&1
+    done
+    python tools/pmc_summary.py $OUT/pmc_c5w32 > $OUT/pmc_c5w32_summary.json
+    step "bench c5w32" env ODPG_LIB=odp_amd/lib/exp_fwd32/libodpg.so timeout -k 10 600 python bench.py --no-cpu \
+      --config c5 > $OUT/bench_c5w32.json 2> $OUT/bench_c5w32.err
+  fi
   for a in "" "-c 4"; do
     tag=$(echo "x$a" | tr -d ' -')
     step "pktio_perf $a" env ODP_RT_PROF=1 timeout -k 10 240 oracle/_ref/odp_pktio_perf -v $a > $OUT/pktio_perf_$tag.txt 2>&1
