@@ -1083,6 +1083,26 @@ __device__ __forceinline__ uint32_t unit_sum_masked(uint64_t addr, int lead, int
 	return acc;
 }
 
+/* unit_sum_masked over a unit already loaded (16-byte chunks at or past re
+ * zero) */
+__device__ __forceinline__ uint32_t unit_sum_regs(const uint4 (&q)[4], int lead, int re)
+{
+	uint32_t acc = 0u;
+
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		const uint32_t w[4] = { q[k].x, q[k].y, q[k].z, q[k].w };
+
+#pragma unroll
+		for (int j = 0; j < 4; ++j) {
+			const int o = 16 * k + 4 * j;
+
+			acc = tail_dot2(w[j] & keep_below(re - o) & ~keep_below(lead - o), acc);
+		}
+	}
+	return acc;
+}
+
 /* Tail sums, fourth form (the default): each tail [a, b) is cut into 64-byte
  * units from c0 = a & ~15. The units that need byte masks — the frame's last
  * one, and its first one when a is not 16-aligned — are summed by the lane
@@ -1204,6 +1224,9 @@ __device__ __forceinline__ uint32_t sweep_frames(const uint8_t *g, uint32_t len,
 #ifndef SEG4_PIPE
 #define SEG4_PIPE 1
 #endif
+#ifndef SEG4_OWNEARLY       /* last units' loads issued before the passes' */
+#define SEG4_OWNEARLY 0
+#endif
 #ifndef SEG4_TAILW          /* last units by whole-word compares (unit_sum_head): */
 #define SEG4_TAILW 0        /* fewer VALU but a dependent reload; C3 +1.5 us */
 #endif
@@ -1252,6 +1275,9 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 	const uint32_t ni = mine ? nu - 1u - f0 : 0u;                   /* shared units */
 	const uint64_t gb = (uint64_t)(uintptr_t)g + c0;
 	uint32_t own = 0u;
+	const bool own_late = SEG4_OWNEARLY && !__ballot(own_first);     /* uniform */
+	uint4 oq[4] = {};
+	int own_re = 0, own_lead = 0;
 
 	/* the lane's own units: last (masked to b, and to a when it is the
 	 * first), then the first when it carries a lead */
@@ -1262,6 +1288,16 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 #endif
 		const uint32_t lu = nu - 1u;
 
+		/* SEG4_OWNEARLY without a first own unit anywhere: the last unit's
+		 * loads now, its sum once the first passes' loads are issued */
+		if (own_late) {
+			own_re = (int)(pd.b - c0 - 64u * lu);
+			own_lead = lu ? 0 : (int)lead;
+#pragma unroll
+			for (int k = 0; k < 4; ++k)
+				if (16 * k < own_re)
+					oq[k] = ld_g16(gb + 64ull * lu + 16u * k);
+		} else
 		/* every last unit starting at its first byte (C3's early tails
 		 * always): whole words by a compare each, the partial one read
 		 * again as a dword (a cache hit) */
@@ -1379,6 +1415,8 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 				addr = owner(128u);
 		}
 	}
+	if (own_late && mine)
+		own = unit_sum_regs(oq, own_lead, own_re);
 	for (uint32_t base = 0; base < total; base += 128u) {           /* uniform */
 		consume(qa, base);
 		if (base + 128u < total) {
@@ -1396,6 +1434,8 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 		}
 	}
 #else
+	if (own_late && mine)
+		own = unit_sum_regs(oq, own_lead, own_re);
 	for (uint32_t base = 0; base < total; base += 64u) {            /* uniform */
 		load(qa, addr);
 		/* the next pass's owners while the loads are in flight */
