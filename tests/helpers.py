@@ -105,3 +105,14 @@ def table_flags(rules):
     from odp_amd import gpu
     img = gpu.compile_rules(rules)
     return int.from_bytes(img[28:32], "little")
+
+
+def make_c_tests():
+    """make -C tests/c under a file lock: xdist workers running two tests that
+    build it must not relink a test program the other is executing"""
+    import fcntl
+    import subprocess
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c")
+    with open(os.path.join(d, ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-C", d], check=True, capture_output=True)

@@ -17,7 +17,7 @@ import subprocess
 
 import pytest
 
-from helpers import GOLDEN
+from helpers import GOLDEN, make_c_tests as _make_c
 from odp_amd import _lib as L
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -61,7 +61,7 @@ def test_reference_classifier_builds_unmodified():
 
 
 def test_loop_test_program_builds():
-    subprocess.run(["make", "-C", os.path.join(HERE, "c")], check=True, capture_output=True)
+    _make_c()
     assert os.access(LOOP_TEST, os.X_OK)
 
 
@@ -220,7 +220,7 @@ def test_host_runtime_under_contention():
     (a second free fails cleanly), 2^21 queue create / destroy cycles (more
     than the registry's slots: destroyed slots are reused and stale handles
     refused) and scheduled queues created / destroyed under 4 schedulers."""
-    subprocess.run(["make", "-C", os.path.join(HERE, "c")], check=True, capture_output=True)
+    _make_c()
     r = subprocess.run(["timeout", "-k", "10", "240", os.path.join(HERE, "c", "odp_rt_host")],
                        capture_output=True, text=True)
     assert r.returncode == 0 and "PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-2000:])

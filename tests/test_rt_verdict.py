@@ -24,7 +24,7 @@ import pytest
 
 import oracle
 import rulesets
-from helpers import ALL_CHKSUM, IFL
+from helpers import ALL_CHKSUM, IFL, make_c_tests
 from odp_amd import _lib as L
 from odp_amd import gen
 
@@ -109,7 +109,7 @@ def _types(m):
 
 
 def test_verdict_program_builds():
-    subprocess.run(["make", "-C", os.path.join(HERE, "c")], check=True, capture_output=True)
+    make_c_tests()
     assert os.access(PROG, os.X_OK)
 
 
