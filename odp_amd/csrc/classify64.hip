@@ -448,12 +448,16 @@ odpg_cls64_kernel(const L64Args A)
 	/* CM 2: the counter layout is read now, not behind the tile loop's
 	 * last wait; the workgroup's last wave to finish flushes the histogram */
 	__shared__ uint32_t waves_done;
-	odpg_cnt_dev C = {};
-
+	__shared__ odpg_cnt_dev cnt_lds;
 	__shared__ uint32_t flush_tot;
 
 	if constexpr (CM == 2) {
-		C = *A.cnt;
+		/* the layout is kept in LDS for the flush: nothing of it is held
+		 * through the tile loop (scalar registers) */
+		const odpg_cnt_dev C = *A.cnt;
+
+		if (threadIdx.x == 0u)
+			cnt_lds = C;
 		const __attribute__((address_space(1))) unsigned long long *r0 =
 			(const __attribute__((address_space(1))) unsigned long long *)(uintptr_t)(C.rows + (size_t)blockIdx.x * C.words);
 
@@ -976,6 +980,7 @@ odpg_cls64_kernel(const L64Args A)
 				return;
 			__threadfence_block();
 		}
+		const odpg_cnt_dev C = cnt_lds;
 		/* global (not flat) pointers: a flat store counts on the LDS counter
 		 * too, so every histogram read would wait for the stores before it */
 		__attribute__((address_space(1))) unsigned long long *r =

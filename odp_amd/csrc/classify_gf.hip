@@ -53,7 +53,10 @@
 #ifndef GF_WAVES_WIDE       /* wider hit maps, counted launches (C3: 100.7 vs */
 #define GF_WAVES_WIDE 4     /* 106.0 us at 5, whose VGPR budget spills) */
 #endif
-#define GF_WAVES_OF(cm, nw) ((cm) == 0 && (nw) == 2 ? GF_WAVES : GF_WAVES_WIDE)
+#ifndef GF_WAVES_CNT        /* counted launches with 2-word hit maps */
+#define GF_WAVES_CNT 5
+#endif
+#define GF_WAVES_OF(cm, nw) ((nw) == 2 ? ((cm) == 0 ? GF_WAVES : GF_WAVES_CNT) : GF_WAVES_WIDE)
 #ifndef GF_ZERO_MIN         /* hit maps of >= this many words: an entry's map read */
 #define GF_ZERO_MIN 2       /* after its value matched (else with it; C2x 45.1 vs */
 #endif                      /* 46.1 us, C3 106.0 vs 110.2 us) */
@@ -618,11 +621,15 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	/* CM 2: the counter layout is read now, not behind the tile loop's
 	 * last wait; the workgroup's last wave to finish flushes the histogram */
 	__shared__ uint32_t waves_done;
+	__shared__ odpg_cnt_dev cnt_lds;
 	__shared__ unsigned long long octets;
-	odpg_cnt_dev C = {};
-
 	if constexpr (CM == 2) {
-		C = *A.cnt;
+		/* the layout is kept in LDS for the flush: nothing of it is held
+		 * through the tile loop (scalar registers) */
+		const odpg_cnt_dev C = *A.cnt;
+
+		if (threadIdx.x == 0u)
+			cnt_lds = C;
 		const __attribute__((address_space(1))) unsigned long long *r0 =
 			(const __attribute__((address_space(1))) unsigned long long *)(uintptr_t)(C.rows + (size_t)blockIdx.x * C.words);
 
@@ -635,7 +642,6 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			octets = 0ull;
 		}
 	}
-	uint32_t lane_oct = 0u;     /* octets this lane handed over (< 2^32 per lane) */
 
 	__syncthreads();
 
@@ -664,6 +670,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		const uint32_t len = live ? d.y : 0u;
 		uint32_t f[16];
 		uint32_t x16 = xn;
+		uint32_t tile_oct = 0u;  /* CM 2: octets this lane hands over */
 
 		if constexpr (GF_SWEEP) {
 			gf_sweep(A.frames, make_uint2(d.x, len), smem + (threadIdx.x & ~63u) * RW, swx,
@@ -1143,8 +1150,17 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 #ifndef GF_EXP_NOBIN      /* experiment builds only: cost of the histogram adds */
 				atomicAdd(&dlv[bn], 1u);
 #endif
-				lane_oct += bn >= GF_BIN_EXTRA ? len : 0u;
+				tile_oct = bn >= GF_BIN_EXTRA ? len : 0u;
 			}
+		}
+		if constexpr (CM == 2) {
+			/* the tile's octets (< 2^32: 64 frames) summed across the wave
+			 * and added to the workgroup's total: no register carried
+			 * through the loop (the counted kernel's VGPR budget) */
+			const uint32_t to = wave_sum_u32(tile_oct);
+
+			if (lane == 0u && to)
+				atomicAdd(&octets, (unsigned long long)to);
 		}
 	}
 	if constexpr (CM == 2) {
@@ -1156,11 +1172,6 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		if (A.num != 12345u)
 			return;
 #endif
-		const uint64_t wo = (uint64_t)wave_sum_u32(lane_oct & 0xffffu) +
-				    ((uint64_t)wave_sum_u32(lane_oct >> 16) << 16);
-
-		if (lane == 0u && wo)
-			atomicAdd(&octets, (unsigned long long)wo);
 		__threadfence_block();
 		uint32_t prev = 0u;
 
@@ -1169,6 +1180,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		if ((uint32_t)__builtin_amdgcn_readfirstlane((int)prev) != GF_BLOCK / 64u - 1u)
 			return;
 		__threadfence_block();
+		const odpg_cnt_dev C = cnt_lds;
 		/* global (not flat) pointers: a flat store counts on the LDS counter
 		 * too, so every histogram read would wait for the stores before it */
 		__attribute__((address_space(1))) unsigned long long *r =
