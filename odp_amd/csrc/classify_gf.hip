@@ -56,6 +56,11 @@
 #ifndef GF_WAVES_CNT        /* counted launches with 2-word hit maps */
 #define GF_WAVES_CNT 5
 #endif
+/* counted launches: the counter row read at the start is held in registers
+ * until the flush (C3 counted 99.4-99.6 vs 99.9-100.4 us) where the VGPR
+ * budget allows; at 5 waves (2-word maps) it spills (C2x 49.7 vs 48.8 us)
+ * and the row goes through LDS at the start */
+#define GF_ROW_REGS(nw) ((nw) > 2)
 #define GF_WAVES_OF(cm, nw) ((nw) == 2 ? ((cm) == 0 ? GF_WAVES : GF_WAVES_CNT) : GF_WAVES_WIDE)
 #ifndef GF_ZERO_MIN         /* hit maps of >= this many words: an entry's map read */
 #define GF_ZERO_MIN 2       /* after its value matched (else with it; C2x 45.1 vs */
@@ -81,7 +86,7 @@ struct GFArgs {
 	xm_layout_t L;
 	const uint32_t *xfc;        /* lazy form: per CoS first complex record | count << 16 */
 	uint32_t num_xflat;         /* lazy form: complex records */
-	const odpg_cnt_dev *cnt;    /* CM 2: the sharded counters' layout */
+	odpg_cnt_dev cnt;           /* CM 2: the sharded counters' layout, by value */
 	uint32_t cnt_words;         /* CM 2: words of a counter row */
 };
 
@@ -622,19 +627,27 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	 * last wait; the workgroup's last wave to finish flushes the histogram */
 	__shared__ uint32_t waves_done;
 	__shared__ odpg_cnt_dev cnt_lds;
+	unsigned long long rowv = 0ull;   /* CM 2: this thread's word of the row */
 	__shared__ unsigned long long octets;
 	if constexpr (CM == 2) {
-		/* the layout is kept in LDS for the flush: nothing of it is held
-		 * through the tile loop (scalar registers) */
-		const odpg_cnt_dev C = *A.cnt;
+		/* the layout (a kernel argument) is kept in LDS for the flush:
+		 * nothing of it is held through the tile loop (scalar registers) */
+		const odpg_cnt_dev C = A.cnt;
 
 		if (threadIdx.x == 0u)
 			cnt_lds = C;
 		const __attribute__((address_space(1))) unsigned long long *r0 =
 			(const __attribute__((address_space(1))) unsigned long long *)(uintptr_t)(C.rows + (size_t)blockIdx.x * C.words);
 
-		for (uint32_t k = threadIdx.x; k < C.words; k += GF_BLOCK)
-			base[k] = r0[k];
+		if (GF_ROW_REGS(NW) && C.words <= GF_BLOCK) {
+			/* one word per thread, held in registers until the flush:
+			 * nothing waits for the row before the tile loop */
+			if (threadIdx.x < C.words)
+				rowv = r0[threadIdx.x];
+		} else {
+			for (uint32_t k = threadIdx.x; k < C.words; k += GF_BLOCK)
+				base[k] = r0[k];
+		}
 		for (uint32_t k = threadIdx.x; k < nbins; k += GF_BLOCK)
 			dlv[k] = 0u;
 		if (threadIdx.x == 0u) {
@@ -1172,6 +1185,8 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		if (A.num != 12345u)
 			return;
 #endif
+		if (GF_ROW_REGS(NW) && A.cnt.words <= GF_BLOCK && threadIdx.x < A.cnt.words)
+			base[threadIdx.x] = rowv;
 		__threadfence_block();
 		uint32_t prev = 0u;
 
@@ -1283,7 +1298,7 @@ extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s)
 
 	A.xlds = a->xm + XM_HDR_WORDS + XM_GROUP_WORDS * a->xm_ngroups;
 	A.xfc = A.xlds + A.L.lds_words;
-	A.cnt = a->cnt.dev;
+	A.cnt = odpg_cnt_layout(&a->cnt);
 	A.cnt_words = a->cnt.row ? a->cnt.words : 0u;
 
 	const size_t lds = odpg_clsgf_lds(a);

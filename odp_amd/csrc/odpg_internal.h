@@ -369,11 +369,24 @@ typedef struct odpg_cnt_dev {
 typedef struct odpg_cnt_args {
 	uint64_t *row;          /* rows base, NULL = no sharded counters */
 	const uint32_t *qcol;   /* device, queue column of each CoS (num_cos + 1) */
-	const odpg_cnt_dev *dev;   /* device copy of this layout (lean kernel) */
 	uint32_t words, rows, ncos, ncols;
 	uint32_t cos;           /* the table has CoS with stats_enable */
 	uint32_t pad;
 } odpg_cnt_args;
+
+/* the layout the lean kernels take by value as a kernel argument */
+static inline odpg_cnt_dev odpg_cnt_layout(const odpg_cnt_args *c)
+{
+	odpg_cnt_dev d;
+
+	d.rows = c->row;
+	d.qcol = c->qcol;
+	d.words = c->words;
+	d.ncos = c->ncos;
+	d.ncols = c->ncols;
+	d.ident = c->ncols == c->ncos;
+	return d;
+}
 
 /* odp_cls.c: drop the classifier's tables / counters bound to a context
  * (called by odpg_ctx_destroy before the context's stream goes away) */

@@ -80,7 +80,6 @@ struct odpg_counters_s {
 	uint32_t any_cos;              /* some CoS has stats_enable */
 	uint64_t *drows;               /* device, rows x words */
 	uint32_t *dqcol;               /* device, queue column of each CoS */
-	odpg_cnt_dev *ddev;            /* device, the layout for the lean kernel */
 	uint64_t *dsum;                /* device, words (fold target) */
 	uint64_t *hsum;                /* pinned host, words */
 	hipEvent_t done;
@@ -462,7 +461,6 @@ static void counters_free(odpg_counters_t *k)
 {
 	hipFree(k->drows);
 	hipFree(k->dqcol);
-	hipFree(k->ddev);
 	hipFree(k->dsum);
 	if (k->hsum)
 		hipHostFree(k->hsum);
@@ -518,26 +516,16 @@ int odpg_counters_create(odpg_ctx_t *c, const odpg_table_t *t, odpg_counters_t *
 
 	if (hipMalloc(&k->drows, rb) != hipSuccess ||
 	    hipMalloc(&k->dqcol, (size_t)(k->ncos + 1u) * 4u) != hipSuccess ||
-	    hipMalloc(&k->ddev, sizeof(odpg_cnt_dev)) != hipSuccess ||
 	    hipMalloc(&k->dsum, (size_t)k->words * 8u) != hipSuccess ||
 	    hipHostMalloc(&k->hsum, (size_t)k->words * 8u, hipHostMallocDefault) != hipSuccess ||
 	    hipEventCreateWithFlags(&k->done, hipEventDisableTiming) != hipSuccess) {
 		counters_free(k);
 		return -ENOMEM;
 	}
-	odpg_cnt_dev hd;
-
-	hd.rows = k->drows;
-	hd.qcol = k->dqcol;
-	hd.words = k->words;
-	hd.ncos = k->ncos;
-	hd.ncols = k->ncols;
-	hd.ident = k->ncols == k->ncos;
 	{
 		std::lock_guard<std::mutex> g(c->lock);
 
-		if (hipMemcpyAsync(k->ddev, &hd, sizeof(hd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-		    hipMemsetAsync(k->drows, 0, rb, c->stream) != hipSuccess ||
+		if (hipMemsetAsync(k->drows, 0, rb, c->stream) != hipSuccess ||
 		    hipMemsetAsync(k->dsum, 0, (size_t)k->words * 8u, c->stream) != hipSuccess ||
 		    hipMemcpyAsync(k->dqcol, k->qcol.data(), (size_t)(k->ncos + 1u) * 4u,
 				   hipMemcpyHostToDevice, c->stream) != hipSuccess ||
@@ -721,7 +709,6 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 
 		a.cnt.row = k->drows;
 		a.cnt.qcol = k->dqcol;
-		a.cnt.dev = k->ddev;
 		a.cnt.words = k->words;
 		a.cnt.rows = k->rows;
 		a.cnt.ncos = k->ncos;
