@@ -518,17 +518,11 @@ def bench_tx(args, world, rank, local, dist):
         if not args.no_cpu and world == 1:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle
-            sub = min(n, 1 << 20)
-            t = time.perf_counter()
-            reps = 0
-            while time.perf_counter() - t < min(args.cpu_seconds, 10.0):
-                oracle.tx_prepare(frames[:sub * 64], sub, stride=64,
+
+            def tx_slice(lo, hi):
+                oracle.tx_prepare(frames[lo * 64:hi * 64], hi - lo, stride=64,
                                   pktout_cfg=cfg.pktout_cfg, hash_proto=hp, num_qs=8)
-                reps += 1
-            dt = time.perf_counter() - t
-            cpu = {"value": round(sub * reps / dt / 1e6, 2), "unit": "Mpps", "cores": 1,
-                   "kind": "port",
-                   "sample": f"{reps} passes x {sub} pkts of the TX batch, 1 thread ({dt:.1f} s)"}
+            cpu = cpu_baseline_mt(tx_slice, n, args, "TX")
         res = {
             "metric": "Mpps TX-prepared (device-resident), 64B pkts, IPv4+UDP checksum insert "
                       "+ crc32c loop queue pick",
@@ -603,16 +597,11 @@ def bench_l3fwd(args, world, rank, local, dist):
         if not args.no_cpu and world == 1:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle
-            sub = min(n, 2_000_000)
-            t = time.perf_counter()
-            reps = 0
-            while time.perf_counter() - t < min(args.cpu_seconds, 10.0):
-                oracle.l3fwd(fw.routes, fw.param, frames[:sub * 64], 64, sub)
-                reps += 1
-            dt = time.perf_counter() - t
-            cpu = {"value": round(sub * reps / dt / 1e6, 2), "unit": "Mpps", "cores": 1,
-                   "kind": "port",
-                   "sample": f"{reps} passes x {sub} pkts of the C5 batch, 1 thread ({dt:.1f} s)"}
+
+            def fwd_passes(lo, hi, reps):
+                return oracle.l3fwd_passes(fw.routes, fw.param, frames[lo * 64:hi * 64], 64,
+                                           hi - lo, reps)
+            cpu = cpu_baseline_mt(None, n, args, "C5", passes=fwd_passes)
         res = {
             "metric": f"Mpps forwarded (device-resident), 64B pkts, l3fwd {args.fwd_mode}, "
                       "10M flows",
@@ -709,6 +698,88 @@ def cpu_baseline(rules, frames, desc, n, stride, opt, args):
             "sample": f"median of {runs} runs, each {reps} passes x {n} pkts of the same "
                       f"{args.config.upper()} batch in host DRAM, {used} threads pinned one per "
                       f"core ({share})"}
+
+
+def cpu_baseline_mt(work, n, args, what, passes=None):
+    """A CPU restatement whose C entry point works on a packet range
+    (work(lo, hi), a ctypes call that releases the GIL) timed on the host's
+    per-GPU core share: one pinned thread per core over its own slice of the
+    batch, median of 5 runs of ~cpu_seconds / 5 each, plus a 1-thread
+    calibration figure (1 thread and all cores). With
+    `passes(lo, hi, reps)` instead (an entry point with per-call setup, such
+    as l3fwd's warmed flow cache), each thread makes one call of `reps`
+    passes and reports their time without the setup; the rate is all
+    threads' packets over the slowest thread's pass time."""
+    import statistics
+    import threading
+
+    cpus, share = cpu_share()
+    threads = args.cpu_threads or len(cpus)
+    cpus = (cpus * (threads // len(cpus) + 1))[:threads]
+
+    def run_passes(nthr, seconds, rate_hint):
+        per = max(1, n // nthr)
+        reps = max(1, int(seconds * rate_hint * 1e6 / per))
+        secs = [0.0] * nthr
+
+        def body(t):
+            try:
+                os.sched_setaffinity(0, {cpus[t]})      # this thread only
+            except (AttributeError, OSError):
+                pass
+            lo = t * per
+            secs[t] = passes(lo, min(n, lo + per), reps)
+        th = [threading.Thread(target=body, args=(t,)) for t in range(nthr)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        return per * reps * nthr / max(secs) / 1e6
+
+    def run(nthr, seconds):
+        per = max(1, n // nthr)
+        done = [0] * nthr
+        stop = time.perf_counter() + seconds
+
+        def body(t):
+            try:
+                os.sched_setaffinity(0, {cpus[t]})      # this thread only
+            except (AttributeError, OSError):
+                pass
+            lo = t * per
+            hi = min(n, lo + per)
+            while time.perf_counter() < stop:
+                work(lo, hi)
+                done[t] += hi - lo
+        th = [threading.Thread(target=body, args=(t,)) for t in range(nthr)]
+        t0 = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        return sum(done) / (time.perf_counter() - t0) / 1e6
+    rates = []
+    if passes is not None:
+        n1 = min(n, 1 << 20)
+        one = n1 / passes(0, n1, 1) / 1e6             # calibration: one pass, 1 thread
+        for _ in range(5):
+            rates.append(run_passes(threads, args.cpu_seconds / 5, one))
+            log(f"cpu baseline {what}: {threads} threads {rates[-1]:.1f} Mpps")
+    else:
+        one = run(1, min(args.cpu_seconds / 5, 4.0))
+        for _ in range(5):
+            rates.append(run(threads, args.cpu_seconds / 5))
+            log(f"cpu baseline {what}: {threads} threads {rates[-1]:.1f} Mpps")
+    return {"value": round(statistics.median(rates), 2), "unit": "Mpps", "cores": threads,
+            "kind": "port", "value_1thread": round(one, 2),
+            "runs_mpps": [round(r, 2) for r in rates], "core_share": share,
+            "sample": f"median of 5 runs of ~{args.cpu_seconds / 5:.0f} s, {threads} threads "
+                      f"pinned one per core ({share}), each over its own {n // threads}-packet "
+                      f"slice of the {what} batch in host DRAM, passes repeated"
+                      + ("; per-call setup (l3fwd's route table / warmed flow cache) outside "
+                         "the timed passes, as the reference builds it before its workers; "
+                         "1-thread figure: one pass over 2^20 packets" if passes is not None
+                         else "; 1-thread figure: one thread over the whole batch")}
 
 
 def cpu_share():

@@ -227,7 +227,15 @@ const char *odpg_build_info(void);
 int         odpg_device_count(void);
 
 /* Context: one per (device, stream). stream is a hipStream_t, or NULL to let
- * the context create its own non-blocking stream. */
+ * the context create its own non-blocking stream.
+ *
+ * Object lifetimes: tables, counters, forwarders (odpg_fwd.h) and fences
+ * may be destroyed in any order relative to each other and to their
+ * context. odpg_ctx_destroy() releases the caller's handle and the odp_cls
+ * bindings made on the context; counters, forwarders and fences created on
+ * it hold a reference, and the context's stream and device memory are freed
+ * when the last of them is destroyed (the context handle itself may not be
+ * used after odpg_ctx_destroy). A table refers to its device only. */
 int  odpg_ctx_create(int device, void *stream, odpg_ctx_t **ctx);
 void odpg_ctx_destroy(odpg_ctx_t *ctx);
 void *odpg_ctx_stream(odpg_ctx_t *ctx);

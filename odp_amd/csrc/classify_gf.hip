@@ -62,10 +62,6 @@
  * and the row goes through LDS at the start */
 #define GF_ROW_REGS(nw) ((nw) > 2)
 #define GF_WAVES_OF(cm, nw) ((nw) == 2 ? ((cm) == 0 ? GF_WAVES : GF_WAVES_CNT) : GF_WAVES_WIDE)
-#ifndef GF_ZERO_MIN         /* hit maps of >= this many words: an entry's map read */
-#define GF_ZERO_MIN 2       /* after its value matched (else with it; C2x 45.1 vs */
-#endif                      /* 46.1 us, C3 106.0 vs 110.2 us) */
-#define GF_ZERO(nw) ((nw) >= GF_ZERO_MIN)
 #ifndef GF_RW               /* LDS row stride per lane, dwords (16-byte multiple) */
 #define GF_RW 20
 #endif
@@ -320,8 +316,8 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 #ifndef GF_SWEEP            /* 1: one coalesced sweep of every frame byte per tile */
 #define GF_SWEEP 0
 #endif
-#ifndef GF_PAIR             /* chain-free groups probed two at a time (C3 */
-#define GF_PAIR 1           /* 99.9-100.0 vs 101.3-101.7 us; C2x unchanged) */
+#ifndef GF_PROBES           /* chain-free groups probed together (2-word maps) */
+#define GF_PROBES 2
 #endif
 #ifndef GF_MARKS            /* tail-pass owners from an LDS mark map (else a */
 #define GF_MARKS 1          /* binary search of bpermutes; C3 -0.7 us) */
@@ -547,7 +543,6 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	uint32_t *tb = dlv + nbins;
 	const uint32_t *xmm = tb + A.L.masks;
 	const uint32_t *xmv = tb + A.L.values;
-	const uint8_t *xms = (const uint8_t *)(tb + A.L.slots);
 	const uint2 *xci = (const uint2 *)(tb + A.L.xci);
 	const uint4 *pdst = (const uint4 *)(tb + A.L.xpd);
 	const uint4 *xfl = (const uint4 *)(tb + A.L.xflat);
@@ -664,11 +659,9 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	const bool def_rules = def_valid && A.coses[A.default_cos].nrule != 0u;
 	/* the chain bits (they start set, groups clear them), uniform */
 	uint32_t chain[NW];
-	/* the key slots the groups read, the groups without chain records,
-	 * the zero entry */
+	/* the key slots the groups read, the groups without chain records */
 	const uint32_t kslots = xhdr[6];
 	const uint32_t ngor = xhdr[7];
-	const uint32_t zent = xhdr[3];
 
 #pragma unroll
 	for (int w = 0; w < NW; ++w)
@@ -834,62 +827,46 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 #pragma unroll
 			for (int w = 0; w < NW; ++w)
 				hm[w] = on ? chain[w] : 0u;
-			/* a group's probe: the masked key word hashed to the group's
-			 * slot byte, the entry's value compared; m = the entry's bit
-			 * map on a hit, zero on a miss */
+			/* a group's probe, branch-free: the masked key word hashed
+			 * to the group's direct entry (cls_compile.cpp "TBL_XMASK"),
+			 * whose value and bit map are read together (one LDS round
+			 * trip); m = the map when the value, the group's gate and
+			 * its CUSTOM_L3 / CUSTOM_FRAME length guard hold, else 0
+			 * (an empty slot's map is 0 too) */
 			auto probe = [&](uint32_t gi, uint32_t (&m)[NW]) {
-				const uint4 q0 = xmg[4u * gi];
-				const uint4 q1 = xmg[4u * gi + 1u];
-				const uint32_t mul = q0.x, shf = q0.y, soff = q0.z, eb = q0.w;
-				const uint32_t sg = q1.x, greq = q1.y, gmask = q1.z;
-				const uint32_t sl = sg & 0xffu;
-				/* CUSTOM_L3 / CUSTOM_FRAME records: frame_len > base +
-				 * off + size (term_cmp's guard) */
-				const bool gok = !(sg >> 31) ||
-						 b.len > ((sg >> 30) & 1u ? 0u : b.l3) + ((sg >> 8) & 0xffffu);
-				const uint32_t key = sl < 16u ? kv[sl] : sl == 16u ? k16 :
-						     sl == 17u ? k17 : len;
-				const uint32_t kvm = key & gmask;
-				const uint32_t si = xms[soff + ((kvm * mul) >> shf)];
-				const uint32_t e = eb + (si != 0xffu ? si : 0u);
+				const uint4 q0 = xmg[4u * gi];       /* mul, shift, slot, entry base */
+				const uint4 q1 = xmg[4u * gi + 1u];  /* guard, gate, mask, L3 mask */
+				const uint32_t sl = q0.z;
+				const uint32_t kl = kv[sl & 15u];
+				const uint32_t kx = (sl & 2u) ? len : (sl & 1u) ? k17 : k16;
+				const uint32_t kvm = (sl >= 16u ? kx : kl) & q1.z;
+				const uint32_t e = q0.w + ((kvm * q0.x) >> q0.y);
+				const uint32_t v = xmv[e];
 
-				if constexpr (GF_ZERO(NW)) {
-					/* wide maps: the entry's map read once the value
-					 * matched, the zero entry past the last on a miss */
-					const bool hit = on && (b.inf_lo & greq) == greq && gok &&
-							 si != 0xffu && xmv[e] == kvm;
-
-					xm_entry<NW>(xmm, hit ? e : zent, m);
-				} else {
-					/* the value and the map read together (entry eb +
-					 * 0 for an empty slot), the map dropped on a miss */
-					xm_entry<NW>(xmm, e, m);
-					const bool hit = on && (b.inf_lo & greq) == greq && gok &&
-							 si != 0xffu && xmv[e] == kvm;
+				xm_entry<NW>(xmm, e, m);
+				const bool hit = (b.inf_lo & q1.y) == q1.y & len >= (b.l3 & q1.w) + q1.x &
+						 v == kvm;
 
 #pragma unroll
-					for (int w = 0; w < NW; ++w)
-						m[w] = hit ? m[w] : 0u;
-				}
+				for (int w = 0; w < NW; ++w)
+					m[w] = hit ? m[w] : 0u;
 			};
-#ifdef GF_EXP_NOHM   /* experiment builds only: cost without the hit map */
-			if (__ballot(on) && A.num == 12345u) {
-#else
 			if (__ballot(on)) {
-#endif
+				/* GF_PROBES probes' LDS round trips in flight together */
+				constexpr uint32_t U = NW == 2 ? GF_PROBES : 2u;
 				uint32_t gi0 = 0;
 
-				if constexpr (GF_PAIR) {
-					/* two probes' LDS round trips in flight together */
-					for (; gi0 + 1u < ngor; gi0 += 2u) {
-						uint32_t m[NW], m2[NW];
+				for (; gi0 + U <= ngor; gi0 += U) {
+					uint32_t m[U][NW];
 
-						probe(gi0, m);
-						probe(gi0 + 1u, m2);
+#pragma unroll
+					for (uint32_t u = 0; u < U; ++u)
+						probe(gi0 + u, m[u]);
+#pragma unroll
+					for (uint32_t u = 0; u < U; ++u)
 #pragma unroll
 						for (int w = 0; w < NW; ++w)
-							hm[w] |= m[w] | m2[w];
-					}
+							hm[w] |= m[u][w];
 				}
 				for (uint32_t gi = gi0; gi < ngor; ++gi) {
 					uint32_t m[NW];
@@ -899,10 +876,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 					for (int w = 0; w < NW; ++w)
 						hm[w] |= m[w];
 				}
-				for (uint32_t gi = ngor; gi < ngroups; ++gi) {
-					uint32_t m[NW];
-
-					probe(gi, m);
+				auto chain_upd = [&](uint32_t gi, const uint32_t (&m)[NW]) {
 					const uint4 a0 = xmg[4u * gi + 2u];
 					const uint4 a1 = xmg[4u * gi + 3u];
 					const uint32_t na[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
@@ -910,6 +884,22 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 #pragma unroll
 					for (int w = 0; w < NW; ++w)
 						hm[w] = (hm[w] & (m[w] | na[w])) | (m[w] & ~chain[w]);
+				};
+				uint32_t gi = ngor;
+
+				for (; gi + 2u <= ngroups; gi += 2u) {
+					uint32_t m[NW], m2[NW];
+
+					probe(gi, m);
+					probe(gi + 1u, m2);
+					chain_upd(gi, m);
+					chain_upd(gi + 1u, m2);
+				}
+				if (gi < ngroups) {
+					uint32_t m[NW];
+
+					probe(gi, m);
+					chain_upd(gi, m);
 				}
 			}
 		}

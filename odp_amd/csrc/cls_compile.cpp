@@ -1084,7 +1084,7 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	 * group's chain members, CH every chain bit. Groups are keyed by (slot
 	 * and guard, gate, mask); each has a collision-free multiplicative hash
 	 * of its distinct masked values (slot = (value * mul) >> shift) into a
-	 * byte table of entry indices, each entry {value, bit map}. Only the
+	 * table of 2^lg direct entries {value, bit map} (empty slots: map 0). Only the
 	 * lowest PMR per (CoS, value) of a single-word group is entered: a
 	 * higher one of the same key matches exactly when that one does.
 	 * When the chain bits do not fit XM_MAX_PMR, the bits are the PMR
@@ -1179,7 +1179,6 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		xm = false;
 	const uint32_t nw = nbits <= 64u ? 2u : nbits <= 128u ? 4u : 8u;
 	std::vector<uint32_t> xmg, xmmask, xmval;
-	std::vector<uint8_t> xmslot;
 	uint64_t rs = 0x9E3779B97F4A7C15ull;
 
 	/* the groups without chain records first (their entries only OR bits
@@ -1236,26 +1235,38 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			xm = false;
 			break;
 		}
-		const uint32_t soff = (uint32_t)xmslot.size();
+		/* direct entries: slot (value * mul) >> shift of the group's
+		 * 2^lg holds that value and its bit map; an empty slot's map is
+		 * zero (a probe landing there changes nothing, as a miss) */
 		const uint32_t ebase = (uint32_t)xmval.size();
-		uint32_t k = 0;
 
-		xmslot.resize(soff + (1u << lg), 0xff);
+		if (ebase + (1u << lg) > XM_MAX_ENTS) {
+			xm = false;
+			break;
+		}
+		xmval.resize(ebase + (1u << lg), 0u);
+		xmmask.resize((size_t)(ebase + (1u << lg)) * nw, 0u);
 		for (auto &v : vm) {
-			xmslot[soff + ((v.first * mul) >> (32u - lg))] = (uint8_t)k++;
-			xmval.push_back(v.first);
+			const uint32_t e = ebase + ((v.first * mul) >> (32u - lg));
 			bm_t m = v.second;
 
 			m.resize(XM_WORDS, 0u);
-			xmmask.insert(xmmask.end(), m.begin(), m.begin() + nw);
+			xmval[e] = v.first;
+			std::copy(m.begin(), m.begin() + nw, xmmask.begin() + (size_t)e * nw);
 		}
 		auto ait = gand.find(git->first);
 		bm_t a = ait == gand.end() ? bm_t(XM_WORDS, 0u) : ait->second;
+		/* the group's key slot and its CUSTOM_L3 / CUSTOM_FRAME length
+		 * guard (term_cmp: frame_len > base + off + size) as
+		 * len >= (l3 & l3mask) + gthr */
+		const uint32_t sg = std::get<0>(git->first);
+		const bool guarded = (sg >> 31) != 0;
+		const uint32_t l3mask = guarded && !((sg >> 30) & 1u) ? ~0u : 0u;
+		const uint32_t gthr = guarded ? ((sg >> 8) & 0xffffu) + 1u : 0u;
 
 		a.resize(XM_WORDS, 0u);
-		xmg.insert(xmg.end(), {mul, 32u - lg, soff, ebase, std::get<0>(git->first),
-				       std::get<1>(git->first), std::get<2>(git->first),
-				       ait == gand.end() ? 0u : 1u});
+		xmg.insert(xmg.end(), {mul, 32u - lg, sg & 0xffu, ebase, gthr,
+				       std::get<1>(git->first), std::get<2>(git->first), l3mask});
 		for (uint32_t w = 0; w < XM_WORDS; w++)
 			xmg.push_back(~a[w]);
 	}
@@ -1286,15 +1297,13 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	std::vector<uint32_t> xmlds, xmhdr;
 
 	if (xm) {
-		xmslot.resize((xmslot.size() + 15u) & ~(size_t)15u, 0xff);
 		xm_layout_t L;
 
-		xm_layout_of(nw, (uint32_t)xmval.size(), (uint32_t)xmslot.size(), ncos, nbits,
+		xm_layout_of(nw, (uint32_t)xmval.size(), 0u, ncos, nbits,
 			     (uint32_t)(xflat.size() / 8), &L);
 		xmlds.assign(L.lds_words, 0u);
 		std::copy(xmmask.begin(), xmmask.end(), xmlds.begin() + L.masks);
 		std::copy(xmval.begin(), xmval.end(), xmlds.begin() + L.values);
-		memcpy(xmlds.data() + L.slots, xmslot.data(), xmslot.size());
 		for (uint32_t c = 0; c < ncos; c++) {
 			xmlds[L.xci + 2 * c] = cbit_start[c] | (cbit_n[c] << 16);
 			xmlds[L.xci + 2 * c + 1] = cos[c].action | ((uint32_t)cos[c].num_queue << 8) |
@@ -1327,7 +1336,7 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		xmhdr[1] = nbits;
 		xmhdr[2] = (uint32_t)gv.size();
 		xmhdr[3] = (uint32_t)xmval.size();
-		xmhdr[4] = (uint32_t)xmslot.size();
+		xmhdr[4] = 0u;
 		xmhdr[5] = (uint32_t)(xflat.size() / 8);
 		/* the key slots the groups read (the kernel extracts them once per
 		 * packet) */
@@ -1338,7 +1347,7 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			xmhdr[8 + w] = chain_all[w];
 		h.flags |= TBL_XMASK;
 		h.num_xment = (uint32_t)xmval.size();
-		h.xm_slot_bytes = (uint32_t)xmslot.size();
+		h.xm_slot_bytes = 0u;
 		h.num_xflat = (uint32_t)(xflat.size() / 8);
 		h.xm_nw = nw;
 		h.xm_nbits = nbits;

@@ -764,6 +764,7 @@ extern "C" int odpg_fwd_create(odpg_ctx_t *ctx, const odpg_route_t *routes, uint
 	if (!f)
 		return -ENOMEM;
 	f->ctx = ctx;
+	odpg_ctx_ref(ctx);
 	f->mode = param->mode;
 	f->nroutes = num_routes;
 	f->num_ports = param->num_ports;
@@ -798,6 +799,7 @@ extern "C" void odpg_fwd_destroy(odpg_fwd_t *f)
 	for (void *b : bufs)
 		if (b)
 			odpg_dev_free(f->ctx, b);
+	odpg_ctx_unref(f->ctx);
 	free(f);
 }
 

@@ -73,6 +73,8 @@ typedef struct rt_pkt {
 	struct rt_pkt *next;       /* queue link */
 } rt_pkt_t;
 
+#define TC_N     64        /* largest per-thread cache of one pool */
+
 typedef struct rt_pool {
 	int valid;
 	char name[ODP_POOL_NAME_LEN];
@@ -83,6 +85,7 @@ typedef struct rt_pool {
 	 * chunks on demand up to param.pkt.num, a header and `buf` data bytes
 	 * each, never returned to the system before odp_pool_destroy */
 	uint32_t gen;              /* create count of this slot: thread caches check it */
+	uint32_t tc_max;           /* buffers a thread's cache may hold (0: no caching) */
 	uint32_t buf;              /* data bytes of a pooled buffer */
 	uint32_t made;             /* buffers made (pooled) or allocated (ext) */
 	rt_pkt_t **stack;          /* free pooled buffers */
@@ -755,6 +758,12 @@ odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param)
 		p->buf = param->pkt.len > param->pkt.seg_len ? param->pkt.len : param->pkt.seg_len;
 		if (p->buf < 64u)
 			p->buf = 64u;
+		/* per-thread caches hold at most 1/32 of the pool each, so
+		 * that buffers freed by other threads cannot strand a small
+		 * pool's allocations (pools of < 64 buffers: no caching) */
+		p->tc_max = param->pkt.num / 32u < TC_N ? param->pkt.num / 32u : TC_N;
+		if (p->tc_max < 2u)
+			p->tc_max = 0u;
 		p->stack = malloc((size_t)param->pkt.num * sizeof(rt_pkt_t *));
 		if (!p->stack)
 			break;
@@ -774,6 +783,10 @@ int odp_pool_destroy(odp_pool_t hdl)
 	int rc = p ? 0 : -1;
 
 	if (p) {
+		/* under the pool's lock: a free or alloc that looked the pool up
+		 * before this re-checks valid there (pool.c destroys under
+		 * pool->lock too) */
+		pthread_mutex_lock(&p->lock);
 		p->valid = 0;
 		for (uint32_t c = 0; c < p->nchunks; c++)
 			free(p->chunks[c]);
@@ -782,6 +795,7 @@ int odp_pool_destroy(odp_pool_t hdl)
 		p->chunks = NULL;
 		p->stack = NULL;
 		p->nchunks = p->nfree = p->made = 0;
+		pthread_mutex_unlock(&p->lock);
 	}
 	pthread_mutex_unlock(&rt.lock);
 	return rc;
@@ -832,7 +846,6 @@ void odp_pool_print_all(void)
 
 /* per-thread buffer caches (pool.c's local cache): a few pools per thread */
 #define TC_POOLS 8
-#define TC_N     64
 static __thread struct {
 	uint32_t pool, gen, n;
 	rt_pkt_t *b[TC_N];
@@ -873,6 +886,8 @@ static int tc_slot(odp_pool_t pool, const rt_pool_t *p)
 	const uint32_t id = (uint32_t)(uintptr_t)pool;
 	int freeslot = -1;
 
+	if (!p->tc_max)
+		return -1;
 	for (int i = 0; i < TC_POOLS; i++) {
 		if (tcache[i].pool == id) {
 			if (tcache[i].gen == p->gen)
@@ -918,12 +933,16 @@ odp_packet_t odp_packet_alloc(odp_pool_t pool, uint32_t len)
 		k = tcache[ts].b[--tcache[ts].n];
 	} else {
 		pthread_mutex_lock(&p->lock);
+		if (!p->valid) {                  /* destroyed meanwhile */
+			pthread_mutex_unlock(&p->lock);
+			return ODP_PACKET_INVALID;
+		}
 		if (!p->nfree)
 			pool_grow_locked(p);
 		if (p->nfree) {
 			k = p->stack[--p->nfree];
 			/* refill the thread's cache with up to half of it */
-			while (ts >= 0 && p->nfree && tcache[ts].n < TC_N / 2)
+			while (ts >= 0 && p->nfree && tcache[ts].n < p->tc_max / 2)
 				tcache[ts].b[tcache[ts].n++] = p->stack[--p->nfree];
 		}
 		p->in_use = p->made - p->nfree;
@@ -968,14 +987,18 @@ void odp_packet_free(odp_packet_t pkt)
 	k->cap = p->buf;
 	const int ts = tc_slot(k->pool, p);
 
-	if (ts >= 0 && tcache[ts].n < TC_N) {
+	if (ts >= 0 && tcache[ts].n < p->tc_max) {
 		tcache[ts].b[tcache[ts].n++] = k;
 		return;
 	}
 	pthread_mutex_lock(&p->lock);
+	if (!p->valid || p->gen != k->pgen) {   /* destroyed meanwhile */
+		pthread_mutex_unlock(&p->lock);
+		return;
+	}
 	p->stack[p->nfree++] = k;
 	/* and half of the thread's cache back */
-	while (ts >= 0 && tcache[ts].n > TC_N / 2)
+	while (ts >= 0 && tcache[ts].n > p->tc_max / 2)
 		p->stack[p->nfree++] = tcache[ts].b[--tcache[ts].n];
 	p->in_use = p->made - p->nfree;
 	pthread_mutex_unlock(&p->lock);
@@ -989,7 +1012,7 @@ static void tcache_flush(void)
 
 		if (p && p->gen == tcache[i].gen && tcache[i].n) {
 			pthread_mutex_lock(&p->lock);
-			while (tcache[i].n)
+			while (p->valid && p->gen == tcache[i].gen && tcache[i].n)
 				p->stack[p->nfree++] = tcache[i].b[--tcache[i].n];
 			p->in_use = p->made - p->nfree;
 			pthread_mutex_unlock(&p->lock);
@@ -2288,7 +2311,13 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 
 	if (rx_launch(hdl, s))
 		return -1;
-	odpg_fence_wait(s->fence);
+	if (odpg_fence_wait(s->fence)) {
+		ERR("receive burst failed on the GPU: dropped\n");
+		odpg_cls_pktio_recv_end(s->token);
+		s->token = NULL;
+		rx_drop(s);
+		return -1;
+	}
 	const uint64_t t2 = rxprof.on > 0 ? prof_ns() : 0;
 
 	rx_deliver(p, hdl, s, pkts, nret);
@@ -2321,10 +2350,20 @@ static int rx_to_inq(rt_pktio_t *p, odp_pktio_t hdl, int drain)
 		rx_slot_t *s = p->slot[p->rx_head];
 		int nret = 0;
 
-		if (drain)
-			odpg_fence_wait(s->fence);
-		else if (odpg_fence_query(s->fence) == 0)
+		const int fs = drain ? (odpg_fence_wait(s->fence) ? -1 : 1) : odpg_fence_query(s->fence);
+
+		if (fs == 0)
 			break;
+		if (fs < 0) {
+			/* the launch failed: its verdicts were never written */
+			ERR("receive burst failed on the GPU: dropped\n");
+			odpg_cls_pktio_recv_end(s->token);
+			s->token = NULL;
+			rx_drop(s);
+			p->rx_head = (p->rx_head + 1u) % RT_INFLIGHT;
+			p->rx_count--;
+			continue;
+		}
 		const uint64_t t2 = rxprof.on > 0 ? prof_ns() : 0;
 
 		got += (int)s->n;
@@ -2454,12 +2493,16 @@ int odp_pktin_recv(odp_pktin_queue_t queue, odp_packet_t packets[], int num)
 		pthread_mutex_unlock(&rt.poll_lock);
 		return -1;
 	}
-	/* one launch classifies everything waiting (up to RT_BURST), as a NIC
-	 * fills its receive ring: what the caller did not ask for is handed out
-	 * by the next calls, in order, without a launch of their own */
+	/* a loop device: one launch classifies everything waiting (up to
+	 * RT_BURST), as a NIC fills its receive ring; what the caller did not
+	 * ask for is handed out by the next calls, in order, without a launch
+	 * of their own (its frames already sit in packets). A capture is read
+	 * `num` frames at a time, as pcap_recv does: each of its frames needs
+	 * a packet from the pool, and frames read ahead would be dropped when
+	 * the pool is short */
 	if (num > 0 && !p->ahead) {
 		odp_packet_t got[RT_BURST];
-		const int rc = rx_burst(p, queue.pktio, got, RT_BURST, &nret);
+		const int rc = rx_burst(p, queue.pktio, got, p->loopdev ? RT_BURST : num, &nret);
 
 		if (rc < 0) {
 			pthread_mutex_unlock(&rt.poll_lock);

@@ -106,24 +106,29 @@ typedef struct dcos_s {
 			       * (cls_compile.cpp "TBL_XMASK") */
 #define XM_MAX_PMR     256
 #define XM_WORDS       8     /* hit-map words per packet (XM_MAX_PMR / 32) */
-#define XM_MAX_LG      10    /* largest per-group slot table: 1024 bytes */
+#define XM_MAX_LG      9     /* largest per-group entry table: 512 entries */
+#define XM_MAX_ENTS    4096  /* direct entries of all groups (LDS: (nw + 1) words each) */
 #define XM_MAX_XTERMS  512   /* complex-PMR terms the kernel evaluates per packet */
 #define XM_MAX_GROUPS  64    /* groups read per packet */
-#define XM_GROUP_WORDS 16    /* xmg descriptor: {mul, shift, slot offset, entry base},
-			      * {slot | guard << 8, gate, mask, has chain members},
-			      * not-member words[8] */
+#define XM_GROUP_WORDS 16    /* xmg descriptor: {mul, shift, key index, entry base},
+			      * {slot | guard << 8, gate, mask, L3 mask of the
+			      * length guard}, {guard threshold, has chain members,
+			      * 0, 0}, not-member words[8] (only the first 4 of
+			      * them for hit maps of <= 4 words... all 8 stored) */
 #define XM_HDR_WORDS   16    /* region header: nw, nbits, ngroups, num_xment,
-			      * slot bytes, num_xflat, key slots the groups read
-			      * (bit mask), groups without chain members (they
-			      * come first), chain bits[8] */
+			      * 0, num_xflat, key slots the groups read (bit
+			      * mask), groups without chain members (they come
+			      * first), chain bits[8] */
 
 /* TBL_XMASK region, after the header and the group descriptors: the part
  * every workgroup copies to LDS (word offsets, each part 16-byte aligned),
  * then xfc[num_cos]. Shared by cls_compile.cpp and classify_gf.hip. */
 typedef struct xm_layout_s {
-	uint32_t masks;     /* [num_xment + 1..4][nw] entry bit maps (zero past the last) */
+	uint32_t masks;     /* [num_xment + 1..4][nw] entry bit maps: each group's
+			     * 2^lg direct entries (slot = value * mul >> shift),
+			     * an empty slot's map zero */
 	uint32_t values;    /* [num_xment] masked key values */
-	uint32_t slots;     /* per-group byte tables of entry indices */
+	uint32_t slots;     /* unused (slot_bytes 0) */
 	uint32_t xci;       /* uint2 [num_cos]: {bit start | bits << 16, cinfo.y} */
 	uint32_t xpd;       /* uint4 [nbits]: {dst | mark << 16, dst's xci.x, dst's
 			     * xfc, 0} */
@@ -394,6 +399,16 @@ static inline odpg_cnt_dev odpg_cnt_layout(const odpg_cnt_args *c)
 extern "C"
 #endif
 void odpg_cls_ctx_release(struct odpg_ctx_s *ctx);
+/* context references held by objects created on it (runtime.hip; odpg.h
+ * "object lifetimes") */
+#ifdef __cplusplus
+extern "C" {
+#endif
+void odpg_ctx_ref(struct odpg_ctx_s *ctx);
+void odpg_ctx_unref(struct odpg_ctx_s *ctx);
+#ifdef __cplusplus
+}
+#endif
 
 /* kernel launch arguments (runtime.hip -> classify.hip) */
 #include "../../include/odpg.h"

@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <stdlib.h>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -56,6 +57,10 @@ struct odpg_ctx_s {
 	hipEvent_t ev[NUM_EVENTS];
 	int kernel_mode;   /* 0 auto, 1 walk, 2 evaluate-all, 3 hash walk */
 	std::mutex lock;
+	/* the caller's handle + one per counters / forwarder / fence created on
+	 * the context (odpg.h "object lifetimes"): the stream and device memory
+	 * are freed when the last of them is released */
+	std::atomic<int> refs;
 };
 
 static void free_stage(odpg_ctx_t *c);
@@ -201,6 +206,7 @@ int odpg_ctx_create(int device, void *stream, odpg_ctx_t **out)
 	c->ws = nullptr;
 	c->ws_bytes = 0;
 	c->kernel_mode = 0;
+	c->refs.store(1);
 	if (hipSetDevice(device) != hipSuccess) {
 		delete c;
 		return -EIO;
@@ -239,11 +245,9 @@ int odpg_ctx_create(int device, void *stream, odpg_ctx_t **out)
 	return 0;
 }
 
-void odpg_ctx_destroy(odpg_ctx_t *c)
+/* the context's resources, once nothing refers to it any more */
+static void ctx_free(odpg_ctx_t *c)
 {
-	if (!c)
-		return;
-	odpg_cls_ctx_release(c);
 	hipSetDevice(c->device);
 	hipStreamSynchronize(c->stream);
 	hipStreamSynchronize(c->copy_stream);
@@ -262,6 +266,27 @@ void odpg_ctx_destroy(odpg_ctx_t *c)
 	if (c->own_stream)
 		hipStreamDestroy(c->stream);
 	delete c;
+}
+
+void odpg_ctx_ref(odpg_ctx_t *c)
+{
+	c->refs.fetch_add(1);
+}
+
+void odpg_ctx_unref(odpg_ctx_t *c)
+{
+	if (c->refs.fetch_sub(1) == 1)
+		ctx_free(c);
+}
+
+void odpg_ctx_destroy(odpg_ctx_t *c)
+{
+	if (!c)
+		return;
+	/* the odp_cls bindings on this context go now (their counters and
+	 * tables); objects the caller still holds keep the context alive */
+	odpg_cls_ctx_release(c);
+	odpg_ctx_unref(c);
 }
 
 int odpg_ctx_set_kernel_mode(odpg_ctx_t *c, int mode)
@@ -459,6 +484,8 @@ extern "C" int odpg_launch_counters_fold(uint64_t *rows, uint32_t nrows, uint32_
 
 static void counters_free(odpg_counters_t *k)
 {
+	odpg_ctx_t *c = k->ctx;
+
 	hipFree(k->drows);
 	hipFree(k->dqcol);
 	hipFree(k->dsum);
@@ -467,6 +494,7 @@ static void counters_free(odpg_counters_t *k)
 	if (k->done)
 		hipEventDestroy(k->done);
 	delete k;
+	odpg_ctx_unref(c);
 }
 
 int odpg_counters_create(odpg_ctx_t *c, const odpg_table_t *t, odpg_counters_t **out)
@@ -480,6 +508,7 @@ int odpg_counters_create(odpg_ctx_t *c, const odpg_table_t *t, odpg_counters_t *
 	odpg_counters_t *k = new odpg_counters_t();
 
 	k->ctx = c;
+	odpg_ctx_ref(c);
 	k->qsig = t->qsig;
 	k->ncos = h.num_cos;
 	k->qcol.resize(h.num_cos + 1u);
@@ -496,7 +525,7 @@ int odpg_counters_create(odpg_ctx_t *c, const odpg_table_t *t, odpg_counters_t *
 	k->ncols = col;
 	k->words = 4u + k->ncos + k->ncols;
 	if (((size_t)k->ncos + k->ncols) * 4u > CNT_MAX_LDS) {
-		delete k;
+		counters_free(k);
 		return -E2BIG;
 	}
 	int cus = 0;
@@ -509,7 +538,7 @@ int odpg_counters_create(odpg_ctx_t *c, const odpg_table_t *t, odpg_counters_t *
 	while (k->rows > (uint32_t)cus && (size_t)k->rows * k->words * 8u > CNT_MAX_BYTES)
 		k->rows >>= 1;
 	if ((size_t)k->rows * k->words * 8u > CNT_MAX_BYTES) {
-		delete k;
+		counters_free(k);
 		return -E2BIG;
 	}
 	const size_t rb = (size_t)k->rows * k->words * 8u;
@@ -1068,6 +1097,7 @@ int odpg_event_record(odpg_ctx_t *c, int slot)
 struct odpg_fence_s {
 	hipEvent_t ev;
 	int device;
+	odpg_ctx_t *ctx;   /* referenced: any destroy order (odpg.h) */
 };
 
 int odpg_fence_create(odpg_ctx_t *c, odpg_fence_t **fence)
@@ -1079,11 +1109,13 @@ int odpg_fence_create(odpg_ctx_t *c, odpg_fence_t **fence)
 	if (!f)
 		return -ENOMEM;
 	f->device = c->device;
+	f->ctx = c;
 	hipSetDevice(c->device);
 	if (hipEventCreateWithFlags(&f->ev, hipEventDisableTiming) != hipSuccess) {
 		delete f;
 		return -EIO;
 	}
+	odpg_ctx_ref(c);
 	*fence = f;
 	return 0;
 }
@@ -1119,6 +1151,7 @@ void odpg_fence_destroy(odpg_fence_t *f)
 		return;
 	hipSetDevice(f->device);
 	hipEventDestroy(f->ev);
+	odpg_ctx_unref(f->ctx);
 	delete f;
 }
 

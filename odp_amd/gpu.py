@@ -97,7 +97,7 @@ class Counters:
         h = C.c_void_p()
         L.check(lib.odpg_counters_create(ctx.h, table.h, C.byref(h)), "odpg_counters_create")
         self.h = h.value
-        self.ctx = ctx          # counters are destroyed before their context
+        self.ctx = ctx
         self.num_cos = table.num_cos
         self.words = 4 + self.num_cos + self.num_cos * L.COS_QUEUE_MAX
 
@@ -114,8 +114,9 @@ class Counters:
 
     def close(self):
         if self.h:
-            if self.ctx.h:      # after the context: leaked to process exit
-                lib.odpg_counters_destroy(self.h)
+            # valid after the context's destroy too: the counters hold a
+            # reference to it (odpg.h "object lifetimes")
+            lib.odpg_counters_destroy(self.h)
             self.h = None
 
     def __del__(self):

@@ -39,6 +39,8 @@ def _load():
     lib.oracle_helper_udp_tcp_chksum.argtypes = [vp, u32, u32, u32, i32, i32, i32, vp]
     lib.oracle_l3fwd.restype = i32
     lib.oracle_l3fwd.argtypes = [vp, u32, vp, vp, u32, u32, i32, i32, vp]
+    lib.oracle_l3fwd_reps.restype = i32
+    lib.oracle_l3fwd_reps.argtypes = [vp, u32, vp, vp, u32, u32, i32, i32, vp, u32, vp]
     lib.oracle_tx_prepare.restype = i32
     lib.oracle_tx_prepare.argtypes = [vp, vp, u32, u32, vp, vp, vp]
     lib.oracle_packet_parse_multi.restype = i32
@@ -151,6 +153,21 @@ def l3fwd(routes, param, frames, stride, num, src_port=0, error_check=False):
     if rc:
         raise ValueError("route set outside the restated domain")
     return out, fr
+
+
+def l3fwd_passes(routes, param, frames, stride, num, reps):
+    """`reps` passes of the l3fwd restatement over a private copy of
+    `frames`, the trie / warmed flow cache built once before them (as
+    l3fwd's init does): returns the seconds the passes took (CPU baseline)."""
+    fr = np.array(frames, dtype=np.uint8, copy=True)
+    out = np.zeros(num, np.int32)
+    ns = C.c_uint64(0)
+    rc = lib.oracle_l3fwd_reps(C.cast(routes, C.c_void_p) if len(routes) else None, len(routes),
+                               C.byref(param), fr.ctypes.data, stride, num, 0, 0,
+                               out.ctypes.data, reps, C.byref(ns))
+    if rc:
+        raise ValueError("route set outside the restated domain")
+    return ns.value * 1e-9
 
 
 def fib_lookup(routes, ips):

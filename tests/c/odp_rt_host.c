@@ -104,6 +104,17 @@ static void *pool_thread(void *arg)
 	return NULL;
 }
 
+/* ---- a small pool: allocated by one thread, freed by another ------------------- */
+static odp_packet_t xfer[32];
+
+static void *free_thread(void *arg)
+{
+	(void)arg;
+	for (int k = 0; k < 32; k++)
+		odp_packet_free(xfer[k]);
+	return NULL;
+}
+
 /* ---- scheduled queues created / destroyed under schedulers -------------------- */
 static int sched_stop;
 
@@ -213,6 +224,32 @@ int main(void)
 		CHECK(odp_pool_destroy(churn_pool) == 0, "pool destroy 2");
 	}
 	printf("pool: %d threads x 20000 x 48 alloc/free, limits, re-create\n", NT);
+
+	/* a 32-buffer pool whose buffers one thread allocates and another frees
+	 * (a producer and a worker): the freeing thread's cache must not strand
+	 * them, every buffer is allocatable again */
+	{
+		odp_pool_param_init(&pp);
+		pp.type = ODP_POOL_PACKET;
+		pp.pkt.num = 32;
+		pp.pkt.len = 128;
+		odp_pool_t small = odp_pool_create("small", &pp);
+
+		CHECK(small != ODP_POOL_INVALID, "small pool");
+		for (int round = 0; round < 3; round++) {
+			int n = 0;
+
+			for (; n < 32; n++)
+				if ((xfer[n] = odp_packet_alloc(small, 64)) == ODP_PACKET_INVALID)
+					break;
+			CHECK(n == 32, "round %d: %d of 32 buffers", round, n);
+			if (n < 32)
+				break;
+			run(free_thread, 1);
+		}
+		CHECK(odp_pool_destroy(small) == 0, "small pool destroy");
+		printf("pool: 32 buffers, allocated here and freed by another thread, 3 rounds\n");
+	}
 
 	/* queue registry: more create / destroy cycles than slots */
 	odp_queue_t first = odp_queue_create("q", NULL), q = first;

@@ -414,6 +414,54 @@ static void case_pcap_loops(odp_pool_t pool)
 	unlink(path);
 }
 
+/* E: DIRECT receive of a capture one frame at a time into a 4-packet pool:
+ * a capture frame needs a packet from the pool, so the receive reads `num`
+ * frames per call (pcap_recv) and loses none, whatever the pool's size */
+static void case_pcap_small_pool(void)
+{
+	char path[] = "/tmp/odp_rt_loop_XXXXXX";
+	const int fd = mkstemp(path);
+	odp_pool_param_t pp;
+
+	CHECK(fd >= 0 && write_pcap(path) == 0, "write capture");
+	if (fd < 0)
+		return;
+	close(fd);
+	odp_pool_param_init(&pp);
+	pp.type = ODP_POOL_PACKET;
+	pp.pkt.num = 4;
+	pp.pkt.len = 1600;
+	odp_pool_t small = odp_pool_create("small", &pp);
+	char dev[128];
+	odp_pktin_queue_t inq;
+	int got = 0, tries = 0;
+
+	CHECK(small != ODP_POOL_INVALID, "small pool");
+	snprintf(dev, sizeof(dev), "pcap:in=%s", path);
+	odp_pktio_t pktio = open_loop(dev, small, ODP_PKTIN_MODE_DIRECT, ODP_PKTOUT_MODE_DIRECT, 0);
+
+	CHECK(pktio != ODP_PKTIO_INVALID, "open %s", dev);
+	if (pktio != ODP_PKTIO_INVALID) {
+		CHECK(odp_pktin_queue(pktio, &inq, 1) == 1 && odp_pktio_start(pktio) == 0,
+		      "start pcap");
+		for (; tries < 100; tries++) {
+			odp_packet_t pkt;
+			const int n = odp_pktin_recv(inq, &pkt, 1);
+
+			if (n <= 0)
+				break;
+			CHECK(which_frame(pkt) == got, "frame %d out of order", got);
+			got++;
+			odp_packet_free(pkt);
+		}
+		CHECK(got == 20, "one at a time into 4 packets: %d of 20 frames", got);
+		CHECK(odp_pktio_stop(pktio) == 0 && odp_pktio_close(pktio) == 0, "stop/close pcap");
+	}
+	CHECK(odp_pool_destroy(small) == 0, "small pool destroy");
+	printf("E pcap small pool: %d packets\n", got);
+	unlink(path);
+}
+
 int main(void)
 {
 	odp_instance_t inst;
@@ -440,6 +488,7 @@ int main(void)
 	case_sched_cls(pool);
 	case_queue(pool);
 	case_pcap_loops(pool);
+	case_pcap_small_pool();
 	CHECK(odp_pool_destroy(pool) == 0, "pool destroy");
 	odp_term_local();
 	odp_term_global(inst);

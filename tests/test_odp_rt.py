@@ -158,6 +158,7 @@ def test_loop_device_through_gpu_classifier():
     assert r.returncode == 0 and "PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-2000:])
     assert "A direct: received 300" in r.stdout and "C queue: 300 packets" in r.stdout
     assert "D pcap loops=3: 40 packets" in r.stdout
+    assert "E pcap small pool: 20 packets" in r.stdout
 
 
 @pytest.mark.gpu

@@ -56,6 +56,7 @@ class XmTable:
         assert (self.nw, self.nbits, self.ngroups) == (h["xm_nw"], h["xm_nbits"], h["xm_ngroups"])
         assert (nx, sb, nxf) == (h["num_xment"], h["xm_slot_bytes"], h["num_xflat"])
         self.chain = self._big(w[8:16])
+        self.ngor = int(w[7])
         self.groups = w[XM_HDR_WORDS:XM_HDR_WORDS + XM_GROUP_WORDS * self.ngroups] \
             .reshape(-1, XM_GROUP_WORDS).astype(np.uint64)
         base = XM_HDR_WORDS + XM_GROUP_WORDS * self.ngroups
@@ -64,7 +65,6 @@ class XmTable:
         lds = w[base:base + L["lds_words"]]
         self.masks = lds[L["masks"]:L["masks"] + nx * self.nw].reshape(-1, self.nw) if nx else None
         self.values = lds[L["values"]:L["values"] + nx]
-        self.slots = lds[L["slots"]:L["xci"]].view(np.uint8)
         self.xci = lds[L["xci"]:L["xci"] + 2 * ncos].reshape(-1, 2)
         self.xpd = lds[L["xpd"]:L["xpd"] + 4 * self.nbits].reshape(-1, 4)
         self.xflat = lds[L["xflat"]:L["xflat"] + 8 * nxf].reshape(-1, 8)
@@ -109,16 +109,17 @@ class XmTable:
 
         full = (1 << (32 * self.nw)) - 1
         hm = self.chain
-        for g in self.groups:
-            mul, shf, soff, eb, sg, req, gmask, gand = (int(x) for x in g[:8])
-            gok = not (sg >> 31) or n > ((0 if (sg >> 30) & 1 else l3) + ((sg >> 8) & 0xFFFF))
+        for gi, g in enumerate(self.groups):
+            mul, shf, slot, eb, gthr, req, gmask, l3mask = (int(x) for x in g[:8])
+            # direct entries: slot (value * mul) >> shift; an empty slot's
+            # map is zero, so a probe landing there acts as a miss
             h = 0
-            if (inf & req) == req and gok:
-                kv = key(sg & 0xFF) & gmask
-                si = int(self.slots[soff + (((kv * mul) & 0xFFFFFFFF) >> shf)])
-                if si != 0xFF and int(self.values[eb + si]) == kv:
-                    h = self._big(self.masks[eb + si])
-            if gand:
+            if (inf & req) == req and n >= (l3 & l3mask) + gthr:
+                kv = key(slot) & gmask
+                e = eb + (((kv * mul) & 0xFFFFFFFF) >> shf)
+                if int(self.values[e]) == kv:
+                    h = self._big(self.masks[e])
+            if gi >= self.ngor:
                 na = self._big(g[8:16])
                 hm = ((hm & (h | na)) | (h & ~self.chain)) & full
             else:
