@@ -426,7 +426,7 @@ __device__ __forceinline__ void gf_sweep(const uint8_t *frames, uint2 d, uint32_
 		for (int k = 0; k < 16; k += 4)
 			*(uint4 *)(rows + GF_RW * lane + k) = make_uint4(0u, 0u, 0u, 0u);
 	}
-	auto consume = [&](const SwUnit &U, uint32_t base) {
+	auto consume = [&](const SwUnit &U, uint32_t base) __attribute__((always_inline)) {
 		const uint32_t uo = U.ou & 63u, uu = (U.ou >> 6) & 0x3ffu, rem = U.ou >> 16;
 		const uint32_t nw = rem >> 2;
 		const uint32_t pb = rem & 3u;
@@ -514,6 +514,55 @@ __device__ __forceinline__ void xm_entry(const uint32_t *xmm, uint32_t e, uint32
 	}
 }
 
+/* a packet's key words 16, 17 (L4 + 0, 4) and 18 (frame length) */
+typedef uint32_t gf_kx_t __attribute__((ext_vector_type(4)));
+
+/* U hit-map groups' probes for this lane's packet, branch-free: each masked
+ * key word hashed to its group's direct entry (cls_compile.cpp
+ * "TBL_XMASK"), whose value and bit map are read together; m[u] = the
+ * entry's map and hm_[u] all-ones when the value, the group's gate and its
+ * CUSTOM_L3 / CUSTOM_FRAME length guard (len >= (l3 & l3mask) + threshold)
+ * hold, else 0 (the map counts as 0; an empty slot's map is 0 too). All U descriptors are loaded first and all LDS reads issued
+ * together: scalar and LDS loads share one counter, so a descriptor load
+ * issued behind a probe's reads would wait for them. Key words by value: a
+ * uniform slot index reads them with v_movrels. */
+template <int NW, int U>
+__device__ __forceinline__ void gf_probes(const uint4 *__restrict__ xmg, uint32_t gi, gf_kv_t kv,
+					  gf_kx_t kx, uint32_t inf_lo, uint32_t l3, uint32_t len,
+					  const uint32_t *xmv, const uint32_t *xmm, uint32_t (&m)[U][NW],
+					  uint32_t (&hm_)[U])
+{
+	uint4 q0[U], q1[U];
+	uint32_t e[U], kvm[U], v[U];
+
+#pragma unroll
+	for (int u = 0; u < U; ++u) {
+		q0[u] = xmg[4u * (gi + u)];        /* mul, shift, slot, entry base */
+		q1[u] = xmg[4u * (gi + u) + 1u];   /* guard, gate, mask, L3 mask */
+	}
+#pragma unroll
+	for (int u = 0; u < U; ++u) {
+		const uint32_t sl = q0[u].z;
+		const uint32_t key = sl < 16u ? kv[sl & 15u] : kx[sl & 3u];
+
+		kvm[u] = key & q1[u].z;
+		e[u] = q0[u].w + ((kvm[u] * q0[u].x) >> q0[u].y);
+	}
+#pragma unroll
+	for (int u = 0; u < U; ++u) {
+		v[u] = xmv[e[u]];
+		xm_entry<NW>(xmm, e[u], m[u]);
+	}
+#pragma unroll
+	for (int u = 0; u < U; ++u) {
+		const bool hit = ((inf_lo & q1[u].y) == q1[u].y) & (len >= (l3 & q1[u].w) + q1[u].x) &
+				 (v[u] == kvm[u]);
+		/* all-ones on a hit: the callers fold it into their OR / AND
+		 * (v_and_or_b32) instead of a select per word */
+		hm_[u] = 0u - (uint32_t)hit;
+	}
+}
+
 /* CM: counters of the launch, 0 none, 2 sharded counter rows (odpg.h);
  * NW: hit-map words per packet (the table's rule bits, 2 / 4 / 8 x 32) */
 template <int CM, int NW>
@@ -567,7 +616,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 
 	/* the first tile's descriptors and windows are issued before the table
 	 * copy below */
-	auto load_desc = [&](uint32_t t) -> uint2 {
+	auto load_desc = [&](uint32_t t) __attribute__((always_inline)) -> uint2 {
 		const uint32_t i = t * 64u + lane;
 
 		if (t < ntiles && i < num)
@@ -576,7 +625,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	};
 	/* a frame's first 64 bytes (16-byte chunks holding frame bytes only: the
 	 * chunk with the last byte is masked), and its dword at byte 64 */
-	auto load_win = [&](uint32_t (&f)[16], uint32_t &x16, uint2 d) {
+	auto load_win = [&](uint32_t (&f)[16], uint32_t &x16, uint2 d) __attribute__((always_inline)) {
 		const uint8_t *g = A.frames + d.x;
 		const uint32_t len = d.y;
 
@@ -598,7 +647,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	/* GF_EARLY: the tails of a tile's frames, bytes [64, len), as each
 	 * lane's one's-complement partial (seg_tail_sums4; the whole wave) */
 	const bool l4ck = (A.opt & (ODPG_PKTIN_UDP_CHKSUM | ODPG_PKTIN_TCP_CHKSUM)) != 0u;
-	auto early_tails = [&](uint2 d, uint32_t t) -> uint32_t {
+	auto early_tails = [&](uint2 d, uint32_t t) __attribute__((always_inline)) -> uint32_t {
 		const uint32_t len = t < ntiles && t * 64u + lane < num ? d.y : 0u;
 		const uint64_t m = __ballot(len > 64u);
 
@@ -746,7 +795,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		}
 		const bool fastw = __ballot(live && !plain_gf(f, x16, len, sh)) == 0ull;
 
-		auto bases = [&]() {
+		auto bases = [&]() __attribute__((always_inline)) {
 			b.l2 = p.l2;
 			b.l3 = p.l3;
 			b.l4 = p.l4;
@@ -827,79 +876,61 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 #pragma unroll
 			for (int w = 0; w < NW; ++w)
 				hm[w] = on ? chain[w] : 0u;
-			/* a group's probe, branch-free: the masked key word hashed
-			 * to the group's direct entry (cls_compile.cpp "TBL_XMASK"),
-			 * whose value and bit map are read together (one LDS round
-			 * trip); m = the map when the value, the group's gate and
-			 * its CUSTOM_L3 / CUSTOM_FRAME length guard hold, else 0
-			 * (an empty slot's map is 0 too) */
-			auto probe = [&](uint32_t gi, uint32_t (&m)[NW]) {
-				const uint4 q0 = xmg[4u * gi];       /* mul, shift, slot, entry base */
-				const uint4 q1 = xmg[4u * gi + 1u];  /* guard, gate, mask, L3 mask */
-				const uint32_t sl = q0.z;
-				const uint32_t kl = kv[sl & 15u];
-				const uint32_t kx = (sl & 2u) ? len : (sl & 1u) ? k17 : k16;
-				const uint32_t kvm = (sl >= 16u ? kx : kl) & q1.z;
-				const uint32_t e = q0.w + ((kvm * q0.x) >> q0.y);
-				const uint32_t v = xmv[e];
-
-				xm_entry<NW>(xmm, e, m);
-				const bool hit = (b.inf_lo & q1.y) == q1.y & len >= (b.l3 & q1.w) + q1.x &
-						 v == kvm;
-
-#pragma unroll
-				for (int w = 0; w < NW; ++w)
-					m[w] = hit ? m[w] : 0u;
-			};
+			const gf_kv_t kvv = kv;
+			const gf_kx_t kxv = {k16, k17, (uint32_t)len, 0u};
+			const uint32_t inf_lo = b.inf_lo, l3 = b.l3, flen = len;
 			if (__ballot(on)) {
-				/* GF_PROBES probes' LDS round trips in flight together */
+				/* GF_PROBES groups' probes in flight together */
 				constexpr uint32_t U = NW == 2 ? GF_PROBES : 2u;
-				uint32_t gi0 = 0;
+				uint32_t gi = 0;
 
-				for (; gi0 + U <= ngor; gi0 += U) {
-					uint32_t m[U][NW];
+#pragma unroll 1
+				for (; gi + U <= ngor; gi += U) {
+					uint32_t m[U][NW], hk[U];
 
-#pragma unroll
-					for (uint32_t u = 0; u < U; ++u)
-						probe(gi0 + u, m[u]);
+					gf_probes<NW, U>(xmg, gi, kvv, kxv, inf_lo, l3, flen, xmv, xmm, m, hk);
 #pragma unroll
 					for (uint32_t u = 0; u < U; ++u)
 #pragma unroll
 						for (int w = 0; w < NW; ++w)
-							hm[w] |= m[u][w];
+							hm[w] |= m[u][w] & hk[u];
 				}
-				for (uint32_t gi = gi0; gi < ngor; ++gi) {
-					uint32_t m[NW];
+#pragma unroll 1
+				for (; gi < ngor; ++gi) {
+					uint32_t m[1][NW], hk[1];
 
-					probe(gi, m);
+					gf_probes<NW, 1>(xmg, gi, kvv, kxv, inf_lo, l3, flen, xmv, xmm, m, hk);
 #pragma unroll
 					for (int w = 0; w < NW; ++w)
-						hm[w] |= m[w];
+						hm[w] |= m[0][w] & hk[0];
 				}
-				auto chain_upd = [&](uint32_t gi, const uint32_t (&m)[NW]) {
-					const uint4 a0 = xmg[4u * gi + 2u];
-					const uint4 a1 = xmg[4u * gi + 3u];
+				/* the AND-chain groups: a chain bit stays set only where
+				 * every group holding one of its records has it */
+				auto chain_upd = [&](uint32_t g, const uint32_t (&mm)[NW], uint32_t h) __attribute__((always_inline)) {
+					const uint4 a0 = xmg[4u * g + 2u];
+					const uint4 a1 = xmg[4u * g + 3u];
 					const uint32_t na[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
 
 #pragma unroll
-					for (int w = 0; w < NW; ++w)
-						hm[w] = (hm[w] & (m[w] | na[w])) | (m[w] & ~chain[w]);
+					for (int w = 0; w < NW; ++w) {
+						const uint32_t x = mm[w] & h;
+
+						hm[w] = (hm[w] & (x | na[w])) | (x & ~chain[w]);
+					}
 				};
-				uint32_t gi = ngor;
-
+#pragma unroll 1
 				for (; gi + 2u <= ngroups; gi += 2u) {
-					uint32_t m[NW], m2[NW];
+					uint32_t m[2][NW], hk[2];
 
-					probe(gi, m);
-					probe(gi + 1u, m2);
-					chain_upd(gi, m);
-					chain_upd(gi + 1u, m2);
+					gf_probes<NW, 2>(xmg, gi, kvv, kxv, inf_lo, l3, flen, xmv, xmm, m, hk);
+					chain_upd(gi, m[0], hk[0]);
+					chain_upd(gi + 1u, m[1], hk[1]);
 				}
 				if (gi < ngroups) {
-					uint32_t m[NW];
+					uint32_t m[1][NW], hk[1];
 
-					probe(gi, m);
-					chain_upd(gi, m);
+					gf_probes<NW, 1>(xmg, gi, kvv, kxv, inf_lo, l3, flen, xmv, xmm, m, hk);
+					chain_upd(gi, m[0], hk[0]);
 				}
 			}
 		}
@@ -910,7 +941,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		 * error CoS, which error packets get without a walk): persistent
 		 * waves that start together would otherwise stream and walk in
 		 * step, leaving the memory idle while they all walk */
-		auto tails = [&]() {
+		auto tails = [&]() __attribute__((always_inline)) {
 			if constexpr (GF_EARLY && !GF_SWEEP) {
 				/* the early partial of [64, len), less the bytes [64, a)
 				 * when the L4 header starts past the window (as the
@@ -1194,7 +1225,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)C.qcol;
 		const uint32_t nc = A.num_cos < C.ncos ? A.num_cos : C.ncos;
 		/* without hash queues each CoS owns one column */
-		auto col = [&](uint32_t c) { return 4u + C.ncos + qc[c]; };
+		auto col = [&](uint32_t c) __attribute__((always_inline)) { return 4u + C.ncos + qc[c]; };
 		const uint32_t ne = dlv[GF_BIN_ERR], np = dlv[GF_BIN_PDROP];
 		const uint32_t ec = A.error_cos < 0 ? 0xffffffffu : (uint32_t)A.error_cos;
 		/* error packets: delivered to the error CoS unless it drops;
@@ -1206,7 +1237,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		 * workgroup owns its row; launches on the stream are ordered) */
 		/* the identity case (no hash queues) in a loop of its own without
 		 * loads: a load there would wait for every store before it */
-		auto flush_cols = [&](auto cf) {
+		auto flush_cols = [&](auto cf) __attribute__((always_inline)) {
 			for (uint32_t k0 = 0; k0 < nc; k0 += 64u) {
 				const uint32_t k = k0 + lane;
 				const uint32_t x = k < nc ? dlv[GF_BIN_EXTRA + k] : 0u;

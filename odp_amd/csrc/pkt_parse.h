@@ -967,7 +967,7 @@ __device__ __forceinline__ uint32_t seg_tail_sums3(uint64_t m, const uint8_t *g,
 	/* the owner of slot base + lane: a binary search of incl over the lanes
 	 * that can own a unit of the pass, then its fields */
 	auto owner = [&](uint32_t base, uint32_t &olo, uint32_t &ohi, uint32_t &opk,
-			 uint32_t &ofirst) {
+			 uint32_t &ofirst) __attribute__((always_inline)) {
 		const uint32_t slot = base + lane;
 		const uint64_t past = __ballot(incl > base);
 		const uint64_t beyond = __ballot(incl > base + 63u);
@@ -1259,6 +1259,37 @@ __device__ __forceinline__ uint32_t unit_sum_head(uint64_t addr, uint32_t re)
 	}
 	return acc;
 }
+/* unit_sum_head with the partial word's dword load issued first, beside the
+ * chunk loads (not behind their sums): bytes [0, re) of the 64-byte unit at
+ * addr, 1 <= re <= 64; the words below re / 4 kept by a compare each, the
+ * one holding the last byte (a cache hit: its chunk is loaded too) masked.
+ * A third of unit_sum_masked's instructions. */
+__device__ __forceinline__ uint32_t unit_sum_end(uint64_t addr, uint32_t re)
+{
+	const uint32_t nw = re >> 2, pb = re & 3u;
+	/* the partial word (at a loaded word of the unit when there is none) */
+	const uint32_t pwv = *(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)
+			     (addr + 4u * (pb ? nw : 0u));
+	uint4 q[4];
+
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		q[k] = make_uint4(0u, 0u, 0u, 0u);
+		if (16u * k < re)
+			q[k] = ld_g16(addr + 16u * k);
+	}
+	uint32_t acc = tail_dot2(pb ? pwv & ((1u << (8u * pb)) - 1u) : 0u, 0u);
+
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		acc = tail_dot2(4 * k + 0 < (int)nw ? q[k].x : 0u, acc);
+		acc = tail_dot2(4 * k + 1 < (int)nw ? q[k].y : 0u, acc);
+		acc = tail_dot2(4 * k + 2 < (int)nw ? q[k].z : 0u, acc);
+		acc = tail_dot2(4 * k + 3 < (int)nw ? q[k].w : 0u, acc);
+	}
+	return acc;
+}
+
 __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g, const L4Pend &pd,
 						uint32_t *marks = nullptr)
 {
@@ -1303,6 +1334,10 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 		 * again as a dword (a cache hit) */
 		if (SEG4_TAILW && !__ballot(mine && lead != 0u && lu == 0u))
 			own = unit_sum_head(gb + 64ull * lu, pd.b - c0 - 64u * lu);
+		else if (!__ballot(mine && lead != 0u && lu == 0u))
+			/* every last unit starts at its first byte (C3's early
+			 * tails: a = 64, always) */
+			own = unit_sum_end(gb + 64ull * lu, pd.b - c0 - 64u * lu);
 		else
 			own = unit_sum_masked(gb + 64ull * lu, lu ? 0 : (int)lead,
 					      (int)(pd.b - c0 - 64u * lu));
@@ -1320,7 +1355,7 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 
 	/* base address of the owner of slot min(base + lane, total - 1): binary
 	 * search of incl over the lanes that can own a slot of the pass */
-	auto owner = [&](uint32_t base) -> uint64_t {
+	auto owner = [&](uint32_t base) __attribute__((always_inline)) -> uint64_t {
 		const uint32_t slot = min(base + lane, total - 1u);
 #ifdef SEG4_EXP_NOOWNER     /* experiment builds only: cost of the owner search */
 		return (((uint64_t)cb_hi << 32) | cb_lo) + 64ull * slot;
@@ -1371,7 +1406,7 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 	};
 	/* a pass's sum: each lane's unit, then every frame's share of the pass
 	 * from the pass prefix sum (its slots of the pass are lanes [fl, ll]) */
-	auto consume = [&](const uint4 (&q)[4], uint32_t base) {
+	auto consume = [&](const uint4 (&q)[4], uint32_t base) __attribute__((always_inline)) {
 		uint32_t s = 0u;
 
 #pragma unroll
@@ -1394,7 +1429,7 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 
 		acc += in ? hv - (fl ? lv : 0u) : 0u;
 	};
-	auto load = [&](uint4 (&q)[4], uint64_t a) {
+	auto load = [&](uint4 (&q)[4], uint64_t a) __attribute__((always_inline)) {
 #pragma unroll
 		for (int k = 0; k < 4; ++k)
 			q[k] = ld_g16(a + 16u * k);

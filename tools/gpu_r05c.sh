@@ -11,6 +11,6 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 rc=$?; echo "tests: $rc"; tail -3 gpurun_out/r05c/pytest.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   for c in c2x c3; do
-    CFG=$c TAG=_c$r BENCH_EXTRA=--no-cpu VARIANTS="base exp_p4 exp_w4 exp_p4w4 exp_nogen" bash tools/ab.sh || exit $?
+    CFG=$c TAG=_c$r BENCH_EXTRA=--no-cpu VARIANTS="base exp_p4 exp_w4 exp_nogen" bash tools/ab.sh || exit $?
   done
 done
