@@ -332,15 +332,9 @@ template <int W, bool COOP, bool GF, bool DESC, int MODE, bool FAST, bool LEAN>
 #ifndef GEN_WAVES
 #define GEN_WAVES 6
 #endif
-#ifndef ODPG_TAIL_DEFER
-#define ODPG_TAIL_DEFER 1
-#endif
 #ifndef ODPG_DEFER_MOD          /* waves w with w % MOD < K sum tails after the walk */
 #define ODPG_DEFER_MOD 3
 #define ODPG_DEFER_K 1
-#endif
-#ifndef ODPG_SWEEP
-#define ODPG_SWEEP 0
 #endif
 __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) void odpg_classify_kernel(
 	const uint8_t *__restrict__ frames, const odpg_desc_t *__restrict__ desc,
@@ -362,12 +356,6 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 	uint32_t num_xwords, const odpg_cnt_args cnt)
 {
 	constexpr uint32_t RW = W / 4 + 1;       /* odd dword row stride */
-	/* descriptor batches with the 64-byte window: one coalesced sweep of
-	 * every frame byte per tile (sweep_frames). Experiment build
-	 * (-DODPG_SWEEP=1): HBM reads at the algorithmic bytes (C3 1.04x vs
-	 * 1.27x) but 139 vs 126 us, as the walk no longer overlaps other
-	 * waves' tail passes */
-	constexpr bool SWEEP = GF && DESC && W == 64 && !FAST && !COOP && ODPG_SWEEP;
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 	/* u64 hit-map kernel: mask-group entries (16 B aligned, after the rows)
 	 * and the one-read-per-level resolve table */
@@ -509,7 +497,6 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 
 	uint32_t f[16];
 	bool wave_fast = false;
-	uint32_t sweep_sum = 0u;
 
 	if constexpr (FAST) {
 		/* 64-byte frames straight into 16 registers, 4 x 16 B per lane;
@@ -562,11 +549,6 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 			dst[2] = x.z;
 			dst[3] = x.w;
 		}
-	} else if (SWEEP) {
-		/* every byte of the wave's frames in one coalesced sweep: the
-		 * windows land in the LDS rows, the sums of bytes [64, len) in
-		 * sweep_sum (pkt_parse.h) */
-		sweep_sum = sweep_frames(g, len, smem + (tid & ~63u) * RW, RW);
 	} else {
 #pragma unroll
 		for (uint32_t part = 0; part < W / 16; ++part) {
@@ -634,32 +616,14 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 	 * waves in each order the memory-bound tail passes of some waves run
 	 * while others issue their walks. Launches that count per-CoS packets
 	 * keep the original order (the walk counts the CoSes it visits). */
-	const bool defer = GF && !SWEEP && ODPG_TAIL_DEFER && !do_cos_stats &&
+	const bool defer = GF && !do_cos_stats &&
 			   (((blockIdx.x * (BLOCK / 64u)) + (tid >> 6)) % ODPG_DEFER_MOD) <
 				   ODPG_DEFER_K;
 	auto run_tails = [&]() {
 		const uint64_t pm = __ballot(ret == PARSE_PEND);
 
-		if (SWEEP && pm) {
-			/* the sweep summed [64, len); tails that start later (L4
-			 * header past the window) are summed again, rare */
-			const uint64_t late = __ballot(ret == PARSE_PEND && pd.a != (uint32_t)W);
-			const uint32_t t2 = late ? seg_tail_sums4(late, g, pd) : 0u;
-
-			if (ret == PARSE_PEND)
-				ret = finish_l4(p, pd, pd.a == (uint32_t)W ? sweep_sum : t2, opt);
-		} else if (pm) {
-#if defined(ODPG_COOP_TAIL)   /* experiment builds only: the per-frame wave passes */
-			const uint32_t tail = coop_tail_sums(pm, g, pd);
-#elif defined(ODPG_SEG_V1)    /* experiment builds only: per-frame pass loops */
-			const uint32_t tail = seg_tail_sums(pm, g, pd);
-#elif defined(ODPG_SEG_V2)    /* experiment builds only: 16-byte units */
-			const uint32_t tail = seg_tail_sums2(pm, g, pd);
-#elif defined(ODPG_SEG_V3)    /* experiment builds only: masked shared units */
-			const uint32_t tail = seg_tail_sums3(pm, g, pd);
-#else
+		if (pm) {
 			const uint32_t tail = seg_tail_sums4(pm, g, pd);
-#endif
 
 			if (ret == PARSE_PEND)
 				ret = finish_l4(p, pd, tail, opt);
@@ -843,11 +807,7 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 				 * one PMR at a time across the wave (uniform index:
 				 * scalar term loads, as MODE 0) */
 				uint32_t xk = 0u;
-#ifdef ODPG_EXP_NOXLIST        /* experiment builds only: cost without complex rules */
-				bool xp = false;
-#else
 				bool xp = active && xn != 0u && xlist_l[xs].x < best;
-#endif
 
 				while (__ballot(xp)) {
 					if (xp) {

@@ -51,9 +51,6 @@
 #ifndef L64_WAVES_HW     /* CoS-keyed cuckoo (walk-group) tables, e.g. C4 */
 #define L64_WAVES_HW 6
 #endif
-#ifndef L64_BUF          /* frames / verdicts through range-checked buffer ops */
-#define L64_BUF 0
-#endif
 #ifndef L64_BLOCK        /* threads per workgroup */
 #define L64_BLOCK 256
 #endif
@@ -66,26 +63,7 @@
 #ifndef L64_BLOCK_CNT     /* threads per workgroup of the sharded-counter kernels */
 #define L64_BLOCK_CNT L64_BLOCK
 #endif
-#ifdef L64_CNT_FIRST     /* experiment builds only: counted HW launches at L64_BLOCK_CNT */
-#define LBH(hw, cm) ((cm) == 2 ? L64_BLOCK_CNT : (hw) ? L64_BLOCK_HW : L64_BLOCK)
-#else
 #define LBH(hw, cm) ((hw) ? L64_BLOCK_HW : (cm) == 2 ? L64_BLOCK_CNT : L64_BLOCK)
-#endif
-#ifndef L64_MG_BARRIER   /* experiment builds only: mask-group counted flush by every wave */
-#define L64_MG_BARRIER 0
-#endif
-#ifndef L64_HW_LASTWAVE  /* experiment builds only: HW counted flush by the last wave */
-#define L64_HW_LASTWAVE 0
-#endif
-#ifndef L64_PP           /* two frame buffers used in turn (else one, rotated) */
-#define L64_PP 0
-#endif
-#ifndef L64_COAL         /* coalesced tile loads + swizzled LDS transpose */
-#define L64_COAL 1
-#endif
-#ifndef L64_NT           /* L64_COAL: the tile loads nontemporal */
-#define L64_NT 1
-#endif
 
 struct L64Args {
 	const uint4 *frames;
@@ -104,8 +82,6 @@ struct L64Args {
 	const uint4 *pinfo4;   /* mask groups: {dst | mark << 16, action, rule mask lo, hi} */
 	uint32_t def_mlo, def_mhi;   /* the default CoS's rule mask */
 	uint32_t def_cgmask;
-	uint32_t slot_n;       /* tiles per wave of each CU workgroup slot (4 bits each), 0 = round robin */
-	uint32_t ncu;          /* CUs (workgroups per slot) */
 	uint32_t err_cos;      /* error CoS, or ODPG_COS_NONE */
 	uint32_t err_act;      /* its action */
 	uint32_t def_cos;      /* CoS of error-free packets before the walk */
@@ -260,9 +236,7 @@ __device__ __forceinline__ uint4 lds_ent(const uint4 *p)
 {
 	const uint4 e = *p;
 
-#ifndef L64_NO_B128     /* experiment builds only: let the read narrow */
 	asm volatile("" ::"v"(e.w));
-#endif
 	return e;
 }
 
@@ -273,17 +247,6 @@ __device__ __forceinline__ uint4 lds_ent(const uint4 *p)
 #define BIN_DROP   3u
 #define BIN_EXTRA  4u
 
-#ifdef L64_EXP_TIMES   /* experiment builds only: per-wave start / end times */
-/* {s_memrealtime at the wave's start, at its end | tiles << 48} per wave */
-__device__ unsigned long long g_l64_times[2 * 65536];
-
-extern "C" int odpg_diag_l64_times(unsigned long long *out, uint32_t nwaves)
-{
-	if (nwaves > 65536u)
-		return -EINVAL;
-	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_l64_times), 16u * nwaves) == hipSuccess ? 0 : -EIO;
-}
-#endif
 
 /* ---- the kernel ------------------------------------------------------------
  * NG > 0: the table has exactly NG mask groups (HW: walk groups); their
@@ -299,10 +262,6 @@ odpg_cls64_kernel(const L64Args A)
 {
 	static_assert(!HW || NG > 0, "walk groups are hoisted");
 	constexpr uint32_t LBK = LBH(HW, CM);
-#ifdef L64_EXP_TIMES
-	const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-	uint32_t n_tiles = 0u;
-#endif
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 	constexpr uint32_t RW = 17;                     /* odd dword row stride */
 	uint32_t *row = smem + threadIdx.x * RW;        /* generic-parse LDS row */
@@ -329,33 +288,12 @@ odpg_cls64_kernel(const L64Args A)
 	const uint32_t ntiles = (A.num + 63u) >> 6;
 	const uint32_t num = A.num;
 	uint32_t fn[16];
-	/* This wave's tiles: tw0 + k * tws, k < twn. Round robin over the
-	 * waves by default; with slot counts (A.slot_n: 4 bits per workgroup
-	 * slot of a CU, slot = blockIdx / ncu, the order workgroups are
-	 * dispatched in) a wave of slot s runs n_s tiles: the oldest waves on a
-	 * CU win the vector-memory arbitration and finish first, so giving them
-	 * more tiles keeps every wave busy until the end (the drain after the
-	 * last loads). */
-	uint32_t tw0 = gw, tws = nwaves, twn = gw < ntiles ? (ntiles - gw + nwaves - 1u) / nwaves : 0u;
-
-	if (A.slot_n) {
-		const uint32_t wpc = A.ncu * (LBK / 64);           /* waves per slot */
-		const uint32_t sl = blockIdx.x / A.ncu;
-		const uint32_t r = (blockIdx.x - sl * A.ncu) * (LBK / 64) + (threadIdx.x >> 6);
-		uint32_t b0 = 0u;
-
-		for (uint32_t q = 0; q < sl; ++q)
-			b0 += ((A.slot_n >> (4u * q)) & 15u) * wpc;
-		const uint32_t n = (A.slot_n >> (4u * sl)) & 15u;
-
-		tw0 = __builtin_amdgcn_readfirstlane(b0 + r);
-		tws = wpc;
-		/* tiles past the batch are not run */
-		twn = __builtin_amdgcn_readfirstlane(tw0 < ntiles ? min(n, (ntiles - tw0 + wpc - 1u) / wpc) : 0u);
-	}
+	/* This wave's tiles: tw0 + k * tws, k < twn, round robin over the waves */
+	const uint32_t tw0 = gw, tws = nwaves;
+	const uint32_t twn = gw < ntiles ? (ntiles - gw + nwaves - 1u) / nwaves : 0u;
 
 	MGd mg[NG > 0 ? NG : 1];
-	/* L64_COAL: a tile's 4 KiB arrive as coalesced 16-byte loads, lane l
+	/* A tile's 4 KiB arrive as coalesced nontemporal 16-byte loads, lane l
 	 * holding chunks l, l + 64, l + 128, l + 192 of the tile (each load
 	 * instruction reads 1 KiB of contiguous lines, not 64 frames' first 16
 	 * bytes), and are transposed to one frame per lane through the wave's own
@@ -379,7 +317,7 @@ odpg_cls64_kernel(const L64Args A)
 #pragma unroll
 		for (int q = 0; q < 4; ++q) {
 			const uint32_t c = min(c0 + 64u * q, lim);
-			const uint4 x = L64_NT ? ld_nt16(A.frames + c) : ld_stream(A.frames + c);
+			const uint4 x = ld_nt16(A.frames + c);
 
 			dst[4 * q + 0] = x.x;
 			dst[4 * q + 1] = x.y;
@@ -405,26 +343,8 @@ odpg_cls64_kernel(const L64Args A)
 			f[4 * j + 3] = x.w;
 		}
 	};
-	(void)stage;
 	/* the first tile's frames are issued before the table copy below */
-	if (L64_COAL) {
-		load_raw(fn, twn ? tw0 : ntiles);
-	} else {
-		const uint32_t n0 = twn ? min(num - tw0 * 64u, 64u) : 0u;
-		const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-			(void *)(A.frames + (size_t)(gw < ntiles ? gw : 0u) * 256u), 0, (int)(n0 * 64u),
-			0x00020000);
-
-#pragma unroll
-		for (int q = 0; q < 4; ++q) {
-			const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(lane * 64u + q * 16u), 0, 0);
-
-			fn[4 * q + 0] = x.x;
-			fn[4 * q + 1] = x.y;
-			fn[4 * q + 2] = x.z;
-			fn[4 * q + 3] = x.w;
-		}
-	}
+	load_raw(fn, twn ? tw0 : ntiles);
 
 	if constexpr (HW) {
 		for (uint32_t k = threadIdx.x; k < A.num_cent; k += LBK)
@@ -634,19 +554,8 @@ odpg_cls64_kernel(const L64Args A)
 			const uint32_t b = pdrop ? BIN_PDROP : err ? BIN_ERR :
 					   cos >= A.num_cos ? BIN_NOCOS : act == 1u ? BIN_DROP : BIN_EXTRA + cos;
 
-#if defined(L64_EXP_BINLANE)   /* experiment builds only: conflict-free bins */
-			if (live)
-				atomicAdd(&dlv[(b & 0u) + lane], 1u);
-#elif defined(L64_EXP_BINZERO)  /* experiment builds only: one bin */
-			if (live)
-				atomicAdd(&dlv[b & 0u], 1u);
-#elif defined(L64_EXP_BINNONE)
-			if (b == 12345u)
-				atomicAdd(&dlv[0], 1u);
-#else
 			if (live)
 				atomicAdd(&dlv[b], 1u);
-#endif
 		} else if constexpr (CM == 1) {
 			/* in_packets: delivered error-free (cls ret 0); in_errors:
 			 * parse ret != 0; in_discards: cls ret -1 (no CoS; a CoS loop
@@ -679,49 +588,10 @@ odpg_cls64_kernel(const L64Args A)
 	auto tile_n = [&](uint32_t t) -> uint32_t {    /* frames of tile t in the batch */
 		return t < ntiles ? min(num - t * 64u, 64u) : 0u;
 	};
-	auto load_tile = [&](uint32_t (&dst)[16], uint32_t t) {
-#if L64_BUF
-		const uint32_t tt = t < ntiles ? t : 0u;
-		const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-			(void *)(A.frames + (size_t)tt * 256u), 0, (int)(tile_n(t) * 64u), 0x00020000);
-
-#pragma unroll
-		for (int q = 0; q < 4; ++q) {
-			const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(lane * 64u + q * 16u), 0, 0);
-
-			dst[4 * q + 0] = x.x;
-			dst[4 * q + 1] = x.y;
-			dst[4 * q + 2] = x.z;
-			dst[4 * q + 3] = x.w;
-		}
-#else
-		if (t >= ntiles)
-			return;
-		const uint4 *src = A.frames + (size_t)min(t * 64u + lane, num - 1u) * 4u;
-
-#pragma unroll
-		for (int q = 0; q < 4; ++q) {
-			const uint4 x = ld_stream(src + q);
-
-			dst[4 * q + 0] = x.x;
-			dst[4 * q + 1] = x.y;
-			dst[4 * q + 2] = x.z;
-			dst[4 * q + 3] = x.w;
-		}
-#endif
-	};
 	uint32_t pend_t = NO_TILE, pend_w = 0u;
 	auto store_pending = [&]() {
-#if L64_BUF
-		const uint32_t tt = pend_t < ntiles ? pend_t : 0u;
-		const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-			(void *)(A.out + (size_t)tt * 64u), 0, (int)(tile_n(pend_t) * 4u), 0x00020000);
-
-		__builtin_amdgcn_raw_buffer_store_b32(pend_w, r, (int)(lane * 4u), 0, 0);
-#else
 		if (lane < tile_n(pend_t))
 			A.out[pend_t * 64u + lane] = pend_w;
-#endif
 		pend_t = NO_TILE;
 	};
 
@@ -740,24 +610,9 @@ odpg_cls64_kernel(const L64Args A)
 		uint32_t lo = 0u, hi = 0u;
 		uint32_t kv[HW ? NG : 1];
 		bool krq[HW ? NG : 1];
-#ifdef L64_EXP_SKELETON   /* experiment builds only: loads + stores floor */
-		const uint32_t w = f[3] ^ f[9];
-#else
-#ifdef L64_EXP_NOPARSE   /* experiment builds only: match without the parse */
-		FastV r;
-		r.wbits = f[2] & 0x00f00000u;
-		r.inf_lo = (uint32_t)(IF(IFL_L2) | IF(IFL_ETH) | IF(IFL_L3) | IF(IFL_IPV4) |
-				      IF(IFL_L4) | IF(IFL_UDP));
-		r.err = false;
-#else
 		const FastV r = parse_fast64(f, A.opt);
-#endif
 
-#ifdef L64_EXP_NOMATCH   /* experiment builds only: parse without the match */
-		if (false) {
-#else
 		if (walk) {
-#endif
 			const u32x16_t fv = {f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7],
 					     f[8], f[9], f[10], f[11], f[12], f[13], f[14], f[15]};
 			auto fast_key = [&](const MGd &d) -> uint32_t {
@@ -784,21 +639,20 @@ odpg_cls64_kernel(const L64Args A)
 			}
 		}
 		const uint32_t w = finish(live, false, r.err, r.wbits, lo, hi, kv, krq);
-#endif
 		pend_t = t;
 		pend_w = w;
 		return false;
 	};
 
 	/* Tiles in chunks of up to 64 per wave. Inside a chunk only plain waves
-	 * are classified; frames arrive in two register buffers used in turn,
-	 * each refilled with the tile two steps ahead right after its tile is
-	 * classified, so a wave waiting for one tile has the next one in flight.
+	 * are classified; a tile's raw chunks (fn, loaded one tile ahead) are
+	 * transposed into the frame buffer fb through the wave's LDS rows, and
+	 * the next tile's loads are issued before this one is classified.
 	 * A tile with any other frame is marked in `defer` and classified after
 	 * the chunk by the generic parse, with its frames re-read: the hot loop
 	 * stays small (instruction cache) and no prefetch registers are live
 	 * across the generic parse (register pressure). */
-	uint32_t fb[16];   /* second frame buffer (ping-pong with fn) */
+	uint32_t fb[16];   /* this tile's frames, one per lane (fn: the raw chunks) */
 	bool first = true;
 
 	for (uint32_t t0 = tw0, rem = twn; rem;) {
@@ -806,25 +660,9 @@ odpg_cls64_kernel(const L64Args A)
 		uint64_t defer = 0ull;
 
 		if (!first) {
-			if (L64_COAL)
-				load_raw(fn, t0);
-			else
-				load_tile(fn, t0);
+			load_raw(fn, t0);
 		}
 		first = false;
-#if L64_PP
-		load_tile(fb, nk > 1u ? t0 + tws : NO_TILE);
-		for (uint32_t k = 0; k < nk; k += 2u) {
-			const uint32_t t = t0 + k * tws;
-
-			if (tile(fn, t))
-				defer |= 1ull << k;
-			load_tile(fn, k + 2u < nk ? t + 2u * tws : NO_TILE);
-			if (tile(fb, k + 1u < nk ? t + tws : NO_TILE))
-				defer |= 2ull << k;
-			load_tile(fb, k + 3u < nk ? t + 3u * tws : NO_TILE);
-		}
-#elif L64_COAL
 		for (uint32_t k = 0; k < nk; ++k) {
 			const uint32_t t = t0 + k * tws;
 
@@ -833,18 +671,6 @@ odpg_cls64_kernel(const L64Args A)
 			if (tile(fb, t))
 				defer |= 1ull << k;
 		}
-#else
-		for (uint32_t k = 0; k < nk; ++k) {
-			const uint32_t t = t0 + k * tws;
-
-#pragma unroll
-			for (int q = 0; q < 16; ++q)
-				fb[q] = fn[q];
-			load_tile(fn, k + 1u < nk ? t + tws : NO_TILE);
-			if (tile(fb, t))
-				defer |= 1ull << k;
-		}
-#endif
 		store_pending();
 
 		/* ---- the chunk's deferred tiles: generic parse ------------------- */
@@ -938,20 +764,7 @@ odpg_cls64_kernel(const L64Args A)
 		}
 		t0 += nk * tws;
 		rem -= nk;
-#ifdef L64_EXP_TIMES
-		n_tiles += nk;
-#endif
 	}
-#ifdef L64_EXP_TIMES
-	{
-		const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-
-		if (__lane_id() == 0u && gw < 65536u) {
-			g_l64_times[2u * gw] = t_start;
-			g_l64_times[2u * gw + 1u] = t_end | ((unsigned long long)n_tiles << 48);
-		}
-	}
-#endif
 	if constexpr (CM == 2) {
 		/* the workgroup's histogram into its own counter row (odpg.h
 		 * "sharded counters"): plain stores of the row read at the start
@@ -959,10 +772,6 @@ odpg_cls64_kernel(const L64Args A)
 		 * on the stream are ordered). No-return atomics here, ~70 per
 		 * workgroup, all reached L2 together at the kernel's common tail
 		 * (+1 us of 13.3 on C2) */
-#ifdef L64_EXP_NOFLUSH   /* experiment builds only */
-		if (A.num_cos != 12345u)
-			return;
-#endif
 		/* Mask-group tables (<= 64 PMRs, a few dozen bins): no barrier,
 		 * each wave counts itself done after its histogram adds (LDS
 		 * operations of a wave complete in order; the fence makes that
@@ -977,7 +786,7 @@ odpg_cls64_kernel(const L64Args A)
 		if (A.cnt.words <= LBK && threadIdx.x < A.cnt.words)
 			base[threadIdx.x] = rowv;
 
-		if constexpr ((HW || L64_MG_BARRIER) && !L64_HW_LASTWAVE) {
+		if constexpr (HW) {
 			__syncthreads();
 			k_first = threadIdx.x;
 			k_step = LBK;
@@ -1030,7 +839,7 @@ odpg_cls64_kernel(const L64Args A)
 			flush_cols(col);
 		uint32_t t = wave_sum_u32(tot);            /* in_packets, in_octets */
 
-		if constexpr ((HW || L64_MG_BARRIER) && !L64_HW_LASTWAVE) {
+		if constexpr (HW) {
 			/* every wave flushed a slice: the in_packets total over them */
 			if (lane == 0u && t)
 				atomicAdd(&flush_tot, t);
@@ -1108,9 +917,6 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 
 	const bool hw = (a->tbl_flags & TBL_LEAN64HW) && !(a->tbl_flags & TBL_LEAN64);
 	size_t lds = odpg_cls64_lds(*a);
-#ifdef L64_LDS_PAD   /* experiment builds only: occupancy sensitivity */
-	lds += L64_LDS_PAD;
-#endif
 	const uint32_t ntiles = (a->num + 63u) / 64u;
 	const uint32_t lb = LBH(hw, a->cnt.row ? 2 : 0);
 	const uint32_t want = (ntiles + lb / 64u - 1u) / (lb / 64u);
@@ -1131,36 +937,6 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s)
 			grid -= grid / 8u;
 		grid = grid < want ? grid : want;
 		grid = grid < rows ? grid : rows;
-#ifdef L64_EXP_GRIDENV   /* experiment builds only: ODPG_L64_GRID workgroups */
-		if (const char *ge = getenv("ODPG_L64_GRID"))
-			grid = (uint32_t)atoi(ge);
-#endif
-		A.slot_n = 0u;
-		A.ncu = 1u;
-		/* ODPG_L64_SLOTS="n0,n1,...": tiles per wave of each CU workgroup
-		 * slot (experiments), used when they cover the batch */
-		static const char *slots_env = getenv("ODPG_L64_SLOTS");
-		int cus = 0;
-
-		if (slots_env && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) == hipSuccess &&
-		    cus > 0 && grid % (uint32_t)cus == 0u && grid / (uint32_t)cus <= 8u) {
-			uint32_t packed = 0u, cover = 0u, ns = 0u;
-
-			for (const char *c = slots_env; *c && ns < grid / (uint32_t)cus; ns++) {
-				const uint32_t v = (uint32_t)atoi(c) & 15u;
-
-				packed |= v << (4u * ns);
-				cover += v;
-				while (*c && *c != ',')
-					c++;
-				if (*c == ',')
-					c++;
-			}
-			if (ns == grid / (uint32_t)cus && (uint64_t)cover * (uint32_t)cus * (lb / 64u) >= ntiles) {
-				A.slot_n = packed;
-				A.ncu = (uint32_t)cus;
-			}
-		}
 		launch(grid);
 	};
 #define L64_LAUNCH_CM(ng, h, c, k)                                                           \

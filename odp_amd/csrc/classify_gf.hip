@@ -65,9 +65,6 @@
 #ifndef GF_RW               /* LDS row stride per lane, dwords (16-byte multiple) */
 #define GF_RW 20
 #endif
-#ifndef GF_LATE_ODD         /* odd waves sum their tails after the walk */
-#define GF_LATE_ODD 0
-#endif
 
 struct GFArgs {
 	const uint8_t *frames;
@@ -313,183 +310,9 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 	return (fl & FL_ERROR_MASK) != 0u;
 }
 
-#ifndef GF_SWEEP            /* 1: one coalesced sweep of every frame byte per tile */
-#define GF_SWEEP 0
-#endif
 #ifndef GF_PROBES           /* chain-free groups probed together (2-word maps) */
 #define GF_PROBES 2
 #endif
-#ifndef GF_MARKS            /* tail-pass owners from an LDS mark map (else a */
-#define GF_MARKS 1          /* binary search of bpermutes; C3 -0.7 us) */
-#endif
-#ifndef GF_WIN_LATE         /* next tile's windows issued after the walk */
-#define GF_WIN_LATE 0
-#endif
-/* GF_EARLY: a tile's checksum tails are summed one tile ahead (every
- * frame's bytes [64, len), whether or not its parse will want them), right
- * after its windows are issued (1) or after the current tile's walk (2), so
- * a 128-byte line shared by a window and a tail unit is requested twice
- * within a short time instead of a tile apart, when the L2 has let it go
- * (0: 1.24x the algorithmic reads) */
-#ifndef GF_EARLY
-#define GF_EARLY 1
-#endif
-
-/* One coalesced sweep over every byte of a wave's 64 frames: the frames'
- * 64-byte units (unit 0 the window, units 1.. the tail) numbered frame after
- * frame and spread over the lanes, 64 units per pass, two passes in flight;
- * each 128-byte line is requested by neighbouring lanes of one instruction,
- * once. Unit 0 lands in its frame's LDS row (zero past the frame), the first
- * dword of unit 1 in x16s[frame]; every other byte is summed (v_dot2) and
- * attributed to its frame by a wave prefix sum per pass: tsum[lane] = the
- * one's-complement partial of the lane's frame's bytes [64, len). All lanes
- * must be active. */
-struct SwUnit {
-	uint4 q[4];
-	uint32_t pv;
-	uint32_t ou;        /* owner lane | unit << 6 | bytes of the frame it holds << 16 */
-};
-
-/* a pass's unit: its owner (binary search of the prefix sums over the lanes
- * that can own a unit of the pass), the bytes of the owner's frame it holds,
- * and its loads (only 16-byte chunks holding frame bytes; the one partial
- * dword again as a dword). Every lane active: a bpermute under a partial
- * exec mask reads inactive source lanes as 0 */
-struct SwPlan {
-	uint32_t len, nu, incl, first, total, cb_lo, cb_hi;
-};
-
-__device__ __forceinline__ void sw_plan(const SwPlan &S, uint32_t base, SwUnit &U)
-{
-	const uint32_t lane = __lane_id();
-	const uint32_t sl = min(base + lane, S.total - 1u);
-	const bool valid = base + lane < S.total;
-	const uint64_t past = __ballot(S.incl > base);
-	const uint64_t beyond = __ballot(S.incl > base + 63u);
-	const uint32_t lo = past ? (uint32_t)__builtin_ctzll(past) : 63u;
-	const uint32_t hi = beyond ? (uint32_t)__builtin_ctzll(beyond) : 63u;
-	const uint32_t span = hi > lo ? hi - lo : 0u;
-	int pp = -1;
-
-	for (uint32_t st = span ? 1u << (31 - __builtin_clz(span)) : 0u; st; st >>= 1) {
-		const uint32_t cand = (uint32_t)(pp + (int)st);
-		const uint32_t src = lo + cand < 64u ? lo + cand : 63u;
-		const uint32_t v = lane_pull(S.incl, src);
-
-		if (cand <= span && v <= sl)
-			pp = (int)cand;
-	}
-	const uint32_t o = lo + (uint32_t)(pp + 1);
-	const uint64_t a = (((uint64_t)lane_pull(S.cb_hi, o) << 32) | lane_pull(S.cb_lo, o)) +
-			   64ull * sl;
-	const uint32_t ofirst = lane_pull(S.first, o), olen = lane_pull(S.len, o);
-	const uint32_t u = sl - ofirst;
-	/* bytes of the owner's frame in the unit, capped at 65 (> 64: whole) */
-	const uint32_t rb = olen - 64u * u;
-	const uint32_t rem = valid ? (rb > 65u ? 65u : rb) : 0u;   /* >= 1 */
-	const uint32_t nw = rem >> 2;
-	const uint32_t pb = rem & 3u;
-
-	U.ou = o | (u << 6) | (rem << 16);
-	U.pv = 0u;
-	if (rem && pb && nw < 16u)
-		U.pv = *(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)(a + 4u * nw) &
-		       ((1u << (8u * pb)) - 1u);
-#pragma unroll
-	for (int j = 0; j < 4; ++j) {
-		U.q[j] = make_uint4(0u, 0u, 0u, 0u);
-		if (16u * j < rem)
-			U.q[j] = ld_g16(a + 16u * j);
-	}
-}
-
-__device__ __forceinline__ void gf_sweep(const uint8_t *frames, uint2 d, uint32_t *rows,
-					 uint32_t *x16s, uint32_t *tsum)
-{
-	const uint32_t lane = __lane_id();
-	SwPlan S;
-	uint32_t acc = 0u;
-
-	S.len = d.y;
-	S.nu = S.len ? ((S.len - 1u) >> 6) + 1u : 0u;
-	S.incl = wave_scan_u32(S.nu);
-	S.first = S.incl - S.nu;
-	S.total = (uint32_t)__builtin_amdgcn_readlane((int)S.incl, 63);
-	/* unit slot s of this lane's frame starts at cb + 64 s */
-	const uint64_t cb = (uint64_t)(uintptr_t)(frames + d.x) - 64ull * S.first;
-
-	S.cb_lo = (uint32_t)cb;
-	S.cb_hi = (uint32_t)(cb >> 32);
-	x16s[lane] = 0u;
-	if (S.len == 0u) {                               /* empty frame: zero window */
-#pragma unroll
-		for (int k = 0; k < 16; k += 4)
-			*(uint4 *)(rows + GF_RW * lane + k) = make_uint4(0u, 0u, 0u, 0u);
-	}
-	auto consume = [&](const SwUnit &U, uint32_t base) __attribute__((always_inline)) {
-		const uint32_t uo = U.ou & 63u, uu = (U.ou >> 6) & 0x3ffu, rem = U.ou >> 16;
-		const uint32_t nw = rem >> 2;
-		const uint32_t pb = rem & 3u;
-		uint32_t w[16];
-
-#pragma unroll
-		for (int j = 0; j < 4; ++j) {
-			w[4 * j + 0] = 4 * j + 0 < (int)nw ? U.q[j].x : 0u;
-			w[4 * j + 1] = 4 * j + 1 < (int)nw ? U.q[j].y : 0u;
-			w[4 * j + 2] = 4 * j + 2 < (int)nw ? U.q[j].z : 0u;
-			w[4 * j + 3] = 4 * j + 3 < (int)nw ? U.q[j].w : 0u;
-		}
-		uint32_t sum = 0u;
-
-		if (rem && uu == 0u) {
-			uint32_t *r = rows + GF_RW * uo;
-
-#pragma unroll
-			for (int k = 0; k < 16; ++k)
-				if (pb && (uint32_t)k == nw)
-					w[k] = U.pv;
-#pragma unroll
-			for (int k = 0; k < 16; k += 4)
-				*(uint4 *)(r + k) = make_uint4(w[k], w[k + 1], w[k + 2], w[k + 3]);
-		} else {
-			if (rem && uu == 1u)
-				x16s[uo] = nw ? w[0] : U.pv;
-#pragma unroll
-			for (int k = 0; k < 16; ++k)
-				sum = tail_dot2(w[k], sum);
-			sum = tail_dot2(U.pv, sum);
-		}
-		/* this lane's frame: its units of the pass are lanes [fl, ll] */
-		const uint32_t ps = wave_scan_u32(oc_fold(sum));
-		const bool in = S.nu && S.incl > base && S.first < base + 64u;
-		const uint32_t fl = in && S.first > base ? S.first - base : 0u;
-		const uint32_t ll = in ? (S.incl - 1u < base + 63u ? S.incl - 1u - base : 63u) : 0u;
-		const uint32_t hv = lane_pull(ps, ll);
-		const uint32_t lv = lane_pull(ps, fl ? fl - 1u : 0u);
-
-		acc += in ? hv - (fl ? lv : 0u) : 0u;
-	};
-	SwUnit ua, ub;
-
-	if (S.total) {                                          /* uniform */
-		sw_plan(S, 0u, ua);
-		if (64u < S.total)
-			sw_plan(S, 64u, ub);
-	}
-	for (uint32_t base = 0; base < S.total; base += 128u) {    /* uniform */
-		consume(ua, base);
-		if (base + 128u < S.total)
-			sw_plan(S, base + 128u, ua);
-		if (base + 64u < S.total) {
-			consume(ub, base + 64u);
-			if (base + 192u < S.total)
-				sw_plan(S, base + 192u, ub);
-		}
-	}
-	tsum[lane] = oc_fold(acc);
-	/* the rows written by other lanes are read next by their own lanes */
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-}
 
 /* the hit map's NW words of entry e (NW 2: one ds_read_b64; 4: one
  * ds_read_b128; 8: two) */
@@ -598,14 +421,10 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	/* CM 2: the workgroup's counter row as it stood before this launch
 	 * (read at the start; the flush stores row + histogram) */
 	unsigned long long *base = (unsigned long long *)(tb + ((A.L.lds_words + 1u) & ~1u));
-	/* GF_SWEEP: the wave's x16 words and tail partials (2 x 64 dwords) */
-	uint32_t *swx = tb + ((A.L.lds_words + 1u) & ~1u) + (CM == 2 ? 2u * A.cnt_words : 0u) +
-			(threadIdx.x >> 6) * 128u;
-	/* GF_MARKS: the wave's 64-dword scratch of the tail pass's owner map
+	/* the wave's 64-dword scratch of the tail pass's owner map
 	 * (seg_tail_sums4) */
-	uint32_t *marks = GF_MARKS ? tb + ((A.L.lds_words + 1u) & ~1u) + (CM == 2 ? 2u * A.cnt_words : 0u) +
-					     (GF_SWEEP ? GF_BLOCK * 2u : 0u) + (threadIdx.x >> 6) * 64u
-				   : nullptr;
+	uint32_t *marks = tb + ((A.L.lds_words + 1u) & ~1u) + (CM == 2 ? 2u * A.cnt_words : 0u) +
+			  (threadIdx.x >> 6) * 64u;
 
 	const uint32_t lane = __lane_id();
 	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (GF_BLOCK / 64) +
@@ -644,8 +463,13 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	};
 	uint32_t fn[16] = {}, xn = 0u;
 	uint2 dn = load_desc(gw), dnn;
-	/* GF_EARLY: the tails of a tile's frames, bytes [64, len), as each
-	 * lane's one's-complement partial (seg_tail_sums4; the whole wave) */
+	/* The tails of a tile's frames, bytes [64, len), as each lane's
+	 * one's-complement partial (seg_tail_sums4; the whole wave), summed one
+	 * tile ahead (every frame's, whether or not its parse will want them),
+	 * right after the tile's windows are issued: a 128-byte line shared by
+	 * a window and a tail unit is then requested twice within a short time
+	 * instead of a tile apart, when the L2 has let it go (tails summed in
+	 * their own tile read 1.24x the algorithmic bytes) */
 	const bool l4ck = (A.opt & (ODPG_PKTIN_UDP_CHKSUM | ODPG_PKTIN_TCP_CHKSUM)) != 0u;
 	auto early_tails = [&](uint2 d, uint32_t t) __attribute__((always_inline)) -> uint32_t {
 		const uint32_t len = t < ntiles && t * 64u + lane < num ? d.y : 0u;
@@ -659,9 +483,8 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	};
 	uint32_t tn = 0u;
 
-	if (!GF_SWEEP)
-		load_win(fn, xn, dn);
-	if (GF_EARLY && !GF_SWEEP && l4ck)
+	load_win(fn, xn, dn);
+	if (l4ck)
 		tn = early_tails(dn, gw);
 	dnn = load_desc(gw + nwaves);
 
@@ -720,27 +543,14 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		const uint32_t i = t * 64u + lane;
 		const bool live = i < num;
 		const uint2 d = dn;
-		const uint32_t tsum = tn;       /* GF_EARLY: this tile's [64, len) */
+		const uint32_t tsum = tn;       /* this tile's tails [64, len) */
 		const uint8_t *g = A.frames + d.x;
 		const uint32_t len = live ? d.y : 0u;
 		uint32_t f[16];
 		uint32_t x16 = xn;
 		uint32_t tile_oct = 0u;  /* CM 2: octets this lane hands over */
 
-		if constexpr (GF_SWEEP) {
-			gf_sweep(A.frames, make_uint2(d.x, len), smem + (threadIdx.x & ~63u) * RW, swx,
-				 swx + 64u);
-#pragma unroll
-			for (int q = 0; q < 16; q += 4) {
-				const uint4 x = *(const uint4 *)(row + q);
-
-				f[q] = x.x;
-				f[q + 1] = x.y;
-				f[q + 2] = x.z;
-				f[q + 3] = x.w;
-			}
-			x16 = swx[lane];
-		} else if (__ballot(live && len < 64u)) {
+		if (__ballot(live && len < 64u)) {
 #pragma unroll
 			for (int q = 0; q < 16; ++q) {
 				/* bytes past the frame read as zero (the reference's
@@ -809,11 +619,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		gf_kv_t kv = {};
 		uint32_t k16 = 0u, k17 = 0u;
 
-#ifdef GF_EXP_NOGEN
-		if (true) {
-#else
 		if (fastw) {
-#endif
 			if (live)
 				ret = parse_fast_gf(p, pd, f, s14, s15, len, opt, sh, qinq);
 			bases();
@@ -941,72 +747,30 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		 * error CoS, which error packets get without a walk): persistent
 		 * waves that start together would otherwise stream and walk in
 		 * step, leaving the memory idle while they all walk */
-		auto tails = [&]() __attribute__((always_inline)) {
-			if constexpr (GF_EARLY && !GF_SWEEP) {
-				/* the early partial of [64, len), less the bytes [64, a)
-				 * when the L4 header starts past the window (as the
-				 * sweep below) */
-				if (ret == PARSE_PEND) {
-					uint32_t tail = tsum;
+		/* ---- the UDP / TCP checksum bytes past the window: the partial
+		 * of [64, len) summed a tile ahead, less the bytes [64, a) when the
+		 * L4 header starts past the window (generic frames: the residue mod
+		 * 0xffff is the tail's, and the pending sum holds the nonzero
+		 * protocol term, so the verdict is the same) */
+		if (ret == PARSE_PEND) {
+			uint32_t tail = tsum;
 
-					if (pd.a > 64u) {
-						Pkt<64, true> v;
+			if (pd.a > 64u) {
+				Pkt<64, true> v;
 
-						v.row = row;
-						v.g = g;
-						v.len = len;
-						tail = oc_add(tail, 0xffffu - oc_fold(sum_range(v, 64u, pd.a)));
-					}
-					ret = finish_l4(p, pd, tail, (uint64_t)opt);
-				}
-				return;
+				v.row = row;
+				v.g = g;
+				v.len = len;
+				tail = oc_add(tail, 0xffffu - oc_fold(sum_range(v, 64u, pd.a)));
 			}
-			if constexpr (GF_SWEEP) {
-				/* the sweep's partial of [64, len), less the bytes [64, a)
-				 * when the L4 header starts past the window (generic frames:
-				 * the residue mod 0xffff is the tail's, and the pending sum
-				 * holds the nonzero protocol term, so the verdict is the
-				 * same) */
-				if (ret == PARSE_PEND) {
-					uint32_t tail = swx[64u + lane];
+			ret = finish_l4(p, pd, tail, (uint64_t)opt);
+		}
 
-					if (pd.a > 64u) {
-						Pkt<64, true> v;
-
-						v.row = row;
-						v.g = g;
-						v.len = len;
-						tail = oc_add(tail, 0xffffu - oc_fold(sum_range(v, 64u, pd.a)));
-					}
-					ret = finish_l4(p, pd, tail, (uint64_t)opt);
-				}
-				return;
-			}
-			const uint64_t pm = __ballot(ret == PARSE_PEND);
-
-#ifdef GF_EXP_NOTAIL
-			if (false) {
-#else
-			if (pm) {
-#endif
-				const uint32_t tail = seg_tail_sums4(pm, g, pd, marks);
-
-				if (ret == PARSE_PEND)
-					ret = finish_l4(p, pd, tail, (uint64_t)opt);
-			}
-		};
-		const bool late = GF_LATE_ODD && (gw & 1u);
-
-		if (!late)
-			tails();
-
-		/* the next tile's windows, in flight during the walk. GF_EARLY 1:
-		 * the next tile's tails right behind them; 2: after the walk */
-		if (!GF_SWEEP && !GF_WIN_LATE)
-			load_win(fn, xn, dn);
-		if (GF_EARLY == 1 && !GF_SWEEP && l4ck)
+		/* the next tile's windows, in flight during the walk, and its
+		 * tails right behind them */
+		load_win(fn, xn, dn);
+		if (l4ck)
 			tn = early_tails(dn, t + nwaves);
-		const uint2 dnext = dn;
 		dnn = load_desc(t + 2u * nwaves);
 
 		/* ---- CoS walk (cls_select_cos + match_pmr_cos) ------------------ */
@@ -1026,9 +790,6 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 				cos = A.default_cos < 0 ? ODPG_COS_NONE : (uint32_t)A.default_cos;
 			}
 		}
-#ifdef GF_EXP_NOWALK   /* experiment builds only: cost without the walk */
-		active = false;
-#endif
 		{
 			/* a level: the lowest set bit of the CoS's bit range [start,
 			 * start + n) in the hit map; (lazy form) the CoS's complex PMRs
@@ -1121,25 +882,6 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			}
 		}
 
-		if (GF_EARLY == 2 && !GF_SWEEP && l4ck)
-			tn = early_tails(dnext, t + nwaves);
-
-		if (late) {
-			tails();
-			if (want_cls && !err && (p.fl & FL_ERROR_MASK)) {
-				/* cls_select_cos's error branch (no PMR walk) */
-				cos = A.error_cos < 0 ? ODPG_COS_NONE : (uint32_t)A.error_cos;
-				any_match = false;
-				mark = 0u;
-			}
-			err = (p.fl & FL_ERROR_MASK) != 0u;
-		}
-
-		/* GF_WIN_LATE: the next tile's windows after the walk, so that their
-		 * lines are still in L2 when that tile's tails read the rest */
-		if (!GF_SWEEP && GF_WIN_LATE)
-			load_win(fn, xn, dn);
-
 		/* ---- verdict word (odpg.h) ------------------------------------- */
 		if (live) {
 			int cret = 0;
@@ -1181,9 +923,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 						    cos >= A.num_cos ? GF_BIN_NOCOS :
 						    cret == 1 ? GF_BIN_DROP : GF_BIN_EXTRA + cos;
 
-#ifndef GF_EXP_NOBIN      /* experiment builds only: cost of the histogram adds */
 				atomicAdd(&dlv[bn], 1u);
-#endif
 				tile_oct = bn >= GF_BIN_EXTRA ? len : 0u;
 			}
 		}
@@ -1202,10 +942,6 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		 * delivery counts into this workgroup's counter row: no barrier,
 		 * each wave counts itself done after its adds, the last one of the
 		 * workgroup flushes while the others have exited */
-#ifdef GF_EXP_NOFLUSH      /* experiment builds only: cost of the flush */
-		if (A.num != 12345u)
-			return;
-#endif
 		if (GF_ROW_REGS(NW) && A.cnt.words <= GF_BLOCK && threadIdx.x < A.cnt.words)
 			base[threadIdx.x] = rowv;
 		__threadfence_block();
@@ -1292,7 +1028,7 @@ extern "C" size_t odpg_clsgf_lds(const odpg_launch_args *a)
 
 	return (size_t)GF_BLOCK * GF_RW * 4u + bins + (size_t)((L.lds_words + 1u) & ~1u) * 4u +
 	       (a->cnt.row ? (size_t)a->cnt.words * 8u : 0u) +
-	       (GF_SWEEP ? (size_t)GF_BLOCK * 2u * 4u : 0u) + (GF_MARKS ? (size_t)GF_BLOCK * 4u : 0u);
+	       (size_t)GF_BLOCK * 4u;
 }
 
 extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s)

@@ -368,10 +368,6 @@ __global__ __launch_bounds__(FBLOCK) void odpg_l3fwd_kernel(
 
 			dp[0] = make_uint4(f[0], f[1], f[2], f[3]);
 			dp[1] = make_uint4(f[4], f[5], f[6], f[7]);
-#ifdef FWD_FULLW
-			dp[2] = make_uint4(f[8], f[9], f[10], f[11]);
-			dp[3] = make_uint4(f[12], f[13], f[14], f[15]);
-#endif
 		} else {
 			uint32_t *w = (uint32_t *)fr;
 			const uint32_t ttl = v.u8(l3 + 8u);
@@ -404,12 +400,6 @@ __global__ __launch_bounds__(FBLOCK) void odpg_l3fwd_kernel(
 #endif
 #ifndef FWD_WAVES           /* waves per SIMD the launch bounds ask for */
 #define FWD_WAVES 8
-#endif
-#ifndef FWD_NT              /* nontemporal tile loads */
-#define FWD_NT 0
-#endif
-#ifndef FWD_COALW           /* fast waves store through the LDS transpose: 1 bytes 0..31, 2 all 64 */
-#define FWD_COALW 2
 #endif
 
 template <bool LPM>
@@ -445,7 +435,7 @@ __global__ __launch_bounds__(FWD_PBLOCK, FWD_WAVES * 256 / FWD_PBLOCK) void odpg
 #pragma unroll
 		for (int q = 0; q < 4; ++q) {
 			const size_t c = c0 + 64u * q;
-			const uint4 x = FWD_NT ? ld_nt16(frames + (c < lim ? c : lim)) : frames[c < lim ? c : lim];
+			const uint4 x = frames[c < lim ? c : lim];
 
 			dst[4 * q + 0] = x.x;
 			dst[4 * q + 1] = x.y;
@@ -542,39 +532,27 @@ __global__ __launch_bounds__(FWD_PBLOCK, FWD_WAVES * 256 / FWD_PBLOCK) void odpg
 
 			if (LPM)
 				load_raw(fn, t + nwaves);
-			if (FWD_COALW) {
-				/* the rewritten frame back through the same LDS slots, then
-				 * each lane stores the chunks it loaded (1 KiB contiguous
-				 * per store instruction) */
-				const uint4 c0 = make_uint4(mac.x, mac.y, mac.z, f[3]);
-				const uint4 c1 = make_uint4(f[4], ttl_csum_word5(f[5]),
-							    (f[6] & 0xffff0000u) | csum_update(f[6] & 0xffffu), f[7]);
+			/* the rewritten frame back through the same LDS slots, then each
+			 * lane stores the chunks it loaded (1 KiB contiguous per store
+			 * instruction; whole frames: a partial-sector write costs more
+			 * than the whole sector) */
+			const uint4 c0 = make_uint4(mac.x, mac.y, mac.z, f[3]);
+			const uint4 c1 = make_uint4(f[4], ttl_csum_word5(f[5]),
+						    (f[6] & 0xffff0000u) | csum_update(f[6] & 0xffffu), f[7]);
 
-				*(uint4 *)(stg + 16u * lane + 4u * ((0u + sw_c) & 3u)) = c0;
-				*(uint4 *)(stg + 16u * lane + 4u * ((1u + sw_c) & 3u)) = c1;
-				if (live)
-					out_port[i] = dif;
-				const size_t cb = (size_t)t * 256u + lane;
-				const size_t nc = (size_t)num * 4u;
+			*(uint4 *)(stg + 16u * lane + 4u * ((0u + sw_c) & 3u)) = c0;
+			*(uint4 *)(stg + 16u * lane + 4u * ((1u + sw_c) & 3u)) = c1;
+			if (live)
+				out_port[i] = dif;
+			const size_t cb = (size_t)t * 256u + lane;
+			const size_t nc = (size_t)num * 4u;
 
 #pragma unroll
-				for (int q = 0; q < 4; ++q) {
-					const size_t c = cb + 64u * q;
+			for (int q = 0; q < 4; ++q) {
+				const size_t c = cb + 64u * q;
 
-					if ((FWD_COALW == 2 || (lane & 3u) < 2u) && c < nc)
-						frames[c] = *(const uint4 *)(stg + sw_w + 256u * q);
-				}
-				continue;
-			}
-			if (live) {
-				fr[0] = make_uint4(mac.x, mac.y, mac.z, f[3]);
-				fr[1] = make_uint4(f[4], ttl_csum_word5(f[5]),
-						   (f[6] & 0xffff0000u) | csum_update(f[6] & 0xffffu), f[7]);
-#ifdef FWD_FULLW
-				fr[2] = make_uint4(f[8], f[9], f[10], f[11]);
-				fr[3] = make_uint4(f[12], f[13], f[14], f[15]);
-#endif
-				out_port[i] = dif;
+				if (c < nc)
+					frames[c] = *(const uint4 *)(stg + sw_w + 256u * q);
 			}
 			continue;
 		}
@@ -815,7 +793,6 @@ extern "C" int odpg_l3fwd(odpg_ctx_t *ctx, const odpg_fwd_t *f, const odpg_fwd_b
 	const uint32_t grid = (b->num + FBLOCK - 1) / FBLOCK;
 	const uint32_t layer = b->error_check ? LAYER_ALL : LAYER_L4;
 
-#ifndef FWD_NONPERSIST      /* experiment builds only: the one-pass kernel at stride 64 */
 	if (b->stride == 64u) {
 		const uint32_t ntiles = (b->num + 63u) / 64u;
 		const uint32_t want = (ntiles + FWD_PBLOCK / 64u - 1u) / (FWD_PBLOCK / 64u);
@@ -835,7 +812,6 @@ extern "C" int odpg_l3fwd(odpg_ctx_t *ctx, const odpg_fwd_t *f, const odpg_fwd_b
 					   s, (uint4 *)b->frames, b->num, b->src_port, layer, f->d_rmac,
 					   f->nroutes, f->d_l1, f->d_pool, f->d_pmac, out_port);
 	} else
-#endif
 	if (b->stride == 64u)
 		hipLaunchKernelGGL((odpg_l3fwd_kernel<64, false>), dim3(grid), dim3(FBLOCK), 0, s,
 				   b->frames, b->stride, b->num, b->src_port, layer, f->mode,

@@ -594,13 +594,6 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x)
 	       (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
-/* mask of the first `n` bytes (0..4) of a little-endian word */
-__device__ __forceinline__ uint32_t byte_mask(int n)
-{
-	n = n < 0 ? 0 : n > 4 ? 4 : n;
-	return (uint32_t)((1ull << (8 * n)) - 1ull);
-}
-
 /* this lane's share of frame j's tail [a, b): 16-byte chunks c0 + 16 * idx,
  * idx = lane, lane + 64, ...; only the chunk holding byte b - 1 (and the
  * first one when a is not 16-aligned) is masked, with wave-uniform masks.
@@ -614,99 +607,6 @@ __device__ __forceinline__ uint32_t tail_dot2(uint32_t w, uint32_t acc)
 				      __builtin_bit_cast(tail_us2, 0x00010001u), acc, false);
 }
 
-__device__ __forceinline__ uint32_t tail_share(const uint8_t *gp, uint32_t a, uint32_t b,
-					       uint32_t lane)
-{
-	const uint32_t c0 = a & ~15u;
-	const uint32_t last = (b - 1u - c0) >> 4;          /* uniform */
-	const int rem = (int)(((b - 1u) & 15u) + 1u);       /* bytes of the last chunk */
-	const uint32_t e0 = byte_mask(rem), e1 = byte_mask(rem - 4), e2 = byte_mask(rem - 8),
-		       e3 = byte_mask(rem - 12);
-	const int lead = (int)(a & 15u);                    /* bytes to drop at the start */
-	const uint32_t s0 = ~byte_mask(lead), s1 = ~byte_mask(lead - 4),
-		       s2 = ~byte_mask(lead - 8), s3 = ~byte_mask(lead - 12);
-	uint32_t acc = 0u;
-
-	for (uint32_t base = 0; base <= last; base += 64u) {   /* uniform: 1-2 passes for IMIX */
-		const uint32_t idx = base + lane;
-
-		if (idx <= last) {
-			const uint4 q = *(const uint4 *)(gp + c0 + 16u * idx);
-			const bool end = idx == last, start = idx == 0u;
-			const uint32_t w0 = q.x & (end ? e0 : ~0u) & (start ? s0 : ~0u);
-			const uint32_t w1 = q.y & (end ? e1 : ~0u) & (start ? s1 : ~0u);
-			const uint32_t w2 = q.z & (end ? e2 : ~0u) & (start ? s2 : ~0u);
-			const uint32_t w3 = q.w & (end ? e3 : ~0u) & (start ? s3 : ~0u);
-
-			/* sums of the 16-bit halves (v_dot2_u32_u16): the same value
-			 * mod 0xffff as the 32-bit word sum; at most 8 x 0xffff per
-			 * pass, so no carry out below 8 MiB tails */
-			acc = tail_dot2(w0, acc);
-			acc = tail_dot2(w1, acc);
-			acc = tail_dot2(w2, acc);
-			acc = tail_dot2(w3, acc);
-		}
-	}
-	return oc_fold(acc);
-}
-
-#ifndef COOP_BATCH
-#define COOP_BATCH 4
-#endif
-/* Wave-cooperative sums of the frame tails [a, b) of the lanes in `m`: the
- * whole wave reads one frame's tail with coalesced 16-byte loads (1 KiB per
- * wave instruction), COOP_BATCH pairs of frames at a time so their loads
- * overlap. Each lane folds its share to 16 bits; two frames travel packed in
- * one lane reduction (64 x 0xffff < 2^22 per half). Lane j receives its own
- * tail sum. */
-__device__ __forceinline__ uint32_t coop_tail_sums(uint64_t m, const uint8_t *g, const L4Pend &pd)
-{
-	const uint32_t lane = __lane_id();
-	const uint64_t gv = (uint64_t)(uintptr_t)g;
-	uint32_t mine = 0u;
-
-#ifdef ODPG_EXP_NOTAIL      /* experiment builds only: cost without the tail reads */
-	return 0u;
-#endif
-	while (m) {
-		int jj[2 * COOP_BATCH];
-		uint32_t sh[2 * COOP_BATCH];
-
-#pragma unroll
-		for (int k = 0; k < 2 * COOP_BATCH; ++k) {
-			jj[k] = m ? __builtin_ctzll(m) : -1;
-			m &= m - 1ull;
-		}
-#pragma unroll
-		for (int k = 0; k < 2 * COOP_BATCH; ++k) {
-			sh[k] = 0u;
-			if (jj[k] >= 0) {
-				const uint32_t glo = __builtin_amdgcn_readlane((int)(uint32_t)gv, jj[k]);
-				const uint32_t ghi = __builtin_amdgcn_readlane((int)(uint32_t)(gv >> 32), jj[k]);
-				const uint8_t *gp = (const uint8_t *)(uintptr_t)(((uint64_t)ghi << 32) | glo);
-				const uint32_t a = __builtin_amdgcn_readlane((int)pd.a, jj[k]);
-				const uint32_t b = __builtin_amdgcn_readlane((int)pd.b, jj[k]);
-
-				sh[k] = tail_share(gp, a, b, lane);
-			}
-		}
-#pragma unroll
-		for (int k = 0; k < COOP_BATCH; ++k) {
-			if (jj[2 * k] >= 0) {
-				const uint32_t t0 = wave_sum_u32(sh[2 * k]);
-				const uint32_t t1 = jj[2 * k + 1] >= 0 ? wave_sum_u32(sh[2 * k + 1]) : 0u;
-
-				if (lane == (uint32_t)jj[2 * k])
-					mine = oc_fold(t0);
-				if (lane == (uint32_t)jj[2 * k + 1])
-					mine = oc_fold(t1);
-			}
-		}
-	}
-	return mine;
-}
-
-
 /* inclusive prefix sum over the 64 lanes (DPP row scans, then the row
  * carries by row_bcast:15 / row_bcast:31); every lane must be active */
 __device__ __forceinline__ uint32_t wave_scan_u32(uint32_t x)
@@ -718,107 +618,6 @@ __device__ __forceinline__ uint32_t wave_scan_u32(uint32_t x)
 	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
 	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
 	return x;
-}
-
-/* Tail sums of the lanes in `m` as one balanced segmented reduction: the
- * 16-byte chunks of every pending tail [a, b) (chunk-aligned at a & ~15 of
- * the lane's frame g) are numbered across the wave in lane order (prefix sum
- * of the per-frame chunk counts) and spread over the 64 lanes, 64 chunks per
- * pass: a pass loads 1 KiB of tails with every lane busy, whatever the mix
- * of frame lengths. Each lane masks its chunk to [a, b), sums its 16-bit
- * halves (v_dot2) and folds; one wave prefix sum per pass then gives every
- * frame's share of the pass as a difference of two lanes. Lane j receives
- * its own tail sum (the same value coop_tail_sums returns: the one's-
- * complement residue and zero-ness of the exact sum are kept). */
-#ifndef SEG_BATCH
-#define SEG_BATCH 4
-#endif
-__device__ __forceinline__ uint32_t seg_tail_sums(uint64_t m, const uint8_t *g, const L4Pend &pd)
-{
-#ifdef ODPG_EXP_NOTAIL      /* experiment builds only: cost without the tail reads */
-	return 0u;
-#endif
-	const uint32_t lane = __lane_id();
-	const uint64_t gv = (uint64_t)(uintptr_t)g;
-	const bool mine = ((m >> lane) & 1ull) && pd.b > pd.a;
-	const uint32_t c0 = pd.a & ~15u;
-	const uint32_t n = mine ? ((pd.b - 1u - c0) >> 4) + 1u : 0u;   /* chunks */
-	const uint32_t incl = wave_scan_u32(n);
-	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-	uint32_t acc = 0u;
-
-	/* SEG_BATCH passes at a time: their loads are all issued before the
-	 * first is summed, so a wave keeps several KiB of tails in flight */
-	for (uint32_t b0 = 0; b0 < total; b0 += 64u * SEG_BATCH) {   /* uniform */
-		uint4 q[SEG_BATCH];
-		uint32_t lead[SEG_BATCH], rem[SEG_BATCH];
-		uint64_t pass_frames[SEG_BATCH];
-
-#pragma unroll
-		for (int k = 0; k < SEG_BATCH; ++k) {
-			const uint32_t base = b0 + 64u * (uint32_t)k;
-			const uint32_t slot = base + lane;
-			const uint64_t in_pass = base < total ?
-				__ballot(n && incl > base && incl - n < base + 64u) : 0ull;
-			uint32_t own = 64u, first = 0u, glo = 0u, ghi = 0u, oa = 0u, ob = 0u, on = 0u;
-
-			pass_frames[k] = in_pass;
-			/* the frame owning this lane's chunk, and its fields */
-			for (uint64_t f = in_pass; f; f &= f - 1ull) {
-				const int j = __builtin_ctzll(f);
-				const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)incl, j);
-				const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)n, j);
-				const bool hit = slot >= ij - nj && slot < ij;
-
-				own = hit ? (uint32_t)j : own;
-				first = hit ? ij - nj : first;
-				on = hit ? nj : on;
-				glo = hit ? (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gv, j) : glo;
-				ghi = hit ? (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(gv >> 32), j) : ghi;
-				oa = hit ? (uint32_t)__builtin_amdgcn_readlane((int)pd.a, j) : oa;
-				ob = hit ? (uint32_t)__builtin_amdgcn_readlane((int)pd.b, j) : ob;
-			}
-			const uint32_t idx = slot - first;
-
-			q[k] = make_uint4(0u, 0u, 0u, 0u);
-			lead[k] = idx == 0u ? (oa & 15u) : 0u;
-			rem[k] = own < 64u ? (idx + 1u == on ? ((ob - 1u) & 15u) + 1u : 16u) : 0u;
-			if (own < 64u) {
-				const uint8_t *gp = (const uint8_t *)(uintptr_t)(((uint64_t)ghi << 32) | glo);
-
-				q[k] = *(const uint4 *)(gp + (oa & ~15u) + 16u * idx);
-			}
-		}
-#pragma unroll
-		for (int k = 0; k < SEG_BATCH; ++k) {
-			if (!pass_frames[k])
-				continue;
-			const uint32_t base = b0 + 64u * (uint32_t)k;
-			const int le = (int)lead[k], re = (int)rem[k];
-			uint32_t acc4 = 0u;
-
-			acc4 = tail_dot2(q[k].x & byte_mask(re) & ~byte_mask(le), acc4);
-			acc4 = tail_dot2(q[k].y & byte_mask(re - 4) & ~byte_mask(le - 4), acc4);
-			acc4 = tail_dot2(q[k].z & byte_mask(re - 8) & ~byte_mask(le - 8), acc4);
-			acc4 = tail_dot2(q[k].w & byte_mask(re - 12) & ~byte_mask(le - 12), acc4);
-			/* frames own contiguous lanes: a frame's share of the pass is
-			 * the prefix sum at its last lane minus the one before its first */
-			const uint32_t ps = wave_scan_u32(oc_fold(acc4));
-
-			for (uint64_t f = pass_frames[k]; f; f &= f - 1ull) {
-				const int j = __builtin_ctzll(f);
-				const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)incl, j);
-				const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)n, j);
-				const uint32_t lo = ij - nj > base ? ij - nj - base : 0u;
-				const uint32_t hi = (ij < base + 64u ? ij : base + 64u) - base - 1u;
-				const uint32_t sh = (uint32_t)__builtin_amdgcn_readlane((int)ps, (int)hi) -
-						    (lo ? (uint32_t)__builtin_amdgcn_readlane((int)ps, (int)lo - 1) : 0u);
-
-				acc += lane == (uint32_t)j ? sh : 0u;
-			}
-		}
-	}
-	return mine ? oc_fold(acc) : 0u;
 }
 
 /* inclusive prefix max over the 64 lanes (wave_scan_u32's DPP steps with
@@ -840,209 +639,12 @@ __device__ __forceinline__ uint32_t lane_pull(uint32_t v, uint32_t src)
 	return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
 }
 
-/* seg_tail_sums with the per-pass bookkeeping done lane-parallel (round 2,
- * second form): the owner of a lane's chunk is found by a binary search of
- * the inclusive chunk counts over the lanes that can own a chunk of this
- * pass (ds_bpermute per step: log2 of that lane range, 2-4 steps for IMIX),
- * the owner's chunk base address and bounds are pulled in four more
- * bpermutes, and each frame pulls its share of the pass from two lanes of
- * the pass's prefix sum. No per-frame loops: the pass costs the same
- * whatever number of frames it touches. Same result as seg_tail_sums. */
-__device__ __forceinline__ uint32_t seg_tail_sums2(uint64_t m, const uint8_t *g, const L4Pend &pd)
-{
-#ifdef ODPG_EXP_NOTAIL
-	return 0u;
-#endif
-	const uint32_t lane = __lane_id();
-	const bool mine = ((m >> lane) & 1ull) && pd.b > pd.a;
-	const uint32_t c0 = pd.a & ~15u;
-	const uint32_t n = mine ? ((pd.b - 1u - c0) >> 4) + 1u : 0u;   /* chunks */
-	const uint32_t incl = wave_scan_u32(n);
-	const uint32_t first = incl - n;                                /* first slot */
-	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-	/* the address of slot s of this lane's frame is cb + 16 s */
-	const uint64_t cb = (uint64_t)(uintptr_t)g + c0 - 16ull * first;
-	const uint32_t cb_lo = (uint32_t)cb, cb_hi = (uint32_t)(cb >> 32);
-	const uint32_t pk = (incl & 0xffffffu) | ((pd.a & 15u) << 24) | (((pd.b - 1u) & 15u) << 28);
-	uint32_t acc = 0u;
-
-	for (uint32_t b0 = 0; b0 < total; b0 += 64u * SEG_BATCH) {   /* uniform */
-		uint4 q[SEG_BATCH];
-		uint32_t lead[SEG_BATCH], rem[SEG_BATCH];
-
-#pragma unroll
-		for (int k = 0; k < SEG_BATCH; ++k) {
-			const uint32_t base = b0 + 64u * (uint32_t)k;
-			const uint32_t slot = base + lane;
-			const bool valid = slot < total;
-			/* owners of this pass's chunks lie in lanes [lo, hi] (uniform) */
-			const uint64_t past = __ballot(incl > base);
-			const uint64_t beyond = __ballot(incl > base + 63u);
-			const uint32_t lo = past ? (uint32_t)__builtin_ctzll(past) : 63u;
-			const uint32_t hi = beyond ? (uint32_t)__builtin_ctzll(beyond) : 63u;
-			const uint32_t span = hi > lo ? hi - lo : 0u;
-			int p = -1;        /* lanes lo .. lo + p hold incl <= slot */
-
-			for (uint32_t step = span ? 1u << (31 - __builtin_clz(span)) : 0u; step;
-			     step >>= 1) {                                  /* uniform */
-				const uint32_t cand = (uint32_t)(p + (int)step);
-				const uint32_t src = lo + cand < 64u ? lo + cand : 63u;
-				const uint32_t v = lane_pull(incl, src);
-
-				if (cand <= span && v <= slot)
-					p = (int)cand;
-			}
-			const uint32_t own = lo + (uint32_t)(p + 1);
-			const uint32_t olo = lane_pull(cb_lo, own), ohi = lane_pull(cb_hi, own);
-			const uint32_t opk = lane_pull(pk, own), ofirst = lane_pull(first, own);
-
-			q[k] = make_uint4(0u, 0u, 0u, 0u);
-			lead[k] = slot == ofirst ? (opk >> 24) & 15u : 0u;
-			rem[k] = !valid ? 0u : slot + 1u == (opk & 0xffffffu) ? (opk >> 28) + 1u : 16u;
-			if (valid)
-				q[k] = *(const uint4 *)(uintptr_t)((((uint64_t)ohi << 32) | olo) +
-								   16ull * slot);
-		}
-#pragma unroll
-		for (int k = 0; k < SEG_BATCH; ++k) {
-			const uint32_t base = b0 + 64u * (uint32_t)k;
-
-			if (base >= total)                                  /* uniform */
-				break;
-			const int le = (int)lead[k], re = (int)rem[k];
-			uint32_t acc4 = 0u;
-
-			acc4 = tail_dot2(q[k].x & byte_mask(re) & ~byte_mask(le), acc4);
-			acc4 = tail_dot2(q[k].y & byte_mask(re - 4) & ~byte_mask(le - 4), acc4);
-			acc4 = tail_dot2(q[k].z & byte_mask(re - 8) & ~byte_mask(le - 8), acc4);
-			acc4 = tail_dot2(q[k].w & byte_mask(re - 12) & ~byte_mask(le - 12), acc4);
-			const uint32_t ps = wave_scan_u32(oc_fold(acc4));
-			/* this lane's frame: its chunks of the pass are lanes [fl, ll] */
-			const bool in = n && incl > base && first < base + 64u;
-			const uint32_t fl = in && first > base ? first - base : 0u;
-			const uint32_t ll = in ? (incl - 1u < base + 63u ? incl - 1u - base : 63u) : 0u;
-			const uint32_t hv = lane_pull(ps, ll);
-			const uint32_t lv = lane_pull(ps, fl ? fl - 1u : 0u);
-
-			acc += in ? hv - (fl ? lv : 0u) : 0u;
-		}
-	}
-	return mine ? oc_fold(acc) : 0u;
-}
-
 /* bytes [0, n) of a little-endian word, n clamped to [0, 4] */
 __device__ __forceinline__ uint32_t keep_below(int n)
 {
 	const int c = n < 0 ? 0 : n > 4 ? 4 : n;
 
 	return c >= 4 ? ~0u : ~(~0u << (8 * c));
-}
-
-/* seg_tail_sums2 over 64-byte units (third form, the default): a lane
- * loads and sums 64 contiguous bytes of one tail per pass (4 x 16 B), so the
- * per-pass bookkeeping — owner search, owner fields, the pass prefix sum
- * and the per-frame shares — is paid once per 64 bytes instead of once per
- * 16, and the next pass's owners are found while this pass's loads are in
- * flight. A unit's bytes outside [a, b) are masked per word. Same result as
- * seg_tail_sums. */
-__device__ __forceinline__ uint32_t seg_tail_sums3(uint64_t m, const uint8_t *g, const L4Pend &pd)
-{
-#ifdef ODPG_EXP_NOTAIL
-	return 0u;
-#endif
-	const uint32_t lane = __lane_id();
-	const bool mine = ((m >> lane) & 1ull) && pd.b > pd.a;
-	const uint32_t c0 = pd.a & ~15u;
-	const uint32_t n = mine ? ((pd.b - 1u - c0) >> 6) + 1u : 0u;   /* 64-byte units */
-	const uint32_t incl = wave_scan_u32(n);
-	const uint32_t first = incl - n;                                /* first unit slot */
-	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-	/* unit slot s of this lane's frame starts at cb + 64 s */
-	const uint64_t cb = (uint64_t)(uintptr_t)g + c0 - 64ull * first;
-	const uint32_t cb_lo = (uint32_t)cb, cb_hi = (uint32_t)(cb >> 32);
-	/* inclusive end slot | bytes to drop at the start | bytes of the last unit - 1 */
-	const uint32_t pk = (incl & 0xfffffu) | ((pd.a & 15u) << 20) | (((pd.b - 1u - c0) & 63u) << 24);
-	uint32_t acc = 0u;
-
-	/* the owner of slot base + lane: a binary search of incl over the lanes
-	 * that can own a unit of the pass, then its fields */
-	auto owner = [&](uint32_t base, uint32_t &olo, uint32_t &ohi, uint32_t &opk,
-			 uint32_t &ofirst) __attribute__((always_inline)) {
-		const uint32_t slot = base + lane;
-		const uint64_t past = __ballot(incl > base);
-		const uint64_t beyond = __ballot(incl > base + 63u);
-		const uint32_t lo = past ? (uint32_t)__builtin_ctzll(past) : 63u;
-		const uint32_t hi = beyond ? (uint32_t)__builtin_ctzll(beyond) : 63u;
-		const uint32_t span = hi > lo ? hi - lo : 0u;
-		int p = -1;
-
-		for (uint32_t step = span ? 1u << (31 - __builtin_clz(span)) : 0u; step;
-		     step >>= 1) {                                     /* uniform */
-			const uint32_t cand = (uint32_t)(p + (int)step);
-			const uint32_t src = lo + cand < 64u ? lo + cand : 63u;
-			const uint32_t v = lane_pull(incl, src);
-
-			if (cand <= span && v <= slot)
-				p = (int)cand;
-		}
-		const uint32_t own = lo + (uint32_t)(p + 1);
-
-		olo = lane_pull(cb_lo, own);
-		ohi = lane_pull(cb_hi, own);
-		opk = lane_pull(pk, own);
-		ofirst = lane_pull(first, own);
-	};
-	uint32_t olo, ohi, opk, ofirst;
-
-	if (total)                                                     /* uniform */
-		owner(0u, olo, ohi, opk, ofirst);
-	for (uint32_t base = 0; base < total; base += 64u) {            /* uniform */
-		const uint32_t slot = base + lane;
-		const bool valid = slot < total;
-		const int le = slot == ofirst ? (int)((opk >> 20) & 15u) : 0;
-		const int re = !valid ? 0 : slot + 1u == (opk & 0xfffffu) ? (int)(opk >> 24) + 1 : 64;
-		uint4 q[4];
-
-#pragma unroll
-		for (int k = 0; k < 4; ++k)
-			q[k] = make_uint4(0u, 0u, 0u, 0u);
-		if (valid) {
-			const uint4 *src = (const uint4 *)(uintptr_t)((((uint64_t)ohi << 32) | olo) +
-								     64ull * slot);
-#pragma unroll
-			for (int k = 0; k < 4; ++k)
-				q[k] = src[k];
-		}
-		/* the next pass's owners while the loads are in flight */
-		if (base + 64u < total)                                 /* uniform */
-			owner(base + 64u, olo, ohi, opk, ofirst);
-		uint32_t acc4 = 0u;
-
-#pragma unroll
-		for (int k = 0; k < 4; ++k) {
-			const uint32_t w[4] = { q[k].x, q[k].y, q[k].z, q[k].w };
-
-#pragma unroll
-			for (int j = 0; j < 4; ++j) {
-				const int o = 16 * k + 4 * j;
-				uint32_t msk = keep_below(re - o);
-
-				if (k == 0)
-					msk &= ~keep_below(le - o);
-				acc4 = tail_dot2(w[j] & msk, acc4);
-			}
-		}
-		const uint32_t ps = wave_scan_u32(oc_fold(acc4));
-		/* this lane's frame: its units of the pass are lanes [fl, ll] */
-		const bool in = n && incl > base && first < base + 64u;
-		const uint32_t fl = in && first > base ? first - base : 0u;
-		const uint32_t ll = in ? (incl - 1u < base + 63u ? incl - 1u - base : 63u) : 0u;
-		const uint32_t hv = lane_pull(ps, ll);
-		const uint32_t lv = lane_pull(ps, fl ? fl - 1u : 0u);
-
-		acc += in ? hv - (fl ? lv : 0u) : 0u;
-	}
-	return mine ? oc_fold(acc) : 0u;
 }
 
 /* 16-byte load through a global (address space 1) pointer: an address
@@ -1083,187 +685,11 @@ __device__ __forceinline__ uint32_t unit_sum_masked(uint64_t addr, int lead, int
 	return acc;
 }
 
-/* unit_sum_masked over a unit already loaded (16-byte chunks at or past re
- * zero) */
-__device__ __forceinline__ uint32_t unit_sum_regs(const uint4 (&q)[4], int lead, int re)
-{
-	uint32_t acc = 0u;
-
-#pragma unroll
-	for (int k = 0; k < 4; ++k) {
-		const uint32_t w[4] = { q[k].x, q[k].y, q[k].z, q[k].w };
-
-#pragma unroll
-		for (int j = 0; j < 4; ++j) {
-			const int o = 16 * k + 4 * j;
-
-			acc = tail_dot2(w[j] & keep_below(re - o) & ~keep_below(lead - o), acc);
-		}
-	}
-	return acc;
-}
-
-/* Tail sums, fourth form (the default): each tail [a, b) is cut into 64-byte
- * units from c0 = a & ~15. The units that need byte masks — the frame's last
- * one, and its first one when a is not 16-aligned — are summed by the lane
- * itself, once per frame; every other unit is a whole 64 bytes inside the
- * tail, and those are spread over the wave as in seg_tail_sums3 but need no
- * masks, no per-unit bounds and only the owner's base address (two
- * bpermutes). All loads go through global pointers. Same result as
- * seg_tail_sums. */
-/* One coalesced sweep over every byte of a wave's 64 frames (descriptor
- * batches, 64-byte window): frame f's 64-byte units [0, len) are numbered
- * across the wave frame after frame (a DPP prefix sum of the per-frame unit
- * counts) and spread over the lanes, 64 units per pass, so a frame's window,
- * its tail and the neighbouring frames' bytes are requested by neighbouring
- * lanes of the same or the next load instruction: each 128-byte line is
- * fetched once. A lane holding a frame's unit 0 writes it (zero past the
- * frame) into that frame's LDS row, the window the parse reads; every other
- * unit is masked to the frame and summed (v_dot2). Returns the lane's own
- * frame's sum of bytes [64, len) as a one's-complement partial (residue and
- * zero-ness kept). `rows` is the wave's first row, `rw` the row stride in
- * dwords. All lanes must be active. */
-__device__ __forceinline__ uint32_t sweep_frames(const uint8_t *g, uint32_t len, uint32_t *rows,
-						 uint32_t rw)
-{
-	const uint32_t lane = __lane_id();
-	const uint32_t nu = len ? ((len - 1u) >> 6) + 1u : 0u;
-	const uint32_t incl = wave_scan_u32(nu);
-	const uint32_t first = incl - nu;
-	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-	/* unit slot s of this lane's frame starts at cb + 64 s */
-	const uint64_t cb = (uint64_t)(uintptr_t)g - 64ull * first;
-	const uint32_t cb_lo = (uint32_t)cb, cb_hi = (uint32_t)(cb >> 32);
-	uint32_t acc = 0u;
-
-	if (len == 0u) {                                  /* empty frame: zero window */
-#pragma unroll
-		for (int w = 0; w < 16; ++w)
-			rows[lane * rw + w] = 0u;
-	}
-	for (uint32_t base = 0; base < total; base += 64u) {            /* uniform */
-		const uint32_t slot = min(base + lane, total - 1u);
-		const bool valid = base + lane < total;
-		const uint64_t past = __ballot(incl > base);
-		const uint64_t beyond = __ballot(incl > base + 63u);
-		const uint32_t lo = past ? (uint32_t)__builtin_ctzll(past) : 63u;
-		const uint32_t hi = beyond ? (uint32_t)__builtin_ctzll(beyond) : 63u;
-		const uint32_t span = hi > lo ? hi - lo : 0u;
-		int p = -1;
-
-		for (uint32_t st = span ? 1u << (31 - __builtin_clz(span)) : 0u; st;
-		     st >>= 1) {                                       /* uniform */
-			const uint32_t cand = (uint32_t)(p + (int)st);
-			const uint32_t src = lo + cand < 64u ? lo + cand : 63u;
-			const uint32_t v = lane_pull(incl, src);
-
-			if (cand <= span && v <= slot)
-				p = (int)cand;
-		}
-		const uint32_t o = lo + (uint32_t)(p + 1);
-		const uint64_t a = (((uint64_t)lane_pull(cb_hi, o) << 32) | lane_pull(cb_lo, o)) +
-				   64ull * slot;
-		/* pulled with every lane active: a bpermute under a partial exec
-		 * mask reads inactive source lanes as 0 */
-		const uint32_t ofirst = lane_pull(first, o), olen = lane_pull(len, o);
-		const uint32_t u = slot - ofirst;
-		const int rem = valid ? (int)(olen - 64u * u) : 0;     /* >= 1 */
-		/* whole words below rem kept by a compare each; the one partial
-		 * word (rem not a multiple of 4) is read again as a dword (a cache
-		 * hit: its 16 bytes were just loaded) and masked */
-		const uint32_t nw = rem > 0 ? (uint32_t)rem >> 2 : 0u;
-		const uint32_t pb = (uint32_t)rem & 3u;
-		uint32_t pv = 0u;
-		uint32_t w[16];
-
-		if (rem > 0 && pb && nw < 16u)
-			pv = *(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)(a + 4u * nw) &
-			     ((1u << (8u * pb)) - 1u);
-#pragma unroll
-		for (int j = 0; j < 4; ++j) {
-			uint4 q = make_uint4(0u, 0u, 0u, 0u);
-
-			if (16 * j < rem)
-				q = ld_g16(a + 16u * j);
-			w[4 * j + 0] = 4 * j + 0 < (int)nw ? q.x : 0u;
-			w[4 * j + 1] = 4 * j + 1 < (int)nw ? q.y : 0u;
-			w[4 * j + 2] = 4 * j + 2 < (int)nw ? q.z : 0u;
-			w[4 * j + 3] = 4 * j + 3 < (int)nw ? q.w : 0u;
-		}
-		uint32_t sum = 0u;
-
-		if (valid && u == 0u) {
-			uint32_t *r = rows + o * rw;
-
-#pragma unroll
-			for (int k = 0; k < 16; ++k)
-				r[k] = w[k];
-			if (pb && nw < 16u)
-				r[nw] = pv;
-		} else {
-#pragma unroll
-			for (int k = 0; k < 16; ++k)
-				sum = tail_dot2(w[k], sum);
-			sum = tail_dot2(pv, sum);
-		}
-		/* this lane's frame: its units of the pass are lanes [fl, ll] */
-		const uint32_t ps = wave_scan_u32(oc_fold(sum));
-		const bool in = nu && incl > base && first < base + 64u;
-		const uint32_t fl = in && first > base ? first - base : 0u;
-		const uint32_t ll = in ? (incl - 1u < base + 63u ? incl - 1u - base : 63u) : 0u;
-		const uint32_t hv = lane_pull(ps, ll);
-		const uint32_t lv = lane_pull(ps, fl ? fl - 1u : 0u);
-
-		acc += in ? hv - (fl ? lv : 0u) : 0u;
-	}
-	/* the rows written by other lanes are read next by their own lanes */
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-	return oc_fold(acc);
-}
-
-#ifndef SEG4_PIPE
-#define SEG4_PIPE 1
-#endif
-#ifndef SEG4_OWNEARLY       /* last units' loads issued before the passes' */
-#define SEG4_OWNEARLY 0
-#endif
-#ifndef SEG4_TAILW          /* last units by whole-word compares (unit_sum_head): */
-#define SEG4_TAILW 0        /* fewer VALU but a dependent reload; C3 +1.5 us */
-#endif
-
-/* sum of bytes [0, re) of the 64-byte unit at addr (16-byte aligned),
- * 1 <= re <= 64, as 16-bit halves: words below re / 4 by a compare each,
- * the word holding the last byte read again as a dword and masked (its 16
- * bytes were just loaded). unit_sum_masked's result for lead 0 at a third
- * of its instructions. */
-__device__ __forceinline__ uint32_t unit_sum_head(uint64_t addr, uint32_t re)
-{
-	const uint32_t nw = re >> 2, pb = re & 3u;
-	uint32_t acc = 0u;
-
-#pragma unroll
-	for (int k = 0; k < 4; ++k) {
-		uint4 q = make_uint4(0u, 0u, 0u, 0u);
-
-		if (16u * k < re)
-			q = ld_g16(addr + 16u * k);
-		acc = tail_dot2(4 * k + 0 < (int)nw ? q.x : 0u, acc);
-		acc = tail_dot2(4 * k + 1 < (int)nw ? q.y : 0u, acc);
-		acc = tail_dot2(4 * k + 2 < (int)nw ? q.z : 0u, acc);
-		acc = tail_dot2(4 * k + 3 < (int)nw ? q.w : 0u, acc);
-	}
-	if (pb) {
-		const uint32_t w = *(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)(addr + 4u * nw);
-
-		acc = tail_dot2(w & ((1u << (8u * pb)) - 1u), acc);
-	}
-	return acc;
-}
-/* unit_sum_head with the partial word's dword load issued first, beside the
- * chunk loads (not behind their sums): bytes [0, re) of the 64-byte unit at
- * addr, 1 <= re <= 64; the words below re / 4 kept by a compare each, the
- * one holding the last byte (a cache hit: its chunk is loaded too) masked.
- * A third of unit_sum_masked's instructions. */
+/* Bytes [0, re) of the 64-byte unit at addr, 1 <= re <= 64, as 16-bit
+ * halves: the words below re / 4 kept by a compare each, the one holding
+ * the last byte masked, its dword loaded first, beside the chunk loads (a
+ * cache hit: its chunk is loaded too), not behind their sums. A third of
+ * unit_sum_masked's instructions. */
 __device__ __forceinline__ uint32_t unit_sum_end(uint64_t addr, uint32_t re)
 {
 	const uint32_t nw = re >> 2, pb = re & 3u;
@@ -1293,9 +719,6 @@ __device__ __forceinline__ uint32_t unit_sum_end(uint64_t addr, uint32_t re)
 __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g, const L4Pend &pd,
 						uint32_t *marks = nullptr)
 {
-#ifdef ODPG_EXP_NOTAIL
-	return 0u;
-#endif
 	const uint32_t lane = __lane_id();
 	const bool mine = ((m >> lane) & 1ull) && pd.b > pd.a;
 	const uint32_t c0 = pd.a & ~15u;
@@ -1306,36 +729,14 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 	const uint32_t ni = mine ? nu - 1u - f0 : 0u;                   /* shared units */
 	const uint64_t gb = (uint64_t)(uintptr_t)g + c0;
 	uint32_t own = 0u;
-	const bool own_late = SEG4_OWNEARLY && !__ballot(own_first);     /* uniform */
-	uint4 oq[4] = {};
-	int own_re = 0, own_lead = 0;
 
 	/* the lane's own units: last (masked to b, and to a when it is the
 	 * first), then the first when it carries a lead */
-#ifdef SEG4_EXP_NOOWN       /* experiment builds only: cost of the own units */
-	if (mine && pd.b == 12345u) {
-#else
 	if (mine) {
-#endif
 		const uint32_t lu = nu - 1u;
 
-		/* SEG4_OWNEARLY without a first own unit anywhere: the last unit's
-		 * loads now, its sum once the first passes' loads are issued */
-		if (own_late) {
-			own_re = (int)(pd.b - c0 - 64u * lu);
-			own_lead = lu ? 0 : (int)lead;
-#pragma unroll
-			for (int k = 0; k < 4; ++k)
-				if (16 * k < own_re)
-					oq[k] = ld_g16(gb + 64ull * lu + 16u * k);
-		} else
-		/* every last unit starting at its first byte (C3's early tails
-		 * always): whole words by a compare each, the partial one read
-		 * again as a dword (a cache hit) */
-		if (SEG4_TAILW && !__ballot(mine && lead != 0u && lu == 0u))
-			own = unit_sum_head(gb + 64ull * lu, pd.b - c0 - 64u * lu);
-		else if (!__ballot(mine && lead != 0u && lu == 0u))
-			/* every last unit starts at its first byte (C3's early
+		if (!__ballot(mine && lead != 0u && lu == 0u))
+			/* every last unit starting at its first byte (C3's early
 			 * tails: a = 64, always) */
 			own = unit_sum_end(gb + 64ull * lu, pd.b - c0 - 64u * lu);
 		else
@@ -1357,9 +758,6 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 	 * search of incl over the lanes that can own a slot of the pass */
 	auto owner = [&](uint32_t base) __attribute__((always_inline)) -> uint64_t {
 		const uint32_t slot = min(base + lane, total - 1u);
-#ifdef SEG4_EXP_NOOWNER     /* experiment builds only: cost of the owner search */
-		return (((uint64_t)cb_hi << 32) | cb_lo) + 64ull * slot;
-#endif
 		if (marks) {
 			/* with a wave's 64-dword LDS scratch: every frame with a
 			 * slot in the pass marks the lane of its first one (the
@@ -1416,10 +814,6 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 			s = tail_dot2(q[k].z, s);
 			s = tail_dot2(q[k].w, s);
 		}
-#ifdef SEG4_EXP_NOSCAN      /* experiment builds only: cost of the pass attribution */
-		acc += s;
-		return;
-#endif
 		const uint32_t ps = wave_scan_u32(base + lane < total ? oc_fold(s) : 0u);
 		const bool in = ni && incl > base && first < base + 64u;
 		const uint32_t fl = in && first > base ? first - base : 0u;
@@ -1437,7 +831,6 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 	uint64_t addr = total ? owner(0u) : 0ull;
 	uint4 qa[4], qb[4];
 
-#if SEG4_PIPE
 	/* two passes in flight (8 KiB per wave): pass p + 2's loads are issued
 	 * as soon as pass p is summed, and each pass's owners are found while
 	 * the loads before it are in flight */
@@ -1450,8 +843,6 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 				addr = owner(128u);
 		}
 	}
-	if (own_late && mine)
-		own = unit_sum_regs(oq, own_lead, own_re);
 	for (uint32_t base = 0; base < total; base += 128u) {           /* uniform */
 		consume(qa, base);
 		if (base + 128u < total) {
@@ -1468,18 +859,6 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 			}
 		}
 	}
-#else
-	if (own_late && mine)
-		own = unit_sum_regs(oq, own_lead, own_re);
-	for (uint32_t base = 0; base < total; base += 64u) {            /* uniform */
-		load(qa, addr);
-		/* the next pass's owners while the loads are in flight */
-		if (base + 64u < total)                                 /* uniform */
-			addr = owner(base + 64u);
-		consume(qa, base);
-	}
-	(void)qb;
-#endif
 	return mine ? oc_fold(oc_add(oc_fold(acc), oc_fold(own))) : 0u;
 }
 

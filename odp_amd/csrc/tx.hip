@@ -583,7 +583,6 @@ extern "C" int odpg_tx_prepare(odpg_ctx_t *ctx, const odpg_tx_batch_t *b,
 	A.out = out;
 	hipStream_t s = (hipStream_t)odpg_ctx_stream(ctx);
 
-#ifndef TX_ONEPASS      /* experiment builds only: the one-pass kernel at stride 64 */
 	if (b->stride == 64u && !b->desc && !b->meta && b->num < (1u << 30)) {
 		const uint32_t want = ((b->num + 63u) / 64u + TX_BLOCK / 64u - 1u) / (TX_BLOCK / 64u);
 		uint32_t grid = odpg_resident_grid((const void *)odpg_tx64_kernel, TX_BLOCK, 0);
@@ -592,7 +591,6 @@ extern "C" int odpg_tx_prepare(odpg_ctx_t *ctx, const odpg_tx_batch_t *b,
 		hipLaunchKernelGGL(odpg_tx64_kernel, dim3(grid ? grid : 1u), dim3(TX_BLOCK), 0, s, A);
 		return hipGetLastError() == hipSuccess ? 0 : -EIO;
 	}
-#endif
 	hipLaunchKernelGGL(odpg_tx_kernel, dim3((b->num + TX_BLOCK - 1) / TX_BLOCK), dim3(TX_BLOCK),
 			   0, s, A);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;

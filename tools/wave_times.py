@@ -1,10 +1,11 @@
 """Per-wave start / end times of the lean 64-byte kernel (experiment build
-with -DL64_EXP_TIMES: tools/exp_build.sh exp_times "-DL64_EXP_TIMES",
-REBUILD=classify64), on the bench's C2 launch shape: how long after the
+with the tools/exp/l64_times.patch experiment patch,
+on the bench's C2 launch shape: how long after the
 kernel's first wave each wave ends, by the number of tiles it ran. Shows
 the tile-drain tail. s_memrealtime ticks at 100 MHz.
 
-Usage: ODPG_LIB=odp_amd/lib/exp_times/libodpg.so python tools/wave_times.py [--config c2]
+Usage: PATCHES=l64_times REBUILD=classify64 bash tools/exp_build.sh exp_times
+       ODPG_LIB=odp_amd/lib/exp_times/libodpg.so python tools/wave_times.py [--config c2]
 """
 import argparse
 import ctypes as C
