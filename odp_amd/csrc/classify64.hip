@@ -371,6 +371,7 @@ odpg_cls64_kernel(const L64Args A)
 	__shared__ odpg_cnt_dev cnt_lds;
 	__shared__ uint32_t flush_tot;
 	unsigned long long rowv = 0ull;   /* CM 2: this thread's word of the row */
+	bool row_out = false;             /* CM 2: rowv written to LDS */
 
 	if constexpr (CM == 2) {
 		/* the layout (a kernel argument) is kept in LDS for the flush:
@@ -577,13 +578,6 @@ odpg_cls64_kernel(const L64Args A)
 	 * stays small (instruction cache) and no prefetch registers are live
 	 * across the generic parse (register pressure); the last tile of a chunk
 	 * issues no prefetch (a wave never re-reads past its last tile). */
-	/* Frames are read and verdicts written through buffer resources built
-	 * per tile from wave-uniform values: a resource covers exactly the
-	 * tile's frames in the batch (zero bytes for NO_TILE), so loads past
-	 * the batch return zeros without touching memory and stores past it are
-	 * dropped by the range check. Every load and store below is therefore
-	 * issued unconditionally, in a fixed order, and the compiler's counted
-	 * waits leave the other buffer's loads in flight. */
 	constexpr uint32_t NO_TILE = 0xffffffffu;
 	auto tile_n = [&](uint32_t t) -> uint32_t {    /* frames of tile t in the batch */
 		return t < ntiles ? min(num - t * 64u, 64u) : 0u;
@@ -670,6 +664,16 @@ odpg_cls64_kernel(const L64Args A)
 			load_raw(fn, k + 1u < nk ? t + tws : NO_TILE);
 			if (tile(fb, t))
 				defer |= 1ull << k;
+			if (CM == 2 && !row_out) {
+				/* the counter row's word into LDS behind the first
+				 * tile: its wait (the compiler's vmcnt(0), the load
+				 * long landed) then only covers the next tile's loads,
+				 * which the next stage waits for anyway; at the flush
+				 * it would wait for every verdict store first */
+				if (A.cnt.words <= LBK && threadIdx.x < A.cnt.words)
+					base[threadIdx.x] = rowv;
+				row_out = true;
+			}
 		}
 		store_pending();
 
@@ -783,8 +787,8 @@ odpg_cls64_kernel(const L64Args A)
 		uint32_t k_first = lane, k_step = 64u;
 		bool lead = lane == 0u;
 
-		if (A.cnt.words <= LBK && threadIdx.x < A.cnt.words)
-			base[threadIdx.x] = rowv;
+		if (!row_out && A.cnt.words <= LBK && threadIdx.x < A.cnt.words)
+			base[threadIdx.x] = rowv;      /* a wave without tiles */
 
 		if constexpr (HW) {
 			__syncthreads();

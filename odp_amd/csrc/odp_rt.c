@@ -94,13 +94,76 @@ typedef struct rt_pool {
 	uint32_t nchunks;
 } rt_pool_t;
 
+/* a FIFO of handles: v[rd..rd+n) modulo cap (a power of two), grown by
+ * doubling; its owner's lock held. n is also read without the lock (an empty
+ * ring is seen without taking it), so it is stored atomically. */
+typedef struct ptr_ring {
+	void **v;
+	uint32_t cap, rd, n;
+} ptr_ring_t;
+
+/* num handles at the tail, all or none (-1: no memory) */
+static int pring_push(ptr_ring_t *r, void *const h[], uint32_t num)
+{
+	const uint32_t n = r->n;
+
+	if (n + num > r->cap) {
+		uint32_t cap = r->cap ? r->cap : 256u;
+
+		while (cap < n + num)
+			cap *= 2u;
+		void **x = malloc((size_t)cap * sizeof(*x));
+
+		if (!x)
+			return -1;
+		for (uint32_t i = 0; i < n; i++)
+			x[i] = r->v[(r->rd + i) & (r->cap - 1u)];
+		free(r->v);
+		r->v = x;
+		r->cap = cap;
+		r->rd = 0;
+	}
+	const uint32_t w = (r->rd + n) & (r->cap - 1u);
+	const uint32_t k = num < r->cap - w ? num : r->cap - w;
+
+	memcpy(r->v + w, h, (size_t)k * sizeof(*h));
+	memcpy(r->v, h + k, (size_t)(num - k) * sizeof(*h));
+	__atomic_store_n(&r->n, n + num, __ATOMIC_RELEASE);
+	return 0;
+}
+
+/* up to num handles from the head; returns how many */
+static uint32_t pring_pop(ptr_ring_t *r, void *h[], uint32_t num)
+{
+	const uint32_t n = r->n < num ? r->n : num;
+	const uint32_t k = n < r->cap - r->rd ? n : r->cap - r->rd;
+
+	memcpy(h, r->v + r->rd, (size_t)k * sizeof(*h));
+	memcpy(h + k, r->v, (size_t)(n - k) * sizeof(*h));
+	if (n) {
+		r->rd = (r->rd + n) & (r->cap - 1u);
+		__atomic_store_n(&r->n, r->n - n, __ATOMIC_RELAXED);
+	}
+	return n;
+}
+
+/* every handle freed as a packet, the ring emptied and its memory given back */
+static void pring_free_packets(ptr_ring_t *r)
+{
+	for (uint32_t i = 0; i < r->n; i++)
+		odp_packet_free((odp_packet_t)r->v[(r->rd + i) & (r->cap - 1u)]);
+	free(r->v);
+	memset(r, 0, sizeof(*r));
+}
+
 typedef struct rt_queue {
 	uint32_t magic;
 	odp_queue_t hdl;           /* registry handle */
 	char name[ODP_QUEUE_NAME_LEN];
 	odp_queue_param_t param;
 	pthread_mutex_t lock;
-	rt_pkt_t *head, *tail;
+	ptr_ring_t ev;             /* the events (kept when the slot is reused) */
+	int sched;                 /* ODP_QUEUE_TYPE_SCHED: counted in rt.sched_n */
 	struct rt_queue *next_sched;
 	int dead;
 	uint32_t gen;              /* registry slot generation (in the handle) */
@@ -138,8 +201,7 @@ typedef struct rt_pktio {
 	rt_queue_t *inq;           /* pktin event queue (QUEUE / SCHED mode) */
 	rt_queue_t *outq;          /* pktout event queue (QUEUE mode) */
 	pthread_mutex_t ring_lock; /* the loop device's packets in flight */
-	rt_pkt_t *ring_head, *ring_tail;
-	uint32_t ring_n;           /* packets on the ring */
+	ptr_ring_t ring;           /* the transmitted packets, in order */
 	rt_pkt_t *ahead, *ahead_tail;  /* DIRECT mode: received (classified) packets
 				    * beyond what the last odp_pktin_recv asked for */
 	struct rx_slot *slot[RT_INFLIGHT];  /* receive bursts ("receive pipeline") */
@@ -156,9 +218,10 @@ static struct {
 	rt_pool_t pool[RT_MAX_POOL];
 	rt_pktio_t pktio[RT_MAX_PKTIO];
 	rt_queue_t *sched;         /* scheduled queues */
-	uint32_t rr;
+	uint32_t sched_n;          /* events in them (read without a lock) */
+	int polling;               /* a thread is in poll_input */
 } rt = { PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, 0, NULL, {{0}}, {{0}},
-	 NULL, 0 };
+	 NULL, 0, 0 };
 
 /* pinned host memory and its device address (zero-copy launch buffers) */
 static int pinned_alloc(size_t bytes, void **host, void **dev)
@@ -1660,7 +1723,9 @@ static rt_queue_t *queue_new(const char *name, const odp_queue_param_t *param)
 		q->param = *param;
 	else
 		odp_queue_param_init(&q->param);
-	q->head = q->tail = NULL;
+	q->ev.rd = 0;
+	__atomic_store_n(&q->ev.n, 0u, __ATOMIC_RELAXED);
+	q->sched = q->param.type == ODP_QUEUE_TYPE_SCHED;
 	q->next_sched = NULL;
 	q->pktin = q->pktout = ODP_PKTIO_INVALID;
 	q->dead = 0;
@@ -1726,8 +1791,8 @@ int odp_queue_destroy(odp_queue_t queue)
 	if (!q)
 		return -1;
 	pthread_mutex_lock(&q->lock);
-	if (q->head || q->dead) {
-		const int busy = q->head != NULL;
+	if (q->ev.n || q->dead) {
+		const int busy = q->ev.n != 0;
 
 		pthread_mutex_unlock(&q->lock);
 		if (busy)
@@ -1763,17 +1828,16 @@ uint64_t odp_queue_to_u64(odp_queue_t queue)
 	return (uint64_t)(uintptr_t)queue;
 }
 
-/* link a chain of packets at the queue's tail */
-static void queue_append(rt_queue_t *q, rt_pkt_t *first, rt_pkt_t *last)
+/* num events at the queue's tail, all or none (-1: no memory) */
+static int queue_push(rt_queue_t *q, const odp_event_t ev[], uint32_t num)
 {
-	last->next = NULL;
 	pthread_mutex_lock(&q->lock);
-	if (q->tail)
-		q->tail->next = first;
-	else
-		q->head = first;
-	q->tail = last;
+	const int ret = pring_push(&q->ev, (void *const *)ev, num);
+
+	if (!ret && q->sched)
+		__atomic_fetch_add(&rt.sched_n, num, __ATOMIC_RELEASE);
 	pthread_mutex_unlock(&q->lock);
+	return ret;
 }
 
 int odp_queue_enq(odp_queue_t queue, odp_event_t ev)
@@ -1795,10 +1859,7 @@ int odp_queue_enq_multi(odp_queue_t queue, const odp_event_t ev[], int num)
 			return -1;
 	if (q->pktout)                  /* pktout event queue: transmit */
 		return pktout_send_impl(q->pktout, (const odp_packet_t *)ev, num);
-	for (int i = 0; i + 1 < num; i++)
-		((rt_pkt_t *)ev[i])->next = (rt_pkt_t *)ev[i + 1];
-	queue_append(q, (rt_pkt_t *)ev[0], (rt_pkt_t *)ev[num - 1]);
-	return num;
+	return queue_push(q, ev, (uint32_t)num) ? -1 : num;
 }
 
 static int deq_multi(rt_queue_t *q, odp_event_t ev[], int num);
@@ -1816,7 +1877,7 @@ int odp_queue_deq_multi(odp_queue_t queue, odp_event_t ev[], int num)
 
 	if (!q)
 		return -1;
-	if (q->pktin && !__atomic_load_n(&q->head, __ATOMIC_RELAXED))
+	if (q->pktin && !__atomic_load_n(&q->ev.n, __ATOMIC_RELAXED))
 		pktin_queue_fill(q->pktin);     /* QUEUE mode: receive a burst */
 	return deq_multi(q, ev, num);
 }
@@ -1836,19 +1897,17 @@ void odp_event_free_multi(const odp_event_t event[], int num)
 /* up to num events of one queue */
 static int deq_multi(rt_queue_t *q, odp_event_t ev[], int num)
 {
-	int n = 0;
-
+	/* an empty queue without its lock: pollers spinning on empty queues
+	 * keep off the line the producer locks */
+	if (num <= 0 || !__atomic_load_n(&q->ev.n, __ATOMIC_ACQUIRE))
+		return 0;
 	pthread_mutex_lock(&q->lock);
-	while (n < num && q->head) {
-		rt_pkt_t *k = q->head;
+	const uint32_t n = pring_pop(&q->ev, (void **)ev, (uint32_t)num);
 
-		q->head = k->next;
-		ev[n++] = (odp_event_t)k;
-	}
-	if (!q->head)
-		q->tail = NULL;
+	if (n && q->sched)
+		__atomic_fetch_sub(&rt.sched_n, n, __ATOMIC_RELAXED);
 	pthread_mutex_unlock(&q->lock);
-	return n;
+	return (int)n;
 }
 
 /* ---- pktio input ----------------------------------------------------------- */
@@ -1869,19 +1928,16 @@ static void pktio_queue_kill(rt_queue_t **qp)
 	if (!q)
 		return;
 	pthread_mutex_lock(&q->lock);
-	rt_pkt_t *k = q->head;
+	ptr_ring_t ev = q->ev;
 	const int was_dead = q->dead;
 
-	q->head = q->tail = NULL;
+	memset(&q->ev, 0, sizeof(q->ev));
+	if (q->sched && ev.n)
+		__atomic_fetch_sub(&rt.sched_n, ev.n, __ATOMIC_RELAXED);
 	q->dead = 1;
 	q->pktin = q->pktout = ODP_PKTIO_INVALID;
 	pthread_mutex_unlock(&q->lock);
-	while (k) {
-		rt_pkt_t *nx = k->next;
-
-		odp_packet_free((odp_packet_t)k);
-		k = nx;
-	}
+	pring_free_packets(&ev);
 	if (!was_dead)
 		queue_release(q);
 }
@@ -1947,8 +2003,6 @@ void odpg_rt_pktio_close(odp_pktio_t hdl)
 	rt_pktio_t *p = get_rt_pktio(hdl);
 
 	if (p) {
-		rt_pkt_t *k = p->ring_head;
-
 		if (p->have_cap)
 			odpg_pcap_free(&p->cap);
 		pktio_queue_kill(&p->inq);
@@ -1960,12 +2014,7 @@ void odpg_rt_pktio_close(odp_pktio_t hdl)
 			x = nx;
 		}
 		p->ahead = p->ahead_tail = NULL;
-		while (k) {
-			rt_pkt_t *nx = k->next;
-
-			odp_packet_free((odp_packet_t)k);
-			k = nx;
-		}
+		pring_free_packets(&p->ring);
 		rx_release(p);
 		pthread_mutex_destroy(&p->ring_lock);
 		memset(p, 0, sizeof(*p));
@@ -2134,19 +2183,17 @@ static uint32_t rx_stage(rt_pktio_t *p, rx_slot_t *s, uint32_t num)
 	size_t need = 0, off = 0;
 
 	if (p->loopdev) {
+		/* the handles only under the lock (the transmitters wait on
+		 * it); the packets are read after */
+		if (!__atomic_load_n(&p->ring.n, __ATOMIC_ACQUIRE))
+			return 0;
 		pthread_mutex_lock(&p->ring_lock);
-		while (n < num && p->ring_head) {
-			s->src[n] = p->ring_head;
-			p->ring_head = p->ring_head->next;
-			need += ALIGN64(s->src[n]->len);
-			n++;
-		}
-		if (!p->ring_head)
-			p->ring_tail = NULL;
-		p->ring_n -= n;
+		n = pring_pop(&p->ring, (void **)s->src, num);
 		pthread_mutex_unlock(&p->ring_lock);
 		if (!n)
 			return 0;
+		for (uint32_t k = 0; k < n; k++)
+			need += ALIGN64(s->src[k]->len);
 		if (stage_reserve(s, need)) {
 			for (uint32_t k = 0; k < n; k++)
 				odp_packet_free((odp_packet_t)s->src[k]);
@@ -2376,7 +2423,7 @@ static int rx_to_inq(rt_pktio_t *p, odp_pktio_t hdl, int drain)
 	}
 	while (!drain && p->rx_count < RT_INFLIGHT && odpg_cls_pktio_started(hdl)) {
 		if (p->loopdev && p->rx_count &&
-		    __atomic_load_n(&p->ring_n, __ATOMIC_RELAXED) < RT_BURST / 4u)
+		    __atomic_load_n(&p->ring.n, __ATOMIC_RELAXED) < RT_BURST / 4u)
 			break;
 		rx_slot_t *s = slot_get(p, (p->rx_head + p->rx_count) % RT_INFLIGHT);
 
@@ -2430,8 +2477,10 @@ static int poll_input(void)
 {
 	int got = 0;
 
-	if (pthread_mutex_trylock(&rt.poll_lock))
+	/* another thread polls: its flag is read, not the lock's line written */
+	if (__atomic_load_n(&rt.polling, __ATOMIC_RELAXED) || pthread_mutex_trylock(&rt.poll_lock))
 		return 0;
+	__atomic_store_n(&rt.polling, 1, __ATOMIC_RELAXED);
 	for (int i = 0; i < RT_MAX_PKTIO && rt.init; i++) {
 		rt_pktio_t *p = &rt.pktio[i];
 
@@ -2442,6 +2491,7 @@ static int poll_input(void)
 		if (took > 0)
 			got += took;
 	}
+	__atomic_store_n(&rt.polling, 0, __ATOMIC_RELAXED);
 	pthread_mutex_unlock(&rt.poll_lock);
 	return got;
 }
@@ -2625,9 +2675,14 @@ static int sched_once(odp_queue_t *from, odp_event_t ev[], int num)
 {
 	/* the list is walked under the read side of sched_rw: a destroy
 	 * unlinks under the write side before the object is reused */
+	static __thread uint32_t rr;   /* this thread's round-robin start */
+
+	/* nothing queued: the walk (and the lock's shared line) skipped */
+	if (!__atomic_load_n(&rt.sched_n, __ATOMIC_ACQUIRE))
+		return 0;
 	pthread_rwlock_rdlock(&sched_rw);
 	rt_queue_t *list = rt.sched;
-	const uint32_t skip = __atomic_fetch_add(&rt.rr, 1u, __ATOMIC_RELAXED);
+	const uint32_t skip = rr++;
 	int nq = 0, n = 0;
 
 	for (rt_queue_t *q = list; q; q = q->next_sched)
@@ -2793,18 +2848,11 @@ static int pktout_send_impl(odp_pktio_t pktio, const odp_packet_t packets[], int
 	}
 	if (p->loopdev) {
 		pthread_mutex_lock(&p->ring_lock);
-		for (int i = 0; i < n; i++) {
-			rt_pkt_t *k = PK(packets[i]);
+		const int full = pring_push(&p->ring, (void *const *)packets, (uint32_t)n);
 
-			k->next = NULL;
-			if (p->ring_tail)
-				p->ring_tail->next = k;
-			else
-				p->ring_head = k;
-			p->ring_tail = k;
-		}
-		p->ring_n += (uint32_t)n;
 		pthread_mutex_unlock(&p->ring_lock);
+		if (full)
+			return 0;       /* no memory for the ring: nothing sent */
 	} else {
 		odp_packet_free_multi(packets, n);
 	}

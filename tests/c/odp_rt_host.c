@@ -7,8 +7,10 @@
  * odp_init_local / odp_term_local (unique, below ODP_THREAD_COUNT_MAX), named
  * shm reserve / lookup / free (a second free fails cleanly), the packet
  * pool (buffers through per-thread caches, the num limit, long packets,
- * destroy / re-create with a packet outstanding), and the queue registry: create / destroy cycles beyond its slot count, stale handles
- * refused, scheduled queues created and destroyed while other threads
+ * destroy / re-create with a packet outstanding), the queue registry:
+ * create / destroy cycles beyond its slot count, stale handles refused, the
+ * queues' event rings (growth, wrap, FIFO order per producer with several
+ * producers and consumers, through dequeue and the scheduler), and scheduled queues created and destroyed while other threads
  * schedule. Prints PASS or the first failure. Run by tests/test_odp_rt.py.
  */
 #include <pthread.h>
@@ -147,6 +149,93 @@ static void *churn_thread(void *arg)
 	return NULL;
 }
 
+/* ---- queue rings: producers and consumers of tagged handles ---------------- */
+#define QP 4                       /* producers (and consumers) */
+#define QN 200000                  /* events per producer */
+static odp_queue_t fifo;
+static int fifo_sched;             /* consumers call the scheduler */
+static uint32_t fifo_got;
+static uint8_t *fifo_seen;
+
+static odp_event_t tag_ev(uint32_t p, uint32_t i)
+{
+	return (odp_event_t)(uintptr_t)(((uint64_t)(p + 1u) << 32) | i);
+}
+
+static void *fifo_prod(void *arg)
+{
+	const uint32_t p = (uint32_t)(intptr_t)arg;
+	odp_event_t ev[37];
+
+	for (uint32_t i = 0; i < QN && !fails;) {
+		const uint32_t b = 1u + (i * 7u + p) % 37u, k = b < QN - i ? b : QN - i;
+
+		for (uint32_t j = 0; j < k; j++)
+			ev[j] = tag_ev(p, i + j);
+		CHECK(odp_queue_enq_multi(fifo, ev, (int)k) == (int)k, "enq %u", i);
+		i += k;
+	}
+	return NULL;
+}
+
+static void *fifo_cons(void *arg)
+{
+	uint32_t last[QP];
+	odp_event_t ev[29];
+
+	(void)arg;
+	memset(last, 0xff, sizeof(last));
+	while (__atomic_load_n(&fifo_got, __ATOMIC_RELAXED) < QP * QN && !fails) {
+		odp_queue_t from = ODP_QUEUE_INVALID;
+		const int n = fifo_sched ? odp_schedule_multi(&from, ODP_SCHED_NO_WAIT, ev, 29)
+					 : odp_queue_deq_multi(fifo, ev, 29);
+
+		CHECK(n >= 0 && (!n || !fifo_sched || from == fifo), "dequeue");
+		for (int j = 0; j < n; j++) {
+			const uint64_t v = (uint64_t)(uintptr_t)ev[j];
+			const uint32_t p = (uint32_t)(v >> 32) - 1u, i = (uint32_t)v;
+
+			CHECK(p < QP && i < QN, "a handle never enqueued: %llx", (unsigned long long)v);
+			if (p >= QP || i >= QN)
+				break;
+			CHECK(last[p] == 0xffffffffu || i > last[p],
+			      "producer %u: %u after %u (FIFO order)", p, i, last[p]);
+			CHECK(!__atomic_exchange_n(&fifo_seen[p * QN + i], 1, __ATOMIC_RELAXED),
+			      "event %u.%u twice", p, i);
+			last[p] = i;
+		}
+		if (n > 0)
+			__atomic_fetch_add(&fifo_got, (uint32_t)n, __ATOMIC_RELAXED);
+	}
+	return NULL;
+}
+
+/* QP producers and QP consumers through one queue (plain: dequeue; SCHED:
+ * the scheduler), every event exactly once and each producer's in order */
+static void fifo_run(int sched)
+{
+	odp_queue_param_t qp;
+	pthread_t t[2 * QP];
+
+	odp_queue_param_init(&qp);
+	qp.type = sched ? ODP_QUEUE_TYPE_SCHED : ODP_QUEUE_TYPE_PLAIN;
+	fifo = odp_queue_create("fifo", &qp);
+	fifo_sched = sched;
+	fifo_got = 0;
+	fifo_seen = calloc((size_t)QP * QN, 1);
+	CHECK(fifo != ODP_QUEUE_INVALID && fifo_seen, "fifo queue");
+	for (int i = 0; i < QP; i++) {
+		pthread_create(&t[i], NULL, fifo_prod, (void *)(intptr_t)i);
+		pthread_create(&t[QP + i], NULL, fifo_cons, NULL);
+	}
+	for (int i = 0; i < 2 * QP; i++)
+		pthread_join(t[i], NULL);
+	CHECK(fifo_got == QP * QN, "%u of %u events", fifo_got, QP * QN);
+	CHECK(odp_queue_deq(fifo) == ODP_EVENT_INVALID, "events left");
+	CHECK(odp_queue_destroy(fifo) == 0, "fifo destroy");
+	free(fifo_seen);
+}
+
 static void run(void *(*fn)(void *), int n)
 {
 	pthread_t t[NT];
@@ -268,6 +357,34 @@ int main(void)
 	CHECK(live != ODP_QUEUE_INVALID && live != first && live != q, "handle reuse");
 	CHECK(odp_queue_destroy(live) == 0, "destroy live");
 	printf("queues: 2^21 create/destroy cycles\n");
+
+	/* a queue's ring: growth and wrap in FIFO order, one thread */
+	{
+		odp_queue_t f = odp_queue_create("ring", NULL);
+		uint32_t wr = 0, rd = 0;
+
+		for (uint32_t it = 0; it < 20000 && !fails; it++) {
+			odp_event_t ev[300];
+			const uint32_t k = 1u + (it * 131u) % 300u, d = 1u + (it * 97u) % 290u;
+
+			for (uint32_t j = 0; j < k; j++)
+				ev[j] = tag_ev(0, wr++);
+			CHECK(odp_queue_enq_multi(f, ev, (int)k) == (int)k, "ring enq");
+			const int n = odp_queue_deq_multi(f, ev, (int)d);
+
+			for (int j = 0; j < n; j++)
+				CHECK(ev[j] == tag_ev(0, rd + (uint32_t)j), "ring order at %u", rd);
+			rd += (uint32_t)n;
+		}
+		CHECK(odp_queue_destroy(f) == -1, "a non-empty queue destroyed");
+		for (int n; (n = odp_queue_deq_multi(f, (odp_event_t[64]){0}, 64)) > 0;)
+			rd += (uint32_t)n;
+		CHECK(rd == wr && odp_queue_destroy(f) == 0, "ring drained: %u of %u", rd, wr);
+	}
+	fifo_run(0);
+	fifo_run(1);
+	printf("queue rings: growth / wrap, %d producers x %d consumers (plain and scheduled)\n",
+	       QP, QP);
 
 	/* scheduled queues under concurrent schedulers */
 	pthread_t s[4], c[2];
