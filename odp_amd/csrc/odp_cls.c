@@ -93,6 +93,11 @@ typedef struct {
 	int error_cos;          /* -1 = NULL */
 	uint32_t headroom;
 	odp_pktio_stats_t stats;
+	/* the runtime's host-side counts (odpg_cls_pktio_count): added with
+	 * atomics outside the lock (the transmitting threads count every
+	 * send), read into stats by odp_pktio_stats: in_packets, in_octets,
+	 * in_discards, out_packets, out_octets */
+	uint64_t hc[5];
 	struct bind_s *binds;   /* compiled tables, one per context in use */
 } pktio_e;
 
@@ -1306,7 +1311,7 @@ int odp_pktio_start(odp_pktio_t hdl)
 		rc = -1;
 	} else {
 		p->parse_layer = p->cls_enabled ? ODP_PROTO_LAYER_ALL : (int)p->config.parser.layer;
-		p->started = 1;
+		__atomic_store_n(&p->started, 1, __ATOMIC_RELEASE);
 		bump();
 	}
 	UNLOCK();
@@ -1323,7 +1328,7 @@ int odp_pktio_stop(odp_pktio_t hdl)
 	if (!p || !p->started)
 		rc = -1;
 	else
-		p->started = 0;
+		__atomic_store_n(&p->started, 0, __ATOMIC_RELEASE);
 	UNLOCK();
 	if (!rc)
 		odpg_rt_pktio_drain(hdl);
@@ -1341,6 +1346,11 @@ int odp_pktio_stats(odp_pktio_t hdl, odp_pktio_stats_t *stats)
 	}
 	fold_pktio_locked(p);
 	*stats = p->stats;
+	stats->in_packets += __atomic_load_n(&p->hc[0], __ATOMIC_RELAXED);
+	stats->in_octets += __atomic_load_n(&p->hc[1], __ATOMIC_RELAXED);
+	stats->in_discards += __atomic_load_n(&p->hc[2], __ATOMIC_RELAXED);
+	stats->out_packets += __atomic_load_n(&p->hc[3], __ATOMIC_RELAXED);
+	stats->out_octets += __atomic_load_n(&p->hc[4], __ATOMIC_RELAXED);
 	UNLOCK();
 	return 0;
 }
@@ -1356,6 +1366,8 @@ int odp_pktio_stats_reset(odp_pktio_t hdl)
 	}
 	fold_pktio_locked(p);
 	memset(&p->stats, 0, sizeof(p->stats));
+	for (int i = 0; i < 5; i++)
+		__atomic_store_n(&p->hc[i], 0, __ATOMIC_RELAXED);
 	UNLOCK();
 	return 0;
 }
@@ -1756,27 +1768,25 @@ int odpg_cls_pktio_recv_meta_zc(odp_pktio_t hdl, odpg_ctx_t *ctx, const uint8_t 
 void odpg_cls_pktio_count(odp_pktio_t hdl, int64_t in_packets, int64_t in_octets,
 			  uint64_t in_discards, uint64_t out_packets, uint64_t out_octets)
 {
-	LOCK();
+	/* no lock: the pktio slots are a static table (an entry being closed
+	 * counts into a slot nobody reads until it is opened again, and the
+	 * open clears the counts) */
 	pktio_e *p = get_pktio(hdl);
+	const uint64_t v[5] = { (uint64_t)in_packets, (uint64_t)in_octets, in_discards,
+				out_packets, out_octets };
 
-	if (p) {
-		p->stats.in_packets += (uint64_t)in_packets;
-		p->stats.in_octets += (uint64_t)in_octets;
-		p->stats.in_discards += in_discards;
-		p->stats.out_packets += out_packets;
-		p->stats.out_octets += out_octets;
-	}
-	UNLOCK();
+	if (p)
+		for (int i = 0; i < 5; i++)
+			if (v[i])
+				__atomic_fetch_add(&p->hc[i], v[i], __ATOMIC_RELAXED);
 }
 
+/* read without the lock: asked on every send and receive burst */
 int odpg_cls_pktio_started(odp_pktio_t hdl)
 {
-	LOCK();
 	pktio_e *p = get_pktio(hdl);
-	const int r = p && p->started;
 
-	UNLOCK();
-	return r;
+	return p && __atomic_load_n(&p->started, __ATOMIC_ACQUIRE);
 }
 
 int odpg_cls_pktio_classifies(odp_pktio_t hdl)

@@ -54,26 +54,31 @@
 #define RT_MAX_PKTIO 64
 #define RT_MAX_POOL  64
 #define RT_BURST     1024
+#define RX_PF        8         /* packets prefetched ahead in staging / delivery */
 #define RT_INFLIGHT  4              /* receive bursts in flight per pktio */
 
 /* ---- objects -------------------------------------------------------------- */
 #define PKT_MAGIC 0x504b5452u
 
+/* the first 64 bytes hold what receive touches (staging reads len and
+ * data, delivery writes pool .. input): one line per packet there */
 typedef struct rt_pkt {
 	uint32_t magic;
 	uint32_t len;
+	odp_pool_t pool;
+	uint8_t *data;
+	odpg_meta_t meta;          /* parse result: packet_parser_t + cls_mark */
+	odp_cos_t cos;
+	odp_pktio_t input;         /* the pktio it was received on */
 	uint32_t cap;
 	uint32_t ext;              /* data malloc'd on its own (longer than the pool's buffers) */
 	uint32_t pgen;             /* its pool's generation (rt_pool_t.gen) */
-	odp_pool_t pool;
-	odp_cos_t cos;
-	odp_pktio_t input;         /* the pktio it was received on */
-	odpg_meta_t meta;          /* parse result: packet_parser_t + cls_mark */
-	uint8_t *data;
 	struct rt_pkt *next;       /* queue link */
 } rt_pkt_t;
+_Static_assert(__builtin_offsetof(rt_pkt_t, cap) == 64, "rt_pkt_t receive line");
+#define PK(p) ((rt_pkt_t *)(p))
 
-#define TC_N     64        /* largest per-thread cache of one pool */
+#define TC_N     512       /* largest per-thread cache of one pool */
 
 typedef struct rt_pool {
 	int valid;
@@ -93,6 +98,19 @@ typedef struct rt_pool {
 	void **chunks;
 	uint32_t nchunks;
 } rt_pool_t;
+
+/* the runtime's short critical sections (pool stacks, queue rings, the loop
+ * ring): an adaptive mutex spins a while before it sleeps, so workers
+ * meeting on one of them do not pay a futex round trip each */
+static void rt_mutex_init(pthread_mutex_t *m)
+{
+	pthread_mutexattr_t a;
+
+	pthread_mutexattr_init(&a);
+	pthread_mutexattr_settype(&a, PTHREAD_MUTEX_ADAPTIVE_NP);
+	pthread_mutex_init(m, &a);
+	pthread_mutexattr_destroy(&a);
+}
 
 /* a FIFO of handles: v[rd..rd+n) modulo cap (a power of two), grown by
  * doubling; its owner's lock held. n is also read without the lock (an empty
@@ -257,7 +275,8 @@ void odp_init_param_init(odp_init_t *param)
 static struct {
 	int on;
 	uint64_t bursts, pkts, stage_ns, gpu_ns, post_ns;
-} rxprof = { -1, 0, 0, 0, 0, 0 };
+	uint64_t end_ns, enq_ns;   /* of post_ns: the binding's release, the queue appends */
+} rxprof = { -1, 0, 0, 0, 0, 0, 0, 0 };
 
 static uint64_t prof_ns(void)
 {
@@ -301,10 +320,12 @@ int odp_term_global(odp_instance_t instance)
 	parse_release();
 	if (rxprof.on > 0 && rxprof.bursts)
 		fprintf(stderr, "odp_rt: %llu receive bursts, %.1f packets each; per burst: "
-			"staging %.2f us, launch (+ GPU wait in DIRECT mode) %.2f us, delivery %.2f us\n",
+			"staging %.2f us, launch (+ GPU wait in DIRECT mode) %.2f us, delivery %.2f us "
+			"(binding release %.2f us, queue appends %.2f us)\n",
 			(unsigned long long)rxprof.bursts, (double)rxprof.pkts / rxprof.bursts,
 			rxprof.stage_ns / 1e3 / rxprof.bursts, rxprof.gpu_ns / 1e3 / rxprof.bursts,
-			rxprof.post_ns / 1e3 / rxprof.bursts);
+			rxprof.post_ns / 1e3 / rxprof.bursts, rxprof.end_ns / 1e3 / rxprof.bursts,
+			rxprof.enq_ns / 1e3 / rxprof.bursts);
 	pthread_mutex_lock(&rt.poll_lock);
 	for (int i = 0; i < RT_MAX_PKTIO; i++)
 		rx_release(&rt.pktio[i]);
@@ -501,8 +522,64 @@ int32_t odp_cpumask_to_str(const odp_cpumask_t *mask, char *str, int32_t size)
 	return nib + 3;
 }
 
+/* the first CPU of a sysfs CPU list file (the L3's or the core's sharers);
+ * -1 when absent */
+static int cpu_list_first(int cpu, const char *what)
+{
+	char path[128];
+	int first = -1;
+
+	snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/%s", cpu, what);
+	FILE *f = fopen(path, "r");
+
+	if (f) {
+		if (fscanf(f, "%d", &first) != 1)
+			first = -1;
+		fclose(f);
+	}
+	return first;
+}
+
+/* num workers (num > 0) inside one L3 cache: the packets, queues and locks
+ * the workers share then move between cores of one CCD instead of across
+ * the IO die (on a 2 x 64-core EPYC host, 8 workers on CPUs 1-8 span two
+ * CCDs and odp_pktio_perf -c 8 fell to a third of -c 6's rate). One core's
+ * first hardware thread each; the control CPU's own L3 first, else the
+ * first L3 with num free cores. Returns 0 when no L3 holds them (or the
+ * topology is not in sysfs): the caller takes CPUs in order. */
+static int l3_mask(const cpu_set_t *set, int control, int num, odp_cpumask_t *mask)
+{
+	const int ctl_l3 = cpu_list_first(control, "cache/index3/shared_cpu_list");
+
+	if (ctl_l3 < 0)
+		return 0;
+	for (int pass = 0; pass < 2; pass++) {
+		for (int l3 = 0; l3 < CPU_SETSIZE && l3 < ODP_CPUMASK_SIZE; l3++) {
+			if (!CPU_ISSET(l3, set) ||
+			    cpu_list_first(l3, "cache/index3/shared_cpu_list") != l3 ||
+			    (pass == 0) != (l3 == ctl_l3))
+				continue;
+			int n = 0;
+
+			odp_cpumask_zero(mask);
+			for (int c = l3; c < CPU_SETSIZE && c < ODP_CPUMASK_SIZE && n < num; c++)
+				if (c != control && CPU_ISSET(c, set) &&
+				    cpu_list_first(c, "cache/index3/shared_cpu_list") == l3 &&
+				    cpu_list_first(c, "topology/thread_siblings_list") == c) {
+					odp_cpumask_set(mask, c);
+					n++;
+				}
+			if (n == num)
+				return n;
+		}
+	}
+	odp_cpumask_zero(mask);
+	return 0;
+}
+
 /* workers on the CPUs of the affinity mask after the first (the control
- * thread's), as many as asked (0 = all) */
+ * thread's), as many as asked (0 = all): a given number inside one L3 where
+ * one holds them (l3_mask) */
 static int default_mask(odp_cpumask_t *mask, int num, int worker)
 {
 	cpu_set_t set;
@@ -511,6 +588,16 @@ static int default_mask(odp_cpumask_t *mask, int num, int worker)
 	odp_cpumask_zero(mask);
 	if (sched_getaffinity(0, sizeof(set), &set))
 		return 0;
+	if (worker && num > 0 && CPU_COUNT(&set) > num) {
+		int control = 0;
+
+		while (!CPU_ISSET(control, &set))
+			control++;
+		const int n = l3_mask(&set, control, num, mask);
+
+		if (n)
+			return n;
+	}
 	for (int c = 0; c < CPU_SETSIZE && c < ODP_CPUMASK_SIZE; c++) {
 		if (!CPU_ISSET(c, &set))
 			continue;
@@ -830,7 +917,7 @@ odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param)
 		p->stack = malloc((size_t)param->pkt.num * sizeof(rt_pkt_t *));
 		if (!p->stack)
 			break;
-		pthread_mutex_init(&p->lock, NULL);
+		rt_mutex_init(&p->lock);
 		p->valid = 1;
 		ret = (odp_pool_t)(uintptr_t)(i + 1);
 		break;
@@ -1085,14 +1172,92 @@ static void tcache_flush(void)
 	}
 }
 
+/* runs of one pool's packets in one pass: the thread's cache filled, the
+ * rest onto the pool's stack under one lock (with the cache trimmed to half,
+ * as odp_packet_free does) */
 void odp_packet_free_multi(const odp_packet_t pkt[], int num)
 {
-	for (int i = 0; i < num; i++)
-		odp_packet_free(pkt[i]);
+	for (int i = 0; i < num;) {
+		rt_pkt_t *k0 = PK(pkt[i]);
+
+		if (!k0) {
+			i++;
+			continue;
+		}
+		const odp_pool_t pool = k0->pool;
+		const uint32_t pgen = k0->pgen;
+		rt_pool_t *p = get_pool(pool);
+		int j = i;
+
+		while (j < num && pkt[j] && PK(pkt[j])->pool == pool && PK(pkt[j])->pgen == pgen)
+			j++;
+		if (!p || p->gen != pgen) {      /* its pool was destroyed */
+			for (; i < j; i++)
+				odp_packet_free(pkt[i]);
+			continue;
+		}
+		const int ts = tc_slot(pool, p);
+		int over = j;                    /* the first not cached */
+
+		for (int m = i; m < j; m++) {
+			rt_pkt_t *k = PK(pkt[m]);
+
+			k->magic = 0;
+			if (k->ext) {
+				free(k->data);
+				k->data = (uint8_t *)k + PKT_HDR;
+				k->ext = 0;
+			}
+			k->cap = p->buf;
+			if (over == j && ts >= 0 && tcache[ts].n < p->tc_max)
+				tcache[ts].b[tcache[ts].n++] = k;
+			else if (over == j)
+				over = m;
+		}
+		if (over < j) {
+			pthread_mutex_lock(&p->lock);
+			if (p->valid && p->gen == pgen) {
+				for (int m = over; m < j; m++)
+					p->stack[p->nfree++] = PK(pkt[m]);
+				while (ts >= 0 && tcache[ts].n > p->tc_max / 2)
+					p->stack[p->nfree++] = tcache[ts].b[--tcache[ts].n];
+				p->in_use = p->made - p->nfree;
+			}
+			pthread_mutex_unlock(&p->lock);
+		}
+		i = j;
+	}
+}
+
+/* up to n of a pool's buffers for packets of at most its buffer length (the
+ * caller initialises them: pkt_init): the thread's cache first, then the
+ * stack under one lock, the cache refilled to half. Returns how many. */
+static uint32_t pool_take(odp_pool_t pool, rt_pkt_t *out[], uint32_t n)
+{
+	rt_pool_t *p = get_pool(pool);
+	uint32_t got = 0;
+
+	if (!p)
+		return 0;
+	const int ts = tc_slot(pool, p);
+
+	while (ts >= 0 && got < n && tcache[ts].n)
+		out[got++] = tcache[ts].b[--tcache[ts].n];
+	if (got == n)
+		return got;
+	pthread_mutex_lock(&p->lock);
+	if (p->valid) {
+		while (got < n && (p->nfree || !pool_grow_locked(p)))
+			out[got++] = p->stack[--p->nfree];
+		while (ts >= 0 && p->nfree && tcache[ts].n < p->tc_max / 2)
+			tcache[ts].b[tcache[ts].n++] = p->stack[--p->nfree];
+		p->in_use = p->made - p->nfree;
+	}
+	pthread_mutex_unlock(&p->lock);
+	return got;
 }
 
 /* ---- packet accessors ------------------------------------------------------ */
-#define PK(p) ((rt_pkt_t *)(p))
 
 /* _odp_packet_input_flags_t bits (packet_inline_types.h:60-113) */
 enum {
@@ -1712,7 +1877,7 @@ static rt_queue_t *queue_new(const char *name, const odp_queue_param_t *param)
 			ERR("queue registry full\n");
 			return NULL;
 		}
-		pthread_mutex_init(&q->lock, NULL);
+		rt_mutex_init(&q->lock);
 		q->magic = QUEUE_MAGIC;
 	}
 	/* a reused object: the destroyed queue's fields reset (its lock and
@@ -1969,7 +2134,7 @@ int odpg_rt_pktio_open(odp_pktio_t hdl, const char *name, odp_pool_t pool,
 	p->pool = pool;
 	p->mtu = LOOP_MTU;
 	p->loopdev = !strncmp(name, "loop", 4);
-	pthread_mutex_init(&p->ring_lock, NULL);
+	rt_mutex_init(&p->ring_lock);
 	if (!strncmp(name, "pcap:", 5)) {
 		char buf[1024], *save = NULL, *tok;
 
@@ -2192,14 +2357,19 @@ static uint32_t rx_stage(rt_pktio_t *p, rx_slot_t *s, uint32_t num)
 		pthread_mutex_unlock(&p->ring_lock);
 		if (!n)
 			return 0;
-		for (uint32_t k = 0; k < n; k++)
+		for (uint32_t k = 0; k < n; k++) {
+			if (k + RX_PF < n)
+				__builtin_prefetch(s->src[k + RX_PF], 0, 3);
 			need += ALIGN64(s->src[k]->len);
+		}
 		if (stage_reserve(s, need)) {
 			for (uint32_t k = 0; k < n; k++)
 				odp_packet_free((odp_packet_t)s->src[k]);
 			return 0;
 		}
 		for (uint32_t k = 0; k < n; k++) {
+			if (k + RX_PF < n)
+				__builtin_prefetch(s->src[k + RX_PF]->data, 0, 3);
 			memcpy(s->stage + off, s->src[k]->data, s->src[k]->len);
 			s->desc[k].offset = (uint32_t)off;
 			s->desc[k].len = s->src[k]->len;
@@ -2261,17 +2431,47 @@ static int rx_launch(odp_pktio_t hdl, rx_slot_t *s)
 static void rx_deliver(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, odp_packet_t pkts[],
 		       int *nret)
 {
-	odp_packet_t run[RT_BURST];
-	int nrun = 0;
+	odp_packet_t run[RT_BURST], dead[RT_BURST];
+	rt_pkt_t *fresh[RT_BURST];
+	int nrun = 0, ndead = 0;
+	uint32_t want = 0, nfresh = 0, used = 0;
 	odp_cos_t run_cos = ODP_COS_INVALID;
 	odp_queue_t run_q = ODP_QUEUE_INVALID;
+	const rt_pool_t *own = get_pool(p->pool);
+
+	const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
 
 	odpg_cls_pktio_recv_end(s->token);
 	s->token = NULL;
+	if (rxprof.on > 0)
+		rxprof.end_ns += prof_ns() - t0;
+	/* the packets without a CoS that land in the pktio's pool from
+	 * elsewhere (a capture's frames; the loop device's packets from a
+	 * separate transmit pool, loop.c's _odp_pktio_packet_to_pool): their
+	 * buffers in one take, the originals freed in one pass at the end */
+	for (uint32_t k = 0; k < s->n; k++)
+		if (ODPG_OUT_COS(s->out[k]) == ODPG_COS_NOCLS &&
+		    (!s->src[k] || s->src[k]->pool != p->pool))
+			want++;
+	if (want && own)
+		nfresh = pool_take(p->pool, fresh, want);
 	for (uint32_t k = 0; k < s->n; k++) {
 		const uint32_t w = s->out[k];
 		const uint32_t len = s->desc[k].len;
 		rt_pkt_t *have = s->src[k];
+
+		/* the headers' lines were last written on the transmitting
+		 * cores: their ownership requested ahead, not one at a time */
+		if (k + RX_PF < s->n && s->src[k + RX_PF])
+			__builtin_prefetch(s->src[k + RX_PF], 1, 3);
+		/* and the GPU-written verdicts / metadata (pinned host lines
+		 * the device wrote: not in any CPU cache) */
+		if ((k & 7u) == 0 && k + 4u * RX_PF < s->n) {
+			__builtin_prefetch(&s->meta[k + 4u * RX_PF], 0, 3);
+			__builtin_prefetch(&s->meta[k + 4u * RX_PF + 4u], 0, 3);
+			__builtin_prefetch(&s->out[k + 4u * RX_PF], 0, 3);
+			__builtin_prefetch(&s->desc[k + 4u * RX_PF], 0, 3);
+		}
 		odp_cos_t cos = ODP_COS_INVALID;
 		odp_queue_t q = ODP_QUEUE_INVALID;
 		odp_pool_t pool = p->pool;
@@ -2291,11 +2491,16 @@ static void rx_deliver(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, odp_packet_
 			pkt = (odp_packet_t)have;
 		} else {
 			/* into the CoS's pool (_odp_pktio_packet_to_pool) */
-			pkt = odp_packet_alloc(pool, len);
+			if (pool == p->pool && used < nfresh && len <= own->buf) {
+				pkt = (odp_packet_t)fresh[used++];
+				pkt_init(PK(pkt), pool, len);
+			} else {
+				pkt = odp_packet_alloc(pool, len);
+			}
 			if (pkt != ODP_PACKET_INVALID)
 				memcpy(PK(pkt)->data, s->stage + s->desc[k].offset, len);
 			if (have)
-				odp_packet_free((odp_packet_t)have);
+				dead[ndead++] = (odp_packet_t)have;
 			if (pkt == ODP_PACKET_INVALID) {
 				/* loop.c:320-326: in_discards, and never counted
 				 * as received nor handed to the CoS queue */
@@ -2325,6 +2530,11 @@ static void rx_deliver(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, odp_packet_
 		run[nrun++] = pkt;
 	}
 	cos_enq(run_cos, run_q, run, nrun);
+	odp_packet_free_multi(dead, ndead);
+	/* buffers taken and not used (longer packets, errors) go back */
+	for (uint32_t k = used; k < nfresh; k++)
+		pkt_init(fresh[k], p->pool, 0);
+	odp_packet_free_multi((const odp_packet_t *)fresh + used, (int)(nfresh - used));
 	s->n = 0;
 }
 
@@ -2376,9 +2586,13 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 /* a delivered burst's packets without a CoS queue onto the pktin event queue */
 static void to_inq(rt_pktio_t *p, odp_packet_t pkts[], int nret)
 {
+	const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
+
 	if (nret > 0 && (!p->inq || odp_queue_enq_multi(p->inq->hdl, (const odp_event_t *)pkts,
 							 nret) != nret))
 		odp_packet_free_multi(pkts, nret);
+	if (rxprof.on > 0)
+		rxprof.enq_ns += prof_ns() - t0;
 }
 
 /* QUEUE / SCHED mode: deliver the completed bursts (all of them with

@@ -299,8 +299,15 @@ int main(void)
 		memset(odp_packet_data(big), 1, 4000);
 		CHECK(odp_packet_alloc(churn_pool, 64) == ODP_PACKET_INVALID, "num limit with a long packet");
 		odp_packet_free(big);
-		for (int k = 0; k < n; k++)
-			odp_packet_free(all[k]);
+		/* freed in one pass (the cache filled, the rest onto the stack),
+		 * every one allocatable again */
+		odp_packet_free_multi(all, n);
+		int m = 0;
+
+		while (m < n && (all[m] = odp_packet_alloc(churn_pool, 64)) != ODP_PACKET_INVALID)
+			m++;
+		CHECK(m == n, "after odp_packet_free_multi: %d of %d packets", m, n);
+		odp_packet_free_multi(all, m);
 		odp_packet_t stale = odp_packet_alloc(churn_pool, 64);
 
 		CHECK(odp_pool_destroy(churn_pool) == 0, "pool destroy");
