@@ -223,7 +223,11 @@ typedef struct rt_pktio {
 	rt_pkt_t *ahead, *ahead_tail;  /* DIRECT mode: received (classified) packets
 				    * beyond what the last odp_pktin_recv asked for */
 	struct rx_slot *slot[RT_INFLIGHT];  /* receive bursts ("receive pipeline") */
-	uint32_t rx_head, rx_count;  /* the bursts in flight: slots rx_head.. */
+	/* bursts launched / delivered (wrapping counts): the ones in flight
+	 * sit in slots delivered .. launched - 1 (mod RT_INFLIGHT). launched
+	 * moves under rt.poll_lock, delivered under rx_dlock[] (receive
+	 * pipeline: one thread launches while another delivers) */
+	uint32_t launched, delivered;
 } rt_pktio_t;
 
 #define LOOP_MTU 65535u            /* LOOP_MTU_MAX (pktio/loop.c:45) */
@@ -240,6 +244,13 @@ static struct {
 	int polling;               /* a thread is in poll_input */
 } rt = { PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, 0, NULL, {{0}}, {{0}},
 	 NULL, 0, 0 };
+
+/* a pktio's delivery side (receive pipeline), outside the pktio object so
+ * that close can hold it across the object's reset; lock order: poll_lock,
+ * then rx_dlock */
+static pthread_mutex_t rx_dlock[RT_MAX_PKTIO] = { [0 ... RT_MAX_PKTIO - 1] =
+							   PTHREAD_MUTEX_INITIALIZER };
+static int rx_dbusy[RT_MAX_PKTIO];
 
 /* pinned host memory and its device address (zero-copy launch buffers) */
 static int pinned_alloc(size_t bytes, void **host, void **dev)
@@ -327,8 +338,11 @@ int odp_term_global(odp_instance_t instance)
 			rxprof.post_ns / 1e3 / rxprof.bursts, rxprof.end_ns / 1e3 / rxprof.bursts,
 			rxprof.enq_ns / 1e3 / rxprof.bursts);
 	pthread_mutex_lock(&rt.poll_lock);
-	for (int i = 0; i < RT_MAX_PKTIO; i++)
+	for (int i = 0; i < RT_MAX_PKTIO; i++) {
+		pthread_mutex_lock(&rx_dlock[i]);
 		rx_release(&rt.pktio[i]);
+		pthread_mutex_unlock(&rx_dlock[i]);
+	}
 	pthread_mutex_unlock(&rt.poll_lock);
 	pthread_mutex_lock(&rt.lock);
 	if (rt.init) {
@@ -2168,6 +2182,7 @@ void odpg_rt_pktio_close(odp_pktio_t hdl)
 	rt_pktio_t *p = get_rt_pktio(hdl);
 
 	if (p) {
+		pthread_mutex_lock(&rx_dlock[p - rt.pktio]);
 		if (p->have_cap)
 			odpg_pcap_free(&p->cap);
 		pktio_queue_kill(&p->inq);
@@ -2183,6 +2198,7 @@ void odpg_rt_pktio_close(odp_pktio_t hdl)
 		rx_release(p);
 		pthread_mutex_destroy(&p->ring_lock);
 		memset(p, 0, sizeof(*p));
+		pthread_mutex_unlock(&rx_dlock[p - rt.pktio]);
 	}
 	pthread_mutex_unlock(&rt.poll_lock);
 }
@@ -2301,7 +2317,7 @@ static void slots_free(rt_pktio_t *p)
 		free(s);
 		p->slot[i] = NULL;
 	}
-	p->rx_head = p->rx_count = 0;
+	p->launched = p->delivered = 0;
 }
 
 static void rx_drop(struct rx_slot *s);
@@ -2310,15 +2326,13 @@ static void rx_drop(struct rx_slot *s);
  * termination) */
 static void rx_release(rt_pktio_t *p)
 {
-	while (p->rx_count) {
-		rx_slot_t *s = p->slot[p->rx_head];
+	for (; p->delivered != p->launched; p->delivered++) {
+		rx_slot_t *s = p->slot[p->delivered % RT_INFLIGHT];
 
 		odpg_fence_wait(s->fence);
 		odpg_cls_pktio_recv_end(s->token);
 		s->token = NULL;
 		rx_drop(s);
-		p->rx_head = (p->rx_head + 1u) % RT_INFLIGHT;
-		p->rx_count--;
 	}
 	slots_free(p);
 }
@@ -2460,17 +2474,17 @@ static void rx_deliver(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, odp_packet_
 		const uint32_t len = s->desc[k].len;
 		rt_pkt_t *have = s->src[k];
 
-		/* the headers' lines were last written on the transmitting
-		 * cores: their ownership requested ahead, not one at a time */
-		if (k + RX_PF < s->n && s->src[k + RX_PF])
+		/* the lines this touches were last written on other cores (the
+		 * transmitting threads' headers, the receiving threads' freed
+		 * buffers): their ownership requested ahead, not one at a time */
+		if (k + RX_PF < s->n && s->src[k + RX_PF]) {
 			__builtin_prefetch(s->src[k + RX_PF], 1, 3);
-		/* and the GPU-written verdicts / metadata (pinned host lines
-		 * the device wrote: not in any CPU cache) */
-		if ((k & 7u) == 0 && k + 4u * RX_PF < s->n) {
-			__builtin_prefetch(&s->meta[k + 4u * RX_PF], 0, 3);
-			__builtin_prefetch(&s->meta[k + 4u * RX_PF + 4u], 0, 3);
-			__builtin_prefetch(&s->out[k + 4u * RX_PF], 0, 3);
-			__builtin_prefetch(&s->desc[k + 4u * RX_PF], 0, 3);
+			__builtin_prefetch((uint8_t *)s->src[k + RX_PF] + 64, 1, 3);
+		}
+		if (used + RX_PF < nfresh) {
+			__builtin_prefetch(fresh[used + RX_PF], 1, 3);
+			__builtin_prefetch((uint8_t *)fresh[used + RX_PF] + 64, 1, 3);
+			__builtin_prefetch(fresh[used + RX_PF]->data, 1, 3);
 		}
 		odp_cos_t cos = ODP_COS_INVALID;
 		odp_queue_t q = ODP_QUEUE_INVALID;
@@ -2541,11 +2555,12 @@ static void rx_deliver(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, odp_packet_
 static void prof_add(uint64_t bursts, uint64_t pkts, uint64_t t0, uint64_t t1, uint64_t t2,
 		     uint64_t t3)
 {
-	rxprof.bursts += bursts;
-	rxprof.pkts += pkts;
-	rxprof.stage_ns += t1 - t0;
-	rxprof.gpu_ns += t2 - t1;
-	rxprof.post_ns += t3 - t2;
+	/* the launch and delivery sides count from different threads */
+	__atomic_fetch_add(&rxprof.bursts, bursts, __ATOMIC_RELAXED);
+	__atomic_fetch_add(&rxprof.pkts, pkts, __ATOMIC_RELAXED);
+	__atomic_fetch_add(&rxprof.stage_ns, t1 - t0, __ATOMIC_RELAXED);
+	__atomic_fetch_add(&rxprof.gpu_ns, t2 - t1, __ATOMIC_RELAXED);
+	__atomic_fetch_add(&rxprof.post_ns, t3 - t2, __ATOMIC_RELAXED);
 }
 
 /* DIRECT mode: one burst, launched and waited for. Returns the frames taken
@@ -2600,15 +2615,13 @@ static void to_inq(rt_pktio_t *p, odp_packet_t pkts[], int nret)
  * RT_BURST / 4 frames while another is in flight, so that launches stay
  * few at high rates and latency stays one launch at low ones. Returns the
  * frames delivered or launched (0: nothing to do) */
-static int rx_to_inq(rt_pktio_t *p, odp_pktio_t hdl, int drain)
+static int rx_deliver_done(rt_pktio_t *p, odp_pktio_t hdl, int drain)
 {
 	odp_packet_t pkts[RT_BURST];
 	int got = 0;
 
-	if (!rt.init)
-		return 0;
-	while (p->rx_count) {
-		rx_slot_t *s = p->slot[p->rx_head];
+	for (uint32_t d = p->delivered; d != __atomic_load_n(&p->launched, __ATOMIC_ACQUIRE); d++) {
+		rx_slot_t *s = p->slot[d % RT_INFLIGHT];
 		int nret = 0;
 
 		const int fs = drain ? (odpg_fence_wait(s->fence) ? -1 : 1) : odpg_fence_query(s->fence);
@@ -2621,25 +2634,34 @@ static int rx_to_inq(rt_pktio_t *p, odp_pktio_t hdl, int drain)
 			odpg_cls_pktio_recv_end(s->token);
 			s->token = NULL;
 			rx_drop(s);
-			p->rx_head = (p->rx_head + 1u) % RT_INFLIGHT;
-			p->rx_count--;
-			continue;
-		}
-		const uint64_t t2 = rxprof.on > 0 ? prof_ns() : 0;
+		} else {
+			const uint64_t t2 = rxprof.on > 0 ? prof_ns() : 0;
 
-		got += (int)s->n;
-		rx_deliver(p, hdl, s, pkts, &nret);
-		to_inq(p, pkts, nret);
-		if (rxprof.on > 0)
-			prof_add(0, 0, t2, t2, t2, prof_ns());
-		p->rx_head = (p->rx_head + 1u) % RT_INFLIGHT;
-		p->rx_count--;
+			got += (int)s->n;
+			rx_deliver(p, hdl, s, pkts, &nret);
+			to_inq(p, pkts, nret);
+			if (rxprof.on > 0)
+				prof_add(0, 0, t2, t2, t2, prof_ns());
+		}
+		__atomic_store_n(&p->delivered, d + 1u, __ATOMIC_RELEASE);
 	}
-	while (!drain && p->rx_count < RT_INFLIGHT && odpg_cls_pktio_started(hdl)) {
-		if (p->loopdev && p->rx_count &&
-		    __atomic_load_n(&p->ring.n, __ATOMIC_RELAXED) < RT_BURST / 4u)
+	return got;
+}
+
+/* the launch side (rt.poll_lock held): stage and launch while slots are
+ * free and frames wait */
+static int rx_launch_more(rt_pktio_t *p, odp_pktio_t hdl)
+{
+	int got = 0;
+
+	while (odpg_cls_pktio_started(hdl)) {
+		const uint32_t l = p->launched;
+		const uint32_t inflight = l - __atomic_load_n(&p->delivered, __ATOMIC_ACQUIRE);
+
+		if (inflight >= RT_INFLIGHT ||
+		    (p->loopdev && inflight && __atomic_load_n(&p->ring.n, __ATOMIC_RELAXED) < RT_BURST / 4u))
 			break;
-		rx_slot_t *s = slot_get(p, (p->rx_head + p->rx_count) % RT_INFLIGHT);
+		rx_slot_t *s = slot_get(p, l % RT_INFLIGHT);
 
 		if (!s)
 			break;
@@ -2657,9 +2679,25 @@ static int rx_to_inq(rt_pktio_t *p, odp_pktio_t hdl, int drain)
 
 			prof_add(1, n, t0, t1, t2, t2);
 		}
-		p->rx_count++;
+		__atomic_store_n(&p->launched, l + 1u, __ATOMIC_RELEASE);
 		got += (int)n;
 	}
+	return got;
+}
+
+/* both sides in one thread (rt.poll_lock held): QUEUE-mode fill, drain */
+static int rx_to_inq(rt_pktio_t *p, odp_pktio_t hdl, int drain)
+{
+	const uint32_t i = (uint32_t)(p - rt.pktio);
+	int got;
+
+	if (!rt.init)
+		return 0;
+	pthread_mutex_lock(&rx_dlock[i]);
+	got = rx_deliver_done(p, hdl, drain);
+	pthread_mutex_unlock(&rx_dlock[i]);
+	if (!drain)
+		got += rx_launch_more(p, hdl);
 	return got;
 }
 
@@ -2691,19 +2729,33 @@ static int poll_input(void)
 {
 	int got = 0;
 
-	/* another thread polls: its flag is read, not the lock's line written */
-	if (__atomic_load_n(&rt.polling, __ATOMIC_RELAXED) || pthread_mutex_trylock(&rt.poll_lock))
+	if (!rt.init)
 		return 0;
-	__atomic_store_n(&rt.polling, 1, __ATOMIC_RELAXED);
-	for (int i = 0; i < RT_MAX_PKTIO && rt.init; i++) {
+	/* the delivery side: one thread per pktio, the bursts in order (the
+	 * counts and busy flag are read first, not the lock's line written) */
+	for (int i = 0; i < RT_MAX_PKTIO; i++) {
 		rt_pktio_t *p = &rt.pktio[i];
 
-		if (!p->valid || p->in_mode != ODP_PKTIN_MODE_SCHED)
+		if (!p->valid || p->in_mode != ODP_PKTIN_MODE_SCHED ||
+		    __atomic_load_n(&p->launched, __ATOMIC_RELAXED) ==
+			    __atomic_load_n(&p->delivered, __ATOMIC_RELAXED) ||
+		    __atomic_load_n(&rx_dbusy[i], __ATOMIC_RELAXED) || pthread_mutex_trylock(&rx_dlock[i]))
 			continue;
-		const int took = rx_to_inq(p, (odp_pktio_t)(uintptr_t)(i + 1), 0);
+		__atomic_store_n(&rx_dbusy[i], 1, __ATOMIC_RELAXED);
+		if (p->valid && p->in_mode == ODP_PKTIN_MODE_SCHED)   /* not closed meanwhile */
+			got += rx_deliver_done(p, (odp_pktio_t)(uintptr_t)(i + 1), 0);
+		__atomic_store_n(&rx_dbusy[i], 0, __ATOMIC_RELAXED);
+		pthread_mutex_unlock(&rx_dlock[i]);
+	}
+	/* the launch side: another thread at the same time */
+	if (__atomic_load_n(&rt.polling, __ATOMIC_RELAXED) || pthread_mutex_trylock(&rt.poll_lock))
+		return got;
+	__atomic_store_n(&rt.polling, 1, __ATOMIC_RELAXED);
+	for (int i = 0; i < RT_MAX_PKTIO; i++) {
+		rt_pktio_t *p = &rt.pktio[i];
 
-		if (took > 0)
-			got += took;
+		if (p->valid && p->in_mode == ODP_PKTIN_MODE_SCHED)
+			got += rx_launch_more(p, (odp_pktio_t)(uintptr_t)(i + 1));
 	}
 	__atomic_store_n(&rt.polling, 0, __ATOMIC_RELAXED);
 	pthread_mutex_unlock(&rt.poll_lock);
