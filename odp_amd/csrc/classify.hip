@@ -623,7 +623,7 @@ __global__ __launch_bounds__(BLOCK, LEAN ? LEAN_WAVES : FAST ? 5 : GEN_WAVES) vo
 		const uint64_t pm = __ballot(ret == PARSE_PEND);
 
 		if (pm) {
-			const uint32_t tail = seg_tail_sums4(pm, g, pd);
+			const uint32_t tail = seg_tail_sums4<false>(pm, g, pd);
 
 			if (ret == PARSE_PEND)
 				ret = finish_l4(p, pd, tail, opt);

@@ -427,6 +427,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			  (threadIdx.x >> 6) * 64u;
 
 	const uint32_t lane = __lane_id();
+	constexpr bool XW = NW > 2;     /* line-shaped window loads (load_win) */
 	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (GF_BLOCK / 64) +
 							   (threadIdx.x >> 6));
 	const uint32_t nwaves = gridDim.x * (GF_BLOCK / 64);
@@ -443,23 +444,44 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		return make_uint2(0u, 0u);
 	};
 	/* a frame's first 64 bytes (16-byte chunks holding frame bytes only: the
-	 * chunk with the last byte is masked), and its dword at byte 64 */
+	 * chunk with the last byte is masked), and its dword at byte 64. Wide
+	 * hit maps (NW > 2, the C3 launches): line-shaped, instruction k loads
+	 * frames 16k .. 16k + 15 of the tile, four lanes a frame (its 16-byte
+	 * chunk lane & 3), so that one instruction touches 16 lines instead of
+	 * 64 (TA / L1 request slots, not bytes, bound the C3 loads: 98.6 ->
+	 * 92.9 us with the tail passes' line-shaped loads); the tile loop puts
+	 * the chunks through the frames' LDS rows. The 2-word instantiation
+	 * (C2x) keeps lane-per-frame loads: it has no registers for the
+	 * transposition (45.0 vs 39.7 us, spilled) */
 	auto load_win = [&](uint32_t (&f)[16], uint32_t &x16, uint2 d) __attribute__((always_inline)) {
-		const uint8_t *g = A.frames + d.x;
-		const uint32_t len = d.y;
-
+		if constexpr (XW) {
 #pragma unroll
-		for (int q = 0; q < 4; ++q) {
-			uint4 x = make_uint4(0u, 0u, 0u, 0u);
+			for (int k = 0; k < 4; ++k) {
+				const uint32_t src = 16u * k + (lane >> 2), c = lane & 3u;
+				const uint32_t off = lane_pull(d.x, src), ln = lane_pull(d.y, src);
+				uint4 x = make_uint4(0u, 0u, 0u, 0u);
 
-			if (16u * q < len)
-				x = *(const uint4 *)(g + 16u * q);
-			f[4 * q + 0] = x.x;
-			f[4 * q + 1] = x.y;
-			f[4 * q + 2] = x.z;
-			f[4 * q + 3] = x.w;
+				if (16u * c < ln)
+					x = *(const uint4 *)(A.frames + off + 16u * c);
+				f[4 * k + 0] = x.x;
+				f[4 * k + 1] = x.y;
+				f[4 * k + 2] = x.z;
+				f[4 * k + 3] = x.w;
+			}
+		} else {
+#pragma unroll
+			for (int q = 0; q < 4; ++q) {
+				uint4 x = make_uint4(0u, 0u, 0u, 0u);
+
+				if (16u * q < d.y)
+					x = *(const uint4 *)(A.frames + d.x + 16u * q);
+				f[4 * q + 0] = x.x;
+				f[4 * q + 1] = x.y;
+				f[4 * q + 2] = x.z;
+				f[4 * q + 3] = x.w;
+			}
 		}
-		x16 = len > 64u ? *(const uint32_t *)(g + 64u) : 0u;
+		x16 = d.y > 64u ? *(const uint32_t *)(A.frames + d.x + 64u) : 0u;
 	};
 	uint32_t fn[16] = {}, xn = 0u;
 	uint2 dn = load_desc(gw), dnn;
@@ -479,7 +501,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			return 0u;
 		const L4Pend q = {0u, 0u, 64u, len};
 
-		return seg_tail_sums4(m, A.frames + d.x, q, marks);
+		return seg_tail_sums4<XW>(m, A.frames + d.x, q, marks);
 	};
 	uint32_t tn = 0u;
 
@@ -549,6 +571,26 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		uint32_t f[16];
 		uint32_t x16 = xn;
 		uint32_t tile_oct = 0u;  /* CM 2: octets this lane hands over */
+		if constexpr (XW) {
+			/* the staged chunks into the frames' rows, then each lane's
+			 * own row back (a wave's LDS operations complete in order) */
+			uint32_t *wrow = smem + (threadIdx.x - lane) * RW;
+
+#pragma unroll
+			for (int k = 0; k < 4; ++k)
+				*(uint4 *)(wrow + (16u * k + (lane >> 2)) * RW + 4u * (lane & 3u)) =
+					make_uint4(fn[4 * k], fn[4 * k + 1], fn[4 * k + 2], fn[4 * k + 3]);
+			__asm__ volatile("" ::: "memory");
+#pragma unroll
+			for (int q = 0; q < 16; q += 4) {
+				const uint4 x = *(const uint4 *)(row + q);
+
+				fn[q] = x.x;
+				fn[q + 1] = x.y;
+				fn[q + 2] = x.z;
+				fn[q + 3] = x.w;
+			}
+		}
 
 		if (__ballot(live && len < 64u)) {
 #pragma unroll

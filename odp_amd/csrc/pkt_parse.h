@@ -716,6 +716,7 @@ __device__ __forceinline__ uint32_t unit_sum_end(uint64_t addr, uint32_t re)
 	return acc;
 }
 
+template <bool XP = true>
 __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g, const L4Pend &pd,
 						uint32_t *marks = nullptr)
 {
@@ -807,12 +808,32 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 	auto consume = [&](const uint4 (&q)[4], uint32_t base) __attribute__((always_inline)) {
 		uint32_t s = 0u;
 
+		if constexpr (XP) {
+			/* each instruction's chunk sums, added over the unit's quad
+			 * of lanes; lane 4j + m keeps unit 16m + j's, which lane
+			 * 16m + j then takes */
+			uint32_t t = 0u;
+
 #pragma unroll
-		for (int k = 0; k < 4; ++k) {
-			s = tail_dot2(q[k].x, s);
-			s = tail_dot2(q[k].y, s);
-			s = tail_dot2(q[k].z, s);
-			s = tail_dot2(q[k].w, s);
+			for (int k = 0; k < 4; ++k) {
+				uint32_t c = tail_dot2(q[k].x, 0u);
+
+				c = tail_dot2(q[k].y, c);
+				c = tail_dot2(q[k].z, c);
+				c = tail_dot2(q[k].w, c);
+				c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xf, 0xf, false);
+				c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xf, 0xf, false);
+				t = (lane & 3u) == (uint32_t)k ? c : t;
+			}
+			s = lane_pull(t, 4u * (lane & 15u) + (lane >> 4));
+		} else {
+#pragma unroll
+			for (int k = 0; k < 4; ++k) {
+				s = tail_dot2(q[k].x, s);
+				s = tail_dot2(q[k].y, s);
+				s = tail_dot2(q[k].z, s);
+				s = tail_dot2(q[k].w, s);
+			}
 		}
 		const uint32_t ps = wave_scan_u32(base + lane < total ? oc_fold(s) : 0u);
 		const bool in = ni && incl > base && first < base + 64u;
@@ -823,10 +844,26 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 
 		acc += in ? hv - (fl ? lv : 0u) : 0u;
 	};
+	/* line-shaped loads: instruction k reads the 16 units 16k .. 16k + 15 of
+	 * the pass, four lanes a unit (16 bytes each), so that its 1 KiB covers
+	 * whole 128-byte lines of a frame instead of a quarter of 32 lines
+	 * (XP; otherwise a lane reads its own unit: fewer registers) */
 	auto load = [&](uint4 (&q)[4], uint64_t a) __attribute__((always_inline)) {
+		if constexpr (XP) {
+			const uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32);
+
 #pragma unroll
-		for (int k = 0; k < 4; ++k)
-			q[k] = ld_g16(a + 16u * k);
+			for (int k = 0; k < 4; ++k) {
+				const uint32_t src = 16u * k + (lane >> 2);
+
+				q[k] = ld_g16((((uint64_t)lane_pull(ahi, src) << 32) | lane_pull(alo, src)) +
+					      16u * (lane & 3u));
+			}
+		} else {
+#pragma unroll
+			for (int k = 0; k < 4; ++k)
+				q[k] = ld_g16(a + 16u * k);
+		}
 	};
 	uint64_t addr = total ? owner(0u) : 0ull;
 	uint4 qa[4], qb[4];
