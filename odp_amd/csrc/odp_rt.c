@@ -55,6 +55,7 @@
 #define RT_MAX_POOL  64
 #define RT_BURST     1024
 #define RX_PF        8         /* packets prefetched ahead in staging / delivery */
+#define RX_CHUNK     128       /* packets a delivering thread takes at a time */
 #define RT_INFLIGHT  4              /* receive bursts in flight per pktio */
 
 /* ---- objects -------------------------------------------------------------- */
@@ -201,6 +202,16 @@ typedef struct rx_slot {
 	odpg_meta_t *meta, *dmeta;
 	odpg_fence_t *fence;       /* behind the burst's launch */
 	void *token;               /* the launch's binding (odpg_cls_pktio_recv_end) */
+	/* delivery in chunks (receive pipeline): the burst's launch count
+	 * (seq) and next unclaimed chunk packed in one word, so that a thread
+	 * holding an old count cannot claim from a reused slot; chunks hand
+	 * their packets to the queues in order (commit); busy counts the
+	 * threads inside, which a launch into the slot waits out */
+	uint32_t open;             /* 1 while its chunks are being delivered */
+	uint32_t nchunks;
+	uint64_t claimw;           /* seq << 32 | next chunk */
+	uint32_t commit;           /* chunks handed over */
+	uint32_t busy;
 } rx_slot_t;
 
 typedef struct rt_pktio {
@@ -251,6 +262,13 @@ static struct {
 static pthread_mutex_t rx_dlock[RT_MAX_PKTIO] = { [0 ... RT_MAX_PKTIO - 1] =
 							   PTHREAD_MUTEX_INITIALIZER };
 static int rx_dbusy[RT_MAX_PKTIO];
+static uint32_t rx_helpers[RT_MAX_PKTIO];   /* threads in a pktio's delivery side */
+
+/* a spin-wait's pause */
+static inline void cpu_relax(void)
+{
+	__builtin_ia32_pause();
+}
 
 /* pinned host memory and its device address (zero-copy launch buffers) */
 static int pinned_alloc(size_t bytes, void **host, void **dev)
@@ -2183,6 +2201,12 @@ void odpg_rt_pktio_close(odp_pktio_t hdl)
 
 	if (p) {
 		pthread_mutex_lock(&rx_dlock[p - rt.pktio]);
+		/* no new delivering thread looks at the pktio; those inside
+		 * finish their chunks (the bursts in flight are dropped or, when
+		 * opened, delivered by rx_release) */
+		__atomic_store_n(&p->valid, 0, __ATOMIC_SEQ_CST);
+		while (__atomic_load_n(&rx_helpers[p - rt.pktio], __ATOMIC_SEQ_CST))
+			cpu_relax();
 		if (p->have_cap)
 			odpg_pcap_free(&p->cap);
 		pktio_queue_kill(&p->inq);
@@ -2324,16 +2348,36 @@ static void rx_drop(struct rx_slot *s);
 
 /* the bursts in flight waited for and dropped, the slots freed (close,
  * termination) */
+static int rx_help(rt_pktio_t *p, odp_pktio_t hdl);
+
 static void rx_release(rt_pktio_t *p)
 {
-	for (; p->delivered != p->launched; p->delivered++) {
-		rx_slot_t *s = p->slot[p->delivered % RT_INFLIGHT];
+	while (p->delivered != p->launched) {
+		const uint32_t d = p->delivered;
+		rx_slot_t *s = p->slot[d % RT_INFLIGHT];
 
+		if (__atomic_load_n(&s->open, __ATOMIC_ACQUIRE)) {
+			if ((uint32_t)(__atomic_load_n(&s->claimw, __ATOMIC_ACQUIRE) >> 32) == d) {
+				/* partly delivered: the rest goes out too */
+				rx_help(p, (odp_pktio_t)(uintptr_t)(p - rt.pktio + 1));
+				while (__atomic_load_n(&p->delivered, __ATOMIC_ACQUIRE) == d)
+					cpu_relax();
+			} else {
+				/* the slot's previous burst still closing */
+				while (__atomic_load_n(&s->open, __ATOMIC_ACQUIRE))
+					cpu_relax();
+			}
+			continue;
+		}
 		odpg_fence_wait(s->fence);
 		odpg_cls_pktio_recv_end(s->token);
 		s->token = NULL;
 		rx_drop(s);
+		__atomic_store_n(&p->delivered, d + 1u, __ATOMIC_RELEASE);
 	}
+	for (uint32_t i = 0; i < RT_INFLIGHT; i++)
+		while (p->slot[i] && __atomic_load_n(&p->slot[i]->busy, __ATOMIC_ACQUIRE))
+			cpu_relax();
 	slots_free(p);
 }
 
@@ -2440,36 +2484,39 @@ static int rx_launch(odp_pktio_t hdl, rx_slot_t *s)
 	return 0;
 }
 
-/* a completed burst: verdicts to CoS queues and pools; packets without a
- * CoS queue go to pkts[] */
-static void rx_deliver(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, odp_packet_t pkts[],
-		       int *nret)
+/* what a range's delivery hands to the queues, in packet order */
+typedef struct rx_out {
+	int ninq, nq;
+	odp_packet_t inq[RX_CHUNK];        /* no CoS queue: the pktin queue / caller */
+	odp_packet_t qp[RX_CHUNK];         /* to a CoS queue */
+	odp_cos_t qcos[RX_CHUNK];
+	odp_queue_t qq[RX_CHUNK];
+} rx_out_t;
+
+/* packets [k0, k1) of a completed burst (k1 - k0 <= RX_CHUNK): verdicts to
+ * pools, the packets for the queues into *o (handed over by rx_commit, in
+ * chunk order); what is dropped is freed here */
+static void rx_deliver_range(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, uint32_t k0,
+			     uint32_t k1, rx_out_t *o)
 {
-	odp_packet_t run[RT_BURST], dead[RT_BURST];
-	rt_pkt_t *fresh[RT_BURST];
-	int nrun = 0, ndead = 0;
+	odp_packet_t dead[RX_CHUNK];
+	rt_pkt_t *fresh[RX_CHUNK];
+	int ndead = 0;
 	uint32_t want = 0, nfresh = 0, used = 0;
-	odp_cos_t run_cos = ODP_COS_INVALID;
-	odp_queue_t run_q = ODP_QUEUE_INVALID;
 	const rt_pool_t *own = get_pool(p->pool);
 
-	const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
-
-	odpg_cls_pktio_recv_end(s->token);
-	s->token = NULL;
-	if (rxprof.on > 0)
-		rxprof.end_ns += prof_ns() - t0;
+	o->ninq = o->nq = 0;
 	/* the packets without a CoS that land in the pktio's pool from
 	 * elsewhere (a capture's frames; the loop device's packets from a
 	 * separate transmit pool, loop.c's _odp_pktio_packet_to_pool): their
 	 * buffers in one take, the originals freed in one pass at the end */
-	for (uint32_t k = 0; k < s->n; k++)
+	for (uint32_t k = k0; k < k1; k++)
 		if (ODPG_OUT_COS(s->out[k]) == ODPG_COS_NOCLS &&
 		    (!s->src[k] || s->src[k]->pool != p->pool))
 			want++;
 	if (want && own)
 		nfresh = pool_take(p->pool, fresh, want);
-	for (uint32_t k = 0; k < s->n; k++) {
+	for (uint32_t k = k0; k < k1; k++) {
 		const uint32_t w = s->out[k];
 		const uint32_t len = s->desc[k].len;
 		rt_pkt_t *have = s->src[k];
@@ -2477,7 +2524,7 @@ static void rx_deliver(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, odp_packet_
 		/* the lines this touches were last written on other cores (the
 		 * transmitting threads' headers, the receiving threads' freed
 		 * buffers): their ownership requested ahead, not one at a time */
-		if (k + RX_PF < s->n && s->src[k + RX_PF]) {
+		if (k + RX_PF < k1 && s->src[k + RX_PF]) {
 			__builtin_prefetch(s->src[k + RX_PF], 1, 3);
 			__builtin_prefetch((uint8_t *)s->src[k + RX_PF] + 64, 1, 3);
 		}
@@ -2495,7 +2542,7 @@ static void rx_deliver(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, odp_packet_
 			q = dest_queue(w, &cos);
 			if (q == ODP_QUEUE_INVALID) {
 				if (have)                 /* no CoS / drop / parse drop */
-					odp_packet_free((odp_packet_t)have);
+					dead[ndead++] = (odp_packet_t)have;
 				continue;
 			}
 			if (odp_cls_cos_pool(cos) != ODP_POOL_INVALID)
@@ -2531,24 +2578,57 @@ static void rx_deliver(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, odp_packet_
 		PK(pkt)->cos = cos;
 		PK(pkt)->input = hdl;
 		if (q == ODP_QUEUE_INVALID) {
-			pkts[(*nret)++] = pkt;
-			continue;
+			o->inq[o->ninq++] = pkt;
+		} else {
+			o->qp[o->nq] = pkt;
+			o->qcos[o->nq] = cos;
+			o->qq[o->nq++] = q;
 		}
-		/* _odp_cls_enq: runs of the same (CoS, queue) */
-		if (nrun && (q != run_q || cos != run_cos)) {
-			cos_enq(run_cos, run_q, run, nrun);
-			nrun = 0;
-		}
-		run_cos = cos;
-		run_q = q;
-		run[nrun++] = pkt;
 	}
-	cos_enq(run_cos, run_q, run, nrun);
-	odp_packet_free_multi(dead, ndead);
+	if (ndead)
+		odp_packet_free_multi(dead, ndead);
 	/* buffers taken and not used (longer packets, errors) go back */
 	for (uint32_t k = used; k < nfresh; k++)
 		pkt_init(fresh[k], p->pool, 0);
 	odp_packet_free_multi((const odp_packet_t *)fresh + used, (int)(nfresh - used));
+}
+
+static void to_inq(rt_pktio_t *p, odp_packet_t pkts[], int nret);
+
+/* a range's packets to their queues: runs of the same (CoS, queue) in one
+ * enqueue each (_odp_cls_enq), the rest to the pktin queue, or to out[]
+ * (DIRECT mode, *nret advanced) */
+static void rx_commit(rt_pktio_t *p, rx_out_t *o, odp_packet_t out[], int *nret)
+{
+	for (int i = 0; i < o->nq;) {
+		int j = i + 1;
+
+		while (j < o->nq && o->qq[j] == o->qq[i] && o->qcos[j] == o->qcos[i])
+			j++;
+		cos_enq(o->qcos[i], o->qq[i], &o->qp[i], j - i);
+		i = j;
+	}
+	if (out) {
+		memcpy(out + *nret, o->inq, (size_t)o->ninq * sizeof(*out));
+		*nret += o->ninq;
+	} else {
+		to_inq(p, o->inq, o->ninq);
+	}
+}
+
+/* a completed burst delivered by this thread alone (DIRECT mode): the
+ * binding released, the ranges handed over in order */
+static void rx_deliver(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, odp_packet_t pkts[],
+		       int *nret)
+{
+	rx_out_t o;
+
+	odpg_cls_pktio_recv_end(s->token);
+	s->token = NULL;
+	for (uint32_t k0 = 0; k0 < s->n; k0 += RX_CHUNK) {
+		rx_deliver_range(p, hdl, s, k0, k0 + RX_CHUNK < s->n ? k0 + RX_CHUNK : s->n, &o);
+		rx_commit(p, &o, pkts, nret);
+	}
 	s->n = 0;
 }
 
@@ -2610,40 +2690,127 @@ static void to_inq(rt_pktio_t *p, odp_packet_t pkts[], int nret)
 		rxprof.enq_ns += prof_ns() - t0;
 }
 
-/* QUEUE / SCHED mode: deliver the completed bursts (all of them with
- * `drain`, waiting), then launch what has arrived. A new burst waits for
- * RT_BURST / 4 frames while another is in flight, so that launches stay
- * few at high rates and latency stays one launch at low ones. Returns the
- * frames delivered or launched (0: nothing to do) */
-static int rx_deliver_done(rt_pktio_t *p, odp_pktio_t hdl, int drain)
+/* QUEUE / SCHED mode, the delivery side. A burst whose fence has completed
+ * is opened (rx_open, under rx_dlock: one thread) and then delivered in
+ * chunks of RX_CHUNK packets by every thread that polls (rx_help, no lock):
+ * a thread claims the next chunk, classifies its packets into pools
+ * (rx_deliver_range), waits for the chunks before it to reach their queues
+ * and hands its own over (rx_commit), so queue order is packet order. The
+ * thread handing over the last chunk moves `delivered` on. */
+
+/* the oldest burst in flight opened for delivery, if its fence has
+ * completed (waited for with `drain`); a failed launch's burst is dropped.
+ * Returns 1 when the oldest burst is open (now or before), else 0 */
+static int rx_open(rt_pktio_t *p, int drain)
 {
-	odp_packet_t pkts[RT_BURST];
-	int got = 0;
+	for (;;) {
+		const uint32_t d = p->delivered;
 
-	for (uint32_t d = p->delivered; d != __atomic_load_n(&p->launched, __ATOMIC_ACQUIRE); d++) {
+		if (d == __atomic_load_n(&p->launched, __ATOMIC_ACQUIRE))
+			return 0;
 		rx_slot_t *s = p->slot[d % RT_INFLIGHT];
-		int nret = 0;
 
+		if (__atomic_load_n(&s->open, __ATOMIC_ACQUIRE)) {
+			if ((uint32_t)(__atomic_load_n(&s->claimw, __ATOMIC_ACQUIRE) >> 32) == d)
+				return 1;
+			/* the slot's previous burst is still being closed (its
+			 * last chunk's thread clears `open` after moving
+			 * `delivered` on) */
+			if (!drain)
+				return 0;
+			while (__atomic_load_n(&s->open, __ATOMIC_ACQUIRE))
+				cpu_relax();
+			continue;
+		}
 		const int fs = drain ? (odpg_fence_wait(s->fence) ? -1 : 1) : odpg_fence_query(s->fence);
 
 		if (fs == 0)
-			break;
+			return 0;
+		const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
+
+		odpg_cls_pktio_recv_end(s->token);
+		s->token = NULL;
+		if (rxprof.on > 0)
+			rxprof.end_ns += prof_ns() - t0;
 		if (fs < 0) {
 			/* the launch failed: its verdicts were never written */
 			ERR("receive burst failed on the GPU: dropped\n");
-			odpg_cls_pktio_recv_end(s->token);
-			s->token = NULL;
 			rx_drop(s);
-		} else {
-			const uint64_t t2 = rxprof.on > 0 ? prof_ns() : 0;
-
-			got += (int)s->n;
-			rx_deliver(p, hdl, s, pkts, &nret);
-			to_inq(p, pkts, nret);
-			if (rxprof.on > 0)
-				prof_add(0, 0, t2, t2, t2, prof_ns());
+			__atomic_store_n(&p->delivered, d + 1u, __ATOMIC_RELEASE);
+			continue;
 		}
-		__atomic_store_n(&p->delivered, d + 1u, __ATOMIC_RELEASE);
+		s->nchunks = (s->n + RX_CHUNK - 1u) / RX_CHUNK;
+		s->commit = 0;
+		__atomic_store_n(&s->claimw, (uint64_t)d << 32, __ATOMIC_RELEASE);
+		__atomic_store_n(&s->open, 1u, __ATOMIC_RELEASE);
+		return 1;
+	}
+}
+
+/* chunks of the oldest open burst, claimed one at a time until none is
+ * left. Returns the frames this thread delivered */
+static int rx_help(rt_pktio_t *p, odp_pktio_t hdl)
+{
+	const uint32_t d = __atomic_load_n(&p->delivered, __ATOMIC_ACQUIRE);
+	int got = 0;
+
+	if (d == __atomic_load_n(&p->launched, __ATOMIC_ACQUIRE))
+		return 0;
+	rx_slot_t *s = p->slot[d % RT_INFLIGHT];
+
+	if (!s)
+		return 0;
+	__atomic_fetch_add(&s->busy, 1u, __ATOMIC_SEQ_CST);
+	for (;;) {
+		uint64_t cw = __atomic_load_n(&s->claimw, __ATOMIC_ACQUIRE);
+
+		/* a slot reused for a later burst carries that burst's count */
+		if (!__atomic_load_n(&s->open, __ATOMIC_ACQUIRE) || (uint32_t)(cw >> 32) != d ||
+		    (uint32_t)cw >= s->nchunks)
+			break;
+		if (!__atomic_compare_exchange_n(&s->claimw, &cw, cw + 1u, false, __ATOMIC_ACQ_REL,
+						 __ATOMIC_ACQUIRE))
+			continue;
+		const uint32_t c = (uint32_t)cw;
+		const uint32_t k0 = c * RX_CHUNK, k1 = k0 + RX_CHUNK < s->n ? k0 + RX_CHUNK : s->n;
+		const uint64_t t2 = rxprof.on > 0 ? prof_ns() : 0;
+		rx_out_t o;
+
+		rx_deliver_range(p, hdl, s, k0, k1, &o);
+		while (__atomic_load_n(&s->commit, __ATOMIC_ACQUIRE) != c)
+			cpu_relax();
+		rx_commit(p, &o, NULL, NULL);
+		got += (int)(k1 - k0);
+		if (c + 1u == s->nchunks) {
+			/* `delivered` first: while `open` is still set nobody
+			 * can open the burst a second time */
+			s->n = 0;
+			__atomic_store_n(&s->commit, c + 1u, __ATOMIC_RELEASE);
+			__atomic_store_n(&p->delivered, d + 1u, __ATOMIC_RELEASE);
+			__atomic_store_n(&s->open, 0u, __ATOMIC_RELEASE);
+		} else {
+			__atomic_store_n(&s->commit, c + 1u, __ATOMIC_RELEASE);
+		}
+		if (rxprof.on > 0)
+			prof_add(0, 0, t2, t2, t2, prof_ns());
+	}
+	__atomic_fetch_sub(&s->busy, 1u, __ATOMIC_RELEASE);
+	return got;
+}
+
+/* every completed burst (all of them with `drain`, waiting) delivered by
+ * this thread, with whatever help others give (rx_dlock held) */
+static int rx_deliver_done(rt_pktio_t *p, odp_pktio_t hdl, int drain)
+{
+	int got = 0;
+
+	while (rx_open(p, drain)) {
+		const uint32_t d = p->delivered;
+
+		got += rx_help(p, hdl);
+		/* the last chunks may still be with other threads */
+		while (__atomic_load_n(&p->delivered, __ATOMIC_ACQUIRE) == d)
+			cpu_relax();
 	}
 	return got;
 }
@@ -2665,6 +2832,9 @@ static int rx_launch_more(rt_pktio_t *p, odp_pktio_t hdl)
 
 		if (!s)
 			break;
+		/* a thread that looked at the slot's previous burst late is out */
+		while (__atomic_load_n(&s->busy, __ATOMIC_ACQUIRE))
+			cpu_relax();
 		const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
 		const uint32_t n = rx_stage(p, s, RT_BURST);
 
@@ -2731,21 +2901,46 @@ static int poll_input(void)
 
 	if (!rt.init)
 		return 0;
-	/* the delivery side: one thread per pktio, the bursts in order (the
-	 * counts and busy flag are read first, not the lock's line written) */
+	/* the delivery side: a completed burst is opened by one thread
+	 * (rx_dlock) and its chunks delivered by every polling thread; a
+	 * thread counts itself in rx_helpers before it looks at the pktio,
+	 * which close waits out (the counts and busy flag are read first, not
+	 * the locks' lines written) */
 	for (int i = 0; i < RT_MAX_PKTIO; i++) {
 		rt_pktio_t *p = &rt.pktio[i];
+		const odp_pktio_t hdl = (odp_pktio_t)(uintptr_t)(i + 1);
 
 		if (!p->valid || p->in_mode != ODP_PKTIN_MODE_SCHED ||
 		    __atomic_load_n(&p->launched, __ATOMIC_RELAXED) ==
-			    __atomic_load_n(&p->delivered, __ATOMIC_RELAXED) ||
-		    __atomic_load_n(&rx_dbusy[i], __ATOMIC_RELAXED) || pthread_mutex_trylock(&rx_dlock[i]))
+			    __atomic_load_n(&p->delivered, __ATOMIC_RELAXED))
 			continue;
-		__atomic_store_n(&rx_dbusy[i], 1, __ATOMIC_RELAXED);
-		if (p->valid && p->in_mode == ODP_PKTIN_MODE_SCHED)   /* not closed meanwhile */
-			got += rx_deliver_done(p, (odp_pktio_t)(uintptr_t)(i + 1), 0);
-		__atomic_store_n(&rx_dbusy[i], 0, __ATOMIC_RELAXED);
-		pthread_mutex_unlock(&rx_dlock[i]);
+		__atomic_fetch_add(&rx_helpers[i], 1u, __ATOMIC_SEQ_CST);
+		for (int it = 0; it < RT_INFLIGHT && __atomic_load_n(&p->valid, __ATOMIC_SEQ_CST) &&
+				 p->in_mode == ODP_PKTIN_MODE_SCHED; it++) {
+			const uint32_t d = __atomic_load_n(&p->delivered, __ATOMIC_ACQUIRE);
+
+			if (d == __atomic_load_n(&p->launched, __ATOMIC_ACQUIRE))
+				break;
+			if (!__atomic_load_n(&p->slot[d % RT_INFLIGHT]->open, __ATOMIC_ACQUIRE)) {
+				int opened = 0;
+
+				if (__atomic_load_n(&rx_dbusy[i], __ATOMIC_RELAXED) ||
+				    pthread_mutex_trylock(&rx_dlock[i]))
+					break;
+				__atomic_store_n(&rx_dbusy[i], 1, __ATOMIC_RELAXED);
+				opened = rx_open(p, 0);
+				__atomic_store_n(&rx_dbusy[i], 0, __ATOMIC_RELAXED);
+				pthread_mutex_unlock(&rx_dlock[i]);
+				if (!opened)
+					break;
+			}
+			const int n = rx_help(p, hdl);
+
+			got += n;
+			if (!n)
+				break;
+		}
+		__atomic_fetch_sub(&rx_helpers[i], 1u, __ATOMIC_RELEASE);
 	}
 	/* the launch side: another thread at the same time */
 	if (__atomic_load_n(&rt.polling, __ATOMIC_RELAXED) || pthread_mutex_trylock(&rt.poll_lock))
