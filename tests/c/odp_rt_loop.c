@@ -15,11 +15,18 @@
  *   D  pcap input "pcap:in=<file>:loops=<n>": the capture is read
  *      max(1, n - 1) times for n >= 1 (pcapif_init sets loop_cnt = 1 and
  *      _pcapif_reopen stops when ++loop_cnt >= loops, pktio/pcap.c:215,266).
+ *   F  SCHED in, classifier off, 4 receiving threads and a sender, the
+ *      transmit packets from a pool of their own (so that delivery copies
+ *      them into the pktio's pool, as loop.c does): every packet is handed
+ *      out exactly once, and each thread sees one sender's packets in
+ *      sending order (the receive pipeline's chunked delivery keeps queue
+ *      order).
  * Plus the pktio lookup / duplicate-open rule and the mode checks of the
  * queue accessors (odp_packet_io.c:406-410, 798-829, 1696-1843, 2364-2503),
  * and close refused while started (odp_packet_io.c:507-510).
  * Prints one line per check; exit status 0 when all pass.
  */
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -313,6 +320,105 @@ static void case_sched_cls(odp_pool_t pool)
 	printf("B sched+cls: %d packets, %d to net10, %d to default\n", got, n_net, n_def);
 }
 
+/* F: multi-threaded scheduled receive (chunked delivery) */
+#define MT_RX 4
+#define MT_N  200000
+static uint8_t *mt_seen;
+static uint32_t mt_got, mt_bad;
+static int mt_stop;
+static odp_instance_t mt_inst;
+
+static void *mt_rx(void *arg)
+{
+	uint32_t last = 0;
+	int have_last = 0;
+
+	(void)arg;
+	odp_init_local(mt_inst, ODP_THREAD_WORKER);
+	while (!__atomic_load_n(&mt_stop, __ATOMIC_ACQUIRE)) {
+		odp_event_t ev[32];
+		const int n = odp_schedule_multi(NULL, ODP_SCHED_NO_WAIT, ev, 32);
+
+		for (int i = 0; i < n; i++) {
+			odp_packet_t pkt = odp_packet_from_event(ev[i]);
+			const uint8_t *d = odp_packet_data(pkt);
+			uint32_t seq;
+
+			memcpy(&seq, d + 42, 4);
+			if (odp_packet_len(pkt) != 64 || seq >= MT_N ||
+			    __atomic_exchange_n(&mt_seen[seq], 1, __ATOMIC_RELAXED) ||
+			    (have_last && seq <= last))
+				__atomic_fetch_add(&mt_bad, 1u, __ATOMIC_RELAXED);
+			last = seq;
+			have_last = 1;
+			odp_event_free(ev[i]);
+		}
+		if (n > 0)
+			__atomic_fetch_add(&mt_got, (uint32_t)n, __ATOMIC_RELAXED);
+	}
+	odp_term_local();
+	return NULL;
+}
+
+static void case_sched_mt(void)
+{
+	odp_pool_param_t pp;
+	odp_pool_t rxp, txp;
+	odp_pktout_queue_t out;
+	pthread_t t[MT_RX];
+
+	odp_pool_param_init(&pp);
+	pp.type = ODP_POOL_PACKET;
+	pp.pkt.num = 16384;
+	pp.pkt.len = 64;
+	rxp = odp_pool_create("mt_rx", &pp);
+	txp = odp_pool_create("mt_tx", &pp);
+	CHECK(rxp != ODP_POOL_INVALID && txp != ODP_POOL_INVALID, "F pools");
+	odp_pktio_t pktio = open_loop("loop_mt", rxp, ODP_PKTIN_MODE_SCHED, ODP_PKTOUT_MODE_DIRECT, 0);
+
+	CHECK(pktio != ODP_PKTIO_INVALID, "F open");
+	if (pktio == ODP_PKTIO_INVALID)
+		return;
+	mt_seen = calloc(MT_N, 1);
+	CHECK(odp_pktout_queue(pktio, &out, 1) == 1 && odp_pktio_start(pktio) == 0, "F start");
+	for (int i = 0; i < MT_RX; i++)
+		pthread_create(&t[i], NULL, mt_rx, NULL);
+	for (uint32_t seq = 0; seq < MT_N;) {
+		odp_packet_t pk[32];
+		int n = 0;
+
+		for (; n < 32 && seq + (uint32_t)n < MT_N; n++) {
+			pk[n] = odp_packet_alloc(txp, 64);
+			if (pk[n] == ODP_PACKET_INVALID)
+				break;
+			uint8_t *d = odp_packet_data(pk[n]);
+			const uint32_t v = seq + (uint32_t)n;
+
+			memcpy(d, frame[0], 64);
+			memcpy(d + 42, &v, 4);
+		}
+		const int sent = n ? odp_pktout_send(out, pk, n) : 0;
+
+		if (sent > 0)
+			seq += (uint32_t)sent;
+		if (sent < n)
+			odp_packet_free_multi(pk + (sent > 0 ? sent : 0), n - (sent > 0 ? sent : 0));
+		if (sent <= 0)
+			usleep(50);   /* the transmit pool is in flight: let it drain */
+	}
+	for (int w = 0; w < 20000 && __atomic_load_n(&mt_got, __ATOMIC_RELAXED) < MT_N; w++)
+		usleep(500);
+	__atomic_store_n(&mt_stop, 1, __ATOMIC_RELEASE);
+	for (int i = 0; i < MT_RX; i++)
+		pthread_join(t[i], NULL);
+	CHECK(mt_got == MT_N, "F received %u of %u", mt_got, MT_N);
+	CHECK(mt_bad == 0, "F %u packets duplicated, corrupt or out of sending order", mt_bad);
+	CHECK(odp_pktio_stop(pktio) == 0 && odp_pktio_close(pktio) == 0, "F stop / close");
+	CHECK(odp_pool_destroy(rxp) == 0 && odp_pool_destroy(txp) == 0, "F pool destroy");
+	free(mt_seen);
+	printf("F sched, %d threads: %u packets, each once and in order per thread\n", MT_RX, mt_got);
+}
+
 static void case_queue(odp_pool_t pool)
 {
 	odp_pktio_t pktio = open_loop("loop2", pool, ODP_PKTIN_MODE_QUEUE,
@@ -466,6 +572,7 @@ int main(void)
 {
 	odp_instance_t inst;
 	odp_pool_param_t pp;
+
 	odp_pool_capability_t pc;
 	odp_schedule_capability_t sc;
 	odp_pool_t pool;
@@ -489,6 +596,8 @@ int main(void)
 	case_queue(pool);
 	case_pcap_loops(pool);
 	case_pcap_small_pool();
+	mt_inst = inst;
+	case_sched_mt();
 	CHECK(odp_pool_destroy(pool) == 0, "pool destroy");
 	odp_term_local();
 	odp_term_global(inst);
