@@ -732,8 +732,53 @@ __device__ __forceinline__ uint32_t seg_tail_sums4(uint64_t m, const uint8_t *g,
 	uint32_t own = 0u;
 
 	/* the lane's own units: last (masked to b, and to a when it is the
-	 * first), then the first when it carries a lead */
-	if (mine) {
+	 * first), then the first when it carries a lead. XP with no lead in
+	 * the wave (C3: a = 64): the last units in the line shape as well, 16
+	 * a load instruction, four lanes a unit (the units ranked by lane
+	 * through the wave's LDS scratch) */
+	const bool xp_own = XP && marks && !__ballot(mine && lead != 0u);   /* uniform */
+
+	if (xp_own) {
+		const uint64_t mm = __ballot(mine);
+		const uint32_t nown = (uint32_t)__builtin_popcountll(mm);
+		const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
+								__builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+		const uint32_t lu = mine ? nu - 1u : 0u;
+		const uint64_t ua = gb + 64ull * lu;
+		const uint32_t re = mine ? pd.b - c0 - 64u * lu : 0u;   /* 1..64 */
+		const uint32_t ua_lo = (uint32_t)ua, ua_hi = (uint32_t)(ua >> 32);
+		volatile __attribute__((address_space(3))) uint32_t *mk =
+			(volatile __attribute__((address_space(3))) uint32_t *)marks;
+		uint32_t t = 0u;
+
+		if (mine)
+			mk[rank] = lane;
+		__builtin_amdgcn_wave_barrier();
+		for (uint32_t k = 0; 16u * k < nown; ++k) {                 /* uniform, <= 4 */
+			const uint32_t idx = 16u * k + (lane >> 2);
+			const uint32_t src = idx < nown ? mk[idx] : 0u;
+			/* pulls with every lane active: a lane outside the ranks
+			 * may hold a unit another lane reads */
+			const uint32_t rp = lane_pull(re, src);
+			const uint32_t rs = idx < nown ? rp : 0u;
+			const uint64_t as = ((uint64_t)lane_pull(ua_hi, src) << 32) | lane_pull(ua_lo, src);
+			const uint32_t o = 16u * (lane & 3u);
+			uint4 x = make_uint4(0u, 0u, 0u, 0u);
+
+			if (o < rs)
+				x = ld_g16(as + o);
+			uint32_t c = tail_dot2(x.x & keep_below((int)rs - (int)o), 0u);
+
+			c = tail_dot2(x.y & keep_below((int)rs - (int)o - 4), c);
+			c = tail_dot2(x.z & keep_below((int)rs - (int)o - 8), c);
+			c = tail_dot2(x.w & keep_below((int)rs - (int)o - 12), c);
+			c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xf, 0xf, false);
+			c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xf, 0xf, false);
+			t = (lane & 3u) == k ? c : t;
+		}
+		own = lane_pull(t, 4u * (rank & 15u) + (rank >> 4));
+		own = mine ? own : 0u;
+	} else if (mine) {
 		const uint32_t lu = nu - 1u;
 
 		if (!__ballot(mine && lead != 0u && lu == 0u))
