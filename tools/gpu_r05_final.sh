@@ -51,7 +51,7 @@ if [ "${EXTRAS:-1}" = 1 ]; then
   step "bench default" timeout -k 10 600 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err
   cat $OUT/bench_default.json
   step "odp_bench_cls_gpu" timeout -k 10 300 odp_amd/lib/odp_bench_cls_gpu > $OUT/odp_bench_cls_gpu.txt 2>&1
-  for a in "" "-c 4" "-c 8" "-p"; do
+  for a in "" "-c 4" "-c 6" "-c 8" "-p"; do
     tag=$(echo "x$a" | tr -d ' -')
     step "pktio_perf $a" env ODP_RT_PROF=1 timeout -k 10 240 oracle/_ref/odp_pktio_perf -v $a > $OUT/pktio_perf_$tag.txt 2>&1
     grep -E "Maximum|odp_rt:" $OUT/pktio_perf_$tag.txt | tail -3
