@@ -577,30 +577,37 @@ static int cpu_list_first(int cpu, const char *what)
  * the IO die (on a 2 x 64-core EPYC host, 8 workers on CPUs 1-8 span two
  * CCDs and odp_pktio_perf -c 8 fell to a third of -c 6's rate). One core's
  * first hardware thread each; the control CPU's own L3 first, else the
- * first L3 with num free cores. Returns 0 when no L3 holds them (or the
- * topology is not in sysfs): the caller takes CPUs in order. */
+ * first L3 with num free cores; else the same with second hardware threads
+ * added. Returns 0 when no L3 holds them (or the topology is not in sysfs):
+ * the caller takes CPUs in order. */
 static int l3_mask(const cpu_set_t *set, int control, int num, odp_cpumask_t *mask)
 {
 	const int ctl_l3 = cpu_list_first(control, "cache/index3/shared_cpu_list");
 
 	if (ctl_l3 < 0)
 		return 0;
-	for (int pass = 0; pass < 2; pass++) {
+	/* passes: the control's L3, then the others, first hardware threads
+	 * only; then the same with the second hardware threads of its cores
+	 * after the first ones (sharing a core beats crossing the IO die) */
+	for (int pass = 0; pass < 4; pass++) {
+		const int smt = pass >= 2;
+
 		for (int l3 = 0; l3 < CPU_SETSIZE && l3 < ODP_CPUMASK_SIZE; l3++) {
 			if (!CPU_ISSET(l3, set) ||
 			    cpu_list_first(l3, "cache/index3/shared_cpu_list") != l3 ||
-			    (pass == 0) != (l3 == ctl_l3))
+			    ((pass & 1) == 0) != (l3 == ctl_l3))
 				continue;
 			int n = 0;
 
 			odp_cpumask_zero(mask);
-			for (int c = l3; c < CPU_SETSIZE && c < ODP_CPUMASK_SIZE && n < num; c++)
-				if (c != control && CPU_ISSET(c, set) &&
-				    cpu_list_first(c, "cache/index3/shared_cpu_list") == l3 &&
-				    cpu_list_first(c, "topology/thread_siblings_list") == c) {
-					odp_cpumask_set(mask, c);
-					n++;
-				}
+			for (int sib = 0; sib <= smt; sib++)
+				for (int c = l3; c < CPU_SETSIZE && c < ODP_CPUMASK_SIZE && n < num; c++)
+					if (c != control && CPU_ISSET(c, set) &&
+					    cpu_list_first(c, "cache/index3/shared_cpu_list") == l3 &&
+					    (cpu_list_first(c, "topology/thread_siblings_list") == c) == !sib) {
+						odp_cpumask_set(mask, c);
+						n++;
+					}
 			if (n == num)
 				return n;
 		}
