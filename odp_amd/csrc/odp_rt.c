@@ -55,7 +55,9 @@
 #define RT_MAX_POOL  64
 #define RT_BURST     1024
 #define RX_PF        8         /* packets prefetched ahead in staging / delivery */
-#define RX_CHUNK     128       /* packets a delivering thread takes at a time */
+#ifndef RX_CHUNK
+#define RX_CHUNK     64        /* packets a delivering thread takes at a time */
+#endif
 #define RT_INFLIGHT  4              /* receive bursts in flight per pktio */
 
 /* ---- objects -------------------------------------------------------------- */
