@@ -50,7 +50,12 @@ HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 METRIC = "Mpps classified (device-resident), 64B pkts × 64 PMR rules"
 
 
-def parse_args():
+# BASELINE.json's other configs (C1, C3, C4 on one GPU, C5) and SURVEY §8(d)'s
+# second C2 rule mix, measured beside the headline by the default run
+OTHER_CONFIGS = ("c1", "c2x", "c3", "c4", "c5")
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -87,7 +92,13 @@ def parse_args():
     ap.add_argument("--spawn-check", action="store_true",
                     help="ranks print their rank / world size and exit before any GPU "
                          "call (tests the launcher path on CPU)")
-    return ap.parse_args()
+    ap.add_argument("--others", default=None,
+                    help="comma list of further configs measured in the same process and "
+                         "summarised in the line's `other_configs` (default on a 1-GPU "
+                         "headline run: " + ",".join(OTHER_CONFIGS) + "; 'none' to skip)")
+    ap.add_argument("--others-cpu-seconds", type=float, default=6.0,
+                    help="CPU-baseline seconds per further config")
+    return ap.parse_args(argv)
 
 
 def _free_port():
@@ -138,6 +149,67 @@ def main():
         dist = tdist
         world = tdist.get_world_size()
 
+    out = run_config(args, world, rank, local, dist)
+    others = args.others
+    if others is None:
+        others = ",".join(OTHER_CONFIGS) if world == 1 and args.config == "c2" and \
+            args.diag == "full" else "none"
+    if out is not None and others != "none":
+        out["other_configs"] = measure_others(args, others.split(","), world, rank, local, dist)
+    if out is not None:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_config(args, world, rank, local, dist):
+    """One config's measurement; rank 0 gets the line's dict, others None."""
+    if args.config == "c5":
+        return bench_l3fwd(args, world, rank, local, dist)
+    if args.config == "tx":
+        return bench_tx(args, world, rank, local, dist)
+    return bench_classify(args, world, rank, local, dist)
+
+
+def measure_others(args, cfgs, world, rank, local, dist):
+    """The other configs in this process, each with fewer timed launches and
+    a shorter CPU-baseline leg; a compact summary per config (progress on
+    stderr): value (Mpps, this run's clock), kernel_ms (HIP events on the
+    launch stream), frac of HBM peak, traffic_x (committed PMC bytes per
+    launch / algorithmic), counted_kernel_ms (pktio counters on), and the
+    CPU baseline (the per-GPU core share and one thread)."""
+    import copy
+    res = {}
+    for c in cfgs:
+        a = copy.copy(args)
+        a.config, a.others, a.e2e, a.source = c, "none", False, "sharded"
+        a.steps, a.warmup, a.runs = min(args.steps, 100), min(args.warmup, 10), 3
+        a.cpu_seconds = args.others_cpu_seconds
+        a.batch = 1 << 20
+        t0 = time.perf_counter()
+        log(f"other config {c} ...")
+        r = run_config(a, world, rank, local, dist)
+        if r is None:
+            continue
+        rf = r["roofline"]
+        alg = rf["bytes_per_pkt"] * rf["pkts_per_launch"]
+        cpu = r.get("cpu_baseline") or {}
+        e = {"value": r["value"], "kernel_ms": rf["kernel_ms"], "frac": rf["frac"],
+             "traffic_x": round(rf["traffic"] / alg, 3) if rf.get("traffic") else None,
+             "bytes_per_pkt": rf["bytes_per_pkt"], "pkts": rf["pkts_per_launch"]}
+        if "with_pktio_counters" in r:
+            e["counted_kernel_ms"] = r["with_pktio_counters"]["kernel_ms"]
+        if cpu:
+            e["cpu"] = cpu.get("value")
+            e["cpu_1thread"] = cpu.get("value_1thread")
+            e["cpu_cores"] = cpu.get("cores")
+        res[c] = e
+        log(f"other config {c}: {e} ({time.perf_counter() - t0:.1f} s)")
+    return res
+
+
+def bench_classify(args, world, rank, local, dist):
+    """C1 / C2 / C2x / C3 / C4: odpg_classify launches (bench.py docstring)."""
     import ctypes as C
 
     import numpy as np
@@ -145,10 +217,6 @@ def main():
     from odp_amd import _lib as L
     from odp_amd import cls, gen, gpu, shard
 
-    if args.config == "c5":
-        return bench_l3fwd(args, world, rank, local, dist)
-    if args.config == "tx":
-        return bench_tx(args, world, rank, local, dist)
     opt = L.PKTIN_IPV4_CHKSUM | L.PKTIN_UDP_CHKSUM | L.PKTIN_TCP_CHKSUM
     cls.reset()
     if args.config == "c4":
@@ -333,13 +401,12 @@ def main():
                                   dist)
         if out is not None:
             out["scatter_gather"] = sg
-    if out is not None:
-        print(json.dumps(out), flush=True)
     cnt.close()
     del tbl
+    for b in fbufs + obufs + dbufs:
+        b.free()
     ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return out
 
 
 def timed_runs(args, ctx, launch, barrier, dist, dev):
@@ -544,8 +611,10 @@ def bench_tx(args, world, rank, local, dist):
                          "bytes_per_pkt": bytes_per_pkt, "pkts_per_launch": n},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(res), flush=True)
+    for b in fbufs + obufs:
+        b.free()
     ctx.close()
+    return res if rank == 0 else None
 
 
 def bench_l3fwd(args, world, rank, local, dist):
@@ -633,11 +702,11 @@ def bench_l3fwd(args, world, rank, local, dist):
                                         "HBM traffic is 132 B/pkt")},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(res), flush=True)
     del fw
+    for b in fbufs + obufs:
+        b.free()
     ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return res if rank == 0 else None
 
 
 def cpu_baseline(rules, frames, desc, n, stride, opt, args):

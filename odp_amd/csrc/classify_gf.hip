@@ -38,6 +38,7 @@
 #include <errno.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <type_traits>
 
 #include "../../include/odpg.h"
 #include "odpg_internal.h"
@@ -62,6 +63,13 @@
  * and the row goes through LDS at the start */
 #define GF_ROW_REGS(nw) ((nw) > 2)
 #define GF_WAVES_OF(cm, nw) ((nw) == 2 ? ((cm) == 0 ? GF_WAVES : GF_WAVES_CNT) : GF_WAVES_WIDE)
+#ifndef GF_WAVES_S64W       /* fixed 64-byte stride launches (S64) */
+#define GF_WAVES_S64W 6
+#endif
+#ifndef GF_WAVES_S64C       /* ... counted */
+#define GF_WAVES_S64C 5
+#endif
+#define GF_WAVES_S64(cm, nw) ((nw) == 2 ? ((cm) == 0 ? GF_WAVES_S64W : GF_WAVES_S64C) : GF_WAVES_WIDE)
 #ifndef GF_RW               /* LDS row stride per lane, dwords (16-byte multiple) */
 #define GF_RW 20
 #endif
@@ -314,82 +322,94 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 #define GF_PROBES 2
 #endif
 
-/* the hit map's NW words of entry e (NW 2: one ds_read_b64; 4: one
- * ds_read_b128; 8: two) */
-template <int NW>
-__device__ __forceinline__ void xm_entry(const uint32_t *xmm, uint32_t e, uint32_t (&m)[NW])
-{
-	if constexpr (NW == 2) {
-		const uint2 x = *(const uint2 *)(xmm + 2u * e);
-
-		m[0] = x.x;
-		m[1] = x.y;
-	} else {
-#pragma unroll
-		for (int q = 0; q < NW; q += 4) {
-			const uint4 x = *(const uint4 *)(xmm + NW * e + q);
-
-			m[q] = x.x;
-			m[q + 1] = x.y;
-			m[q + 2] = x.z;
-			m[q + 3] = x.w;
-		}
-	}
-}
-
 /* a packet's key words 16, 17 (L4 + 0, 4) and 18 (frame length) */
 typedef uint32_t gf_kx_t __attribute__((ext_vector_type(4)));
 
 /* U hit-map groups' probes for this lane's packet, branch-free: each masked
  * key word hashed to its group's direct entry (cls_compile.cpp
  * "TBL_XMASK"), whose value and bit map are read together; m[u] = the
- * entry's map and hm_[u] all-ones when the value, the group's gate and its
- * CUSTOM_L3 / CUSTOM_FRAME length guard (len >= (l3 & l3mask) + threshold)
- * hold, else 0 (the map counts as 0; an empty slot's map is 0 too). All U descriptors are loaded first and all LDS reads issued
- * together: scalar and LDS loads share one counter, so a descriptor load
- * issued behind a probe's reads would wait for them. Key words by value: a
- * uniform slot index reads them with v_movrels. */
-template <int NW, int U>
+ * entry's map and hk[u] all-ones when the value, the group's gate and (G)
+ * its CUSTOM_L3 / CUSTOM_FRAME length guard (len >= (l3 & l3mask) +
+ * threshold) hold, else 0 (an empty slot's map is 0 too). All U
+ * descriptors are loaded first and all LDS reads issued together: scalar
+ * and LDS loads share one counter, so a descriptor load issued behind a
+ * probe's reads would wait for them. Key words by value, read with a
+ * wave-uniform index (v_movrels): the group's word of the 16-word key
+ * vector, or (KX: the table reads more than 16 slots) its slot, 16..18
+ * selected from kx. The hit test is one compare of (gate & ~inf) |
+ * (value ^ key) with zero, in vector registers (ninf = ~input flags).
+ * 2-word maps: the entry {map0, map1, value, 0} is one ds_read_b128. */
+template <int NW, int U, bool KX, bool G>
 __device__ __forceinline__ void gf_probes(const uint4 *__restrict__ xmg, uint32_t gi, gf_kv_t kv,
-					  gf_kx_t kx, uint32_t inf_lo, uint32_t l3, uint32_t len,
-					  const uint32_t *xmv, const uint32_t *xmm, uint32_t (&m)[U][NW],
-					  uint32_t (&hm_)[U])
+					  gf_kx_t kx, uint32_t ninf, uint32_t l3, uint32_t len,
+					  const uint32_t *tb, const xm_layout_t &L, uint32_t (&m)[U][NW],
+					  uint32_t (&hk)[U])
 {
 	uint4 q0[U], q1[U];
 	uint32_t e[U], kvm[U], v[U];
 
 #pragma unroll
 	for (int u = 0; u < U; ++u) {
-		q0[u] = xmg[4u * (gi + u)];        /* mul, shift, slot, entry base */
+		q0[u] = xmg[4u * (gi + u)];        /* mul, shift, key index, entry base */
 		q1[u] = xmg[4u * (gi + u) + 1u];   /* guard, gate, mask, L3 mask */
 	}
 #pragma unroll
 	for (int u = 0; u < U; ++u) {
-		const uint32_t sl = q0[u].z;
-		const uint32_t key = sl < 16u ? kv[sl & 15u] : kx[sl & 3u];
+		uint32_t key;
 
+		if constexpr (KX) {
+			const uint32_t sl = q0[u].z & 0xffu;
+
+			key = sl < 16u ? kv[sl & 15u] : kx[sl & 3u];
+		} else {
+			key = kv[q0[u].z & 15u];
+		}
 		kvm[u] = key & q1[u].z;
 		e[u] = q0[u].w + ((kvm[u] * q0[u].x) >> q0[u].y);
 	}
 #pragma unroll
 	for (int u = 0; u < U; ++u) {
-		v[u] = xmv[e[u]];
-		xm_entry<NW>(xmm, e[u], m[u]);
+		if constexpr (NW == 2) {
+			const uint4 x = *(const uint4 *)(tb + 4u * e[u]);
+
+			m[u][0] = x.x;
+			m[u][1] = x.y;
+			v[u] = x.z;
+		} else {
+			v[u] = tb[L.values + e[u]];
+#pragma unroll
+			for (int q = 0; q < NW; q += 4) {
+				const uint4 x = *(const uint4 *)(tb + L.masks + NW * e[u] + q);
+
+				m[u][q] = x.x;
+				m[u][q + 1] = x.y;
+				m[u][q + 2] = x.z;
+				m[u][q + 3] = x.w;
+			}
+		}
 	}
 #pragma unroll
 	for (int u = 0; u < U; ++u) {
-		const bool hit = ((inf_lo & q1[u].y) == q1[u].y) & (len >= (l3 & q1[u].w) + q1[u].x) &
-				 (v[u] == kvm[u]);
+		bool hit = ((q1[u].y & ninf) | (v[u] ^ kvm[u])) == 0u;
+
+		if constexpr (G)
+			hit = hit & (len >= (l3 & q1[u].w) + q1[u].x);
 		/* all-ones on a hit: the callers fold it into their OR / AND
 		 * (v_and_or_b32) instead of a select per word */
-		hm_[u] = 0u - (uint32_t)hit;
+		hk[u] = 0u - (uint32_t)hit;
 	}
 }
 
 /* CM: counters of the launch, 0 none, 2 sharded counter rows (odpg.h);
- * NW: hit-map words per packet (the table's rule bits, 2 / 4 / 8 x 32) */
-template <int CM, int NW>
-__global__ __launch_bounds__(GF_BLOCK) __attribute__((amdgpu_waves_per_eu(GF_WAVES_OF(CM, NW)))) void
+ * NW: hit-map words per packet (the table's rule bits, 2 / 4 / 8 x 32);
+ * S64: a fixed 64-byte stride (the C2x launches): every frame is its 64-byte
+ * window, loaded as the lean 64-byte kernel does (coalesced nontemporal
+ * 16-byte loads, 1 KiB of contiguous lines per instruction, transposed to
+ * one frame per lane through the wave's LDS rows), no descriptors and no
+ * checksum tail pass; KX: the table's groups read more than 16 key slots
+ * (slots 16..18 selected per probe, gf_probes) */
+template <int CM, int NW, bool S64, bool KX>
+__global__ __launch_bounds__(GF_BLOCK) __attribute__((amdgpu_waves_per_eu(S64 ? GF_WAVES_S64(CM, NW) : GF_WAVES_OF(CM, NW)))) void
 odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t *__restrict__ xhdr,
 		  const odpg_desc_t *__restrict__ descs, odpg_out_t *__restrict__ out)
 {
@@ -413,8 +433,6 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	 * 8 | absolute << 30 | guarded << 31}, {pmr bit, last record of its
 	 * chain, that record's index, 0} */
 	uint32_t *tb = dlv + nbins;
-	const uint32_t *xmm = tb + A.L.masks;
-	const uint32_t *xmv = tb + A.L.values;
 	const uint2 *xci = (const uint2 *)(tb + A.L.xci);
 	const uint4 *pdst = (const uint4 *)(tb + A.L.xpd);
 	const uint4 *xfl = (const uint4 *)(tb + A.L.xflat);
@@ -427,7 +445,10 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			  (threadIdx.x >> 6) * 64u;
 
 	const uint32_t lane = __lane_id();
-	constexpr bool XW = NW > 2;     /* line-shaped window loads (load_win) */
+	/* line-shaped window loads of descriptor batches (load_win) */
+	constexpr bool XW = NW > 2 && !S64;
+	/* the window chunks go through the frames' LDS rows at the tile start */
+	constexpr bool STG = XW || S64;
 	const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (GF_BLOCK / 64) +
 							   (threadIdx.x >> 6));
 	const uint32_t nwaves = gridDim.x * (GF_BLOCK / 64);
@@ -439,9 +460,31 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	auto load_desc = [&](uint32_t t) __attribute__((always_inline)) -> uint2 {
 		const uint32_t i = t * 64u + lane;
 
+		if constexpr (S64)
+			return make_uint2(0u, 0u);   /* unused: (64 i, 64) */
 		if (t < ntiles && i < num)
 			return A.stride ? make_uint2(i * A.stride, A.stride) : *(const uint2 *)(descs + i);
 		return make_uint2(0u, 0u);
+	};
+	/* S64: tile t's 4 KiB as 4 coalesced nontemporal loads (lane l: chunks
+	 * l, l + 64, l + 128, l + 192 of the tile, i.e. frame 16 q + l / 4, part
+	 * l % 4), clamped to the batch's last chunk (the lean 64-byte kernel's
+	 * load_raw, classify64.hip) */
+	auto load_tile = [&](uint32_t (&f)[16], uint32_t t) __attribute__((always_inline)) {
+		if (t >= ntiles)
+			return;
+		const uint32_t lim = num * 4u - 1u;
+		const uint32_t c0 = t * 256u + lane;
+
+#pragma unroll
+		for (int q = 0; q < 4; ++q) {
+			const uint4 x = ld_nt16((const uint4 *)A.frames + min(c0 + 64u * q, lim));
+
+			f[4 * q + 0] = x.x;
+			f[4 * q + 1] = x.y;
+			f[4 * q + 2] = x.z;
+			f[4 * q + 3] = x.w;
+		}
 	};
 	/* a frame's first 64 bytes (16-byte chunks holding frame bytes only: the
 	 * chunk with the last byte is masked), and its dword at byte 64. Wide
@@ -505,10 +548,14 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	};
 	uint32_t tn = 0u;
 
-	load_win(fn, xn, dn);
-	if (l4ck)
-		tn = early_tails(dn, gw);
-	dnn = load_desc(gw + nwaves);
+	if constexpr (S64) {
+		load_tile(fn, gw);
+	} else {
+		load_win(fn, xn, dn);
+		if (l4ck)
+			tn = early_tails(dn, gw);
+		dnn = load_desc(gw + nwaves);
+	}
 
 	for (uint32_t k = threadIdx.x; k < A.L.lds_words; k += GF_BLOCK)
 		tb[k] = A.xlds[k];
@@ -553,9 +600,11 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	const bool def_rules = def_valid && A.coses[A.default_cos].nrule != 0u;
 	/* the chain bits (they start set, groups clear them), uniform */
 	uint32_t chain[NW];
-	/* the key slots the groups read, the groups without chain records */
+	/* the key slots the groups read; the key-vector words of slots 16..18
+	 * (0xff: none); the group order (odpg_internal.h XM_HDR_WORDS) */
 	const uint32_t kslots = xhdr[6];
-	const uint32_t ngor = xhdr[7];
+	const uint32_t kpos = xhdr[4];
+	const uint32_t gcut = xhdr[7];
 
 #pragma unroll
 	for (int w = 0; w < NW; ++w)
@@ -564,14 +613,14 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 	for (uint32_t t = gw; t < ntiles; t += nwaves) {
 		const uint32_t i = t * 64u + lane;
 		const bool live = i < num;
-		const uint2 d = dn;
+		const uint2 d = S64 ? make_uint2(i * 64u, 64u) : dn;
 		const uint32_t tsum = tn;       /* this tile's tails [64, len) */
 		const uint8_t *g = A.frames + d.x;
 		const uint32_t len = live ? d.y : 0u;
 		uint32_t f[16];
-		uint32_t x16 = xn;
+		uint32_t x16 = S64 ? 0u : xn;
 		uint32_t tile_oct = 0u;  /* CM 2: octets this lane hands over */
-		if constexpr (XW) {
+		if constexpr (STG) {
 			/* the staged chunks into the frames' rows, then each lane's
 			 * own row back (a wave's LDS operations complete in order) */
 			uint32_t *wrow = smem + (threadIdx.x - lane) * RW;
@@ -592,7 +641,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			}
 		}
 
-		if (__ballot(live && len < 64u)) {
+		if (!S64 && __ballot(live && len < 64u)) {
 #pragma unroll
 			for (int q = 0; q < 16; ++q) {
 				/* bytes past the frame read as zero (the reference's
@@ -608,7 +657,8 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			for (int q = 0; q < 16; ++q)
 				f[q] = fn[q];
 		}
-		dn = dnn;
+		if constexpr (!S64)
+			dn = dnn;
 
 		/* ---- parse + checksum verdicts -------------------------------- */
 		Prs p;
@@ -621,10 +671,13 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		p.fl = 0u;
 		p.l2 = p.l3 = p.l4 = 0xffffu;
 		/* the LDS row: the generic parse's window, and the key reads of
-		 * the generic waves (unshifted frame bytes) */
+		 * the generic waves (unshifted frame bytes; S64: the staged row
+		 * already holds them) */
+		if constexpr (!S64) {
 #pragma unroll
-		for (int q = 0; q < 16; q += 4)
-			*(uint4 *)(row + q) = make_uint4(f[q], f[q + 1], f[q + 2], f[q + 3]);
+			for (int q = 0; q < 16; q += 4)
+				*(uint4 *)(row + q) = make_uint4(f[q], f[q + 1], f[q + 2], f[q + 3]);
+		}
 		/* VLAN / QinQ frames: the window shifted by the tag dwords, so that
 		 * the register parse reads their L3 / L4 headers at the untagged
 		 * offsets; the L2 words and the VLAN tag are read from u3..u5 */
@@ -694,7 +747,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			v.g = g;
 			v.len = len;
 			if (live)
-				ret = parse_common(p, v, LAYER_ALL, (uint64_t)opt, &pd);
+				ret = parse_common(p, v, LAYER_ALL, (uint64_t)opt, S64 ? nullptr : &pd);
 			bases();
 			KeySrc<64, true> key;
 
@@ -712,6 +765,15 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			if ((kslots >> 17) & 1u)
 				k17 = key(17u);
 		}
+		if constexpr (!KX) {
+			/* slots 16..18 into their key-vector words (uniform) */
+			if ((kpos & 0xffu) < 16u)
+				kv[kpos & 15u] = k16;
+			if (((kpos >> 8) & 0xffu) < 16u)
+				kv[(kpos >> 8) & 15u] = k17;
+			if (((kpos >> 16) & 0xffu) < 16u)
+				kv[(kpos >> 16) & 15u] = len;
+		}
 		/* the hit map: each group's masked key word, once per packet.
 		 * Single-word rules OR their bits in; a complex rule's chain bit
 		 * (set to start with) stays set only while every group holding one
@@ -726,60 +788,70 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 				hm[w] = on ? chain[w] : 0u;
 			const gf_kv_t kvv = kv;
 			const gf_kx_t kxv = {k16, k17, (uint32_t)len, 0u};
-			const uint32_t inf_lo = b.inf_lo, l3 = b.l3, flen = len;
-			if (__ballot(on)) {
-				/* GF_PROBES groups' probes in flight together */
-				constexpr uint32_t U = NW == 2 ? GF_PROBES : 2u;
-				uint32_t gi = 0;
+			const uint32_t ninf = ~b.inf_lo, l3 = b.l3, flen = len;
+
+			/* the AND-chain groups: a chain bit stays set only where
+			 * every group holding one of its records has it */
+			auto chain_upd = [&](uint32_t g, const uint32_t (&mm)[NW], uint32_t h) __attribute__((always_inline)) {
+				const uint4 a0 = xmg[4u * g + 2u];
+				const uint4 a1 = xmg[4u * g + 3u];
+				const uint32_t na[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+
+#pragma unroll
+				for (int w = 0; w < NW; ++w) {
+					const uint32_t x = mm[w] & h;
+
+					hm[w] = (hm[w] & (x | na[w])) | (x & ~chain[w]);
+				}
+			};
+			/* groups [lo, hi) of one kind (G: length-guarded; CH: with
+			 * chain members), U probes in flight together */
+			auto probe_range = [&](auto gc, auto chc, uint32_t lo, uint32_t hi) __attribute__((always_inline)) {
+				constexpr bool G = decltype(gc)::value;
+				constexpr bool CH = decltype(chc)::value;
+				constexpr uint32_t U = CH || NW != 2 ? 2u : GF_PROBES;
+				uint32_t gi = lo;
 
 #pragma unroll 1
-				for (; gi + U <= ngor; gi += U) {
+				for (; gi + U <= hi; gi += U) {
 					uint32_t m[U][NW], hk[U];
 
-					gf_probes<NW, U>(xmg, gi, kvv, kxv, inf_lo, l3, flen, xmv, xmm, m, hk);
+					gf_probes<NW, U, KX, G>(xmg, gi, kvv, kxv, ninf, l3, flen, tb, A.L, m, hk);
 #pragma unroll
-					for (uint32_t u = 0; u < U; ++u)
+					for (uint32_t u = 0; u < U; ++u) {
+						if constexpr (CH) {
+							chain_upd(gi + u, m[u], hk[u]);
+						} else {
+#pragma unroll
+							for (int w = 0; w < NW; ++w)
+								hm[w] |= m[u][w] & hk[u];
+						}
+					}
+				}
+#pragma unroll 1
+				for (; gi < hi; ++gi) {
+					uint32_t m[1][NW], hk[1];
+
+					gf_probes<NW, 1, KX, G>(xmg, gi, kvv, kxv, ninf, l3, flen, tb, A.L, m, hk);
+					if constexpr (CH) {
+						chain_upd(gi, m[0], hk[0]);
+					} else {
 #pragma unroll
 						for (int w = 0; w < NW; ++w)
-							hm[w] |= m[u][w] & hk[u];
-				}
-#pragma unroll 1
-				for (; gi < ngor; ++gi) {
-					uint32_t m[1][NW], hk[1];
-
-					gf_probes<NW, 1>(xmg, gi, kvv, kxv, inf_lo, l3, flen, xmv, xmm, m, hk);
-#pragma unroll
-					for (int w = 0; w < NW; ++w)
-						hm[w] |= m[0][w] & hk[0];
-				}
-				/* the AND-chain groups: a chain bit stays set only where
-				 * every group holding one of its records has it */
-				auto chain_upd = [&](uint32_t g, const uint32_t (&mm)[NW], uint32_t h) __attribute__((always_inline)) {
-					const uint4 a0 = xmg[4u * g + 2u];
-					const uint4 a1 = xmg[4u * g + 3u];
-					const uint32_t na[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-
-#pragma unroll
-					for (int w = 0; w < NW; ++w) {
-						const uint32_t x = mm[w] & h;
-
-						hm[w] = (hm[w] & (x | na[w])) | (x & ~chain[w]);
+							hm[w] |= m[0][w] & hk[0];
 					}
-				};
-#pragma unroll 1
-				for (; gi + 2u <= ngroups; gi += 2u) {
-					uint32_t m[2][NW], hk[2];
-
-					gf_probes<NW, 2>(xmg, gi, kvv, kxv, inf_lo, l3, flen, xmv, xmm, m, hk);
-					chain_upd(gi, m[0], hk[0]);
-					chain_upd(gi + 1u, m[1], hk[1]);
 				}
-				if (gi < ngroups) {
-					uint32_t m[1][NW], hk[1];
+			};
+			if (__ballot(on)) {
+				typedef std::integral_constant<bool, false> F_;
+				typedef std::integral_constant<bool, true> T_;
+				const uint32_t n0 = gcut & 0xffu, n1 = (gcut >> 8) & 0xffu;
+				const uint32_t n2 = (gcut >> 16) & 0xffu;
 
-					gf_probes<NW, 1>(xmg, gi, kvv, kxv, inf_lo, l3, flen, xmv, xmm, m, hk);
-					chain_upd(gi, m[0], hk[0]);
-				}
+				probe_range(F_(), F_(), 0u, n0);
+				probe_range(T_(), F_(), n0, n1);
+				probe_range(F_(), T_(), n1, n2);
+				probe_range(T_(), T_(), n2, ngroups);
 			}
 		}
 
@@ -794,7 +866,7 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		 * L4 header starts past the window (generic frames: the residue mod
 		 * 0xffff is the tail's, and the pending sum holds the nonzero
 		 * protocol term, so the verdict is the same) */
-		if (ret == PARSE_PEND) {
+		if (!S64 && ret == PARSE_PEND) {
 			uint32_t tail = tsum;
 
 			if (pd.a > 64u) {
@@ -810,10 +882,14 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 
 		/* the next tile's windows, in flight during the walk, and its
 		 * tails right behind them */
-		load_win(fn, xn, dn);
-		if (l4ck)
-			tn = early_tails(dn, t + nwaves);
-		dnn = load_desc(t + 2u * nwaves);
+		if constexpr (S64) {
+			load_tile(fn, t + nwaves);
+		} else {
+			load_win(fn, xn, dn);
+			if (l4ck)
+				tn = early_tails(dn, t + nwaves);
+			dnn = load_desc(t + 2u * nwaves);
+		}
 
 		/* ---- CoS walk (cls_select_cos + match_pmr_cos) ------------------ */
 		bool err = (p.fl & FL_ERROR_MASK) != 0u;
@@ -1116,11 +1192,24 @@ extern "C" int odpg_launch_clsgf(const odpg_launch_args *a, hipStream_t s)
 				   a->desc, a->out);
 	};
 	const bool cm = a->cnt.row != nullptr;
+	/* fixed 64-byte stride, 16-byte aligned frames: the S64 instantiation
+	 * (its chunk indices are 32-bit) */
+	const bool s64 = !a->desc && a->stride == 64u && !((uintptr_t)a->frames & 15u) &&
+			 a->num < (1u << 30);
 
+	/* KX tables (more than 16 key slots read) take the descriptor
+	 * instantiation, whose probes select slots 16..18 */
+	const bool kx = a->xm_kx != 0u;
+
+#define GF_GO(nw)                                                                              \
+	(kx ? (cm ? go(odpg_clsgf_kernel<2, nw, false, true>) : go(odpg_clsgf_kernel<0, nw, false, true>)) \
+	    : s64 ? (cm ? go(odpg_clsgf_kernel<2, nw, true, false>) : go(odpg_clsgf_kernel<0, nw, true, false>)) \
+	    : (cm ? go(odpg_clsgf_kernel<2, nw, false, false>) : go(odpg_clsgf_kernel<0, nw, false, false>)))
 	switch (a->xm_nw) {
-	case 2: cm ? go(odpg_clsgf_kernel<2, 2>) : go(odpg_clsgf_kernel<0, 2>); break;
-	case 4: cm ? go(odpg_clsgf_kernel<2, 4>) : go(odpg_clsgf_kernel<0, 4>); break;
-	default: cm ? go(odpg_clsgf_kernel<2, 8>) : go(odpg_clsgf_kernel<0, 8>); break;
+	case 2: GF_GO(2); break;
+	case 4: GF_GO(4); break;
+	default: GF_GO(8); break;
 	}
+#undef GF_GO
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -1182,19 +1182,46 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	uint64_t rs = 0x9E3779B97F4A7C15ull;
 
 	/* the groups without chain records first (their entries only OR bits
-	 * in), then the AND-chain groups: the kernel runs each kind in a loop
-	 * of its own (the hit map's result does not depend on group order) */
+	 * in), then the AND-chain groups, each kind's groups without a length
+	 * guard first: the kernel runs each of the four in a loop of its own
+	 * (the hit map's result does not depend on group order) */
 	std::vector<decltype(gv.begin())> gorder;
-	uint32_t ngor = 0;
+	uint32_t gcut[3] = {0, 0, 0};
+	auto guarded_key = [](const gkey_t &k) { return (std::get<0>(k) >> 31) != 0; };
 
-	for (auto git = gv.begin(); git != gv.end(); ++git)
-		if (!gand.count(git->first)) {
-			gorder.push_back(git);
-			ngor++;
+	for (int kind = 0; kind < 4; kind++) {
+		for (auto git = gv.begin(); git != gv.end(); ++git)
+			if ((gand.count(git->first) != 0) == (kind >= 2) &&
+			    guarded_key(git->first) == ((kind & 1) != 0))
+				gorder.push_back(git);
+		if (kind < 3)
+			gcut[kind] = (uint32_t)gorder.size();
+	}
+	/* the kernel's 16-word key vector: slot s < 16 at word s; slots 16..18
+	 * (L4 + 0, L4 + 4, frame length) in words no group's slot uses, when
+	 * the groups read at most 16 slots (else xm_kx: the kernel selects
+	 * them per probe) */
+	uint32_t kused = 0, kpos[3] = {0xffu, 0xffu, 0xffu};
+	bool kx = false;
+
+	for (auto &kv : gv)
+		kused |= 1u << (std::get<0>(kv.first) & 0x1fu);
+	{
+		uint32_t freew = ~kused & 0xffffu;
+
+		for (uint32_t s = 16; s < 19; s++) {
+			if (!((kused >> s) & 1u))
+				continue;
+			if (!freew) {
+				kx = true;
+				break;
+			}
+			kpos[s - 16] = (uint32_t)__builtin_ctz(freew);
+			freew &= freew - 1u;
 		}
-	for (auto git = gv.begin(); git != gv.end(); ++git)
-		if (gand.count(git->first))
-			gorder.push_back(git);
+		if (kx)
+			kpos[0] = kpos[1] = kpos[2] = 0xffu;
+	}
 	for (size_t go = 0; xm && go < gorder.size(); ++go) {
 		const auto git = gorder[go];
 		const auto &vm = git->second;
@@ -1260,12 +1287,14 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		 * guard (term_cmp: frame_len > base + off + size) as
 		 * len >= (l3 & l3mask) + gthr */
 		const uint32_t sg = std::get<0>(git->first);
+		const uint32_t slot = sg & 0xffu;
+		const uint32_t kidx = kx || slot < 16u ? slot : kpos[slot - 16u];
 		const bool guarded = (sg >> 31) != 0;
 		const uint32_t l3mask = guarded && !((sg >> 30) & 1u) ? ~0u : 0u;
 		const uint32_t gthr = guarded ? ((sg >> 8) & 0xffffu) + 1u : 0u;
 
 		a.resize(XM_WORDS, 0u);
-		xmg.insert(xmg.end(), {mul, 32u - lg, sg & 0xffu, ebase, gthr,
+		xmg.insert(xmg.end(), {mul, 32u - lg, kidx | (slot << 8), ebase, gthr,
 				       std::get<1>(git->first), std::get<2>(git->first), l3mask});
 		for (uint32_t w = 0; w < XM_WORDS; w++)
 			xmg.push_back(~a[w]);
@@ -1302,8 +1331,11 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		xm_layout_of(nw, (uint32_t)xmval.size(), 0u, ncos, nbits,
 			     (uint32_t)(xflat.size() / 8), &L);
 		xmlds.assign(L.lds_words, 0u);
-		std::copy(xmmask.begin(), xmmask.end(), xmlds.begin() + L.masks);
-		std::copy(xmval.begin(), xmval.end(), xmlds.begin() + L.values);
+		for (size_t e = 0; e < xmval.size(); e++) {
+			for (uint32_t w = 0; w < nw; w++)
+				xmlds[L.masks + e * L.estride + w] = xmmask[e * nw + w];
+			xmlds[L.values + e * L.vstride] = xmval[e];
+		}
 		for (uint32_t c = 0; c < ncos; c++) {
 			xmlds[L.xci + 2 * c] = cbit_start[c] | (cbit_n[c] << 16);
 			xmlds[L.xci + 2 * c + 1] = cos[c].action | ((uint32_t)cos[c].num_queue << 8) |
@@ -1336,13 +1368,13 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		xmhdr[1] = nbits;
 		xmhdr[2] = (uint32_t)gv.size();
 		xmhdr[3] = (uint32_t)xmval.size();
-		xmhdr[4] = 0u;
+		xmhdr[4] = kpos[0] | (kpos[1] << 8) | (kpos[2] << 16) | ((kx ? 1u : 0u) << 24);
 		xmhdr[5] = (uint32_t)(xflat.size() / 8);
 		/* the key slots the groups read (the kernel extracts them once per
 		 * packet) */
 		for (auto &kv : gv)
 			xmhdr[6] |= 1u << (std::get<0>(kv.first) & 0x1fu);
-		xmhdr[7] = ngor;
+		xmhdr[7] = gcut[0] | (gcut[1] << 8) | (gcut[2] << 16);
 		for (uint32_t w = 0; w < XM_WORDS; w++)
 			xmhdr[8 + w] = chain_all[w];
 		h.flags |= TBL_XMASK;
@@ -1352,6 +1384,7 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		h.xm_nw = nw;
 		h.xm_nbits = nbits;
 		h.xm_ngroups = (uint32_t)gv.size();
+		h.xm_kx = kx ? 1u : 0u;
 	}
 	const uint32_t lean_req = (1u << IFL_L2) | (1u << IFL_L3) | (1u << IFL_L4) |
 				  (1u << IFL_ETH) | (1u << IFL_VLAN) | (1u << IFL_IPV4) |

@@ -110,24 +110,36 @@ typedef struct dcos_s {
 #define XM_MAX_ENTS    4096  /* direct entries of all groups (LDS: (nw + 1) words each) */
 #define XM_MAX_XTERMS  512   /* complex-PMR terms the kernel evaluates per packet */
 #define XM_MAX_GROUPS  64    /* groups read per packet */
-#define XM_GROUP_WORDS 16    /* xmg descriptor: {mul, shift, key index, entry base},
-			      * {slot | guard << 8, gate, mask, L3 mask of the
-			      * length guard}, {guard threshold, has chain members,
-			      * 0, 0}, not-member words[8] (only the first 4 of
-			      * them for hit maps of <= 4 words... all 8 stored) */
+#define XM_GROUP_WORDS 16    /* xmg descriptor: {mul, shift, key index | slot << 8,
+			      * entry base}, {guard threshold, gate, mask, L3
+			      * mask of the length guard}, not-member words[8].
+			      * The key index is the group's word in the kernel's
+			      * 16-word key vector: the slot itself for slots < 16,
+			      * slots 16..18 (L4 + 0, L4 + 4, frame length) folded
+			      * into a word no group's slot uses (xhdr[4]); with
+			      * xm_kx (more than 16 slots read) the slot itself */
 #define XM_HDR_WORDS   16    /* region header: nw, nbits, ngroups, num_xment,
-			      * 0, num_xflat, key slots the groups read (bit
-			      * mask), groups without chain members (they come
-			      * first), chain bits[8] */
+			      * the key-vector words of slots 16 / 17 / 18 (bytes
+			      * 0..2, 0xff: not read; byte 3: xm_kx), num_xflat,
+			      * key slots the groups read (bit mask), the group
+			      * order (n0 | n1 << 8 | n2 << 16: groups [0, n0)
+			      * without chain members or length guard, [n0, n1)
+			      * without chain members, guarded, [n1, n2) with
+			      * chain members, unguarded, [n2, ngroups) the rest),
+			      * chain bits[8] */
 
 /* TBL_XMASK region, after the header and the group descriptors: the part
  * every workgroup copies to LDS (word offsets, each part 16-byte aligned),
  * then xfc[num_cos]. Shared by cls_compile.cpp and classify_gf.hip. */
 typedef struct xm_layout_s {
-	uint32_t masks;     /* [num_xment + 1..4][nw] entry bit maps: each group's
-			     * 2^lg direct entries (slot = value * mul >> shift),
-			     * an empty slot's map zero */
-	uint32_t values;    /* [num_xment] masked key values */
+	uint32_t masks;     /* [num_xment + 1..4] entry bit maps (nw words at a
+			     * stride of estride words): each group's 2^lg
+			     * direct entries (slot = value * mul >> shift), an
+			     * empty slot's map zero */
+	uint32_t values;    /* [num_xment] masked key values (stride vstride).
+			     * 2-word maps: entries interleaved {map0, map1,
+			     * value, 0}, one ds_read_b128 per probe */
+	uint32_t estride, vstride;
 	uint32_t slots;     /* unused (slot_bytes 0) */
 	uint32_t xci;       /* uint2 [num_cos]: {bit start | bits << 16, cinfo.y} */
 	uint32_t xpd;       /* uint4 [nbits]: {dst | mark << 16, dst's xci.x, dst's
@@ -148,8 +160,17 @@ void xm_layout_of(uint32_t nw, uint32_t num_xment, uint32_t slot_bytes, uint32_t
 	const uint32_t nx = (num_xment + 4u) & ~3u;
 
 	L->masks = 0u;
-	L->values = L->masks + nx * nw;
-	L->slots = L->values + nx;
+	if (nw == 2u) {
+		L->estride = 4u;
+		L->values = 2u;
+		L->vstride = 4u;
+		L->slots = 4u * nx;
+	} else {
+		L->estride = nw;
+		L->values = L->masks + nx * nw;
+		L->vstride = 1u;
+		L->slots = L->values + nx;
+	}
 	L->xci = L->slots + ((slot_bytes + 15u) & ~15u) / 4u;
 	L->xpd = L->xci + 2u * ((num_cos + 1u) & ~1u);
 	L->xflat = L->xpd + 4u * nbits;
@@ -357,6 +378,9 @@ typedef struct dtable_hdr_s {
 	uint32_t xm_nw;      /* TBL_XMASK hit-map words per packet (2, 4 or 8) */
 	uint32_t xm_nbits;   /* rule bits (chains of the complex PMRs have their own) */
 	uint32_t xm_ngroups; /* groups read per packet */
+	uint32_t xm_kx;      /* TBL_XMASK: the groups read more than 16 key slots, so
+			      * slots 16..18 are not folded into the 16-word key
+			      * vector (classify_gf.hip KX) */
 } dtable_hdr_t;
 
 typedef struct uint2_s { uint32_t x, y; } uint2_t;
@@ -457,7 +481,7 @@ typedef struct odpg_launch_args {
 	uint32_t num_xlist, num_xwords;
 	const uint32_t *xm;         /* TBL_XMASK region */
 	uint32_t num_xment, xm_slot_bytes, num_xflat;
-	uint32_t xm_nw, xm_nbits, xm_ngroups;
+	uint32_t xm_nw, xm_nbits, xm_ngroups, xm_kx;
 	/* lean 64-byte kernel (classify64.hip): CoS start state, from the host
 	 * copy of the table */
 	uint32_t l64_err_cos, l64_err_act, l64_def_cos, l64_def_act, l64_def_ci, l64_def_rules;

@@ -706,6 +706,7 @@ static int classify_on(odpg_ctx_t *c, hipStream_t s, const odpg_table_t *t,
 	a.xm_nw = h.xm_nw;
 	a.xm_nbits = h.xm_nbits;
 	a.xm_ngroups = h.xm_ngroups;
+	a.xm_kx = h.xm_kx;
 	{
 		/* start state of cls_select_cos (odp_classification.c:1669-1701)
 		 * for the lean kernel, as classify.hip derives it per packet */

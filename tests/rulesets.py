@@ -68,6 +68,78 @@ def all_terms_rules(cls, pktio, stats=True):
     return {"default": default, "error": error, "drop": drop, "cos": c, "pmrs": P}
 
 
+def wide_slots_rules(cls, pktio, stats=False):
+    """Rules whose terms read more than 16 of the 19 key slots (DMAC, SMAC,
+    ETHTYPE_X, VLAN_ID_X, DSCP, every word of SIP6 and DIP6, the L4 ports,
+    the IPsec SPI and the frame length): the hit-map table then keeps slots
+    16..18 out of its 16-word key vector (xm_kx, classify_gf.hip KX)."""
+    T = cls.Term
+    q = cls.queue
+    default = cls.cos_create("ws_default", queue=q(0), stats_enable=stats)
+    leaves = [cls.cos_create(f"ws_{k}", queue=q(1 + k), stats_enable=stats) for k in range(12)]
+    assert default and all(leaves)
+    assert cls.default_cos_set(pktio, default) == 0
+    rules = [
+        [T(cls.PMR_DMAC, b"\x02\x00\x00\x00\x00\x01", b"\xff" * 6)],
+        [T(cls.PMR_CUSTOM_FRAME, b"\x00\x00\x00\x02", b"\xff\xff\xff\xff", offset=8)],
+        [T(cls.PMR_ETHTYPE_X, b"\x08\x00", b"\xff\xff")],
+        [T(cls.PMR_VLAN_ID_X, b"\x00\x14", b"\x0f\xff")],
+        [T(cls.PMR_IP_DSCP, b"\x0a", b"\x3f"), T(cls.PMR_IPPROTO, b"\x11", b"\xff")],
+        [T(cls.PMR_SIP6_ADDR, bytes.fromhex("20010db8000000000000000000000001"), b"\xff" * 16)],
+        [T(cls.PMR_DIP6_ADDR, bytes.fromhex("20010db8000100000000000000000002"), b"\xff" * 16)],
+        [T(cls.PMR_UDP_DPORT, b"\x00\x35", b"\xff\xff")],
+        [T(cls.PMR_IPSEC_SPI, b"\x00\x00\x00\x7b", b"\xff\xff\xff\xff")],
+        [T(cls.PMR_LEN, (64).to_bytes(4, "little"), b"\xff\xff\xff\xff"),
+         T(cls.PMR_IPPROTO, b"\x06", b"\xff")],
+        [T(cls.PMR_UDP_SPORT, b"\x00\x00", b"\xff\x00")],
+        [T(cls.PMR_IPPROTO, b"\x11", b"\xff")],
+    ]
+    # at most 8 PMRs per CoS (the reference's limits): rules 7.. hang below
+    # the default CoS's eighth rule (IPPROTO UDP)
+    mid = cls.cos_create("ws_mid", queue=q(13), stats_enable=stats)
+    assert mid
+    P = []
+    for k, terms in enumerate(rules[:7]):
+        h = cls.pmr_create(terms, default, leaves[k], mark=k + 1)
+        assert h, terms
+        P.append(h)
+    P.append(cls.pmr_create([T(cls.PMR_IPPROTO, b"\x11", b"\xff")], default, mid, mark=40))
+    for k, terms in enumerate(rules[7:], 7):
+        h = cls.pmr_create(terms, mid, leaves[k], mark=k + 1)
+        assert h, terms
+        P.append(h)
+    assert all(P)
+    return {"default": default, "leaves": leaves, "pmrs": P}
+
+
+def wide_slots_corpus(n, seed=3):
+    """Frames for wide_slots_rules: IPv4 UDP / TCP (half of them with the
+    ruled DMAC, some VLAN-tagged, DSCP 10 on some), IPv6 UDP with the ruled
+    source / destination addresses on some, then the mutation and IMIX edge
+    corpora. Returns a list of bytes."""
+    rng = np.random.default_rng(seed)
+    out = []
+    m = n // 3
+    for k in range(m):
+        kind = int(rng.integers(0, 6))
+        sport, dport = int(rng.integers(0, 1 << 16)), int(rng.choice([53, 80, 4000]))
+        dm = [0x02, 0, 0, 0, 0, 1 if rng.integers(0, 2) else 9]
+        if kind < 4:
+            proto = gen.PROTO_TCP if kind == 3 else gen.PROTO_UDP
+            length = int(rng.choice([64, 64, 128]))
+            f = gen.ipv4_frames(1, length, np.array([gen.ip4("10.0.0.1")], np.uint64),
+                                np.array([gen.ip4("10.1.0.1")], np.uint64), proto,
+                                np.array([sport]), np.array([dport]), dmac=dm,
+                                tos=(10 << 2) if kind == 2 else 0,
+                                vlan=int(rng.choice([20, 21])) if kind == 1 else None)
+        else:
+            f = gen.ipv6_frames(1, 80, np.array([int(rng.choice([1, 5]))], np.uint64),
+                                np.array([int(rng.choice([2, 7]))], np.uint64), gen.PROTO_UDP,
+                                np.array([sport]), np.array([dport]))
+        out.append(bytes(f.reshape(-1)))
+    return out + mutate_corpus(m, seed=seed + 1) + imix_edge_corpus(n - 2 * m, seed=seed + 2)
+
+
 def mutate_corpus(n, seed=7, max_len=220):
     """Golden frames + generated VLAN / QinQ / SNAP / IPv6-ext / fragment frames,
     then random byte flips and truncations (edge cases the reference tests:

@@ -104,7 +104,7 @@ def test_bench_two_ranks_one_gpu(tmp_path):
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "2", "--steps", "20",
            "--warmup", "4", "--batch", str(1 << 16), "--no-cpu", "--backend", "gloo",
-           "--source", "gpu0"]
+           "--source", "gpu0", "--others", "none"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")]
@@ -152,7 +152,7 @@ def test_bench_rccl_path_on_one_gpu():
     8-GPU run's code path, one rank)."""
     cmd = [sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "1",
            "--steps", "20", "--warmup", "4", "--batch", str(1 << 16), "--no-cpu",
-           "--backend", "nccl", "--source", "gpu0"]
+           "--backend", "nccl", "--source", "gpu0", "--others", "none"]
     env = dict(os.environ, OMP_NUM_THREADS="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -162,6 +162,29 @@ def test_bench_rccl_path_on_one_gpu():
     assert d["n_gpus"] == 1 and d["value"] > 0
     assert d["distributed"]["backend"] == "nccl" and d["distributed"]["world"] == 1
     assert d["scatter_gather"]["value"] > 0 and d["scatter_gather"]["backend"] == "nccl"
+
+
+@pytest.mark.gpu
+def test_bench_other_configs():
+    """The default 1-GPU run's `other_configs`: further configs measured in
+    the same process, one compact entry each (value, kernel time, roofline
+    fraction, traffic ratio, counted-launch time, CPU baseline)."""
+    cmd = [sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"), "--steps", "20",
+           "--warmup", "4", "--runs", "1", "--batch", str(1 << 16), "--cpu-seconds", "1",
+           "--others", "c1,c3,c5", "--others-cpu-seconds", "1"]
+    r = subprocess.run(cmd, env=dict(os.environ, OMP_NUM_THREADS="2"), capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    assert len(line[0]) < 4096
+    d = json.loads(line[0])
+    oc = d["other_configs"]
+    assert sorted(oc) == ["c1", "c3", "c5"]
+    for c, e in oc.items():
+        assert e["value"] > 0 and e["kernel_ms"] > 0 and 0 < e["frac"] < 1.2, (c, e)
+        assert e["cpu"] > 0 and e["cpu_1thread"] > 0, (c, e)
+    assert oc["c1"]["counted_kernel_ms"] > 0 and "counted_kernel_ms" not in oc["c5"]
 
 
 def _whole_l3fwd(n):

@@ -144,3 +144,71 @@ def test_c2x_takes_the_gf_kernel(gpu_ctx, fresh_cls):
     assert L.lib.odpg_last_kernel() == 2
     o = oracle.classify(rules, fr, n, stride=64, opt=ALL_CHKSUM)
     assert np.array_equal(g["out"], o["out"])
+
+
+def _c2x(cls):
+    p = cls.loop_pktio(pktin=ALL_CHKSUM)
+    gen.build_c2x_rules(cls, p)
+    assert cls.pktio_start(p) == 0
+    return cls.pktio_rules(p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 4097, 1 << 18])
+def test_gf_s64_batch_sizes(gpu_ctx, fresh_cls, n):
+    """The fixed 64-byte stride instantiation (S64: coalesced tile loads
+    through the LDS rows, no descriptors, no tail pass) on C2x traffic and
+    the edge corpus cut to 64 bytes, ragged last tiles; verdict-only and
+    counted launches."""
+    from helpers import assert_counters, expected_counters
+    rules = _c2x(fresh_cls)
+    fr = gen.c2x_frames(n, seed=n + 3).reshape(n, 64).copy()
+    edge = rulesets.imix_edge_corpus(max(1, n // 4), seed=n)
+    for k, f in enumerate(edge):          # a quarter of the slots: edge frames
+        b = np.frombuffer(bytes(f)[:64], np.uint8)
+        fr[4 * k % n] = 0
+        fr[4 * k % n, :len(b)] = b
+    fr = fr.reshape(-1)
+    tbl = gpu_ctx.table(rules)
+    o = oracle.classify(rules, fr, n, stride=64, opt=ALL_CHKSUM)
+    g = gpu_ctx.classify(tbl, fr, n, stride=64, opt=ALL_CHKSUM, want_mark=False,
+                         want_meta=False, want_stats=False)
+    assert L.lib.odpg_last_kernel() == 2
+    assert_same({"out": g["out"]}, {"out": o["out"]}, f"s64 n={n}")
+    cnt = gpu_ctx.counters(tbl)
+    g = gpu_ctx.classify(tbl, fr, n, stride=64, opt=ALL_CHKSUM, want_mark=False,
+                         want_meta=False, counters=cnt)
+    assert L.lib.odpg_last_kernel() == 2
+    assert np.array_equal(g["out"], o["out"])
+    assert_counters(cnt.fold(), expected_counters(o, tbl.num_cos), f"s64 counters n={n}")
+    cnt.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["desc", "stride64"])
+def test_gf_kernel_wide_slots(gpu_ctx, fresh_cls, layout):
+    """A table whose groups read more than 16 key slots (xm_kx: slots 16..18
+    selected per probe) on descriptor and fixed-stride batches."""
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    rulesets.wide_slots_rules(fresh_cls, p)
+    assert fresh_cls.pktio_start(p) == 0
+    rules = fresh_cls.pktio_rules(p)
+    assert table_flags(rules) & TBL_XMASK
+    frames = rulesets.wide_slots_corpus(64 * 200 + 11, seed=21)
+    n = len(frames)
+    if layout == "desc":
+        buf, desc = pack(frames)
+        g, o = _verdicts(gpu_ctx, rules, buf, n, desc, ALL_CHKSUM)
+    else:
+        buf = np.zeros((n, 64), np.uint8)
+        for k, f in enumerate(frames):
+            b = np.frombuffer(bytes(f)[:64], np.uint8)
+            buf[k, :len(b)] = b
+        buf = buf.reshape(-1)
+        tbl = gpu_ctx.table(rules)
+        g = gpu_ctx.classify(tbl, buf, n, stride=64, opt=ALL_CHKSUM, want_mark=False,
+                             want_meta=False, want_stats=False)
+        assert L.lib.odpg_last_kernel() == 2
+        o = oracle.classify(rules, buf, n, stride=64, opt=ALL_CHKSUM)
+    assert_same({"out": g["out"]}, {"out": o["out"]}, f"wide slots {layout}")
+    assert len(np.unique(o["out"] & 0xFFFF)) >= 6

@@ -99,6 +99,29 @@ def test_random_mixed(fresh_cls, seed):
     _check(rules, fr, ALL_CHKSUM, f"random {seed}", min_cos=1)
 
 
+def test_wide_slots_kx(fresh_cls):
+    """more than 16 key slots read: slots 16..18 stay out of the 16-word
+    key vector (xm_kx) and the probes select them"""
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    rulesets.wide_slots_rules(fresh_cls, p)
+    assert fresh_cls.pktio_start(p) == 0
+    t = _check(fresh_cls.pktio_rules(p), rulesets.wide_slots_corpus(3000), ALL_CHKSUM,
+               "wide slots", min_cos=6)
+    assert t.kx == 1
+
+
+def test_key_vector_remap(fresh_cls):
+    """at most 16 slots read (C2x reads L4 + 0): slots 16..18 take key-vector
+    words no group reads"""
+    p = fresh_cls.loop_pktio(pktin=ALL_CHKSUM)
+    gen.build_c2x_rules(fresh_cls, p)
+    assert fresh_cls.pktio_start(p) == 0
+    t = XmTable(gpu.compile_rules(fresh_cls.pktio_rules(p)))
+    assert t.kx == 0 and t.kpos[0] < 16
+    used = {int(g[2]) >> 8 for g in t.groups}
+    assert all(k == 0xFF or (k < 16 and k not in used) for k in t.kpos)
+
+
 def test_lazy_form(fresh_cls):
     """more chain bits than XM_MAX_PMR: the bits are the PMR indices and the
     complex PMRs are evaluated per level from their records"""

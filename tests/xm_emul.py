@@ -16,7 +16,7 @@ HDR_FIELDS = ("num_cos default_cos error_cos flags num_pmr num_terms cos_off pmr
               "mgroup_off num_mgroups ment_off num_ment pinfo2_off cgroup_off num_cgroups "
               "cent_off num_cent pinfo3_off pinfo4_off def_cgmask xcos_off xlist_off num_xlist "
               "num_xwords xm_off num_xment xm_slot_bytes num_xflat blob_bytes xm_nw xm_nbits "
-              "xm_ngroups").split()
+              "xm_ngroups xm_kx").split()
 TBL_XMASK = 0x1000
 XM_HDR_WORDS = 16
 XM_GROUP_WORDS = 16
@@ -30,8 +30,11 @@ def xm_layout(nw, num_xment, slot_bytes, num_cos, nbits, num_xflat):
     """odpg_internal.h xm_layout_of (word offsets)"""
     nx = (num_xment + 4) & ~3     # at least one zero entry (a miss's bit map)
     L = {"masks": 0}
-    L["values"] = nx * nw
-    L["slots"] = L["values"] + nx
+    if nw == 2:                   # entries interleaved {map0, map1, value, 0}
+        L.update(estride=4, values=2, vstride=4, slots=4 * nx)
+    else:
+        L.update(estride=nw, values=nx * nw, vstride=1)
+        L["slots"] = L["values"] + nx
     L["xci"] = L["slots"] + ((slot_bytes + 15) & ~15) // 4
     L["xpd"] = L["xci"] + 2 * ((num_cos + 1) & ~1)
     L["xflat"] = L["xpd"] + 4 * nbits
@@ -52,19 +55,29 @@ class XmTable:
         if not self.flags & TBL_XMASK:
             return
         w = np.frombuffer(blob, np.uint32, offset=h["xm_off"])
-        self.nw, self.nbits, self.ngroups, nx, sb, nxf = (int(x) for x in w[:6])
+        self.nw, self.nbits, self.ngroups, nx, _, nxf = (int(x) for x in w[:6])
+        sb = h["xm_slot_bytes"]
         assert (self.nw, self.nbits, self.ngroups) == (h["xm_nw"], h["xm_nbits"], h["xm_ngroups"])
-        assert (nx, sb, nxf) == (h["num_xment"], h["xm_slot_bytes"], h["num_xflat"])
+        assert (nx, sb, nxf) == (h["num_xment"], 0, h["num_xflat"])
         self.chain = self._big(w[8:16])
-        self.ngor = int(w[7])
+        # group order: [0, n0) plain unguarded, [n0, n1) plain guarded,
+        # [n1, n2) chain unguarded, [n2, ngroups) chain guarded
+        self.gcut = (int(w[7]) & 0xFF, (int(w[7]) >> 8) & 0xFF, (int(w[7]) >> 16) & 0xFF)
+        self.ngor = self.gcut[1]
+        self.kpos = [(int(w[4]) >> (8 * k)) & 0xFF for k in range(3)]
+        self.kx = (int(w[4]) >> 24) & 1
+        assert self.kx == h["xm_kx"]
         self.groups = w[XM_HDR_WORDS:XM_HDR_WORDS + XM_GROUP_WORDS * self.ngroups] \
             .reshape(-1, XM_GROUP_WORDS).astype(np.uint64)
         base = XM_HDR_WORDS + XM_GROUP_WORDS * self.ngroups
         ncos = h["num_cos"]
         L = xm_layout(self.nw, nx, sb, ncos, self.nbits, nxf)
         lds = w[base:base + L["lds_words"]]
-        self.masks = lds[L["masks"]:L["masks"] + nx * self.nw].reshape(-1, self.nw) if nx else None
-        self.values = lds[L["values"]:L["values"] + nx]
+        ent = lds[:L["slots"]]
+        es, vs = L["estride"], L["vstride"]
+        self.masks = np.stack([ent[L["masks"] + w::es][:nx] for w in range(self.nw)], 1) \
+            if nx else None
+        self.values = ent[L["values"]::vs][:nx]
         self.xci = lds[L["xci"]:L["xci"] + 2 * ncos].reshape(-1, 2)
         self.xpd = lds[L["xpd"]:L["xpd"] + 4 * self.nbits].reshape(-1, 4)
         self.xflat = lds[L["xflat"]:L["xflat"] + 8 * nxf].reshape(-1, 8)
@@ -109,13 +122,27 @@ class XmTable:
 
         full = (1 << (32 * self.nw)) - 1
         hm = self.chain
+        # the kernel's 16-word key vector (classify_gf.hip): slot s < 16 at
+        # word s, slots 16..18 at the words xhdr[4] names (unless kx)
+        kvec = {}
+        if not self.kx:
+            for s in range(16):
+                kvec[s] = key(s)
+            for k in range(3):
+                if self.kpos[k] != 0xFF:
+                    assert not any(int(g[2]) >> 8 == self.kpos[k] for g in self.groups)
+                    kvec[self.kpos[k]] = key(16 + k)
         for gi, g in enumerate(self.groups):
-            mul, shf, slot, eb, gthr, req, gmask, l3mask = (int(x) for x in g[:8])
+            mul, shf, kw, eb, gthr, req, gmask, l3mask = (int(x) for x in g[:8])
+            slot = kw >> 8
+            guarded = gthr != 0
+            assert guarded == (self.gcut[0] <= gi < self.gcut[1] or gi >= self.gcut[2])
+            kword = key(slot) if self.kx else kvec[kw & 15]
             # direct entries: slot (value * mul) >> shift; an empty slot's
             # map is zero, so a probe landing there acts as a miss
             h = 0
             if (inf & req) == req and n >= (l3 & l3mask) + gthr:
-                kv = key(slot) & gmask
+                kv = kword & gmask
                 e = eb + (((kv * mul) & 0xFFFFFFFF) >> shf)
                 if int(self.values[e]) == kv:
                     h = self._big(self.masks[e])
