@@ -345,6 +345,8 @@ static void parse_release(void);
 
 static void rx_release(rt_pktio_t *p);
 
+static void grave_release(void);
+
 int odp_term_global(odp_instance_t instance)
 {
 	(void)instance;
@@ -371,6 +373,7 @@ int odp_term_global(odp_instance_t instance)
 		rt.init = 0;
 	}
 	pthread_mutex_unlock(&rt.lock);
+	grave_release();
 	return 0;
 }
 
@@ -384,7 +387,8 @@ int odp_init_local(odp_instance_t instance, odp_thread_type_t type)
 		if (thr_used[i / 64] & (1ull << (i % 64)))
 			continue;
 		thr_used[i / 64] |= 1ull << (i % 64);
-		thr_count++;
+		/* read unlocked by odp_thread_count */
+		__atomic_fetch_add(&thr_count, 1, __ATOMIC_RELAXED);
 		thr_id = i;
 		break;
 	}
@@ -406,7 +410,7 @@ int odp_term_local(void)
 		return 0;
 	pthread_mutex_lock(&thr_lock);
 	thr_used[thr_id / 64] &= ~(1ull << (thr_id % 64));
-	thr_count--;
+	__atomic_fetch_sub(&thr_count, 1, __ATOMIC_RELAXED);
 	pthread_mutex_unlock(&thr_lock);
 	thr_id = -1;
 	return 0;
@@ -967,6 +971,54 @@ odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param)
 	return ret;
 }
 
+/* Chunks of pools destroyed while buffers were still out (held by the
+ * application or another thread's cache): a later odp_packet_free of such a
+ * buffer reads its header to find the pool gone (generation check), so the
+ * memory stays mapped until odp_term_global (the reference frees it and
+ * leaves that free undefined; found by the AddressSanitizer build,
+ * tests/c/Makefile "san") */
+static struct {
+	pthread_mutex_t lock;
+	void **chunks;
+	uint32_t n, cap;
+} grave = {PTHREAD_MUTEX_INITIALIZER, NULL, 0, 0};
+
+static void grave_release(void)
+{
+	pthread_mutex_lock(&grave.lock);
+	for (uint32_t c = 0; c < grave.n; c++)
+		free(grave.chunks[c]);
+	free(grave.chunks);
+	grave.chunks = NULL;
+	grave.n = grave.cap = 0;
+	pthread_mutex_unlock(&grave.lock);
+}
+
+/* a destroyed pool's chunks: freed now when every buffer is back on its
+ * stack, else kept until odp_term_global */
+static void pool_chunks_release(rt_pool_t *p)
+{
+	const int out = p->nfree != p->made;
+
+	pthread_mutex_lock(&grave.lock);
+	for (uint32_t c = 0; c < p->nchunks; c++) {
+		if (out && grave.n == grave.cap) {
+			const uint32_t cap = grave.cap ? 2u * grave.cap : 64u;
+			void **nc = realloc(grave.chunks, cap * sizeof(void *));
+
+			if (nc) {
+				grave.chunks = nc;
+				grave.cap = cap;
+			}
+		}
+		if (out && grave.n < grave.cap)
+			grave.chunks[grave.n++] = p->chunks[c];
+		else
+			free(p->chunks[c]);
+	}
+	pthread_mutex_unlock(&grave.lock);
+}
+
 int odp_pool_destroy(odp_pool_t hdl)
 {
 	pthread_mutex_lock(&rt.lock);
@@ -979,8 +1031,7 @@ int odp_pool_destroy(odp_pool_t hdl)
 		 * pool->lock too) */
 		pthread_mutex_lock(&p->lock);
 		p->valid = 0;
-		for (uint32_t c = 0; c < p->nchunks; c++)
-			free(p->chunks[c]);
+		pool_chunks_release(p);
 		free(p->chunks);
 		free(p->stack);
 		p->chunks = NULL;
@@ -2696,7 +2747,7 @@ static void to_inq(rt_pktio_t *p, odp_packet_t pkts[], int nret)
 							 nret) != nret))
 		odp_packet_free_multi(pkts, nret);
 	if (rxprof.on > 0)
-		rxprof.enq_ns += prof_ns() - t0;
+		__atomic_fetch_add(&rxprof.enq_ns, prof_ns() - t0, __ATOMIC_RELAXED);
 }
 
 /* QUEUE / SCHED mode, the delivery side. A burst whose fence has completed
@@ -2740,7 +2791,7 @@ static int rx_open(rt_pktio_t *p, int drain)
 		odpg_cls_pktio_recv_end(s->token);
 		s->token = NULL;
 		if (rxprof.on > 0)
-			rxprof.end_ns += prof_ns() - t0;
+			__atomic_fetch_add(&rxprof.end_ns, prof_ns() - t0, __ATOMIC_RELAXED);
 		if (fs < 0) {
 			/* the launch failed: its verdicts were never written */
 			ERR("receive burst failed on the GPU: dropped\n");
