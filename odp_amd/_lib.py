@@ -386,6 +386,20 @@ SIGNATURES = {
     "odpg_pcap_free": (None, [C.POINTER(odpg_capture_t)]),
     # include/odpg_tx.h
     "odpg_tx_prepare": (_i32, [_vp, C.POINTER(odpg_tx_batch_t), C.POINTER(odpg_tx_cfg_t), _vp]),
+    # include/odpg_group.h
+    "odpg_group_create": (_i32, [C.POINTER(C.c_int), _u32, C.POINTER(_vp)]),
+    "odpg_group_destroy": (None, [_vp]),
+    "odpg_group_size": (_u32, [_vp]),
+    "odpg_group_ctx": (_vp, [_vp, _u32]),
+    "odpg_group_table": (_vp, [_vp, _u32]),
+    "odpg_group_load": (_i32, [_vp, C.POINTER(odpg_rules_t)]),
+    "odpg_group_range": (None, [_u32, _u32, _u32, C.POINTER(_u32), C.POINTER(_u32)]),
+    "odpg_group_classify_host": (_i32, [_vp, C.POINTER(odpg_batch_t), C.POINTER(odpg_result_t),
+                                        _i32, _u32]),
+    "odpg_group_classify": (_i32, [_vp, C.POINTER(odpg_batch_t), C.POINTER(odpg_result_t),
+                                   _i32]),
+    "odpg_group_sync": (_i32, [_vp]),
+    "odpg_group_counters_fold": (_i32, [_vp, C.POINTER(C.c_uint64)]),
 }
 
 

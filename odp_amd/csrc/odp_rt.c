@@ -59,6 +59,7 @@
 #define RX_CHUNK     64        /* packets a delivering thread takes at a time */
 #endif
 #define RT_INFLIGHT  4              /* receive bursts in flight per pktio */
+#define RT_MAX_DEV   16             /* device contexts (ODPG_DEVICES) */
 
 /* ---- objects -------------------------------------------------------------- */
 #define PKT_MAGIC 0x504b5452u
@@ -203,6 +204,7 @@ typedef struct rx_slot {
 	odpg_out_t *out, *dout;
 	odpg_meta_t *meta, *dmeta;
 	odpg_fence_t *fence;       /* behind the burst's launch */
+	odpg_ctx_t *ctx;           /* the device context its bursts launch on */
 	void *token;               /* the launch's binding (odpg_cls_pktio_recv_end) */
 	/* delivery in chunks (receive pipeline): the burst's launch count
 	 * (seq) and next unclaimed chunk packed in one word, so that a thread
@@ -255,8 +257,12 @@ static struct {
 	rt_queue_t *sched;         /* scheduled queues */
 	uint32_t sched_n;          /* events in them (read without a lock) */
 	int polling;               /* a thread is in poll_input */
+	/* the device contexts receive bursts launch on (ODPG_DEVICES; ctx is
+	 * the first; slot_get) */
+	odpg_ctx_t *ctxs[RT_MAX_DEV];
+	uint32_t nctx;
 } rt = { PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, 0, NULL, {{0}}, {{0}},
-	 NULL, 0, 0 };
+	 NULL, 0, 0, {NULL}, 0 };
 
 /* a pktio's delivery side (receive pipeline), outside the pktio object so
  * that close can hold it across the object's reset; lock order: poll_lock,
@@ -325,14 +331,32 @@ int odp_init_global(odp_instance_t *instance, const odp_init_t *param, const voi
 		rxprof.on = getenv("ODP_RT_PROF") && atoi(getenv("ODP_RT_PROF"));
 	pthread_mutex_lock(&rt.lock);
 	if (!rt.init) {
-		int rc = odpg_ctx_create(0, NULL, &rt.ctx);
+		/* ODPG_DEVICES="0,1,..." (default "0"): one context per entry
+		 * (a device may repeat: its contexts share the GPU); receive
+		 * bursts spread over them (odpg_group.h is the same sharding for
+		 * a single batch) */
+		const char *dl = getenv("ODPG_DEVICES");
+		char buf[256];
+		int rc = 0;
 
-		if (rc) {
+		snprintf(buf, sizeof(buf), "%s", dl && *dl ? dl : "0");
+		rt.nctx = 0;
+		for (char *save = NULL, *tok = strtok_r(buf, ", ", &save);
+		     tok && rt.nctx < RT_MAX_DEV && !rc; tok = strtok_r(NULL, ", ", &save)) {
+			rc = odpg_ctx_create((int)strtol(tok, NULL, 0), NULL, &rt.ctxs[rt.nctx]);
+			if (!rc)
+				rt.nctx++;
+		}
+		if (rc || !rt.nctx) {
+			for (uint32_t k = 0; k < rt.nctx; k++)
+				odpg_ctx_destroy(rt.ctxs[k]);
+			rt.nctx = 0;
 			pthread_mutex_unlock(&rt.lock);
-			ERR("no MI355X context (odpg_ctx_create: %d): the classifier runs only on "
-			    "the GPU\n", rc);
+			ERR("no MI355X context (odpg_ctx_create: %d, ODPG_DEVICES=%s): the "
+			    "classifier runs only on the GPU\n", rc, dl ? dl : "0");
 			return -1;
 		}
+		rt.ctx = rt.ctxs[0];
 		rt.init = 1;
 	}
 	pthread_mutex_unlock(&rt.lock);
@@ -368,7 +392,9 @@ int odp_term_global(odp_instance_t instance)
 	pthread_mutex_unlock(&rt.poll_lock);
 	pthread_mutex_lock(&rt.lock);
 	if (rt.init) {
-		odpg_ctx_destroy(rt.ctx);
+		for (uint32_t k = 0; k < rt.nctx; k++)
+			odpg_ctx_destroy(rt.ctxs[k]);
+		rt.nctx = 0;
 		rt.ctx = NULL;
 		rt.init = 0;
 	}
@@ -2371,10 +2397,14 @@ static rx_slot_t *slot_get(rt_pktio_t *p, uint32_t i)
 		return s;
 	if (!(s = calloc(1, sizeof(*s))))
 		return NULL;
+	/* bursts of pktio k in slot i launch on device context (k RT_INFLIGHT +
+	 * i) mod nctx: a pktio's bursts in flight spread over the devices,
+	 * and several pktios over all of them */
+	s->ctx = rt.ctxs[((uint32_t)(p - rt.pktio) * RT_INFLIGHT + i) % (rt.nctx ? rt.nctx : 1u)];
 	if (pinned_alloc(RT_BURST * sizeof(odpg_desc_t), (void **)&s->desc, (void **)&s->ddesc) ||
 	    pinned_alloc(RT_BURST * sizeof(odpg_out_t), (void **)&s->out, (void **)&s->dout) ||
 	    pinned_alloc(RT_BURST * sizeof(odpg_meta_t), (void **)&s->meta, (void **)&s->dmeta) ||
-	    odpg_fence_create(rt.ctx, &s->fence)) {
+	    odpg_fence_create(s->ctx, &s->fence)) {
 		odpg_host_free_pinned(s->desc);
 		odpg_host_free_pinned(s->out);
 		odpg_host_free_pinned(s->meta);
@@ -2535,7 +2565,7 @@ static void rx_drop(rx_slot_t *s)
 
 static int rx_launch(odp_pktio_t hdl, rx_slot_t *s)
 {
-	if (odpg_cls_pktio_recv_start_zc(hdl, rt.ctx, s->dstage, s->ddesc, s->n, s->dout, s->dmeta,
+	if (odpg_cls_pktio_recv_start_zc(hdl, s->ctx, s->dstage, s->ddesc, s->n, s->dout, s->dmeta,
 					 s->fence, &s->token)) {
 		ERR("classify failed\n");
 		rx_drop(s);

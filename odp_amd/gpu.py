@@ -277,6 +277,107 @@ class Context:
         return res
 
 
+def group_range(num, n, member):
+    """odpg_group_range: member's packet range [lo, hi) of a num-packet batch
+    over n members (host arithmetic, no device)."""
+    lo, hi = C.c_uint32(), C.c_uint32()
+    lib.odpg_group_range(num, n, member, C.byref(lo), C.byref(hi))
+    return lo.value, hi.value
+
+
+class Group:
+    """Several device contexts classifying one batch by packet range
+    (include/odpg_group.h): the table compiled once and imported per member,
+    per-member counters summed when folded."""
+
+    def __init__(self, devices):
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        L.check(lib.odpg_group_create(devs, len(devices), C.byref(h)), "odpg_group_create")
+        self.h = h.value
+        self.n = len(devices)
+        self.num_cos = 0
+
+    def close(self):
+        if self.h:
+            lib.odpg_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        if sys.is_finalizing():   # the HIP runtime may be torn down already
+            return
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load(self, rules):
+        L.check(lib.odpg_group_load(self.h, C.byref(rules)), "odpg_group_load")
+        self.num_cos = lib.odpg_table_num_cos(lib.odpg_group_table(self.h, 0))
+
+    def ctx_handle(self, member):
+        return lib.odpg_group_ctx(self.h, member)
+
+    def classify_host(self, frames, num, stride=0, desc=None, opt=0, layer=L.LAYER_ALL,
+                      counted=False, chunk=0):
+        """Host arrays in, verdict words out (odpg_group_classify_host)."""
+        _, desc_dt = L.np_dtypes()
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        dptr = None
+        if desc is not None:
+            desc = np.ascontiguousarray(desc, dtype=desc_dt)
+            dptr = desc.ctypes.data
+        out = np.zeros(num, np.uint32)
+        b = L.odpg_batch_t(frames.ctypes.data, dptr, stride, num, opt, layer, 1)
+        r = L.odpg_result_t(out.ctypes.data, None, None, None, None)
+        L.check(lib.odpg_group_classify_host(self.h, C.byref(b), C.byref(r), int(counted), chunk),
+                "odpg_group_classify_host")
+        return out
+
+    def classify_shards(self, frames, num, stride, opt=0, counted=False):
+        """Fixed-stride host frames: member i's range uploaded to its own HBM,
+        all members launched (odpg_group_classify), synced, verdicts
+        gathered."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        B = (L.odpg_batch_t * self.n)()
+        R = (L.odpg_result_t * self.n)()
+        bufs = []
+        for i in range(self.n):
+            lo, hi = group_range(num, self.n, i)
+            ctx = _CtxView(self.ctx_handle(i))
+            fb = DeviceBuffer(ctx, max(16, (hi - lo) * stride))
+            ob = DeviceBuffer(ctx, max(16, 4 * (hi - lo)))
+            if hi > lo:
+                fb.upload(frames[lo * stride:hi * stride])
+            B[i] = L.odpg_batch_t(fb.ptr, None, stride, hi - lo, opt, L.LAYER_ALL, 1)
+            R[i] = L.odpg_result_t(ob.ptr, None, None, None, None)
+            bufs.append((lo, hi, fb, ob))
+        L.check(lib.odpg_group_classify(self.h, B, R, int(counted)), "odpg_group_classify")
+        L.check(lib.odpg_group_sync(self.h), "odpg_group_sync")
+        out = np.zeros(num, np.uint32)
+        for lo, hi, fb, ob in bufs:
+            if hi > lo:
+                out[lo:hi] = ob.download(np.uint32, hi - lo)
+            fb.free()
+            ob.free()
+        return out
+
+    def fold(self):
+        w = np.zeros(4 + self.num_cos + self.num_cos * L.COS_QUEUE_MAX, np.uint64)
+        L.check(lib.odpg_group_counters_fold(self.h, w.ctypes.data_as(C.POINTER(C.c_uint64))),
+                "odpg_group_counters_fold")
+        n = self.num_cos
+        return {"pktio": w[:4], "cos": w[4:4 + n],
+                "queue": w[4 + n:].reshape(n, L.COS_QUEUE_MAX)}
+
+
+class _CtxView:
+    """A member context of a Group, for DeviceBuffer (not owned)."""
+
+    def __init__(self, h):
+        self.h = h
+
+
 class Forwarder:
     """example/l3fwd forwarding table on the device (include/odpg_fwd.h)."""
 

@@ -162,6 +162,18 @@ def test_loop_device_through_gpu_classifier():
 
 
 @pytest.mark.gpu
+def test_loop_device_over_several_device_contexts():
+    """ODPG_DEVICES=0,0,0: the runtime opens three device contexts (here all
+    on the one GPU) and spreads receive bursts over them (odp_rt.c
+    slot_get); every check of the loop program holds, including the
+    4-thread ordered delivery."""
+    r = subprocess.run(["timeout", "-k", "10", "100", LOOP_TEST], capture_output=True, text=True,
+                       env=dict(os.environ, ODPG_DEVICES="0,0,0"))
+    assert r.returncode == 0 and "PASS" in r.stdout, (r.stdout[-3000:], r.stderr[-2000:])
+    assert "F sched, 4 threads: 200000 packets, each once and in order per thread" in r.stdout
+
+
+@pytest.mark.gpu
 @pytest.mark.skipif(not os.path.exists(REF_BENCH), reason="reference bench not built here")
 def test_reference_bench_pktio_sp_runs_every_case():
     r = subprocess.run(["timeout", "-k", "10", "100", REF_BENCH, "-r", "20"],

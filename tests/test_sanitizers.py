@@ -27,10 +27,15 @@ def san_build():
     assert r.returncode == 0, r.stderr[-3000:]
 
 
-@pytest.mark.parametrize("prog", ["odp_rt_host", "odp_rt_loop"])
+@pytest.mark.parametrize("prog", ["odp_rt_host", "odp_rt_loop", "odp_rt_loop:0,0,0"])
 @pytest.mark.parametrize("san", ["tsan", "asan"])
 def test_runtime_under_sanitizer(san_build, prog, san):
+    """odp_rt_loop:0,0,0 runs with three device contexts (ODPG_DEVICES):
+    receive bursts spread over them"""
     env = dict(os.environ)
+    prog, _, devs = prog.partition(":")
+    if devs:
+        env["ODPG_DEVICES"] = devs
     env["TSAN_OPTIONS"] = "halt_on_error=1 second_deadlock_stack=1"
     env["ASAN_OPTIONS"] = "detect_leaks=1:abort_on_error=0"
     env["UBSAN_OPTIONS"] = "print_stacktrace=1"
