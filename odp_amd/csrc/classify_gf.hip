@@ -45,6 +45,10 @@
 #include "pkt_parse.h"
 #include "cls_match.h"
 
+/* the register parse combines its compares with bitwise & / | on purpose
+ * (branch-free: plain_gf, parse_fast_gf) */
+#pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"
+
 #ifndef GF_BLOCK            /* threads per workgroup */
 #define GF_BLOCK 256
 #endif
@@ -154,167 +158,133 @@ __device__ __forceinline__ uint32_t tag_dwords(const uint32_t (&f)[16], bool &qi
 __device__ __forceinline__ bool plain_gf(const uint32_t (&f)[16], uint32_t x16, uint32_t len,
 					 uint32_t sh)
 {
+	/* branch-free: compares combined with & / | (a wave mixes IPv4 / IPv6
+	 * and UDP / TCP frames; divergent ifs ran both sides with exec-mask
+	 * bookkeeping around each) */
 	const uint32_t et = f[3] & 0xffffu;
 	const uint32_t vb = (f[3] >> 16) & 0xffu;
-	const bool v4 = et == 0x0008u && vb == 0x45u;
-	const bool v6 = et == 0xdd86u && (vb & 0xf0u) == 0x60u && sh <= 1u;
 	const uint32_t l3 = 14u + 4u * sh;
+	const uint32_t room = len - l3;             /* bytes from the L3 header on */
+	const bool v4 = (et == 0x0008u) & (vb == 0x45u) & (swap16(f[4] & 0xffffu) <= room);
+	const bool v6 = (et == 0xdd86u) & ((vb & 0xf0u) == 0x60u) & (sh <= 1u) &
+			(swap16(f[4] >> 16) + 40u <= room);
+	/* IPv4 with IHL 5: protocol byte 23, UDP length at 38, TCP data offset
+	 * at 46; IPv6: next header byte 20, UDP length at 58, port at 56, TCP
+	 * data offset past the window (x16) */
+	const uint32_t proto = v6 ? (f[5] & 0xffu) : (f[5] >> 24);
+	const uint32_t uw = v6 ? f[14] : f[9];
+	const bool udp_ok = (proto == 0x11u) & (swap16(uw >> 16) >= 8u) &
+			    !(v6 & (swap16(uw & 0xffffu) == 4500u));
+	const uint32_t doff = v6 ? (x16 >> 20) & 0xfu : (f[11] >> 20) & 0xfu;
+	const bool tcp_ok = (proto == 0x06u) & (doff >= 5u) & !(v6 & ((sh != 0u) | (len < 74u)));
 
-	if (len < 64u || !(v4 || v6))
-		return false;
-	if (v4) {
-		const uint32_t tot_len = swap16(f[4] & 0xffffu);
-		const uint32_t proto = f[5] >> 24;
-
-		if (tot_len > len - l3)
-			return false;
-		if (proto == 0x11u)
-			return swap16(f[9] >> 16) >= 8u;
-		if (proto == 0x06u)
-			return ((f[11] >> 20) & 0xfu) >= 5u;
-		return false;
-	}
-	const uint32_t payload = swap16(f[4] >> 16);
-	const uint32_t nh = f[5] & 0xffu;
-
-	if (payload + 40u > len - l3)
-		return false;
-	if (nh == 0x11u)
-		return swap16(f[14] >> 16) >= 8u && swap16(f[14] & 0xffffu) != 4500u;
-	if (nh == 0x06u)
-		return sh == 0u && len >= 74u && ((x16 >> 20) & 0xfu) >= 5u;
-	return false;
+	return (len >= 64u) & (v4 | v6) & (udp_ok | tcp_ok);
 }
 
 /* parse_common() of a plain_gf() frame from its tag-shifted window
  * registers: returns 0 / 1 (error flagged) or PARSE_PEND with the UDP / TCP
  * checksum left for the tail bytes [64, len) (pd: the pseudo header + window
  * part). s14 / s15: g[14] / g[15] as the window sums take them (zero where
- * they hold bytes past the frame's byte 64, which the tail pass sums). */
+ * they hold bytes past the frame's byte 64, which the tail pass sums).
+ * Branch-free over IPv4 / IPv6 and UDP / TCP: the pseudo-header addresses
+ * and the segment are one contiguous byte range of the window ([26, 64) for
+ * IPv4, [22, 64) for IPv6), so the L4 sum is one v_dot2 chain whose first two
+ * weights depend on the version. */
 __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t (&f)[16],
 					     uint32_t s14, uint32_t s15, uint32_t len, uint32_t opt,
 					     uint32_t sh, bool qinq)
 {
 	const bool v6 = (f[3] & 0xffffu) == 0xdd86u;
-	uint64_t inf = IF(IFL_L2) | IF(IFL_ETH) | IF(IFL_L3) | IF(IFL_L4) |
-		       (v6 ? IF(IFL_IPV6) : IF(IFL_IPV4));
-	uint32_t fl = 0u;
+	const uint32_t l3 = 14u + 4u * sh;
+	/* input flags, low and high words (the checksum-done / zero bits are
+	 * >= 32) */
+	uint32_t lo = (uint32_t)(IF(IFL_L2) | IF(IFL_ETH) | IF(IFL_L3) | IF(IFL_L4)) |
+		      (v6 ? (uint32_t)IF(IFL_IPV6) : (uint32_t)IF(IFL_IPV4)) |
+		      (sh ? (uint32_t)IF(IFL_VLAN) : 0u) | (qinq ? (uint32_t)IF(IFL_VLAN_QINQ) : 0u) |
+		      (len > 1514u ? (uint32_t)IF(IFL_JUMBO) : 0u) |
+		      ((f[0] & 0x1u) ? (uint32_t)IF(IFL_ETH_MCAST) : 0u) |
+		      (((f[0] == 0xffffffffu) & ((f[1] & 0xffffu) == 0xffffu)) ? (uint32_t)IF(IFL_ETH_BCAST) : 0u);
+	uint32_t hi = 0u;
 
-	p.l2 = 0u;
-	p.l3 = 14u + 4u * sh;
-	if (sh)
-		inf |= IF(IFL_VLAN);
-	if (qinq)
-		inf |= IF(IFL_VLAN_QINQ);
-	if (len > 1514u)
-		inf |= IF(IFL_JUMBO);
-	if (f[0] & 0x1u)
-		inf |= IF(IFL_ETH_MCAST);
-	if (f[0] == 0xffffffffu && (f[1] & 0xffffu) == 0xffffu)
-		inf |= IF(IFL_ETH_BCAST);
+	/* parse_ipv4 (odp_parse.c:113-169): the header checksum over bytes
+	 * 14..33; a bad one is ip_err (no L4 parse, no L4 flag) */
+	const bool ck3 = !v6 & ((opt & ODPG_PKTIN_IPV4_CHKSUM) != 0u);
+	uint32_t hs = gd2(f[3], GW01, 0u);
 
-	bool frag = false;
-	uint32_t proto, pseudo, win, ulen_raw, csum_raw, dport;
+	hs = gd2(f[4], GW11, hs);
+	hs = gd2(f[5], GW11, hs);
+	hs = gd2(f[6], GW11, hs);
+	hs = gd2(f[7], GW11, hs);
+	hs = gd2(f[8], GW10, hs);
+	const bool l3bad = ck3 & (gfold(hs) != 0xffffu);
 
-	if (!v6) {
-		/* parse_ipv4 (odp_parse.c:113-169) */
-		if (opt & ODPG_PKTIN_IPV4_CHKSUM) {
-			uint32_t s = gd2(f[3], GW01, 0u);
+	hi |= ck3 ? (uint32_t)(IF(IFL_L3_CHKSUM_DONE) >> 32) : 0u;
+	const uint32_t lo3 = lo, hi3 = hi;          /* what an ip_err frame keeps */
 
-			s = gd2(f[4], GW11, s);
-			s = gd2(f[5], GW11, s);
-			s = gd2(f[6], GW11, s);
-			s = gd2(f[7], GW11, s);
-			s = gd2(f[8], GW10, s);
-			inf |= IF(IFL_L3_CHKSUM_DONE);
-			if (gfold(s) != 0xffffu) {
-				/* ip_err: no L4 offset, ip_proto 0 -> no L4 flag */
-				p.inf = inf & ~IF(IFL_L4);
-				p.fl = FB(FL_IP_ERR) | FB(FL_L3_CHKSUM_ERR);
-				p.l4 = 0xffffu;
-				return 1;
-			}
-		}
-		frag = (swap16(f[5] & 0xffffu) & 0x3fffu) != 0u;
-		const uint32_t dst_be = __builtin_bswap32(wb<30>(f));
+	const bool frag = !v6 & ((swap16(f[5] & 0xffffu) & 0x3fffu) != 0u);
+	const uint32_t dst_be = __builtin_bswap32(wb<30>(f));
+	const bool mc = v6 ? ((f[9] >> 16) & 0xffu) == 0xffu : (dst_be >> 28) == 0xeu;
 
-		if (frag)
-			inf |= IF(IFL_IPFRAG);
-		if (dst_be == 0xffffffffu)
-			inf |= IF(IFL_IP_BCAST);
-		if ((dst_be >> 28) == 0xeu)
-			inf |= IF(IFL_IP_MCAST);
-		proto = f[5] >> 24;
-		pseudo = gd2(f[8], GW10, gd2(f[7], GW11, gd2(f[6], GW01, 0u)));   /* bytes 26..33 */
-		win = gd2(f[8], GW01, 0u);                                      /* bytes 34..63 */
+	lo |= (frag ? (uint32_t)IF(IFL_IPFRAG) : 0u) |
+	      ((!v6 & (dst_be == 0xffffffffu)) ? (uint32_t)IF(IFL_IP_BCAST) : 0u) |
+	      (mc ? (uint32_t)IF(IFL_IP_MCAST) : 0u);
+	const uint32_t proto = v6 ? (f[5] & 0xffu) : (f[5] >> 24);
+	/* bytes [26, 64) (IPv4: addresses 26..33, segment 34..) or [22, 64)
+	 * (IPv6: addresses 22..53, segment 54..) */
+	uint32_t sum = gd2(f[5], v6 ? GW01 : 0u, 0u);
+
+	sum = gd2(f[6], v6 ? GW11 : GW01, sum);
 #pragma unroll
-		for (int k = 9; k < 14; ++k)
-			win = gd2(f[k], GW11, win);
-		win = gd2(s15, GW11, gd2(s14, GW11, win));
-		ulen_raw = f[9] >> 16;
-		csum_raw = f[10] & 0xffffu;
-		dport = swap16(f[9] & 0xffffu);
-		p.l4 = p.l3 + 20u;
-	} else {
-		/* parse_ipv6 (odp_parse.c:179-245), no extension header */
-		if (((f[9] >> 16) & 0xffu) == 0xffu)
-			inf |= IF(IFL_IP_MCAST);
-		proto = f[5] & 0xffu;
-		pseudo = gd2(f[5], GW01, 0u);                                   /* bytes 22..53 */
-#pragma unroll
-		for (int k = 6; k < 13; ++k)
-			pseudo = gd2(f[k], GW11, pseudo);
-		pseudo = gd2(f[13], GW10, pseudo);
-		win = gd2(s15, GW11, gd2(s14, GW11, gd2(f[13], GW01, 0u)));     /* bytes 54..63 */
-		ulen_raw = f[14] >> 16;
-		csum_raw = f[15] & 0xffffu;
-		dport = swap16(f[14] & 0xffffu);
-		p.l4 = p.l3 + 40u;
-	}
-	bool need = false;
-	uint32_t sum = 0u;
+	for (int k = 7; k < 14; ++k)
+		sum = gd2(f[k], GW11, sum);
+	sum = gd2(s15, GW11, gd2(s14, GW11, sum));
+	const uint32_t uw = v6 ? f[14] : f[9];              /* UDP ports + length */
+	const uint32_t ulen_raw = uw >> 16;
+	const uint32_t csum_raw = (v6 ? f[15] : f[10]) & 0xffffu;
+	const uint32_t l4 = l3 + (v6 ? 40u : 20u);
 	const bool udp = proto == 0x11u;
 
-	if (udp) {                                  /* parse_udp (odp_parse.c:281-322) */
-		const uint32_t udplen = swap16(ulen_raw);
+	lo |= udp ? (uint32_t)IF(IFL_UDP) : (uint32_t)IF(IFL_TCP);
+	/* parse_udp / parse_tcp (odp_parse.c:252-322) */
+	const bool udpck = udp & ((opt & ODPG_PKTIN_UDP_CHKSUM) != 0u) & !frag;
+	const bool tcpck = !udp & ((opt & ODPG_PKTIN_TCP_CHKSUM) != 0u) & !frag;
+	const bool zero = udpck & (csum_raw == 0u);
+	uint32_t fl = (zero & v6) ? FB(FL_L4_CHKSUM_ERR) : 0u;
 
-		inf |= IF(IFL_UDP);
-		if ((opt & ODPG_PKTIN_UDP_CHKSUM) && !frag) {
-			if (csum_raw == 0u) {
-				inf |= IF(IFL_L4_CHKSUM_DONE) | IF(IFL_UDP_CHKSUM_ZERO);
-				if (v6)
-					fl |= FB(FL_L4_CHKSUM_ERR);
-			} else {
-				sum = pseudo + ulen_raw + (0x11u << 8) + win;
-				need = true;
-			}
-		}
-		if (!v6 && dport == 4500u && udplen > 4u && wb<42>(f) != 0u)
-			inf |= IF(IFL_IPSEC) | IF(IFL_IPSEC_UDP);
-	} else {                                    /* parse_tcp (odp_parse.c:252-274) */
-		inf |= IF(IFL_TCP);
-		if ((opt & ODPG_PKTIN_TCP_CHKSUM) && !frag) {
-			sum = pseudo + swap16((len - p.l4) & 0xffffu) + (0x06u << 8) + win;
-			need = true;
-		}
+	hi |= zero ? (uint32_t)((IF(IFL_L4_CHKSUM_DONE) | IF(IFL_UDP_CHKSUM_ZERO)) >> 32) : 0u;
+	/* the IPsec-over-UDP marker (port 4500, a non-zero SPI at byte 42) */
+	if (!v6 & udp & (swap16(uw & 0xffffu) == 4500u) & (swap16(ulen_raw) > 4u) & (wb<42>(f) != 0u)) {
+		lo |= (uint32_t)IF(IFL_IPSEC);
+		hi |= (uint32_t)(IF(IFL_IPSEC_UDP) >> 32);
 	}
-	if (need && !fl) {
-		if (len > 64u) {
-			pd.kind = udp ? 1u : 2u;
-			pd.sum = sum;
-			pd.a = 64u;
-			pd.b = len;
-			p.inf = inf;
-			p.fl = fl;
-			return PARSE_PEND;
-		}
-		/* _odp_packet_l4_chksum (odp_packet.c:1906-1984) within the window */
-		inf |= IF(IFL_L4_CHKSUM_DONE);
-		if (gfold(sum) != 0xffffu)
-			fl |= FB(FL_L4_CHKSUM_ERR) | (udp ? FB(FL_UDP_ERR) : FB(FL_TCP_ERR));
+	const bool need = (udpck & !zero) | tcpck;
+
+	sum += udp ? ulen_raw + (0x11u << 8) : swap16((len - l4) & 0xffffu) + (0x06u << 8);
+	const bool pend = need & (len > 64u);
+	/* _odp_packet_l4_chksum (odp_packet.c:1906-1984) within the window */
+	const bool done = need & !pend;
+	const bool bad = done & (gfold(sum) != 0xffffu);
+
+	hi |= done ? (uint32_t)(IF(IFL_L4_CHKSUM_DONE) >> 32) : 0u;
+	fl |= bad ? FB(FL_L4_CHKSUM_ERR) | (udp ? FB(FL_UDP_ERR) : FB(FL_TCP_ERR)) : 0u;
+	p.l2 = 0u;
+	p.l3 = l3;
+	if (l3bad) {
+		p.inf = ((uint64_t)hi3 << 32) | (lo3 & ~(uint32_t)IF(IFL_L4));
+		p.fl = FB(FL_IP_ERR) | FB(FL_L3_CHKSUM_ERR);
+		p.l4 = 0xffffu;
+		return 1;
 	}
-	p.inf = inf;
+	p.inf = ((uint64_t)hi << 32) | lo;
 	p.fl = fl;
+	p.l4 = l4;
+	if (pend) {
+		pd.kind = udp ? 1u : 2u;
+		pd.sum = sum;
+		pd.a = 64u;
+		pd.b = len;
+		return PARSE_PEND;
+	}
 	return (fl & FL_ERROR_MASK) != 0u;
 }
 
@@ -715,8 +685,8 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 		uint32_t k16 = 0u, k17 = 0u;
 
 		if (fastw) {
-			if (live)
-				ret = parse_fast_gf(p, pd, f, s14, s15, len, opt, sh, qinq);
+			/* dead lanes too (no branch): their results are unused */
+			ret = parse_fast_gf(p, pd, f, s14, s15, len, opt, sh, qinq);
 			bases();
 			const bool v6 = (b.inf_lo & (uint32_t)IF(IFL_IPV6)) != 0u;
 			const bool l4ok = b.l4 != 0xffffu;

@@ -1295,7 +1295,9 @@ int odp_pktin_queue_config(odp_pktio_t hdl, const odp_pktin_queue_param_t *param
 	}
 	UNLOCK();
 	if (rc == 0)
-		rc = odpg_rt_pktin_config(hdl, param->classifier_enable ? 1u : param->num_queues);
+		rc = odpg_rt_pktin_config(hdl, param->classifier_enable ? 1u : param->num_queues,
+					  param->classifier_enable || !param->hash_enable ? 0u :
+					  param->hash_proto.all_bits);
 	return rc;
 }
 

@@ -60,6 +60,7 @@
 #endif
 #define RT_INFLIGHT  4              /* receive bursts in flight per pktio */
 #define RT_MAX_DEV   16             /* device contexts (ODPG_DEVICES) */
+#define RT_MAXQ      16             /* input / output queues of a loop device */
 
 /* ---- objects -------------------------------------------------------------- */
 #define PKT_MAGIC 0x504b5452u
@@ -191,6 +192,7 @@ typedef struct rt_queue {
 	uint32_t gen;              /* registry slot generation (in the handle) */
 	odp_pktio_t pktin;         /* a QUEUE-mode pktin queue: dequeue polls it */
 	odp_pktio_t pktout;        /* a pktout event queue: enqueue transmits */
+	uint32_t pindex;           /* its pktin / pktout queue index */
 } rt_queue_t;
 #define QUEUE_MAGIC 0x51554555u
 
@@ -198,6 +200,7 @@ typedef struct rt_queue {
 typedef struct rx_slot {
 	uint32_t n;                /* frames in the burst */
 	rt_pkt_t *src[RT_BURST];   /* loop device: the transmitted packets */
+	uint8_t qi[RT_BURST];      /* the input queue each came in on */
 	uint8_t *stage, *dstage;   /* frames (pinned host, and its device address) */
 	size_t stage_cap;
 	odpg_desc_t *desc, *ddesc;
@@ -231,12 +234,26 @@ typedef struct rt_pktio {
 	int promisc;
 	uint32_t mtu;
 	uint32_t num_in, num_out;  /* configured input / output queues */
-	rt_queue_t *inq;           /* pktin event queue (QUEUE / SCHED mode) */
-	rt_queue_t *outq;          /* pktout event queue (QUEUE mode) */
+	uint32_t hash_bits;        /* odp_pktin_hash_proto_t of the input queues
+				    * (hash_enable), 0: no hashing */
+	rt_queue_t *inq[RT_MAXQ];  /* pktin event queues (QUEUE / SCHED mode) */
+	rt_queue_t *outq[RT_MAXQ]; /* pktout event queues (QUEUE mode) */
 	pthread_mutex_t ring_lock; /* the loop device's packets in flight */
-	ptr_ring_t ring;           /* the transmitted packets, in order */
-	rt_pkt_t *ahead, *ahead_tail;  /* DIRECT mode: received (classified) packets
-				    * beyond what the last odp_pktin_recv asked for */
+	/* the transmitted packets per input queue, in order (loop.c's loopqs[],
+	 * one queue per input queue: get_dest_queue picks it); ring_n: all
+	 * of them (read unlocked) */
+	ptr_ring_t ring[RT_MAXQ];
+	uint32_t ring_n;
+	uint32_t rr;               /* event modes: the ring a burst starts at */
+	/* DIRECT mode, per input queue: received (classified) packets beyond
+	 * what the last odp_pktin_recv asked for */
+	rt_pkt_t *ahead[RT_MAXQ], *ahead_tail[RT_MAXQ];
+	/* per-queue counters of a device with more than one input / output
+	 * queue (loop.c loopqs[].stats); one queue reports the interface's */
+	struct {
+		uint64_t in_octets, in_packets, in_discards, in_errors;
+		uint64_t out_octets, out_packets;
+	} qst[RT_MAXQ];
 	struct rx_slot *slot[RT_INFLIGHT];  /* receive bursts ("receive pipeline") */
 	/* bursts launched / delivered (wrapping counts): the ones in flight
 	 * sit in slots delivered .. launched - 1 (mod RT_INFLIGHT). launched
@@ -1925,7 +1942,8 @@ void odp_packet_parse_result_multi(const odp_packet_t pkt[], odp_packet_parse_re
 }
 
 /* ---- queues: a registry of tagged handles ---------------------------------- */
-static int pktout_send_impl(odp_pktio_t pktio, const odp_packet_t packets[], int num);
+static int pktout_send_impl(odp_pktio_t pktio, uint32_t index, const odp_packet_t packets[],
+			    int num);
 static void pktin_queue_fill(odp_pktio_t pktio);
 
 #define QH_TAG      0x0DD0000000000000ull  /* no user-space pointer has these bits */
@@ -2141,7 +2159,7 @@ int odp_queue_enq_multi(odp_queue_t queue, const odp_event_t ev[], int num)
 		if (!ev[i])
 			return -1;
 	if (q->pktout)                  /* pktout event queue: transmit */
-		return pktout_send_impl(q->pktout, (const odp_packet_t *)ev, num);
+		return pktout_send_impl(q->pktout, q->pindex, (const odp_packet_t *)ev, num);
 	return queue_push(q, ev, (uint32_t)num) ? -1 : num;
 }
 
@@ -2295,16 +2313,18 @@ void odpg_rt_pktio_close(odp_pktio_t hdl)
 			cpu_relax();
 		if (p->have_cap)
 			odpg_pcap_free(&p->cap);
-		pktio_queue_kill(&p->inq);
-		pktio_queue_kill(&p->outq);
-		for (rt_pkt_t *x = p->ahead; x;) {
-			rt_pkt_t *nx = x->next;
+		for (uint32_t q = 0; q < RT_MAXQ; q++) {
+			pktio_queue_kill(&p->inq[q]);
+			pktio_queue_kill(&p->outq[q]);
+			for (rt_pkt_t *x = p->ahead[q]; x;) {
+				rt_pkt_t *nx = x->next;
 
-			odp_packet_free((odp_packet_t)x);
-			x = nx;
+				odp_packet_free((odp_packet_t)x);
+				x = nx;
+			}
+			p->ahead[q] = p->ahead_tail[q] = NULL;
+			pring_free_packets(&p->ring[q]);
 		}
-		p->ahead = p->ahead_tail = NULL;
-		pring_free_packets(&p->ring);
 		rx_release(p);
 		pthread_mutex_destroy(&p->ring_lock);
 		memset(p, 0, sizeof(*p));
@@ -2313,9 +2333,10 @@ void odpg_rt_pktio_close(odp_pktio_t hdl)
 	pthread_mutex_unlock(&rt.poll_lock);
 }
 
-/* the input queues odp_pktin_queue_config() asked for; QUEUE / SCHED mode
- * get their event queue ("odp-pktin-<i>-<q>", odp_packet_io.c) */
-int odpg_rt_pktin_config(odp_pktio_t hdl, uint32_t num_queues)
+/* the input queues odp_pktin_queue_config() asked for (a loop device up to
+ * RT_MAXQ, loop.c:206-235; a capture one) and their hash protocols; QUEUE /
+ * SCHED mode get their event queues ("odp-pktin-<i>-<q>", odp_packet_io.c) */
+int odpg_rt_pktin_config(odp_pktio_t hdl, uint32_t num_queues, uint32_t hash_bits)
 {
 	rt_pktio_t *p = get_rt_pktio(hdl);
 	odp_queue_param_t qp;
@@ -2325,22 +2346,27 @@ int odpg_rt_pktin_config(odp_pktio_t hdl, uint32_t num_queues)
 		return -1;
 	if (p->in_mode == ODP_PKTIN_MODE_DISABLED)
 		return 0;
-	if (num_queues > 1) {
+	if (num_queues > (p->loopdev ? RT_MAXQ : 1u)) {
 		ERR("pktio %" PRIu64 ": too many input queues\n", (uint64_t)(uintptr_t)hdl);
 		return -1;
 	}
 	p->num_in = num_queues;
+	p->hash_bits = hash_bits;
+	for (uint32_t q = 0; q < RT_MAXQ; q++)
+		pktio_queue_kill(&p->inq[q]);
 	if (p->in_mode != ODP_PKTIN_MODE_QUEUE && p->in_mode != ODP_PKTIN_MODE_SCHED)
 		return 0;
-	pktio_queue_kill(&p->inq);
 	odp_queue_param_init(&qp);
 	qp.type = p->in_mode == ODP_PKTIN_MODE_SCHED ? ODP_QUEUE_TYPE_SCHED : ODP_QUEUE_TYPE_PLAIN;
-	snprintf(name, sizeof(name), "odp-pktin-%u-0", (unsigned)(uintptr_t)hdl);
-	p->inq = queue_new(name, &qp);
-	if (!p->inq)
-		return -1;
-	if (p->in_mode == ODP_PKTIN_MODE_QUEUE)
-		p->inq->pktin = hdl;
+	for (uint32_t q = 0; q < num_queues; q++) {
+		snprintf(name, sizeof(name), "odp-pktin-%u-%u", (unsigned)(uintptr_t)hdl, q);
+		p->inq[q] = queue_new(name, &qp);
+		if (!p->inq[q])
+			return -1;
+		p->inq[q]->pindex = q;
+		if (p->in_mode == ODP_PKTIN_MODE_QUEUE)
+			p->inq[q]->pktin = hdl;
+	}
 	return 0;
 }
 
@@ -2490,18 +2516,35 @@ static int stage_reserve(rx_slot_t *s, size_t need)
 
 /* up to `num` waiting frames into the slot; returns how many (0: none, or
  * no staging memory: the loop device's frames are then dropped) */
-static uint32_t rx_stage(rt_pktio_t *p, rx_slot_t *s, uint32_t num)
+static uint32_t rx_stage(rt_pktio_t *p, rx_slot_t *s, uint32_t num, int queue)
 {
 	uint32_t n = 0;
 	size_t need = 0, off = 0;
 
 	if (p->loopdev) {
 		/* the handles only under the lock (the transmitters wait on
-		 * it); the packets are read after */
-		if (!__atomic_load_n(&p->ring.n, __ATOMIC_ACQUIRE))
+		 * it); the packets are read after. DIRECT mode takes its queue's
+		 * ring (loopback_recv(index)); the event modes take every ring,
+		 * starting at a rotating one, and remember each packet's queue */
+		if (!__atomic_load_n(&p->ring_n, __ATOMIC_ACQUIRE))
 			return 0;
 		pthread_mutex_lock(&p->ring_lock);
-		n = pring_pop(&p->ring, (void **)s->src, num);
+		if (queue >= 0) {
+			n = pring_pop(&p->ring[queue], (void **)s->src, num);
+			memset(s->qi, queue, n);
+		} else {
+			const uint32_t nq = p->num_in ? p->num_in : 1u;
+
+			for (uint32_t j = 0; j < nq && n < num; j++) {
+				const uint32_t q = (p->rr + j) % nq;
+				const uint32_t m = pring_pop(&p->ring[q], (void **)s->src + n, num - n);
+
+				memset(s->qi + n, (int)q, m);
+				n += m;
+			}
+			p->rr = (p->rr + 1u) % nq;
+		}
+		__atomic_store_n(&p->ring_n, p->ring_n - n, __ATOMIC_RELEASE);
 		pthread_mutex_unlock(&p->ring_lock);
 		if (!n)
 			return 0;
@@ -2547,6 +2590,7 @@ static uint32_t rx_stage(rt_pktio_t *p, rx_slot_t *s, uint32_t num)
 			s->desc[k].offset = (uint32_t)off;
 			s->desc[k].len = d.len;
 			s->src[k] = NULL;
+			s->qi[k] = 0;
 			off += ALIGN64(d.len);
 		}
 		p->pos += n;
@@ -2578,10 +2622,36 @@ static int rx_launch(odp_pktio_t hdl, rx_slot_t *s)
 typedef struct rx_out {
 	int ninq, nq;
 	odp_packet_t inq[RX_CHUNK];        /* no CoS queue: the pktin queue / caller */
+	uint8_t inqi[RX_CHUNK];            /* ... of the input queue they came in on */
 	odp_packet_t qp[RX_CHUNK];         /* to a CoS queue */
 	odp_cos_t qcos[RX_CHUNK];
 	odp_queue_t qq[RX_CHUNK];
 } rx_out_t;
+
+/* a multi-queue device's per-queue input counters for one packet's verdict,
+ * as loopback_recv counts them per queue (loop.c:304-374): a parse drop or
+ * an error packet in_errors, no CoS (or a CoS loop) in_discards, a drop CoS
+ * nothing, otherwise in_packets / in_octets; d = -1 takes a delivered
+ * packet back as a discard (no buffer for it) */
+static void qcount(rt_pktio_t *p, uint32_t qi, uint32_t w, uint32_t len, int d)
+{
+	const uint32_t c = ODPG_OUT_COS(w);
+
+	if (qi >= RT_MAXQ)
+		return;
+	if (d < 0) {
+		__atomic_fetch_sub(&p->qst[qi].in_packets, 1u, __ATOMIC_RELAXED);
+		__atomic_fetch_sub(&p->qst[qi].in_octets, len, __ATOMIC_RELAXED);
+		__atomic_fetch_add(&p->qst[qi].in_discards, 1u, __ATOMIC_RELAXED);
+	} else if (c == ODPG_COS_PDROP || (w & ODPG_OUT_ERROR)) {
+		__atomic_fetch_add(&p->qst[qi].in_errors, 1u, __ATOMIC_RELAXED);
+	} else if (c == ODPG_COS_NONE || c == ODPG_COS_LOOP) {
+		__atomic_fetch_add(&p->qst[qi].in_discards, 1u, __ATOMIC_RELAXED);
+	} else if (!(w & ODPG_OUT_CLS_DROP)) {
+		__atomic_fetch_add(&p->qst[qi].in_packets, 1u, __ATOMIC_RELAXED);
+		__atomic_fetch_add(&p->qst[qi].in_octets, len, __ATOMIC_RELAXED);
+	}
+}
 
 /* packets [k0, k1) of a completed burst (k1 - k0 <= RX_CHUNK): verdicts to
  * pools, the packets for the queues into *o (handed over by rx_commit, in
@@ -2628,6 +2698,9 @@ static void rx_deliver_range(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, uint3
 		odp_pool_t pool = p->pool;
 		odp_packet_t pkt;
 
+		if (p->num_in > 1u)
+			qcount(p, s->qi[k], w, len, 0);
+
 		if (ODPG_OUT_COS(w) != ODPG_COS_NOCLS) {
 			q = dest_queue(w, &cos);
 			if (q == ODP_QUEUE_INVALID) {
@@ -2659,6 +2732,8 @@ static void rx_deliver_range(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, uint3
 
 				odpg_cls_pktio_count(hdl, counted ? -1 : 0,
 						     counted ? -(int64_t)len : 0, 1, 0, 0);
+				if (p->num_in > 1u && counted)
+					qcount(p, s->qi[k], w, len, -1);
 				if (q != ODP_QUEUE_INVALID)
 					odpg_cls_queue_count(cos, q, -1, 0);
 				continue;
@@ -2668,6 +2743,7 @@ static void rx_deliver_range(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, uint3
 		PK(pkt)->cos = cos;
 		PK(pkt)->input = hdl;
 		if (q == ODP_QUEUE_INVALID) {
+			o->inqi[o->ninq] = s->qi[k];
 			o->inq[o->ninq++] = pkt;
 		} else {
 			o->qp[o->nq] = pkt;
@@ -2683,7 +2759,7 @@ static void rx_deliver_range(rt_pktio_t *p, odp_pktio_t hdl, rx_slot_t *s, uint3
 	odp_packet_free_multi((const odp_packet_t *)fresh + used, (int)(nfresh - used));
 }
 
-static void to_inq(rt_pktio_t *p, odp_packet_t pkts[], int nret);
+static void to_inq(rt_pktio_t *p, odp_packet_t pkts[], const uint8_t qi[], int nret);
 
 /* a range's packets to their queues: runs of the same (CoS, queue) in one
  * enqueue each (_odp_cls_enq), the rest to the pktin queue, or to out[]
@@ -2702,7 +2778,7 @@ static void rx_commit(rt_pktio_t *p, rx_out_t *o, odp_packet_t out[], int *nret)
 		memcpy(out + *nret, o->inq, (size_t)o->ninq * sizeof(*out));
 		*nret += o->ninq;
 	} else {
-		to_inq(p, o->inq, o->ninq);
+		to_inq(p, o->inq, o->inqi, o->ninq);
 	}
 }
 
@@ -2735,7 +2811,8 @@ static void prof_add(uint64_t bursts, uint64_t pkts, uint64_t t0, uint64_t t1, u
 
 /* DIRECT mode: one burst, launched and waited for. Returns the frames taken
  * (< 0 on a failed launch); *nret packets without a CoS queue in pkts[] */
-static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num, int *nret)
+static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, int queue, odp_packet_t pkts[], int num,
+		    int *nret)
 {
 	rx_slot_t *s;
 
@@ -2745,7 +2822,7 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 	if (num <= 0 || !rt.init || !odpg_cls_pktio_started(hdl) || !(s = slot_get(p, 0)))
 		return 0;
 	const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
-	const uint32_t n = rx_stage(p, s, (uint32_t)num);
+	const uint32_t n = rx_stage(p, s, (uint32_t)num, queue);
 
 	if (!n)
 		return 0;
@@ -2768,14 +2845,28 @@ static int rx_burst(rt_pktio_t *p, odp_pktio_t hdl, odp_packet_t pkts[], int num
 	return (int)n;
 }
 
-/* a delivered burst's packets without a CoS queue onto the pktin event queue */
-static void to_inq(rt_pktio_t *p, odp_packet_t pkts[], int nret)
+/* a delivered burst's packets without a CoS queue onto the pktin event
+ * queue of the input queue each came in on (runs of one queue in one
+ * enqueue) */
+static void to_inq(rt_pktio_t *p, odp_packet_t pkts[], const uint8_t qi[], int nret)
 {
 	const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
 
-	if (nret > 0 && (!p->inq || odp_queue_enq_multi(p->inq->hdl, (const odp_event_t *)pkts,
-							 nret) != nret))
-		odp_packet_free_multi(pkts, nret);
+	for (int i = 0; i < nret;) {
+		int j = i + 1;
+
+		while (j < nret && qi[j] == qi[i])
+			j++;
+		rt_queue_t *q = qi[i] < RT_MAXQ ? p->inq[qi[i]] : NULL;
+
+		int r = q ? odp_queue_enq_multi(q->hdl, (const odp_event_t *)&pkts[i], j - i) : 0;
+
+		if (r < 0)
+			r = 0;
+		if (r < j - i)
+			odp_packet_free_multi(&pkts[i + r], j - i - r);
+		i = j;
+	}
 	if (rxprof.on > 0)
 		__atomic_fetch_add(&rxprof.enq_ns, prof_ns() - t0, __ATOMIC_RELAXED);
 }
@@ -2916,7 +3007,7 @@ static int rx_launch_more(rt_pktio_t *p, odp_pktio_t hdl)
 		const uint32_t inflight = l - __atomic_load_n(&p->delivered, __ATOMIC_ACQUIRE);
 
 		if (inflight >= RT_INFLIGHT ||
-		    (p->loopdev && inflight && __atomic_load_n(&p->ring.n, __ATOMIC_RELAXED) < RT_BURST / 4u))
+		    (p->loopdev && inflight && __atomic_load_n(&p->ring_n, __ATOMIC_RELAXED) < RT_BURST / 4u))
 			break;
 		rx_slot_t *s = slot_get(p, l % RT_INFLIGHT);
 
@@ -2926,7 +3017,7 @@ static int rx_launch_more(rt_pktio_t *p, odp_pktio_t hdl)
 		while (__atomic_load_n(&s->busy, __ATOMIC_ACQUIRE))
 			cpu_relax();
 		const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
-		const uint32_t n = rx_stage(p, s, RT_BURST);
+		const uint32_t n = rx_stage(p, s, RT_BURST, -1);
 
 		if (!n)
 			break;
@@ -3076,9 +3167,12 @@ int odp_pktin_event_queue(odp_pktio_t pktio, odp_queue_t queues[], int num)
 		return 0;
 	if (p->in_mode != ODP_PKTIN_MODE_QUEUE && p->in_mode != ODP_PKTIN_MODE_SCHED)
 		return -1;
-	if (queues && num > 0 && p->inq)
-		queues[0] = p->inq->hdl;
-	return p->inq ? 1 : 0;
+	int n = 0;
+
+	for (uint32_t q = 0; q < p->num_in && p->inq[q]; q++, n++)
+		if (queues && n < num)
+			queues[n] = p->inq[q]->hdl;
+	return n;
 }
 
 /* DIRECT-mode receive: one burst through the GPU classifier */
@@ -3101,9 +3195,12 @@ int odp_pktin_recv(odp_pktin_queue_t queue, odp_packet_t packets[], int num)
 	 * `num` frames at a time, as pcap_recv does: each of its frames needs
 	 * a packet from the pool, and frames read ahead would be dropped when
 	 * the pool is short */
-	if (num > 0 && !p->ahead) {
+	const int qi = queue.index;
+
+	if (num > 0 && !p->ahead[qi]) {
 		odp_packet_t got[RT_BURST];
-		const int rc = rx_burst(p, queue.pktio, got, p->loopdev ? RT_BURST : num, &nret);
+		const int rc = rx_burst(p, queue.pktio, p->loopdev ? qi : -1, got,
+					p->loopdev ? RT_BURST : num, &nret);
 
 		if (rc < 0) {
 			pthread_mutex_unlock(&rt.poll_lock);
@@ -3112,33 +3209,43 @@ int odp_pktin_recv(odp_pktin_queue_t queue, odp_packet_t packets[], int num)
 		for (int k = nret - 1; k >= 0; k--) {
 			rt_pkt_t *x = (rt_pkt_t *)got[k];
 
-			x->next = p->ahead;
-			p->ahead = x;
+			x->next = p->ahead[qi];
+			p->ahead[qi] = x;
 			if (!x->next)
-				p->ahead_tail = x;
+				p->ahead_tail[qi] = x;
 		}
 	}
 	nret = 0;
-	while (nret < num && p->ahead) {
-		rt_pkt_t *x = p->ahead;
+	while (nret < num && p->ahead[qi]) {
+		rt_pkt_t *x = p->ahead[qi];
 
-		p->ahead = x->next;
+		p->ahead[qi] = x->next;
 		x->next = NULL;
 		packets[nret++] = (odp_packet_t)x;
 	}
-	if (!p->ahead)
-		p->ahead_tail = NULL;
+	if (!p->ahead[qi])
+		p->ahead_tail[qi] = NULL;
 	pthread_mutex_unlock(&rt.poll_lock);
 	return nret;
 }
 
-/* per-queue counters: one input / output queue per pktio here, so queue 0
- * carries the interface's counters (loopback_pktin_stats /
- * loopback_pktout_stats, pktio/loop.c:762-786) */
+/* per-queue counters (loopback_pktin_stats / loopback_pktout_stats,
+ * pktio/loop.c:761-785): with one input (output) queue it carries the
+ * interface's counters; a device with several keeps per-queue counts
+ * (qcount at delivery, the send path) */
 static int in_queue_stats(odp_pktio_t pktio, uint32_t index, odp_pktin_queue_stats_t *st)
 {
 	odp_pktio_stats_t s;
+	rt_pktio_t *p = get_rt_pktio(pktio);
 
+	if (p && st && p->num_in > 1u && index < p->num_in) {
+		memset(st, 0, sizeof(*st));
+		st->octets = __atomic_load_n(&p->qst[index].in_octets, __ATOMIC_RELAXED);
+		st->packets = __atomic_load_n(&p->qst[index].in_packets, __ATOMIC_RELAXED);
+		st->discards = __atomic_load_n(&p->qst[index].in_discards, __ATOMIC_RELAXED);
+		st->errors = __atomic_load_n(&p->qst[index].in_errors, __ATOMIC_RELAXED);
+		return 0;
+	}
 	if (!st || index != 0 || odp_pktio_stats(pktio, &s))
 		return -1;
 	memset(st, 0, sizeof(*st));
@@ -3152,7 +3259,14 @@ static int in_queue_stats(odp_pktio_t pktio, uint32_t index, odp_pktin_queue_sta
 static int out_queue_stats(odp_pktio_t pktio, uint32_t index, odp_pktout_queue_stats_t *st)
 {
 	odp_pktio_stats_t s;
+	rt_pktio_t *p = get_rt_pktio(pktio);
 
+	if (p && st && p->num_out > 1u && index < p->num_out) {
+		memset(st, 0, sizeof(*st));
+		st->octets = __atomic_load_n(&p->qst[index].out_octets, __ATOMIC_RELAXED);
+		st->packets = __atomic_load_n(&p->qst[index].out_packets, __ATOMIC_RELAXED);
+		return 0;
+	}
 	if (!st || index != 0 || odp_pktio_stats(pktio, &s))
 		return -1;
 	memset(st, 0, sizeof(*st));
@@ -3178,10 +3292,12 @@ int odp_pktin_event_queue_stats(odp_pktio_t pktio, odp_queue_t queue,
 {
 	rt_pktio_t *p = get_rt_pktio(pktio);
 
-	if (!p || (p->in_mode != ODP_PKTIN_MODE_SCHED && p->in_mode != ODP_PKTIN_MODE_QUEUE) ||
-	    !p->inq || queue != p->inq->hdl)
+	if (!p || (p->in_mode != ODP_PKTIN_MODE_SCHED && p->in_mode != ODP_PKTIN_MODE_QUEUE))
 		return -1;
-	return in_queue_stats(pktio, 0, stats);
+	for (uint32_t q = 0; q < p->num_in; q++)
+		if (p->inq[q] && queue == p->inq[q]->hdl)
+			return in_queue_stats(pktio, q, stats);
+	return -1;
 }
 
 /* ---- scheduler -------------------------------------------------------------- */
@@ -3286,8 +3402,8 @@ int odp_pktio_capability(odp_pktio_t pktio, odp_pktio_capability_t *capa)
 	if (!get_rt_pktio(pktio) || !capa)
 		return -1;
 	memset(capa, 0, sizeof(*capa));
-	capa->max_input_queues = 1;
-	capa->max_output_queues = 1;
+	capa->max_input_queues = get_rt_pktio(pktio)->loopdev ? RT_MAXQ : 1u;
+	capa->max_output_queues = RT_MAXQ;
 	odp_pktio_config_init(&capa->config);
 	capa->config.pktin.bit.ipv4_chksum = 1;
 	capa->config.pktin.bit.udp_chksum = 1;
@@ -3321,21 +3437,25 @@ int odp_pktout_queue_config(odp_pktio_t pktio, const odp_pktout_queue_param_t *p
 		return -1;
 	if (p->out_mode == ODP_PKTOUT_MODE_DISABLED)
 		return 0;
-	if (param->num_queues == 0 || param->num_queues > 1) {
+	if (param->num_queues == 0 || param->num_queues > RT_MAXQ) {
 		ERR("pktio %" PRIu64 ": invalid number of output queues\n",
 		    (uint64_t)(uintptr_t)pktio);
 		return -1;
 	}
 	p->num_out = param->num_queues;
+	for (uint32_t q = 0; q < RT_MAXQ; q++)
+		pktio_queue_kill(&p->outq[q]);
 	if (p->out_mode != ODP_PKTOUT_MODE_QUEUE)
 		return 0;
-	pktio_queue_kill(&p->outq);
 	odp_queue_param_init(&qp);
-	snprintf(name, sizeof(name), "odp-pktout-%u-0", (unsigned)(uintptr_t)pktio);
-	p->outq = queue_new(name, &qp);
-	if (!p->outq)
-		return -1;
-	p->outq->pktout = pktio;
+	for (uint32_t q = 0; q < p->num_out; q++) {
+		snprintf(name, sizeof(name), "odp-pktout-%u-%u", (unsigned)(uintptr_t)pktio, q);
+		p->outq[q] = queue_new(name, &qp);
+		if (!p->outq[q])
+			return -1;
+		p->outq[q]->pktout = pktio;
+		p->outq[q]->pindex = q;
+	}
 	return 0;
 }
 
@@ -3368,16 +3488,92 @@ int odp_pktout_event_queue(odp_pktio_t pktio, odp_queue_t queues[], int num)
 		return 0;
 	if (p->out_mode != ODP_PKTOUT_MODE_QUEUE)
 		return -1;
-	if (queues && num > 0 && p->outq)
-		queues[0] = p->outq->hdl;
-	return p->outq ? 1 : 0;
+	int n = 0;
+
+	for (uint32_t q = 0; q < p->num_out && p->outq[q]; q++, n++)
+		if (queues && n < num)
+			queues[n] = p->outq[q]->hdl;
+	return n;
+}
+
+/* odp_hash_crc32c (Castagnoli, reflected, no final inversion; the table
+ * built once) */
+static uint32_t crc32c_tbl[256];
+static pthread_once_t crc32c_once = PTHREAD_ONCE_INIT;
+
+static void crc32c_init(void)
+{
+	for (uint32_t i = 0; i < 256; i++) {
+		uint32_t c = i;
+
+		for (int k = 0; k < 8; k++)
+			c = (c & 1u) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+		crc32c_tbl[i] = c;
+	}
+}
+
+static uint32_t crc32c(const uint8_t *d, uint32_t len, uint32_t crc)
+{
+	pthread_once(&crc32c_once, crc32c_init);
+	for (uint32_t i = 0; i < len; i++)
+		crc = crc32c_tbl[(crc ^ d[i]) & 0xffu] ^ (crc >> 8);
+	return crc;
+}
+
+/* get_dest_queue (pktio/loop.c:472-523): the input queue a transmitted
+ * packet goes to. Without hashing the queue of the pktout index; with it
+ * the crc32c of the UDP / TCP ports and the IPv4 / IPv6 addresses the
+ * packet's parse result names (those whose header lies inside the packet),
+ * modulo the input queues. The GPU batch form is odpg_tx_prepare
+ * (include/odpg_tx.h); one send burst is too small for a launch. */
+static uint32_t loop_dest_queue(const rt_pktio_t *p, const rt_pkt_t *k, uint32_t index)
+{
+	const uint32_t nq = p->num_in ? p->num_in : 1u, h = p->hash_bits;
+	const uint64_t inf = k->meta.input_flags;
+	uint8_t data[2 * 2 + 2 * 16];
+	uint32_t n = 0, off;
+
+	if (h == 0u)
+		return index % nq;
+	off = k->meta.l4_offset;
+	if (off != ODP_PACKET_OFFSET_INVALID) {
+		if ((h & 0x9u) && ((inf >> IF_UDP) & 1u)) {          /* ipv4_udp | ipv6_udp */
+			if (off + 8u <= k->len) {
+				memcpy(data, k->data + off, 4);     /* source, destination port */
+				n = 4;
+			}
+		} else if ((h & 0x12u) && ((inf >> IF_TCP) & 1u)) {  /* ipv4_tcp | ipv6_tcp */
+			if (off + 20u <= k->len) {
+				memcpy(data, k->data + off, 4);
+				n = 4;
+			}
+		}
+	}
+	off = k->meta.l3_offset;
+	if (off != ODP_PACKET_OFFSET_INVALID) {
+		if ((h & 0x4u) && ((inf >> IF_IPV4) & 1u)) {
+			if (off + 20u <= k->len) {
+				memcpy(data + n, k->data + off + 12u, 8);   /* source, destination */
+				n += 8;
+			}
+		} else if ((h & 0x20u) && ((inf >> IF_IPV6) & 1u)) {
+			if (off + 40u <= k->len) {
+				memcpy(data + n, k->data + off + 8u, 32);
+				n += 32;
+			}
+		}
+	}
+	return crc32c(data, n, 0u) % nq;
 }
 
 /* transmit (loopback_send, pktio/loop.c:525-580): on a loop device the
- * packets go back to its input, up to the first one over the MTU (-1 if
- * that is the first); the pcap device here has no output file, so its
- * packets are consumed. Counted as out_packets / out_octets. */
-static int pktout_send_impl(odp_pktio_t pktio, const odp_packet_t packets[], int num)
+ * packets go back to its input, each to the input queue get_dest_queue
+ * picks, up to the first one over the MTU (-1 if that is the first); the
+ * pcap device here has no output file, so its packets are consumed.
+ * Counted as out_packets / out_octets (per output queue `index` on a device
+ * with several). */
+static int pktout_send_impl(odp_pktio_t pktio, uint32_t index, const odp_packet_t packets[],
+			    int num)
 {
 	rt_pktio_t *p = get_rt_pktio(pktio);
 	uint64_t octets = 0;
@@ -3398,16 +3594,58 @@ static int pktout_send_impl(odp_pktio_t pktio, const odp_packet_t packets[], int
 		octets += k->len;
 	}
 	if (p->loopdev) {
-		pthread_mutex_lock(&p->ring_lock);
-		const int full = pring_push(&p->ring, (void *const *)packets, (uint32_t)n);
+		uint8_t qd[RT_BURST];
+		int full = 0;
 
+		/* the picks read the packets' headers: before the lock */
+		if (p->num_in > 1u) {
+			if (n > RT_BURST)
+				n = RT_BURST;
+			octets = 0;
+			for (int i = 0; i < n; i++) {
+				qd[i] = (uint8_t)loop_dest_queue(p, PK(packets[i]), index);
+				octets += PK(packets[i])->len;
+			}
+		}
+		pthread_mutex_lock(&p->ring_lock);
+		if (p->num_in > 1u) {
+			/* runs of one queue in one push; the packets of a run go
+			 * in whole or not at all (no memory for the ring) */
+			int i = 0;
+
+			while (i < n && !full) {
+				int j = i + 1;
+
+				while (j < n && qd[j] == qd[i])
+					j++;
+				full = pring_push(&p->ring[qd[i]], (void *const *)&packets[i],
+						  (uint32_t)(j - i));
+				if (!full)
+					i = j;
+			}
+			if (full) {             /* sent: the packets before the run */
+				octets = 0;
+				for (int k = 0; k < i; k++)
+					octets += PK(packets[k])->len;
+				n = i;
+			}
+		} else {
+			full = pring_push(&p->ring[0], (void *const *)packets, (uint32_t)n);
+			if (full)
+				n = 0;
+		}
+		__atomic_store_n(&p->ring_n, p->ring_n + (uint32_t)n, __ATOMIC_RELEASE);
 		pthread_mutex_unlock(&p->ring_lock);
-		if (full)
+		if (!n)
 			return 0;       /* no memory for the ring: nothing sent */
 	} else {
 		odp_packet_free_multi(packets, n);
 	}
 	odpg_cls_pktio_count(pktio, 0, 0, 0, (uint64_t)n, octets);
+	if (p->num_out > 1u && index < RT_MAXQ) {
+		__atomic_fetch_add(&p->qst[index].out_packets, (uint64_t)n, __ATOMIC_RELAXED);
+		__atomic_fetch_add(&p->qst[index].out_octets, octets, __ATOMIC_RELAXED);
+	}
 	return n;
 }
 
@@ -3418,7 +3656,7 @@ int odp_pktout_send(odp_pktout_queue_t queue, const odp_packet_t packets[], int 
 	if (!p || p->out_mode != ODP_PKTOUT_MODE_DIRECT || queue.index < 0 ||
 	    (uint32_t)queue.index >= p->num_out)
 		return -1;
-	return pktout_send_impl(queue.pktio, packets, num);
+	return pktout_send_impl(queue.pktio, (uint32_t)queue.index, packets, num);
 }
 
 /* odp_pktout_queue_stats (odp_packet_io.c:1771-1805): DIRECT mode */
@@ -3438,10 +3676,12 @@ int odp_pktout_event_queue_stats(odp_pktio_t pktio, odp_queue_t queue,
 {
 	rt_pktio_t *p = get_rt_pktio(pktio);
 
-	if (!p || p->out_mode != ODP_PKTOUT_MODE_QUEUE || !p->outq ||
-	    queue != p->outq->hdl)
+	if (!p || p->out_mode != ODP_PKTOUT_MODE_QUEUE)
 		return -1;
-	return out_queue_stats(pktio, 0, stats);
+	for (uint32_t q = 0; q < p->num_out; q++)
+		if (p->outq[q] && queue == p->outq[q]->hdl)
+			return out_queue_stats(pktio, q, stats);
+	return -1;
 }
 
 int odp_pktio_promisc_mode(odp_pktio_t pktio)

@@ -20,9 +20,10 @@ int  odpg_rt_pktio_open(odp_pktio_t pktio, const char *name, odp_pool_t pool,
 void odpg_rt_pktio_close(odp_pktio_t pktio);
 /* odp_rt.c: odp_pktio_stop delivers the receive bursts still in flight */
 void odpg_rt_pktio_drain(odp_pktio_t pktio);
-/* odp_rt.c: odp_pktin_queue_config's input queues (the event queue of
- * SCHED / QUEUE mode); 0 or -1 (too many queues) */
-int  odpg_rt_pktin_config(odp_pktio_t pktio, uint32_t num_queues);
+/* odp_rt.c: odp_pktin_queue_config's input queues (the event queues of
+ * SCHED / QUEUE mode) and their hash protocols (odp_pktin_hash_proto_t bits,
+ * 0 without hash_enable); 0 or -1 (too many queues) */
+int  odpg_rt_pktin_config(odp_pktio_t pktio, uint32_t num_queues, uint32_t hash_bits);
 
 /* odp_cls.c: odpg_pktio_recv_batch's host path, also writing the parse
  * result of every packet (meta may be NULL) */

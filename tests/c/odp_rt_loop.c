@@ -21,6 +21,12 @@
  *      out exactly once, and each thread sees one sender's packets in
  *      sending order (the receive pipeline's chunked delivery keeps queue
  *      order).
+ *   G  4 input queues (DIRECT and SCHED), 2 output queues: with hashing
+ *      (ipv4_udp + ipv4) every packet arrives once, on the input queue the
+ *      oracle's crc32c pick names (loop.c get_dest_queue over the parse
+ *      result the sender's odp_packet_parse gave it), in sending order per
+ *      queue, with per-queue counters; without hashing on the input queue
+ *      of its output queue index (index % queues).
  * Plus the pktio lookup / duplicate-open rule and the mode checks of the
  * queue accessors (odp_packet_io.c:406-410, 798-829, 1696-1843, 2364-2503),
  * and close refused while started (odp_packet_io.c:507-510).
@@ -36,6 +42,9 @@
 #include <odp/helper/odph_api.h>
 
 #define NPKT 300
+
+/* oracle/odp_oracle.c (test infrastructure): odp_hash_crc32c */
+uint32_t oracle_crc32c(const uint8_t *p, uint32_t len, uint32_t init);
 
 static int fails;
 
@@ -320,6 +329,157 @@ static void case_sched_cls(odp_pool_t pool)
 	printf("B sched+cls: %d packets, %d to net10, %d to default\n", got, n_net, n_def);
 }
 
+/* G: the input queue loop.c's get_dest_queue picks for frame k with
+ * ipv4_udp + ipv4 hashing over nq queues: crc32c of the UDP ports and the
+ * IPv4 addresses (none for the ARP frames: queue 0) */
+static int expected_queue(int k, int nq)
+{
+	uint8_t d[12] = {0};
+
+	if (k % 10 == 9)
+		return (int)(oracle_crc32c(d, 0, 0) % (uint32_t)nq);
+	memcpy(d, frame[k] + 34, 4);
+	memcpy(d + 4, frame[k] + 26, 8);
+	return (int)(oracle_crc32c(d, 12, 0) % (uint32_t)nq);
+}
+
+#define MQ_IN  4
+#define MQ_OUT 2
+
+static void case_multiqueue(odp_pool_t pool, odp_pktin_mode_t mode, int hash)
+{
+	odp_pktio_param_t pp;
+	odp_pktin_queue_param_t ip;
+	odp_pktout_queue_param_t op;
+	odp_pktio_capability_t capa;
+	odp_pktin_queue_t inq[MQ_IN];
+	odp_queue_t evq[MQ_IN];
+	odp_pktout_queue_t outq[MQ_OUT];
+	odp_packet_parse_param_t prm;
+	int cnt[MQ_IN] = {0}, last[MQ_IN], got = 0, where_ok = 1, order_ok = 1;
+	uint64_t oct[MQ_IN] = {0};
+	const char *mname = mode == ODP_PKTIN_MODE_DIRECT ? "direct" : "sched";
+
+	odp_pktio_param_init(&pp);
+	pp.in_mode = mode;
+	pp.out_mode = ODP_PKTOUT_MODE_DIRECT;
+	odp_pktio_t pktio = odp_pktio_open("loop3", pool, &pp);
+
+	CHECK(pktio != ODP_PKTIO_INVALID, "open loop3");
+	if (pktio == ODP_PKTIO_INVALID)
+		return;
+	CHECK(odp_pktio_capability(pktio, &capa) == 0 && capa.max_input_queues >= MQ_IN &&
+	      capa.max_output_queues >= MQ_OUT, "multi-queue capability");
+	odp_pktin_queue_param_init(&ip);
+	ip.num_queues = MQ_IN;
+	ip.hash_enable = hash;
+	ip.hash_proto.proto.ipv4_udp = 1;
+	ip.hash_proto.proto.ipv4 = 1;
+	odp_pktout_queue_param_init(&op);
+	op.num_queues = MQ_OUT;
+	CHECK(odp_pktin_queue_config(pktio, &ip) == 0, "%d input queues", MQ_IN);
+	CHECK(odp_pktout_queue_config(pktio, &op) == 0, "%d output queues", MQ_OUT);
+	if (mode == ODP_PKTIN_MODE_DIRECT)
+		CHECK(odp_pktin_queue(pktio, inq, MQ_IN) == MQ_IN, "odp_pktin_queue: %d", MQ_IN);
+	else
+		CHECK(odp_pktin_event_queue(pktio, evq, MQ_IN) == MQ_IN, "event queues: %d", MQ_IN);
+	CHECK(odp_pktout_queue(pktio, outq, MQ_OUT) == MQ_OUT, "odp_pktout_queue: %d", MQ_OUT);
+	CHECK(odp_pktio_start(pktio) == 0, "start");
+	memset(&prm, 0, sizeof(prm));
+	prm.proto = ODP_PROTO_ETH;
+	prm.last_layer = ODP_PROTO_LAYER_ALL;
+	for (int k = 0; k < NPKT; k++) {
+		odp_packet_t pkt = odp_packet_alloc(pool, flen[k]);
+
+		CHECK(pkt != ODP_PACKET_INVALID, "alloc");
+		if (pkt == ODP_PACKET_INVALID)
+			break;
+		memcpy(odp_packet_data(pkt), frame[k], flen[k]);
+		CHECK(odp_packet_parse(pkt, 0, &prm) == 0, "parse frame %d", k);
+		if (odp_pktout_send(outq[k % MQ_OUT], &pkt, 1) != 1) {
+			CHECK(0, "send frame %d", k);
+			odp_packet_free(pkt);
+		}
+	}
+	for (int q = 0; q < MQ_IN; q++)
+		last[q] = -1;
+	/* a received packet: its queue and its place in that queue's order */
+	#define MQ_TAKE(pkt, q) do { \
+		const int k_ = which_frame(pkt); \
+		const int want_ = k_ < 0 ? -1 : hash ? expected_queue(k_, MQ_IN) : (k_ % MQ_OUT) % MQ_IN; \
+		if (k_ < 0 || want_ != (q)) \
+			where_ok = 0; \
+		if (k_ <= last[q]) \
+			order_ok = 0; \
+		if (k_ >= 0) { \
+			last[q] = k_; \
+			oct[q] += flen[k_]; \
+		} \
+		cnt[q]++; \
+		got++; \
+		odp_packet_free(pkt); \
+	} while (0)
+	if (mode == ODP_PKTIN_MODE_DIRECT) {
+		odp_packet_t pkts[64];
+
+		for (int q = 0; q < MQ_IN; q++) {
+			int n;
+
+			while ((n = odp_pktin_recv(inq[q], pkts, 64)) > 0)
+				for (int i = 0; i < n; i++)
+					MQ_TAKE(pkts[i], q);
+			CHECK(n == 0, "odp_pktin_recv on queue %d: %d", q, n);
+		}
+	} else {
+		for (;;) {
+			odp_queue_t from;
+			odp_event_t ev = odp_schedule(&from,
+						      odp_schedule_wait_time(200 * ODP_TIME_MSEC_IN_NS));
+			int q = -1;
+
+			if (ev == ODP_EVENT_INVALID)
+				break;
+			for (int j = 0; j < MQ_IN; j++)
+				if (from == evq[j])
+					q = j;
+			CHECK(q >= 0, "scheduled from a pktin event queue");
+			if (q < 0) {
+				odp_event_free(ev);
+				continue;
+			}
+			MQ_TAKE(odp_packet_from_event(ev), q);
+		}
+	}
+	#undef MQ_TAKE
+	CHECK(got == NPKT, "G %s hash=%d: received %d of %d", mname, hash, got, NPKT);
+	CHECK(where_ok, "G %s hash=%d: every packet on the queue the pick names", mname, hash);
+	CHECK(order_ok, "G %s hash=%d: sending order per queue", mname, hash);
+	int used = 0;
+
+	for (int q = 0; q < MQ_IN; q++) {
+		odp_pktin_queue_stats_t is;
+
+		used += cnt[q] > 0;
+		if (mode == ODP_PKTIN_MODE_DIRECT)
+			CHECK(odp_pktin_queue_stats(inq[q], &is) == 0 && is.packets == (uint64_t)cnt[q] &&
+			      is.octets == oct[q], "queue %d stats %lu vs %d", q,
+			      (unsigned long)is.packets, cnt[q]);
+		else
+			CHECK(odp_pktin_event_queue_stats(pktio, evq[q], &is) == 0 &&
+			      is.packets == (uint64_t)cnt[q], "event queue %d stats", q);
+	}
+	CHECK(used == (hash ? MQ_IN : MQ_OUT), "G %s hash=%d: %d queues used", mname, hash, used);
+	for (int q = 0; q < MQ_OUT; q++) {
+		odp_pktout_queue_stats_t os;
+
+		CHECK(odp_pktout_queue_stats(outq[q], &os) == 0 && os.packets == NPKT / MQ_OUT,
+		      "output queue %d stats", q);
+	}
+	CHECK(odp_pktio_stop(pktio) == 0 && odp_pktio_close(pktio) == 0, "stop / close");
+	printf("G %s hash=%d: %d packets over queues %d/%d/%d/%d, in order\n", mname, hash, got,
+	       cnt[0], cnt[1], cnt[2], cnt[3]);
+}
+
 /* F: multi-threaded scheduled receive (chunked delivery) */
 #define MT_RX 4
 #define MT_N  200000
@@ -596,6 +756,9 @@ int main(void)
 	case_queue(pool);
 	case_pcap_loops(pool);
 	case_pcap_small_pool();
+	case_multiqueue(pool, ODP_PKTIN_MODE_DIRECT, 1);
+	case_multiqueue(pool, ODP_PKTIN_MODE_SCHED, 1);
+	case_multiqueue(pool, ODP_PKTIN_MODE_DIRECT, 0);
 	mt_inst = inst;
 	case_sched_mt();
 	CHECK(odp_pool_destroy(pool) == 0, "pool destroy");

@@ -159,6 +159,8 @@ def test_loop_device_through_gpu_classifier():
     assert "A direct: received 300" in r.stdout and "C queue: 300 packets" in r.stdout
     assert "D pcap loops=3: 40 packets" in r.stdout
     assert "E pcap small pool: 20 packets" in r.stdout
+    for m in ("direct hash=1", "sched hash=1", "direct hash=0"):
+        assert f"G {m}: 300 packets" in r.stdout, r.stdout[-3000:]
 
 
 @pytest.mark.gpu

@@ -47,3 +47,4 @@ def test_runtime_under_sanitizer(san_build, prog, san):
     if prog == "odp_rt_loop":
         assert "F sched, 4 threads: 200000 packets, each once and in order per thread" in r.stdout
         assert "B sched+cls: 300 packets, 150 to net10, 150 to default" in r.stdout
+        assert "G sched hash=1: 300 packets" in r.stdout
