@@ -340,7 +340,11 @@ __device__ __forceinline__ void gf_probes(const uint4 *__restrict__ xmg, uint32_
 #pragma unroll
 	for (int u = 0; u < U; ++u) {
 		if constexpr (NW == 2) {
+			/* whole ds_read_b128 (the unused fourth word kept: narrowed
+			 * to ds_read_b96 it takes twice the LDS cycles) */
 			const uint4 x = *(const uint4 *)(tb + 4u * e[u]);
+
+			asm volatile("" ::"v"(x.w));
 
 			m[u][0] = x.x;
 			m[u][1] = x.y;
@@ -736,13 +740,11 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 				k17 = key(17u);
 		}
 		if constexpr (!KX) {
-			/* slots 16..18 into their key-vector words (uniform) */
-			if ((kpos & 0xffu) < 16u)
-				kv[kpos & 15u] = k16;
-			if (((kpos >> 8) & 0xffu) < 16u)
-				kv[(kpos >> 8) & 15u] = k17;
-			if (((kpos >> 16) & 0xffu) < 16u)
-				kv[(kpos >> 16) & 15u] = len;
+			/* slots 16..18 into their key-vector words (uniform; three
+			 * distinct words no group's slot < 16 uses, cls_compile.cpp) */
+			kv[kpos & 15u] = k16;
+			kv[(kpos >> 8) & 15u] = k17;
+			kv[(kpos >> 16) & 15u] = len;
 		}
 		/* the hit map: each group's masked key word, once per packet.
 		 * Single-word rules OR their bits in; a complex rule's chain bit

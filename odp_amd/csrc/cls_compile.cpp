@@ -1198,9 +1198,11 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 			gcut[kind] = (uint32_t)gorder.size();
 	}
 	/* the kernel's 16-word key vector: slot s < 16 at word s; slots 16..18
-	 * (L4 + 0, L4 + 4, frame length) in words no group's slot uses, when
-	 * the groups read at most 16 slots (else xm_kx: the kernel selects
-	 * them per probe) */
+	 * (L4 + 0, L4 + 4, frame length) in three words no group's slot < 16
+	 * uses (the kernel writes all three unconditionally: a conditional
+	 * indexed write compiled to a copy and a select of the whole vector),
+	 * when at least three are free (else xm_kx: the kernel selects them per
+	 * probe) */
 	uint32_t kused = 0, kpos[3] = {0xffu, 0xffu, 0xffu};
 	bool kx = false;
 
@@ -1209,18 +1211,14 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 	{
 		uint32_t freew = ~kused & 0xffffu;
 
-		for (uint32_t s = 16; s < 19; s++) {
-			if (!((kused >> s) & 1u))
-				continue;
-			if (!freew) {
-				kx = true;
-				break;
+		if (__builtin_popcount(freew) < 3) {
+			kx = true;
+		} else {
+			for (uint32_t s = 16; s < 19; s++) {
+				kpos[s - 16] = (uint32_t)__builtin_ctz(freew);
+				freew &= freew - 1u;
 			}
-			kpos[s - 16] = (uint32_t)__builtin_ctz(freew);
-			freew &= freew - 1u;
 		}
-		if (kx)
-			kpos[0] = kpos[1] = kpos[2] = 0xffu;
 	}
 	for (size_t go = 0; xm && go < gorder.size(); ++go) {
 		const auto git = gorder[go];

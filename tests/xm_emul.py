@@ -128,10 +128,10 @@ class XmTable:
         if not self.kx:
             for s in range(16):
                 kvec[s] = key(s)
+            assert len(set(self.kpos)) == 3 and max(self.kpos) < 16, self.kpos
             for k in range(3):
-                if self.kpos[k] != 0xFF:
-                    assert not any(int(g[2]) >> 8 == self.kpos[k] for g in self.groups)
-                    kvec[self.kpos[k]] = key(16 + k)
+                assert not any(int(g[2]) >> 8 == self.kpos[k] for g in self.groups)
+                kvec[self.kpos[k]] = key(16 + k)
         for gi, g in enumerate(self.groups):
             mul, shf, kw, eb, gthr, req, gmask, l3mask = (int(x) for x in g[:8])
             slot = kw >> 8
