@@ -71,7 +71,7 @@
 #define GF_WAVES_S64W 6
 #endif
 #ifndef GF_WAVES_S64C       /* ... counted */
-#define GF_WAVES_S64C 5
+#define GF_WAVES_S64C 6
 #endif
 #define GF_WAVES_S64(cm, nw) ((nw) == 2 ? ((cm) == 0 ? GF_WAVES_S64W : GF_WAVES_S64C) : GF_WAVES_WIDE)
 #ifndef GF_RW               /* LDS row stride per lane, dwords (16-byte multiple) */
@@ -171,11 +171,15 @@ __device__ __forceinline__ bool plain_gf(const uint32_t (&f)[16], uint32_t x16, 
 	/* IPv4 with IHL 5: protocol byte 23, UDP length at 38, TCP data offset
 	 * at 46; IPv6: next header byte 20, UDP length at 58, port at 56, TCP
 	 * data offset past the window (x16) */
-	const uint32_t proto = v6 ? (f[5] & 0xffu) : (f[5] >> 24);
+	/* both versions' fields computed, then selected (a ?: with a call in
+	 * an arm is emitted as a branch, which stays one in divergent code) */
+	const uint32_t proto4 = f[5] >> 24, proto6 = f[5] & 0xffu;
+	const uint32_t proto = v6 ? proto6 : proto4;
 	const uint32_t uw = v6 ? f[14] : f[9];
-	const bool udp_ok = (proto == 0x11u) & (swap16(uw >> 16) >= 8u) &
-			    !(v6 & (swap16(uw & 0xffffu) == 4500u));
-	const uint32_t doff = v6 ? (x16 >> 20) & 0xfu : (f[11] >> 20) & 0xfu;
+	const uint32_t ulen = swap16(uw >> 16), uport = swap16(uw & 0xffffu);
+	const bool udp_ok = (proto == 0x11u) & (ulen >= 8u) & !(v6 & (uport == 4500u));
+	const uint32_t doff4 = (f[11] >> 20) & 0xfu, doff6 = (x16 >> 20) & 0xfu;
+	const uint32_t doff = v6 ? doff6 : doff4;
 	const bool tcp_ok = (proto == 0x06u) & (doff >= 5u) & !(v6 & ((sh != 0u) | (len < 74u)));
 
 	return (len >= 64u) & (v4 | v6) & (udp_ok | tcp_ok);
@@ -223,12 +227,14 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 
 	const bool frag = !v6 & ((swap16(f[5] & 0xffffu) & 0x3fffu) != 0u);
 	const uint32_t dst_be = __builtin_bswap32(wb<30>(f));
-	const bool mc = v6 ? ((f[9] >> 16) & 0xffu) == 0xffu : (dst_be >> 28) == 0xeu;
+	const bool mc6 = ((f[9] >> 16) & 0xffu) == 0xffu, mc4 = (dst_be >> 28) == 0xeu;
+	const bool mc = v6 ? mc6 : mc4;
 
 	lo |= (frag ? (uint32_t)IF(IFL_IPFRAG) : 0u) |
 	      ((!v6 & (dst_be == 0xffffffffu)) ? (uint32_t)IF(IFL_IP_BCAST) : 0u) |
 	      (mc ? (uint32_t)IF(IFL_IP_MCAST) : 0u);
-	const uint32_t proto = v6 ? (f[5] & 0xffu) : (f[5] >> 24);
+	const uint32_t proto4 = f[5] >> 24, proto6 = f[5] & 0xffu;
+	const uint32_t proto = v6 ? proto6 : proto4;
 	/* bytes [26, 64) (IPv4: addresses 26..33, segment 34..) or [22, 64)
 	 * (IPv6: addresses 22..53, segment 54..) */
 	uint32_t sum = gd2(f[5], v6 ? GW01 : 0u, 0u);
@@ -240,7 +246,8 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 	sum = gd2(s15, GW11, gd2(s14, GW11, sum));
 	const uint32_t uw = v6 ? f[14] : f[9];              /* UDP ports + length */
 	const uint32_t ulen_raw = uw >> 16;
-	const uint32_t csum_raw = (v6 ? f[15] : f[10]) & 0xffffu;
+	const uint32_t cw = v6 ? f[15] : f[10];
+	const uint32_t csum_raw = cw & 0xffffu;
 	const uint32_t l4 = l3 + (v6 ? 40u : 20u);
 	const bool udp = proto == 0x11u;
 
@@ -253,13 +260,17 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 
 	hi |= zero ? (uint32_t)((IF(IFL_L4_CHKSUM_DONE) | IF(IFL_UDP_CHKSUM_ZERO)) >> 32) : 0u;
 	/* the IPsec-over-UDP marker (port 4500, a non-zero SPI at byte 42) */
-	if (!v6 & udp & (swap16(uw & 0xffffu) == 4500u) & (swap16(ulen_raw) > 4u) & (wb<42>(f) != 0u)) {
-		lo |= (uint32_t)IF(IFL_IPSEC);
-		hi |= (uint32_t)(IF(IFL_IPSEC_UDP) >> 32);
-	}
+	const uint32_t uport = swap16(uw & 0xffffu), ulen = swap16(ulen_raw), spi = wb<42>(f);
+	const bool esp = !v6 & udp & (uport == 4500u) & (ulen > 4u) & (spi != 0u);
+
+	lo |= esp ? (uint32_t)IF(IFL_IPSEC) : 0u;
+	hi |= esp ? (uint32_t)(IF(IFL_IPSEC_UDP) >> 32) : 0u;
 	const bool need = (udpck & !zero) | tcpck;
 
-	sum += udp ? ulen_raw + (0x11u << 8) : swap16((len - l4) & 0xffffu) + (0x06u << 8);
+	const uint32_t udp_ph = ulen_raw + (0x11u << 8);
+	const uint32_t tcp_ph = swap16((len - l4) & 0xffffu) + (0x06u << 8);
+
+	sum += udp ? udp_ph : tcp_ph;
 	const bool pend = need & (len > 64u);
 	/* _odp_packet_l4_chksum (odp_packet.c:1906-1984) within the window */
 	const bool done = need & !pend;
@@ -267,25 +278,19 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 
 	hi |= done ? (uint32_t)(IF(IFL_L4_CHKSUM_DONE) >> 32) : 0u;
 	fl |= bad ? FB(FL_L4_CHKSUM_ERR) | (udp ? FB(FL_UDP_ERR) : FB(FL_TCP_ERR)) : 0u;
+	/* the results by select (an early return for ip_err compiled to a
+	 * divergent branch with the rest sunk into it) */
 	p.l2 = 0u;
 	p.l3 = l3;
-	if (l3bad) {
-		p.inf = ((uint64_t)hi3 << 32) | (lo3 & ~(uint32_t)IF(IFL_L4));
-		p.fl = FB(FL_IP_ERR) | FB(FL_L3_CHKSUM_ERR);
-		p.l4 = 0xffffu;
-		return 1;
-	}
-	p.inf = ((uint64_t)hi << 32) | lo;
-	p.fl = fl;
-	p.l4 = l4;
-	if (pend) {
-		pd.kind = udp ? 1u : 2u;
-		pd.sum = sum;
-		pd.a = 64u;
-		pd.b = len;
-		return PARSE_PEND;
-	}
-	return (fl & FL_ERROR_MASK) != 0u;
+	p.inf = l3bad ? ((uint64_t)hi3 << 32) | (lo3 & ~(uint32_t)IF(IFL_L4))
+		      : ((uint64_t)hi << 32) | lo;
+	p.fl = l3bad ? FB(FL_IP_ERR) | FB(FL_L3_CHKSUM_ERR) : fl;
+	p.l4 = l3bad ? 0xffffu : l4;
+	pd.kind = udp ? 1u : 2u;
+	pd.sum = sum;
+	pd.a = 64u;
+	pd.b = len;
+	return l3bad ? 1 : pend ? PARSE_PEND : (int)((fl & FL_ERROR_MASK) != 0u);
 }
 
 #ifndef GF_PROBES           /* chain-free groups probed together (2-word maps) */
@@ -695,25 +700,19 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			const bool v6 = (b.inf_lo & (uint32_t)IF(IFL_IPV6)) != 0u;
 			const bool l4ok = b.l4 != 0xffffu;
 
-			kv[0] = f[0];
-			kv[1] = f[1];
-			kv[2] = f[2];
-			kv[3] = u3;
-			kv[4] = u4;
 			/* the innermost VLAN tag */
-			kv[5] = qinq ? __builtin_amdgcn_alignbyte(u5, u4, 2) : __builtin_amdgcn_alignbyte(u4, u3, 2);
-			kv[6] = wb<14>(f);
-			kv[7] = wb<18>(f);
-			kv[8] = wb<22>(f);
-			kv[9] = wb<26>(f);
-			kv[10] = wb<30>(f);
-			kv[11] = wb<34>(f);
-			kv[12] = wb<38>(f);
-			kv[13] = wb<42>(f);
-			kv[14] = wb<46>(f);
-			kv[15] = wb<50>(f);
-			k16 = !l4ok ? 0u : v6 ? wb<54>(f) : wb<34>(f);
-			k17 = !l4ok ? 0u : v6 ? wb<58>(f) : wb<38>(f);
+			const uint32_t vq = __builtin_amdgcn_alignbyte(u5, u4, 2);
+			const uint32_t vt = __builtin_amdgcn_alignbyte(u4, u3, 2);
+			const uint32_t w34 = wb<34>(f), w38 = wb<38>(f);
+			const uint32_t w54 = wb<54>(f), w58 = wb<58>(f);
+
+			/* one vector literal: built in place (element stores into a
+			 * zero vector compiled to a copy of the whole tuple) */
+			kv = gf_kv_t{f[0], f[1], f[2], u3, u4, qinq ? vq : vt, wb<14>(f), wb<18>(f),
+				     wb<22>(f), wb<26>(f), wb<30>(f), w34, w38, wb<42>(f), wb<46>(f),
+				     wb<50>(f)};
+			k16 = !l4ok ? 0u : v6 ? w54 : w34;
+			k17 = !l4ok ? 0u : v6 ? w58 : w38;
 		} else {
 			Pkt<64, true> v;
 
