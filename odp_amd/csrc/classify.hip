@@ -1477,7 +1477,7 @@ static hipError_t launch_one(const odpg_launch_args &a, uint32_t &grid, hipStrea
 	const uint32_t occ_grid = odpg_resident_grid(
 		(const void *)odpg_classify_kernel<W, COOP, GF, DESC, MODE, FAST, LEAN>, BLOCK, lds);
 
-	if (!getenv("ODPG_GRID_CAP") && grid > occ_grid)
+	if (!odpg_debug_env("ODPG_GRID_CAP") && grid > occ_grid)
 		grid = occ_grid;
 	if (a.cnt.row && grid > a.cnt.rows)
 		grid = a.cnt.rows;   /* one counter row per workgroup */
@@ -1532,7 +1532,7 @@ extern "C" int odpg_launch_cls64(const odpg_launch_args *a, hipStream_t s);
  * full parse with classification and no drop options */
 static bool lean64_ok(const odpg_launch_args &a)
 {
-	static const bool off = getenv("ODPG_NO_LEAN64") != nullptr;
+	static const bool off = odpg_debug_env("ODPG_NO_LEAN64") != nullptr;
 	const uint64_t drops = ODPG_PKTIN_DROP_IPV4_ERR | ODPG_PKTIN_DROP_IPV6_ERR |
 			       ODPG_PKTIN_DROP_UDP_ERR | ODPG_PKTIN_DROP_TCP_ERR |
 			       ODPG_PKTIN_DROP_SCTP_ERR;
@@ -1564,7 +1564,7 @@ extern "C" size_t odpg_clsgf_lds(const odpg_launch_args *a);
  * no drop options */
 static bool gf_ok(const odpg_launch_args &a)
 {
-	static const bool off = getenv("ODPG_NO_GF") != nullptr;
+	static const bool off = odpg_debug_env("ODPG_NO_GF") != nullptr;
 	const uint64_t drops = ODPG_PKTIN_DROP_IPV4_ERR | ODPG_PKTIN_DROP_IPV6_ERR |
 			       ODPG_PKTIN_DROP_UDP_ERR | ODPG_PKTIN_DROP_TCP_ERR |
 			       ODPG_PKTIN_DROP_SCTP_ERR;
@@ -1711,7 +1711,7 @@ extern "C" uint32_t odpg_launch_grid(uint32_t num)
 	static uint32_t cap = 0;
 
 	if (cap == 0) {
-		const char *e = getenv("ODPG_GRID_CAP");
+		const char *e = odpg_debug_env("ODPG_GRID_CAP");
 		long v = e ? strtol(e, nullptr, 0) : 0;
 
 		cap = v > 0 ? (uint32_t)v : DEFAULT_GRID_CAP;

@@ -894,24 +894,36 @@ odpg_clsgf_kernel(const GFArgs A, const uint4 *__restrict__ xmg, const uint32_t 
 			while (__ballot(active)) {
 				if (active) {
 					uint32_t best = 0xffffffffu;
-					uint32_t bi = crs & 0xffffu;
-					const uint32_t end = bi + (crs >> 16);
 
-					while (bi < end) {
-						const uint32_t w = bi >> 5;
-						uint32_t x = hm[0];
+					if constexpr (NW == 2) {
+						/* 2-word maps: the CoS's bit range of the 64-bit
+						 * map, branch-free (a CoS with rules has 1..64
+						 * bits starting below 64) */
+						const uint32_t st = crs & 0x3fu, n = crs >> 16;
+						uint64_t x = (((uint64_t)hm[1] << 32) | hm[0]) >> st;
+
+						x &= n < 64u ? (1ull << n) - 1ull : ~0ull;
+						best = x ? st + (uint32_t)__builtin_ctzll(x) : best;
+					} else {
+						uint32_t bi = crs & 0xffffu;
+						const uint32_t end = bi + (crs >> 16);
+
+						while (bi < end) {
+							const uint32_t w = bi >> 5;
+							uint32_t x = hm[0];
 
 #pragma unroll
-						for (uint32_t k = 1; k < NW; ++k)
-							x = w == k ? hm[k] : x;
-						x >>= bi & 31u;
-						if (end - bi < 32u)
-							x &= (1u << (end - bi)) - 1u;
-						if (x) {
-							best = bi + (uint32_t)__builtin_ctz(x);
-							break;
+							for (uint32_t k = 1; k < NW; ++k)
+								x = w == k ? hm[k] : x;
+							x >>= bi & 31u;
+							if (end - bi < 32u)
+								x &= (1u << (end - bi)) - 1u;
+							if (x) {
+								best = bi + (uint32_t)__builtin_ctz(x);
+								break;
+							}
+							bi = (w + 1u) << 5;
 						}
-						bi = (w + 1u) << 5;
 					}
 					uint32_t j = cxf & 0xffffu;
 					const uint32_t jend = j + (cxf >> 16);

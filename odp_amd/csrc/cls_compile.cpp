@@ -1114,8 +1114,9 @@ int odpg_compile_rules(const odpg_rules_t *r, std::vector<uint8_t> &blob, dtable
 		}
 		cbit_n[c] = nbits - cbit_start[c];
 	}
-	/* ODPG_XM_LAZY=1 forces the lazy form (experiments / A-B runs) */
-	static const bool force_lazy = getenv("ODPG_XM_LAZY") && atoi(getenv("ODPG_XM_LAZY"));
+	/* ODPG_XM_LAZY=1 forces the lazy form (experiment builds only,
+	 * ODPG_DEBUG_KNOBS: A/B runs) */
+	static const bool force_lazy = odpg_debug_env("ODPG_XM_LAZY") && atoi(odpg_debug_env("ODPG_XM_LAZY"));
 
 	if (xm && (nbits > XM_MAX_PMR || force_lazy)) {
 		/* lazy form: bit = PMR index, complex PMRs from their records */

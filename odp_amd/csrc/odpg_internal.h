@@ -7,6 +7,21 @@
 #define ODPG_INTERNAL_H_
 
 #include <stdint.h>
+#include <stdlib.h>
+
+/* Strategy switches for A/B experiment builds (ODPG_NO_LEAN64, ODPG_NO_GF,
+ * ODPG_GRID_CAP, ODPG_XM_LAZY): read from the environment only in a build
+ * made with -DODPG_DEBUG_KNOBS (make EXTRA=-DODPG_DEBUG_KNOBS); the shipped
+ * library ignores them */
+static inline const char *odpg_debug_env(const char *name)
+{
+#ifdef ODPG_DEBUG_KNOBS
+	return getenv(name);
+#else
+	(void)name;
+	return (const char *)0;
+#endif
+}
 
 /* _odp_packet_input_flags_t bit positions (packet_inline_types.h:60-113) */
 enum {
