@@ -99,10 +99,11 @@ def test_pktio_lookup_modes_and_capabilities():
     assert lib.odp_pktin_event_queue(C.c_void_p(b), qs, 4) == 1 and qs[0]
     assert lib.odp_pktout_queue(C.c_void_p(b), pq, 4) == -1
     assert lib.odp_pktout_event_queue(C.c_void_p(b), qs, 4) == 1 and qs[0]
-    # one input / output queue per pktio: more is refused
+    # up to 16 output queues per loop pktio (loop.c's max_output_queues):
+    # more is refused
     pq2 = (C.c_uint8 * 512)()
     lib.odp_pktout_queue_param_init(pq2)
-    struct.pack_into("<I", pq2, 4, 2)                     # num_queues (after op_mode)
+    struct.pack_into("<I", pq2, 4, 17)                    # num_queues (after op_mode)
     assert lib.odp_pktout_queue_config(C.c_void_p(a), pq2) == -1
     assert lib.odp_pktio_close(C.c_void_p(a)) == 0 and lib.odp_pktio_close(C.c_void_p(b)) == 0
     assert not lib.odp_pktio_lookup(b"loop")
