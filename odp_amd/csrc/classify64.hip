@@ -452,6 +452,47 @@ odpg_cls64_kernel(const L64Args A)
 			bool active = live && !pdrop && !err && walk;
 			uint32_t steps = 0u, gm = A.def_cgmask;
 
+			if (A.depth - 1u < 4u) {
+				/* acyclic table, longest chain A.depth rules: exactly
+				 * that many levels without divergent branches. A group
+				 * is skipped (a uniform branch) when no lane of the wave
+				 * is at a CoS with rules in it; otherwise every lane
+				 * reads its candidates and a lane without the group in
+				 * its CoS's mask ignores them. A lane whose level finds
+				 * no rule keeps its state and is inactive from then on. */
+#pragma unroll
+				for (uint32_t l = 0; l < 4u; ++l) {
+					if (l >= A.depth || !__ballot(active))
+						break;
+					uint32_t best = 0xffffffffu;
+
+#pragma unroll
+					for (int g = 0; g < NG; ++g) {
+						const bool v = active & krq[g] & (((gm >> g) & 1u) != 0u);
+
+						if (!__ballot(v))
+							continue;
+						const uint32_t x = cgroup_key(kv[g], cos);
+						const uint2 e1 = cents[mg[g].off + ((x * mg[g].m1) >> mg[g].sh)];
+						const uint2 e2 = cents[mg[g].off + ((x * mg[g].m2) >> mg[g].sh)];
+						const bool h1 = v & (e1.x == kv[g]) & ((e1.y & 0xffffu) == cos);
+						const bool h2 = v & (e2.x == kv[g]) & ((e2.y & 0xffffu) == cos);
+
+						best = min(best, min(h1 ? e1.y >> 16 : 0xffffffffu,
+								     h2 ? e2.y >> 16 : 0xffffffffu));
+					}
+					const bool hit = best != 0xffffffffu;
+					const uint2 pi = pinfo3[hit ? best : 0u];
+
+					cos = hit ? (pi.x & 0xffffu) : cos;
+					mark = hit ? (pi.x >> 16) : mark;
+					act = hit ? (pi.y & 0xffu) : act;
+					any_match |= hit;
+					active = hit & (((pi.y >> 8) & 1u) != 0u);   /* rules below */
+					gm = pi.y >> 12;
+				}
+				active = false;
+			}
 			while (active) {
 				uint32_t best = 0xffffffffu;
 

@@ -193,7 +193,11 @@ __device__ __forceinline__ bool plain_gf(const uint32_t (&f)[16], uint32_t x16, 
  * Branch-free over IPv4 / IPv6 and UDP / TCP: the pseudo-header addresses
  * and the segment are one contiguous byte range of the window ([26, 64) for
  * IPv4, [22, 64) for IPv6), so the L4 sum is one v_dot2 chain whose first two
- * weights depend on the version. */
+ * weights depend on the version. The ip_err / pending / IPsec results stay
+ * behind (uniform-heavy) ifs: computing every arm and selecting made the
+ * 8-word-map instantiation (C3, 128 VGPRs) spill one register, 6 for the
+ * counted one, whose scratch traffic took C3 from 404 to 410 MB per launch;
+ * the fixed-stride instantiation compiles the same either way. */
 __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t (&f)[16],
 					     uint32_t s14, uint32_t s15, uint32_t len, uint32_t opt,
 					     uint32_t sh, bool qinq)
@@ -227,14 +231,12 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 
 	const bool frag = !v6 & ((swap16(f[5] & 0xffffu) & 0x3fffu) != 0u);
 	const uint32_t dst_be = __builtin_bswap32(wb<30>(f));
-	const bool mc6 = ((f[9] >> 16) & 0xffu) == 0xffu, mc4 = (dst_be >> 28) == 0xeu;
-	const bool mc = v6 ? mc6 : mc4;
+	const bool mc = v6 ? ((f[9] >> 16) & 0xffu) == 0xffu : (dst_be >> 28) == 0xeu;
 
 	lo |= (frag ? (uint32_t)IF(IFL_IPFRAG) : 0u) |
 	      ((!v6 & (dst_be == 0xffffffffu)) ? (uint32_t)IF(IFL_IP_BCAST) : 0u) |
 	      (mc ? (uint32_t)IF(IFL_IP_MCAST) : 0u);
-	const uint32_t proto4 = f[5] >> 24, proto6 = f[5] & 0xffu;
-	const uint32_t proto = v6 ? proto6 : proto4;
+	const uint32_t proto = v6 ? (f[5] & 0xffu) : (f[5] >> 24);
 	/* bytes [26, 64) (IPv4: addresses 26..33, segment 34..) or [22, 64)
 	 * (IPv6: addresses 22..53, segment 54..) */
 	uint32_t sum = gd2(f[5], v6 ? GW01 : 0u, 0u);
@@ -246,8 +248,7 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 	sum = gd2(s15, GW11, gd2(s14, GW11, sum));
 	const uint32_t uw = v6 ? f[14] : f[9];              /* UDP ports + length */
 	const uint32_t ulen_raw = uw >> 16;
-	const uint32_t cw = v6 ? f[15] : f[10];
-	const uint32_t csum_raw = cw & 0xffffu;
+	const uint32_t csum_raw = (v6 ? f[15] : f[10]) & 0xffffu;
 	const uint32_t l4 = l3 + (v6 ? 40u : 20u);
 	const bool udp = proto == 0x11u;
 
@@ -260,17 +261,13 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 
 	hi |= zero ? (uint32_t)((IF(IFL_L4_CHKSUM_DONE) | IF(IFL_UDP_CHKSUM_ZERO)) >> 32) : 0u;
 	/* the IPsec-over-UDP marker (port 4500, a non-zero SPI at byte 42) */
-	const uint32_t uport = swap16(uw & 0xffffu), ulen = swap16(ulen_raw), spi = wb<42>(f);
-	const bool esp = !v6 & udp & (uport == 4500u) & (ulen > 4u) & (spi != 0u);
-
-	lo |= esp ? (uint32_t)IF(IFL_IPSEC) : 0u;
-	hi |= esp ? (uint32_t)(IF(IFL_IPSEC_UDP) >> 32) : 0u;
+	if (!v6 & udp & (swap16(uw & 0xffffu) == 4500u) & (swap16(ulen_raw) > 4u) & (wb<42>(f) != 0u)) {
+		lo |= (uint32_t)IF(IFL_IPSEC);
+		hi |= (uint32_t)(IF(IFL_IPSEC_UDP) >> 32);
+	}
 	const bool need = (udpck & !zero) | tcpck;
 
-	const uint32_t udp_ph = ulen_raw + (0x11u << 8);
-	const uint32_t tcp_ph = swap16((len - l4) & 0xffffu) + (0x06u << 8);
-
-	sum += udp ? udp_ph : tcp_ph;
+	sum += udp ? ulen_raw + (0x11u << 8) : swap16((len - l4) & 0xffffu) + (0x06u << 8);
 	const bool pend = need & (len > 64u);
 	/* _odp_packet_l4_chksum (odp_packet.c:1906-1984) within the window */
 	const bool done = need & !pend;
@@ -282,15 +279,23 @@ __device__ __forceinline__ int parse_fast_gf(Prs &p, L4Pend &pd, const uint32_t 
 	 * divergent branch with the rest sunk into it) */
 	p.l2 = 0u;
 	p.l3 = l3;
-	p.inf = l3bad ? ((uint64_t)hi3 << 32) | (lo3 & ~(uint32_t)IF(IFL_L4))
-		      : ((uint64_t)hi << 32) | lo;
-	p.fl = l3bad ? FB(FL_IP_ERR) | FB(FL_L3_CHKSUM_ERR) : fl;
-	p.l4 = l3bad ? 0xffffu : l4;
-	pd.kind = udp ? 1u : 2u;
-	pd.sum = sum;
-	pd.a = 64u;
-	pd.b = len;
-	return l3bad ? 1 : pend ? PARSE_PEND : (int)((fl & FL_ERROR_MASK) != 0u);
+	if (l3bad) {
+		p.inf = ((uint64_t)hi3 << 32) | (lo3 & ~(uint32_t)IF(IFL_L4));
+		p.fl = FB(FL_IP_ERR) | FB(FL_L3_CHKSUM_ERR);
+		p.l4 = 0xffffu;
+		return 1;
+	}
+	p.inf = ((uint64_t)hi << 32) | lo;
+	p.fl = fl;
+	p.l4 = l4;
+	if (pend) {
+		pd.kind = udp ? 1u : 2u;
+		pd.sum = sum;
+		pd.a = 64u;
+		pd.b = len;
+		return PARSE_PEND;
+	}
+	return (fl & FL_ERROR_MASK) != 0u;
 }
 
 #ifndef GF_PROBES           /* chain-free groups probed together (2-word maps) */
