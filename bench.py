@@ -157,7 +157,9 @@ def main():
     if out is not None and others != "none":
         out["other_configs"] = measure_others(args, others.split(","), world, rank, local, dist)
     if out is not None:
-        print(json.dumps(out), flush=True)
+        # compact separators: the line (with other_configs) stays near 2 KB,
+        # inside the tail the driver keeps
+        print(json.dumps(out, separators=(",", ":")), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -177,13 +179,16 @@ def measure_others(args, cfgs, world, rank, local, dist):
     stderr): value (Mpps, this run's clock), kernel_ms (HIP events on the
     launch stream), frac of HBM peak, traffic_x (committed PMC bytes per
     launch / algorithmic), counted_kernel_ms (pktio counters on), and the
-    CPU baseline (the per-GPU core share and one thread)."""
+    CPU baseline (cpu: the per-GPU core share, as the headline's
+    cpu_baseline.cores; cpu_1thread: one thread)."""
     import copy
     res = {}
     for c in cfgs:
         a = copy.copy(args)
         a.config, a.others, a.e2e, a.source = c, "none", False, "sharded"
-        a.steps, a.warmup, a.runs = min(args.steps, 100), min(args.warmup, 10), 3
+        # 100 warmup launches: the first ~10 ms of heavy traffic run with
+        # the memory side still clocking up (DESIGN §3 "C3 under the trace")
+        a.steps, a.warmup, a.runs = min(args.steps, 100), 100, 3
         a.cpu_seconds = args.others_cpu_seconds
         a.batch = 1 << 20
         t0 = time.perf_counter()
@@ -194,15 +199,13 @@ def measure_others(args, cfgs, world, rank, local, dist):
         rf = r["roofline"]
         alg = rf["bytes_per_pkt"] * rf["pkts_per_launch"]
         cpu = r.get("cpu_baseline") or {}
-        e = {"value": r["value"], "kernel_ms": rf["kernel_ms"], "frac": rf["frac"],
-             "traffic_x": round(rf["traffic"] / alg, 3) if rf.get("traffic") else None,
-             "bytes_per_pkt": rf["bytes_per_pkt"], "pkts": rf["pkts_per_launch"]}
+        e = {"value": round(r["value"]), "kernel_ms": rf["kernel_ms"], "frac": round(rf["frac"], 3),
+             "traffic_x": round(rf["traffic"] / alg, 3) if rf.get("traffic") else None}
         if "with_pktio_counters" in r:
             e["counted_kernel_ms"] = r["with_pktio_counters"]["kernel_ms"]
         if cpu:
-            e["cpu"] = cpu.get("value")
-            e["cpu_1thread"] = cpu.get("value_1thread")
-            e["cpu_cores"] = cpu.get("cores")
+            e["cpu"] = round(cpu.get("value"), 1)
+            e["cpu_1thread"] = round(cpu.get("value_1thread"), 1)
         res[c] = e
         log(f"other config {c}: {e} ({time.perf_counter() - t0:.1f} s)")
     return res
@@ -346,9 +349,7 @@ def bench_classify(args, world, rank, local, dist):
                    "kernel_ms": round(kernel_ms_st, 5),
                    "runs_ms_per_step": run_ms_st,
                    "fold_ms": round(fold_ms, 3),
-                   "what": "same launches + pktio and per-queue counters (per-workgroup rows of "
-                           "odpg_counters_t, no extra kernel per launch; fold_ms = the one "
-                           "read-time fold)"}
+                   "what": "same launches + pktio/queue counters; fold_ms: read-time fold"}
 
     ms_per_step = wall * 1e3 / max(args.steps, 1)
     total_pkts = n * world * args.steps
@@ -381,7 +382,7 @@ def bench_classify(args, world, rank, local, dist):
                        "frame_bytes": round(frame_bytes, 2),
                        "pmr_rules": nrules, "rotating_buffers": nbuf,
                        "kernel_mode": ["auto", "walk", "evaluate-all", "hash-walk"][args.kernel_mode],
-                       "parallelism": f"dp{world} (packet shards, no data-path collective)"},
+                       "parallelism": f"dp{world} (packet shards, no collective)"},
             "roofline": roofline, "cpu_baseline": cpu,
         }
         if counted:
@@ -523,12 +524,11 @@ def pmc_traffic(config):
         rec = json.load(open(tf))
     except (OSError, ValueError):
         return None, "no PMC summary for this config"
-    src = (f"profiles/pmc_traffic_{config}.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of "
-           f"{rec.get('kernel')} in a separate run, not this one")
+    src = f"profiles/pmc_traffic_{config}.json (rocprofv3 --pmc, separate run"
     if rec.get("kernel_sources_sha256") == fingerprint():
-        src += "; collected on these kernel sources"
+        src += ", these kernel sources)"
     else:
-        src += "; STALE: collected on other kernel sources"
+        src += "; STALE: other kernel sources)"
     return rec.get("bytes_per_launch"), src
 
 
@@ -602,7 +602,7 @@ def bench_tx(args, world, rank, local, dist):
             "config": {"workload": "loop pktio TX: 64B IPv4/UDP with zeroed checksums, pktout "
                                    "ipv4+udp+tcp insert, hash ipv4_udp+ipv4 over 8 queues",
                        "batch_per_gpu": n, "frame_bytes": 64, "rotating_buffers": nbuf,
-                       "parallelism": f"dp{world} (packet shards, no data-path collective)"},
+                       "parallelism": f"dp{world} (packet shards, no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(args.config)[0],
@@ -685,7 +685,7 @@ def bench_l3fwd(args, world, rank, local, dist):
                                    "64B IPv4 UDP/TCP, in-place TTL/checksum/MAC rewrite",
                        "batch_per_gpu": n, "frame_bytes": 64, "routes": len(routes),
                        "rotating_buffers": nbuf,
-                       "parallelism": f"dp{world} (packet shards, no data-path collective)"},
+                       "parallelism": f"dp{world} (packet shards, no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(args.config)[0],
@@ -749,9 +749,7 @@ def cpu_baseline(rules, frames, desc, n, stride, opt, args):
         aff = list(range(os.cpu_count() or 1))
     if len(aff) > used:
         allc = {"value": None,
-                "note": f"not measured: the affinity mask lists {len(aff)} CPUs but the host "
-                        f"grants this job {used} ({share}); threads beyond the grant share "
-                        f"its cores"}
+                "note": f"not measured: {len(aff)} CPUs in the mask, {used} granted"}
     model = ""
     try:
         for ln in open("/proc/cpuinfo"):
@@ -762,11 +760,9 @@ def cpu_baseline(rules, frames, desc, n, stride, opt, args):
         pass
     return {"value": round(statistics.median(rates), 2), "unit": "Mpps", "cores": used,
             "kind": "port", "value_1thread": round(one, 2), "cpu_model": model,
-            "runs_mpps": [round(r, 2) for r in rates], "core_share": share,
-            "all_cores": allc,
-            "sample": f"median of {runs} runs, each {reps} passes x {n} pkts of the same "
-                      f"{args.config.upper()} batch in host DRAM, {used} threads pinned one per "
-                      f"core ({share})"}
+            "runs_mpps": [round(r, 2) for r in rates], "all_cores": allc,
+            "sample": f"median of {runs} runs x {reps} passes over the {n}-pkt "
+                      f"{args.config.upper()} batch in host DRAM, {used} threads pinned ({share})"}
 
 
 def cpu_baseline_mt(work, n, args, what, passes=None):
@@ -841,7 +837,7 @@ def cpu_baseline_mt(work, n, args, what, passes=None):
             log(f"cpu baseline {what}: {threads} threads {rates[-1]:.1f} Mpps")
     return {"value": round(statistics.median(rates), 2), "unit": "Mpps", "cores": threads,
             "kind": "port", "value_1thread": round(one, 2),
-            "runs_mpps": [round(r, 2) for r in rates], "core_share": share,
+            "runs_mpps": [round(r, 2) for r in rates],
             "sample": f"median of 5 runs of ~{args.cpu_seconds / 5:.0f} s, {threads} threads "
                       f"pinned one per core ({share}), each over its own {n // threads}-packet "
                       f"slice of the {what} batch in host DRAM, passes repeated"
@@ -862,8 +858,7 @@ def cpu_share():
         aff = list(range(os.cpu_count() or 1))
     cap = os.environ.get("OMP_NUM_THREADS")
     if cap and cap.isdigit() and 0 < int(cap) < len(aff):
-        return aff[:int(cap)], (f"{int(cap)} of the {len(aff)} CPUs in the affinity mask: the "
-                                f"host's per-GPU share (OMP_NUM_THREADS={cap})")
+        return aff[:int(cap)], f"{int(cap)} of {len(aff)} CPUs, OMP_NUM_THREADS={cap}"
     return aff, f"all {len(aff)} CPUs of the affinity mask"
 
 

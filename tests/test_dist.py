@@ -177,7 +177,7 @@ def test_bench_other_configs():
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(line) == 1, r.stdout[-2000:]
-    assert len(line[0]) < 4096
+    assert len(line[0]) < 2048    # three entries here; all five stay near 2 KB
     d = json.loads(line[0])
     oc = d["other_configs"]
     assert sorted(oc) == ["c1", "c3", "c5"]

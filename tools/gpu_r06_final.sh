@@ -32,7 +32,7 @@ for cfg in ${CFGS:-c2 c1 c2x c3 c4 c5 tx}; do
   python tools/pmc_summary.py $OUT/pmc_$cfg --write $cfg > $OUT/pmc_${cfg}_summary.json && \
     cp profiles/pmc_traffic_$cfg.json $OUT/
   step "stats $cfg" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$cfg -o run \
-    -- python3 bench.py --no-cpu --config $cfg --others none --steps 100 --warmup 10 --runs 1 > $OUT/prof_$cfg.log 2>&1
+    -- python3 bench.py --no-cpu --config $cfg --others none --steps 100 --warmup 300 --runs 1 > $OUT/prof_$cfg.log 2>&1
   extra=""; [ $cfg = c2 ] || [ $cfg = c3 ] && extra="--e2e"
   step "bench $cfg" timeout -k 10 600 python bench.py --config $cfg --others none $extra > $OUT/bench_$cfg.json 2> $OUT/bench_$cfg.err
   cat $OUT/bench_$cfg.json | cut -c1-400
