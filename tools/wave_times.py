@@ -56,6 +56,10 @@ def main():
     raw = np.zeros(2 * 65536, np.uint64)
     L.check(L.lib.odpg_diag_l64_times(raw.ctypes.data_as(C.c_void_p), 65536), "times")
     raw = raw.reshape(-1, 2)
+    pro = None
+    if hasattr(L.lib, "odpg_diag_l64_tpro"):          # tools/exp/l64_times_pro.patch
+        pro = np.zeros(65536, np.uint64)
+        L.check(L.lib.odpg_diag_l64_tpro(pro.ctypes.data_as(C.c_void_p), 65536), "tpro")
     used = raw[:, 0] != 0
     gws = np.nonzero(used)[0]
     st = raw[used, 0].astype(np.int64)
@@ -66,12 +70,19 @@ def main():
     last = st >= t0
     st, en, tiles, gws = st[last], en[last], tiles[last], gws[last]
     base = st.min()
+    if pro is not None:
+        # the workgroup's prologue (table copy to LDS + barrier): wave start
+        # to the first tile
+        pr = pro[gws].astype(np.int64) - st
+        prologue = {q: round(float(np.percentile(pr, q)) / 100.0, 3) for q in (0, 50, 90, 100)}
+    else:
+        prologue = None
     out = {"config": a.config, "counted": a.counted, "waves": int(len(st)),
            "kernel_span_us": round((en.max() - base) / 100.0, 3),
            "start_spread_us": round((st.max() - base) / 100.0, 3),
            "end_us": {q: round(float(np.percentile(en - base, q)) / 100.0, 3)
                       for q in (0, 10, 50, 90, 100)},
-           "by_tiles": {}}
+           "prologue_us": prologue, "by_tiles": {}}
     for k in sorted(set(tiles.tolist())):
         m = tiles == k
         out["by_tiles"][int(k)] = {"waves": int(m.sum()),
