@@ -345,14 +345,28 @@ __device__ __forceinline__ void gf_probes(const uint4 *__restrict__ xmg, uint32_
 			key = kv[q0[u].z & 15u];
 		}
 		kvm[u] = key & q1[u].z;
-		e[u] = q0[u].w + ((kvm[u] * q0[u].x) >> q0[u].y);
+		const uint32_t h = (kvm[u] * q0[u].x) >> q0[u].y;
+
+		/* 2-word maps: the entry's byte offset as one shift-add of the
+		 * hash onto the base scaled on the scalar unit (written as asm:
+		 * the compiler otherwise adds first and shifts the sum, one more
+		 * vector instruction per probe; s_mul_i32, unlike s_lshl_b32,
+		 * leaves SCC alone, which the compiler may hold across it) */
+		if constexpr (NW == 2) {
+			uint32_t wb;
+
+			asm("s_mul_i32 %0, %1, 16" : "=s"(wb) : "s"(q0[u].w));
+			e[u] = (h << 4) + wb;
+		} else {
+			e[u] = q0[u].w + h;
+		}
 	}
 #pragma unroll
 	for (int u = 0; u < U; ++u) {
 		if constexpr (NW == 2) {
 			/* whole ds_read_b128 (the unused fourth word kept: narrowed
 			 * to ds_read_b96 it takes twice the LDS cycles) */
-			const uint4 x = *(const uint4 *)(tb + 4u * e[u]);
+			const uint4 x = *(const uint4 *)((const uint8_t *)tb + e[u]);
 
 			asm volatile("" ::"v"(x.w));
 
