@@ -253,6 +253,9 @@ typedef struct odp_pool_param_t {
 		uint32_t seg_len;
 		uint32_t uarea_size;
 		uint32_t headroom;
+		/* buffers a thread may keep in its local cache (0: none; the
+		 * runtime caps it at 1/32 of num and max_cache_size) */
+		uint32_t cache_size;
 	} pkt;
 	uint64_t reserved[8];
 } odp_pool_param_t;

@@ -289,10 +289,15 @@ static pthread_mutex_t rx_dlock[RT_MAX_PKTIO] = { [0 ... RT_MAX_PKTIO - 1] =
 static int rx_dbusy[RT_MAX_PKTIO];
 static uint32_t rx_helpers[RT_MAX_PKTIO];   /* threads in a pktio's delivery side */
 
-/* a spin-wait's pause */
-static inline void cpu_relax(void)
+/* a spin-wait's step: a pause, and from the 1024th step on a yield of the
+ * CPU (the thread waited for may have been preempted: more workers than
+ * CPUs, or two pinned to one) */
+static inline void spin_wait(uint32_t *steps)
 {
-	__builtin_ia32_pause();
+	if (++*steps < 1024u)
+		__builtin_ia32_pause();
+	else
+		sched_yield();
 }
 
 /* pinned host memory and its device address (zero-copy launch buffers) */
@@ -631,29 +636,48 @@ static int cpu_list_first(int cpu, const char *what)
  * the caller takes CPUs in order. */
 static int l3_mask(const cpu_set_t *set, int control, int num, odp_cpumask_t *mask)
 {
-	const int ctl_l3 = cpu_list_first(control, "cache/index3/shared_cpu_list");
+	enum { NC = CPU_SETSIZE < ODP_CPUMASK_SIZE ? CPU_SETSIZE : ODP_CPUMASK_SIZE };
+	/* per CPU of the set, read once: its L3 (the first CPU of the L3's
+	 * sharers, which need not be in the set: a cpuset slice may start
+	 * inside an L3) and whether it is its core's first hardware thread */
+	int l3of[NC], first[NC], ids[NC], nid = 0;
 
-	if (ctl_l3 < 0)
+	for (int c = 0; c < NC; c++) {
+		l3of[c] = -1;
+		if (!CPU_ISSET(c, set))
+			continue;
+		l3of[c] = cpu_list_first(c, "cache/index3/shared_cpu_list");
+		if (l3of[c] < 0)
+			return 0;
+		first[c] = cpu_list_first(c, "topology/thread_siblings_list") == c;
+		int k = 0;
+
+		while (k < nid && ids[k] != l3of[c])
+			k++;
+		if (k == nid)
+			ids[nid++] = l3of[c];
+	}
+	if (control < 0 || control >= NC || l3of[control] < 0)
 		return 0;
+	const int ctl_l3 = l3of[control];
+
 	/* passes: the control's L3, then the others, first hardware threads
 	 * only; then the same with the second hardware threads of its cores
 	 * after the first ones (sharing a core beats crossing the IO die) */
 	for (int pass = 0; pass < 4; pass++) {
 		const int smt = pass >= 2;
 
-		for (int l3 = 0; l3 < CPU_SETSIZE && l3 < ODP_CPUMASK_SIZE; l3++) {
-			if (!CPU_ISSET(l3, set) ||
-			    cpu_list_first(l3, "cache/index3/shared_cpu_list") != l3 ||
-			    ((pass & 1) == 0) != (l3 == ctl_l3))
+		for (int k = 0; k < nid; k++) {
+			const int l3 = ids[k];
+
+			if (((pass & 1) == 0) != (l3 == ctl_l3))
 				continue;
 			int n = 0;
 
 			odp_cpumask_zero(mask);
 			for (int sib = 0; sib <= smt; sib++)
-				for (int c = l3; c < CPU_SETSIZE && c < ODP_CPUMASK_SIZE && n < num; c++)
-					if (c != control && CPU_ISSET(c, set) &&
-					    cpu_list_first(c, "cache/index3/shared_cpu_list") == l3 &&
-					    (cpu_list_first(c, "topology/thread_siblings_list") == c) == !sib) {
+				for (int c = 0; c < NC && n < num; c++)
+					if (c != control && l3of[c] == l3 && first[c] == !sib) {
 						odp_cpumask_set(mask, c);
 						n++;
 					}
@@ -959,6 +983,8 @@ int odp_pool_capability(odp_pool_capability_t *capa)
 	capa->pkt.min_seg_len = 1;
 	capa->pkt.max_seg_len = LOOP_MTU;
 	capa->pkt.max_num_subparam = 0;
+	capa->pkt.min_cache_size = 0;
+	capa->pkt.max_cache_size = TC_N;
 	return 0;
 }
 
@@ -969,6 +995,7 @@ void odp_pool_param_init(odp_pool_param_t *param)
 	param->pkt.seg_len = 1856;
 	param->pkt.len = 1856;
 	param->pkt.num = 1024;
+	param->pkt.cache_size = 256;        /* the reference's default local cache */
 }
 
 odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param)
@@ -996,10 +1023,13 @@ odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param)
 		p->buf = param->pkt.len > param->pkt.seg_len ? param->pkt.len : param->pkt.seg_len;
 		if (p->buf < 64u)
 			p->buf = 64u;
-		/* per-thread caches hold at most 1/32 of the pool each, so
-		 * that buffers freed by other threads cannot strand a small
-		 * pool's allocations (pools of < 64 buffers: no caching) */
+		/* per-thread caches hold the pool's cache_size (0: no
+		 * caching), at most 1/32 of the pool each, so that buffers
+		 * freed by other threads cannot strand a small pool's
+		 * allocations (pools of < 64 buffers: no caching) */
 		p->tc_max = param->pkt.num / 32u < TC_N ? param->pkt.num / 32u : TC_N;
+		if (param->pkt.cache_size < p->tc_max)
+			p->tc_max = param->pkt.cache_size;
 		if (p->tc_max < 2u)
 			p->tc_max = 0u;
 		p->stack = malloc((size_t)param->pkt.num * sizeof(rt_pkt_t *));
@@ -2309,8 +2339,8 @@ void odpg_rt_pktio_close(odp_pktio_t hdl)
 		 * finish their chunks (the bursts in flight are dropped or, when
 		 * opened, delivered by rx_release) */
 		__atomic_store_n(&p->valid, 0, __ATOMIC_SEQ_CST);
-		while (__atomic_load_n(&rx_helpers[p - rt.pktio], __ATOMIC_SEQ_CST))
-			cpu_relax();
+		for (uint32_t sp = 0; __atomic_load_n(&rx_helpers[p - rt.pktio], __ATOMIC_SEQ_CST);)
+			spin_wait(&sp);
 		if (p->have_cap)
 			odpg_pcap_free(&p->cap);
 		for (uint32_t q = 0; q < RT_MAXQ; q++) {
@@ -2476,12 +2506,12 @@ static void rx_release(rt_pktio_t *p)
 			if ((uint32_t)(__atomic_load_n(&s->claimw, __ATOMIC_ACQUIRE) >> 32) == d) {
 				/* partly delivered: the rest goes out too */
 				rx_help(p, (odp_pktio_t)(uintptr_t)(p - rt.pktio + 1));
-				while (__atomic_load_n(&p->delivered, __ATOMIC_ACQUIRE) == d)
-					cpu_relax();
+				for (uint32_t sp = 0; __atomic_load_n(&p->delivered, __ATOMIC_ACQUIRE) == d;)
+					spin_wait(&sp);
 			} else {
 				/* the slot's previous burst still closing */
-				while (__atomic_load_n(&s->open, __ATOMIC_ACQUIRE))
-					cpu_relax();
+				for (uint32_t sp = 0; __atomic_load_n(&s->open, __ATOMIC_ACQUIRE);)
+					spin_wait(&sp);
 			}
 			continue;
 		}
@@ -2492,8 +2522,8 @@ static void rx_release(rt_pktio_t *p)
 		__atomic_store_n(&p->delivered, d + 1u, __ATOMIC_RELEASE);
 	}
 	for (uint32_t i = 0; i < RT_INFLIGHT; i++)
-		while (p->slot[i] && __atomic_load_n(&p->slot[i]->busy, __ATOMIC_ACQUIRE))
-			cpu_relax();
+		for (uint32_t sp = 0; p->slot[i] && __atomic_load_n(&p->slot[i]->busy, __ATOMIC_ACQUIRE);)
+			spin_wait(&sp);
 	slots_free(p);
 }
 
@@ -2899,8 +2929,8 @@ static int rx_open(rt_pktio_t *p, int drain)
 			 * `delivered` on) */
 			if (!drain)
 				return 0;
-			while (__atomic_load_n(&s->open, __ATOMIC_ACQUIRE))
-				cpu_relax();
+			for (uint32_t sp = 0; __atomic_load_n(&s->open, __ATOMIC_ACQUIRE);)
+				spin_wait(&sp);
 			continue;
 		}
 		const int fs = drain ? (odpg_fence_wait(s->fence) ? -1 : 1) : odpg_fence_query(s->fence);
@@ -2958,8 +2988,8 @@ static int rx_help(rt_pktio_t *p, odp_pktio_t hdl)
 		rx_out_t o;
 
 		rx_deliver_range(p, hdl, s, k0, k1, &o);
-		while (__atomic_load_n(&s->commit, __ATOMIC_ACQUIRE) != c)
-			cpu_relax();
+		for (uint32_t sp = 0; __atomic_load_n(&s->commit, __ATOMIC_ACQUIRE) != c;)
+			spin_wait(&sp);
 		rx_commit(p, &o, NULL, NULL);
 		got += (int)(k1 - k0);
 		if (c + 1u == s->nchunks) {
@@ -2990,8 +3020,8 @@ static int rx_deliver_done(rt_pktio_t *p, odp_pktio_t hdl, int drain)
 
 		got += rx_help(p, hdl);
 		/* the last chunks may still be with other threads */
-		while (__atomic_load_n(&p->delivered, __ATOMIC_ACQUIRE) == d)
-			cpu_relax();
+		for (uint32_t sp = 0; __atomic_load_n(&p->delivered, __ATOMIC_ACQUIRE) == d;)
+			spin_wait(&sp);
 	}
 	return got;
 }
@@ -3014,8 +3044,8 @@ static int rx_launch_more(rt_pktio_t *p, odp_pktio_t hdl)
 		if (!s)
 			break;
 		/* a thread that looked at the slot's previous burst late is out */
-		while (__atomic_load_n(&s->busy, __ATOMIC_ACQUIRE))
-			cpu_relax();
+		for (uint32_t sp = 0; __atomic_load_n(&s->busy, __ATOMIC_ACQUIRE);)
+			spin_wait(&sp);
 		const uint64_t t0 = rxprof.on > 0 ? prof_ns() : 0;
 		const uint32_t n = rx_stage(p, s, RT_BURST, -1);
 

@@ -347,6 +347,34 @@ int main(void)
 		printf("pool: 32 buffers, allocated here and freed by another thread, 3 rounds\n");
 	}
 
+	/* pkt.cache_size 0: no per-thread caches, so after the churn threads
+	 * every buffer is allocatable here (the reference's set_pool_cache_size
+	 * honours 0 the same way) */
+	{
+		odp_pool_capability_t capa;
+		static odp_packet_t all2[1100];
+		int n = 0;
+
+		CHECK(odp_pool_capability(&capa) == 0 && capa.pkt.min_cache_size == 0 &&
+		      capa.pkt.max_cache_size >= 256, "pool capability cache sizes");
+		odp_pool_param_init(&pp);
+		CHECK(pp.pkt.cache_size == 256, "default cache_size %u", pp.pkt.cache_size);
+		pp.type = ODP_POOL_PACKET;
+		pp.pkt.num = 1024;
+		pp.pkt.len = 128;
+		pp.pkt.seg_len = 128;
+		pp.pkt.cache_size = 0;
+		churn_pool = odp_pool_create("nocache", &pp);
+		CHECK(churn_pool != ODP_POOL_INVALID, "pool without caches");
+		run(pool_thread, NT);
+		while (n < 1100 && (all2[n] = odp_packet_alloc(churn_pool, 64)) != ODP_PACKET_INVALID)
+			n++;
+		CHECK(n == 1024, "cache_size 0: %d of 1024 packets after the churn", n);
+		odp_packet_free_multi(all2, n);
+		CHECK(odp_pool_destroy(churn_pool) == 0, "nocache pool destroy");
+		printf("pool: cache_size 0, all 1024 buffers allocatable after %d threads' churn\n", NT);
+	}
+
 	/* queue registry: more create / destroy cycles than slots */
 	odp_queue_t first = odp_queue_create("q", NULL), q = first;
 
