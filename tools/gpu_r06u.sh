@@ -1,6 +1,6 @@
 #!/bin/bash
 # odp_pktio_perf (-c 8, and 1 + 1) with the runtime's spin waits yielding
-# after 1024 pauses (base) against pause-only waits (exp_spin), interleaved.
+# after 2^15 pauses (base) against pause-only waits (exp_spin), interleaved.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
