@@ -5,6 +5,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/r06u; mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
+  tests/test_odp_rt.py tests/test_rt_verdict.py tests/test_group.py -m gpu > $OUT/pytest.log 2>&1
+rc=$?; echo "runtime tests: $rc"; tail -1 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   for v in base exp_spin; do
     lp=""; [ $v = base ] || lp=$PWD/odp_amd/lib/$v
