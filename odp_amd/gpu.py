@@ -334,10 +334,11 @@ class Group:
                 "odpg_group_classify_host")
         return out
 
-    def classify_shards(self, frames, num, stride, opt=0, counted=False):
-        """Fixed-stride host frames: member i's range uploaded to its own HBM,
-        all members launched (odpg_group_classify), synced, verdicts
-        gathered."""
+    def classify_shards(self, frames, num, stride, opt=0, counted=False, desc=None):
+        """Device-resident shards: member i's range uploaded to its own HBM
+        (fixed stride: its frames; with descriptors: the whole frame buffer
+        and its range's descriptors, offsets relative to that buffer), all
+        members launched (odpg_group_classify), synced, verdicts gathered."""
         frames = np.ascontiguousarray(frames, dtype=np.uint8)
         B = (L.odpg_batch_t * self.n)()
         R = (L.odpg_result_t * self.n)()
@@ -345,21 +346,33 @@ class Group:
         for i in range(self.n):
             lo, hi = group_range(num, self.n, i)
             ctx = _CtxView(self.ctx_handle(i))
-            fb = DeviceBuffer(ctx, max(16, (hi - lo) * stride))
+            db = None
+            if desc is None:
+                fb = DeviceBuffer(ctx, max(16, (hi - lo) * stride))
+                if hi > lo:
+                    fb.upload(frames[lo * stride:hi * stride])
+            else:
+                fb = DeviceBuffer(ctx, max(16, frames.nbytes))
+                fb.upload(frames)
+                d = np.ascontiguousarray(desc[lo:hi])
+                db = DeviceBuffer(ctx, max(16, d.nbytes))
+                if hi > lo:
+                    db.upload(d)
             ob = DeviceBuffer(ctx, max(16, 4 * (hi - lo)))
-            if hi > lo:
-                fb.upload(frames[lo * stride:hi * stride])
-            B[i] = L.odpg_batch_t(fb.ptr, None, stride, hi - lo, opt, L.LAYER_ALL, 1)
+            B[i] = L.odpg_batch_t(fb.ptr, db.ptr if db else None, 0 if db else stride, hi - lo,
+                                  opt, L.LAYER_ALL, 1)
             R[i] = L.odpg_result_t(ob.ptr, None, None, None, None)
-            bufs.append((lo, hi, fb, ob))
+            bufs.append((lo, hi, fb, ob, db))
         L.check(lib.odpg_group_classify(self.h, B, R, int(counted)), "odpg_group_classify")
         L.check(lib.odpg_group_sync(self.h), "odpg_group_sync")
         out = np.zeros(num, np.uint32)
-        for lo, hi, fb, ob in bufs:
+        for lo, hi, fb, ob, db in bufs:
             if hi > lo:
                 out[lo:hi] = ob.download(np.uint32, hi - lo)
             fb.free()
             ob.free()
+            if db:
+                db.free()
         return out
 
     def fold(self):

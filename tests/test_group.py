@@ -115,6 +115,25 @@ def test_group_device_shards(gpu_ctx, fresh_cls, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [5, 64 * 300 + 5])
+def test_group_device_shards_descriptors(gpu_ctx, fresh_cls, n):
+    """Device-resident C3 shards (IMIX frames behind descriptors, the
+    descriptor kernel, checksum tails): each member holds the frame buffer
+    and its range's descriptors; three members, counted."""
+    rules = _rules(fresh_cls, "c3")
+    frames, desc = gen.c3_frames(n, seed=7)
+    o = oracle.classify(rules, frames, n, stride=0, desc=desc, opt=ALL_CHKSUM)
+    g = gpu.Group([0, 0, 0])
+    try:
+        g.load(rules)
+        out = g.classify_shards(frames, n, 0, opt=ALL_CHKSUM, counted=True, desc=desc)
+        assert np.array_equal(out, o["out"])
+        assert_counters(g.fold(), expected_counters(o, g.num_cos), "group C3 shards")
+    finally:
+        g.close()
+
+
+@pytest.mark.gpu
 def test_group_reload_keeps_counts_of_the_same_layout(gpu_ctx, fresh_cls):
     rules = _rules(fresh_cls, "c2")
     n = 5000
