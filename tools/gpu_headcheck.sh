@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-OUT=gpurun_out/r04head
+OUT=gpurun_out/${OUTDIR:-r06head}
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest: $rc"; tail -2 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
