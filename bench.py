@@ -28,7 +28,9 @@ scattered over the ranks and the verdicts gathered back.
 
 Rank 0 prints one JSON line (contract in the task description) with a
 `roofline` object (kernel time from HIP events on the classify stream) and a
-`cpu_baseline` object (the CPU restatement timed on this host's cores).
+`cpu_baseline` object (the CPU restatement timed on this host's cores). The
+default 1-GPU run also measures the other BASELINE configs (C1, C2x, C3, C4,
+C5) in the same process and summarises them in `other_configs` (--others).
 """
 from __future__ import annotations
 
