@@ -165,6 +165,43 @@ int odpg_table_create(odpg_ctx_t *ctx, const odpg_rules_t *rules, odpg_table_t *
 	return 0;
 }
 
+/* the compiled image (odpg_rules_compile / odpg_table_import) of the stub:
+ * a tag and the caller's rule snapshot pointer, imported in the same process
+ * while the snapshot lives (the device groups' load, group.cpp) */
+#define STUB_IMAGE_TAG 0x53545542u
+
+struct stub_image {
+	uint32_t tag;
+	const odpg_rules_t *rules;
+};
+
+int odpg_rules_compile(const odpg_rules_t *rules, void *buf, size_t *size)
+{
+	if (!rules || !size)
+		return -EINVAL;
+	if (!buf || *size < sizeof(struct stub_image)) {
+		*size = sizeof(struct stub_image);
+		return -ENOSPC;
+	}
+	struct stub_image im = { STUB_IMAGE_TAG, rules };
+
+	memcpy(buf, &im, sizeof(im));
+	*size = sizeof(im);
+	return 0;
+}
+
+int odpg_table_import(odpg_ctx_t *ctx, const void *image, size_t size, odpg_table_t **tbl)
+{
+	struct stub_image im;
+
+	if (!image || size != sizeof(im))
+		return -EINVAL;
+	memcpy(&im, image, sizeof(im));
+	if (im.tag != STUB_IMAGE_TAG)
+		return -EINVAL;
+	return odpg_table_create(ctx, im.rules, tbl);
+}
+
 int odpg_table_update(odpg_ctx_t *ctx, odpg_table_t *tbl, const odpg_rules_t *rules)
 {
 	odpg_table_t n;

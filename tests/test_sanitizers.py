@@ -6,6 +6,8 @@ contention; odp_rt_loop.c: the loop pktio in DIRECT / SCHED / QUEUE / pcap
 input modes and the chunked, ordered hand-over between four receiving
 threads) with the device entry points replaced by tests/c/gpu_stub.c
 (classification through the CPU oracle, fences complete on record). The
+device groups (group.cpp: groups of 1, 3 and 5 contexts, host batches and
+per-member shards, against one context) run the same way. The
 reference's CI runs its suites under ASan + UBSan the same way
 (.github/workflows/ci-pipeline.yml:399-412). A sanitizer report, a failed
 check or a nonzero exit fails the test."""
@@ -27,11 +29,12 @@ def san_build():
     assert r.returncode == 0, r.stderr[-3000:]
 
 
-@pytest.mark.parametrize("prog", ["odp_rt_host", "odp_rt_loop", "odp_rt_loop:0,0,0"])
+@pytest.mark.parametrize("prog", ["odp_rt_host", "odp_rt_loop", "odp_rt_loop:0,0,0", "group_host"])
 @pytest.mark.parametrize("san", ["tsan", "asan"])
 def test_runtime_under_sanitizer(san_build, prog, san):
     """odp_rt_loop:0,0,0 runs with three device contexts (ODPG_DEVICES):
-    receive bursts spread over them"""
+    receive bursts spread over them. group_host: device groups of 1, 3 and 5
+    contexts (group.cpp, one host thread per member) against one context"""
     env = dict(os.environ)
     prog, _, devs = prog.partition(":")
     if devs:
@@ -48,3 +51,5 @@ def test_runtime_under_sanitizer(san_build, prog, san):
         assert "F sched, 4 threads: 200000 packets, each once and in order per thread" in r.stdout
         assert "B sched+cls: 300 packets, 150 to net10, 150 to default" in r.stdout
         assert "G sched hash=1: 300 packets" in r.stdout
+    if prog == "group_host":
+        assert "verdicts and counters equal one context's" in r.stdout
