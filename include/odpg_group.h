@@ -34,6 +34,12 @@ extern "C" {
 
 typedef struct odpg_group_s odpg_group_t;
 
+/* Threads: odpg_group_load must not overlap a classify call on the same
+ * group (it replaces the members' tables). Classify calls may come from
+ * several threads; odpg_group_counters_fold may run beside them and then
+ * sees the launches each member's stream had completed (as the reference's
+ * counters read at query time). */
+
 /* A group of n (1..64) device contexts, member i on devices[i] (a device may
  * repeat: its members then share the GPU, each with its own stream). */
 int  odpg_group_create(const int *devices, uint32_t n, odpg_group_t **grp);
